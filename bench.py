@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""Headline benchmark: DDRNet-23 training throughput at 1024x2048, 19 classes.
+
+BASELINE.json metric: "train images/sec (whole node) + single-GPU inference
+FPS, DDRNet-23 1024x2048 19-class".  One process per GPU (torchrun), RCCL
+all-reduce for N>1.  The timed region is the production training step of
+``SegTrainer.train_step`` -- forward (bf16 autocast, channels-last), OHEM loss on
+the main head + aux head (fused HIP kernels), backward, DDP gradient
+all-reduce, SGD step, OneCycle LR step and EMA update -- on synthetic
+device-resident batches (random-init weights; no datasets/checkpoints here).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+  torchrun --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line.  ``value`` = images/s over all ranks (weak
+scaling: B images per GPU per step); ``extra.infer_fps_*`` are single-GPU
+eval-mode FPS numbers for the same model at 1024x2048, batch 1.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from realtime_semantic_segmentation_pytorch_amd.configs import BaseConfig  # noqa: E402
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=8, help="images per GPU per step")
+    p.add_argument("--height", type=int, default=1024)
+    p.add_argument("--width", type=int, default=2048)
+    p.add_argument("--arch", default="DDRNet-23")
+    p.add_argument("--no-infer", action="store_true", help="skip the inference-FPS measurement")
+    p.add_argument("--fp32", action="store_true", help="disable bf16 autocast (diagnostic)")
+    p.add_argument("--no-fused-loss", action="store_true")
+    p.add_argument("--nchw", action="store_true")
+    p.add_argument("--profile-steps", type=int, default=0)
+    return p.parse_args()
+
+
+def make_config(a, world):
+    c = BaseConfig()
+    c.dataset = "cityscapes"
+    c.num_class = 19
+    c.model = "ddrnet"
+    c.arch_type = a.arch
+    c.use_aux = True
+    c.loss_type = "ohem"
+    c.optimizer_type = "sgd"
+    c.train_bs = a.batch
+    c.amp_training = not a.fp32
+    c.amp_dtype = "bf16"
+    c.channels_last = not a.nchw
+    c.fused_loss = not a.no_fused_loss
+    c.synthetic_data = True
+    c.synthetic_size = (a.height, a.width)
+    c.synthetic_len = a.batch * world * (a.steps + a.warmup + 8)
+    c.total_epoch = 4
+    c.crop_size = a.height
+    c.crop_h, c.crop_w = a.height, a.width
+    c.base_workers = 0
+    c.save_ckpt = False
+    c.use_tb = False
+    c.load_ckpt = False
+    c.save_dir = os.environ.get("RTSEG_BENCH_DIR", "/tmp/rtseg_bench")
+    c.is_testing = False
+    c.use_ema = True
+    return c
+
+
+@torch.no_grad()
+def infer_fps(model, h, w, dtype, channels_last, iters=30, warm=10):
+    model.eval()
+    x = torch.randn(1, 3, h, w, device="cuda")
+    if channels_last:
+        x = x.contiguous(memory_format=torch.channels_last)
+    ctx = torch.autocast("cuda", dtype=dtype, enabled=dtype != torch.float32)
+    with ctx:
+        for _ in range(warm):
+            model(x)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            model(x)
+        torch.cuda.synchronize()
+    return iters / (time.perf_counter() - t0)
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 and "LOCAL_RANK" not in os.environ:
+        raise SystemExit("N>1 must be launched with torchrun (one process per GPU)")
+    if a.gpus != world:
+        print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    if world == 1:
+        os.environ.pop("LOCAL_RANK", None)
+
+    from realtime_semantic_segmentation_pytorch_amd import ops
+    from realtime_semantic_segmentation_pytorch_amd.core import SegTrainer
+    from realtime_semantic_segmentation_pytorch_amd.datasets import DeviceBatches
+    from realtime_semantic_segmentation_pytorch_amd.parallel import de_parallel
+
+    torch.backends.cudnn.benchmark = True
+    cfg = make_config(a, world)
+    ops.load()
+    trainer = SegTrainer(cfg)
+    trainer.parallel_model(cfg)
+    trainer.model.train()
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    dev = trainer.device
+    data = DeviceBatches(a.batch, (a.height, a.width), cfg.num_class, cfg.ignore_index, device=dev,
+                         pool=2, channels_last=cfg.channels_last, seed=1234 + rank)
+
+    def step():
+        imgs, masks = data.next()
+        return trainer.train_step(imgs, masks)
+
+    for _ in range(a.warmup):
+        step()
+
+    def sync_all():
+        torch.cuda.synchronize()
+        if dist.is_initialized():
+            dist.barrier(device_ids=[dev.index])
+        torch.cuda.synchronize()
+
+    sync_all()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss, _ = step()
+    sync_all()
+    elapsed = time.perf_counter() - t0
+    if dist.is_initialized():
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loss_val = float(loss)
+
+    if a.profile_steps > 0 and rank == 0:
+        from torch.profiler import ProfilerActivity, profile
+
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+            for _ in range(a.profile_steps):
+                step()
+            torch.cuda.synchronize()
+        os.makedirs("gpurun_out", exist_ok=True)
+        with open("gpurun_out/torch_profile.txt", "w") as f:
+            f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
+
+    ms = elapsed / a.steps * 1e3
+    imgs_per_s = a.batch * world * a.steps / elapsed
+    extra = {"loss_last": loss_val, "per_gpu_batch": a.batch,
+             "peak_mem_gb": torch.cuda.max_memory_allocated(dev) / 2 ** 30,
+             "hip_ext_loaded": bool(ops.load()), "channels_last": cfg.channels_last,
+             "fused_loss": cfg.fused_loss}
+    if rank == 0 and not a.no_infer:
+        m = de_parallel(trainer.model)
+        extra["infer_fps_bf16_bs1_1024x2048"] = round(infer_fps(m, a.height, a.width, torch.bfloat16,
+                                                                cfg.channels_last), 2)
+        extra["infer_fps_fp32_bs1_1024x2048"] = round(infer_fps(m, a.height, a.width, torch.float32,
+                                                                cfg.channels_last), 2)
+    if dist.is_initialized():
+        dist.barrier(device_ids=[dev.index])
+    if rank == 0:
+        out = {
+            "metric": "train_images_per_sec",
+            "value": round(imgs_per_s, 3),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32" if a.fp32 else "bf16",
+            "data": "synthetic (device-resident random 1024x2048 images, blocky 19-class masks, "
+                    "random-init weights)",
+            "config": {"model": a.arch, "global_batch": a.batch * world,
+                       "seq_len": f"{a.height}x{a.width}", "parallelism": f"dp{world}",
+                       "num_class": 19, "loss": "ohem+aux", "optimizer": "sgd+onecycle+ema"},
+            "extra": extra,
+        }
+        print(json.dumps(out), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,189 @@
+"""Segmentation trainer (parity: reference core/seg_trainer.py:16-191).
+
+The training step keeps the reference's objective exactly -- main loss + aux
+heads (nearest-resized masks, coefficients ``aux_coef``) or the STDC detail
+head (Laplacian detail GT, Dice+BCE) + optional Hinton KD -- but is arranged
+for the GPU:
+
+* the model runs under bf16 autocast (fp16 + GradScaler when ``amp_dtype='fp16'``)
+  on channels-last activations;
+* ``defer_final_upsample`` makes the model hand back head-resolution logits and
+  the fused HIP loss kernel upsamples inside the loss (no full-resolution
+  logits in HBM); aux losses read nearest-resized labels in-kernel;
+* there is no host synchronisation inside a step: the loss is only copied to
+  the host every ``log_interval`` iterations (the reference syncs >= 5x/step).
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+from PIL import Image
+
+from .. import ops
+from ..models import get_teacher_model
+from ..parallel import de_parallel
+from ..utils import get_colormap, get_seg_metrics, sampler_set_epoch
+from .base_trainer import BaseTrainer
+from .loss import kd_loss_fn
+
+
+class SegTrainer(BaseTrainer):
+    def __init__(self, config):
+        super().__init__(config)
+        self.config = config
+        if config.is_testing:
+            self.colormap = torch.tensor(get_colormap(config), dtype=torch.uint8, device=self.device)
+        else:
+            self.teacher_model = get_teacher_model(config, self.device)
+            if self.teacher_model is not None and getattr(config, "channels_last", False) and self.device.type == "cuda":
+                self.teacher_model = self.teacher_model.to(memory_format=torch.channels_last)
+            self.metrics = get_seg_metrics(config).to(self.device)
+            if config.use_detail_head:
+                from ..models.stdc import LaplacianConv
+                from .loss import get_detail_loss_fn
+
+                self.laplacian_conv = LaplacianConv(self.device)
+                self.detail_loss_fn = get_detail_loss_fn(config)
+
+    # ------------------------------------------------------------------ step
+    def _autocast(self):
+        cfg = self.config
+        return torch.autocast(device_type=self.device.type, dtype=self.amp_dtype,
+                              enabled=bool(cfg.amp_training))
+
+    def _prep(self, images, masks):
+        images = images.to(self.device, dtype=torch.float32, non_blocking=True)
+        if getattr(self.config, "channels_last", False) and self.device.type == "cuda":
+            images = images.contiguous(memory_format=torch.channels_last)
+        masks = masks.to(self.device, dtype=torch.long, non_blocking=True)
+        return images, masks
+
+    def compute_loss(self, images, masks):
+        """Forward + total loss. Returns (loss, main_preds, extras dict)."""
+        cfg = self.config
+        extras = {}
+        defer = bool(getattr(cfg, "fused_loss", True)) and not cfg.use_detail_head
+        with self._autocast(), ops.defer_final_upsample(defer):
+            if cfg.use_aux:
+                preds, preds_aux = self.model(images, is_training=True)
+                loss = self.loss_fn(preds, masks)
+                if cfg.aux_coef is None:
+                    cfg.aux_coef = [1.0] * len(preds_aux)
+                coefs = cfg.aux_coef if isinstance(cfg.aux_coef, (list, tuple)) else [cfg.aux_coef]
+                if len(coefs) != len(preds_aux):
+                    raise ValueError("Auxiliary loss coefficient length does not match.")
+                for coef, aux in zip(coefs, preds_aux):
+                    loss = loss + float(coef) * self.loss_fn.aux(aux, masks)
+            elif cfg.use_detail_head:
+                detail_gt = self.laplacian_conv(masks.unsqueeze(1).float())
+                detail_gt = de_parallel(self.model).detail_conv(detail_gt)
+                detail_gt = (detail_gt > cfg.detail_thrs).to(detail_gt.dtype)
+                preds, preds_detail = self.model(images, is_training=True)
+                preds_detail = F.interpolate(preds_detail, detail_gt.shape[2:], mode="bilinear",
+                                             align_corners=True)
+                loss_detail = self.detail_loss_fn(preds_detail.float(), detail_gt.float())
+                loss = self.loss_fn(preds, masks) + cfg.detail_loss_coef * loss_detail
+                extras["loss_detail"] = loss_detail
+            else:
+                preds = self.model(images)
+                loss = self.loss_fn(preds, masks)
+            if cfg.kd_training:
+                with torch.no_grad(), ops.defer_final_upsample(False):
+                    teacher_preds = self.teacher_model(images)
+                loss_kd = kd_loss_fn(cfg, preds, teacher_preds)
+                extras["loss_main"] = loss
+                loss = loss + cfg.kd_loss_coefficient * loss_kd
+                extras["loss_kd"] = loss_kd
+        return loss, preds, extras
+
+    def train_step(self, images, masks):
+        self.optimizer.zero_grad(set_to_none=True)
+        loss, _, extras = self.compute_loss(images, masks)
+        self.scaler.scale(loss).backward()
+        self.scaler.step(self.optimizer)
+        self.scaler.update()
+        total = getattr(self.scheduler, "total_steps", None)
+        if total is None or self.scheduler.last_epoch < total:  # never step OneCycle past its end
+            self.scheduler.step()
+        self.train_itrs += 1
+        self.ema_model.update(self.model, self.train_itrs)
+        return loss.detach(), extras
+
+    # ----------------------------------------------------------------- epoch
+    def train_one_epoch(self, config):
+        self.model.train()
+        sampler_set_epoch(config, self.train_loader, self.cur_epoch)
+        log_every = max(1, int(getattr(config, "log_interval", 20)))
+        max_itrs = getattr(config, "max_train_itrs", None)
+        for cur_itrs, (images, masks) in enumerate(self.train_loader):
+            if max_itrs is not None and cur_itrs >= max_itrs:
+                break
+            self.cur_itrs = cur_itrs
+            images, masks = self._prep(images, masks)
+            loss, extras = self.train_step(images, masks)
+            if self.main_rank and (cur_itrs % log_every == 0):
+                lv = float(loss)
+                if config.use_tb and self.writer is not None:
+                    self.writer.add_scalar("train/loss", lv, self.train_itrs)
+                    if "loss_detail" in extras:
+                        self.writer.add_scalar("train/loss_detail", float(extras["loss_detail"]), self.train_itrs)
+                    if "loss_kd" in extras:
+                        self.writer.add_scalar("train/loss_kd", float(extras["loss_kd"]), self.train_itrs)
+                        self.writer.add_scalar("train/loss_total", lv, self.train_itrs)
+                if self.logger is not None:
+                    self.logger.info(f"Epoch:{self.cur_epoch}/{config.total_epoch}    | "
+                                     f"Itr:{cur_itrs}/{len(self.train_loader)}    | Loss:{lv:4.4g}")
+
+    @torch.no_grad()
+    def validate(self, config, val_best=False):
+        model = self.ema_model.ema
+        model.eval()
+        for images, masks in self.val_loader:
+            images, masks = self._prep(images, masks)
+            with self._autocast():
+                preds = model(images)
+            self.metrics.update(preds, masks)
+        iou = self.metrics.compute()
+        score = float(iou.mean())
+        if self.main_rank:
+            if val_best:
+                self._log(f"\n\nTrain {config.total_epoch} epochs finished.\n\nBest mIoU is: {score:.4f}\n")
+            else:
+                self._log(f" Epoch{self.cur_epoch} mIoU: {score:.4f}    | best mIoU so far: {self.best_score:.4f}\n")
+            if config.use_tb and self.writer is not None and self.cur_epoch < config.total_epoch and not val_best:
+                self.writer.add_scalar("val/mIoU", score, self.cur_epoch + 1)
+                for i in range(config.num_class):
+                    self.writer.add_scalar(f"val/IoU_cls{i:02d}", float(iou[i]), self.cur_epoch + 1)
+        self.metrics.reset()
+        return score
+
+    @torch.no_grad()
+    def predict(self, config):
+        if config.DDP:
+            raise ValueError("Predict mode currently does not support DDP.")
+        self._log("\nStart predicting...\n")
+        out_dir = os.path.join(config.save_dir, "predicts")
+        os.makedirs(out_dir, exist_ok=True)
+        self.model.eval()
+        for images, images_aug, names in self.test_loader:
+            images_aug = images_aug.to(self.device, dtype=torch.float32)
+            if getattr(config, "channels_last", False) and self.device.type == "cuda":
+                images_aug = images_aug.contiguous(memory_format=torch.channels_last)
+            with self._autocast():
+                preds = self.model(images_aug)
+            colored = self.colormap[ops.materialize(preds).argmax(1)].cpu().numpy()
+            for i, name in enumerate(names):
+                path = os.path.join(out_dir, name)
+                suffix = name.rsplit(".", 1)[-1] if "." in name else "png"
+                mask_img = Image.fromarray(colored[i].astype(np.uint8))
+                if config.save_mask:
+                    mask_img.save(path)
+                if config.blend_prediction:
+                    raw = Image.fromarray(np.asarray(images[i]).astype(np.uint8))
+                    if raw.size != mask_img.size:
+                        raw = raw.resize(mask_img.size, Image.BILINEAR)
+                    Image.blend(raw, mask_img, config.blend_alpha).save(
+                        path[: -len(suffix) - 1] + f"_blend.{suffix}" if "." in name else path + "_blend.png")

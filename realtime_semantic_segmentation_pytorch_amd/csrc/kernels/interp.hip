@@ -1,0 +1,283 @@
+// Bilinear resize (align_corners True/False) with a fused "+ skip, activation"
+// epilogue, and an atomic-free gather backward.
+//
+// Replaces the reference's F.interpolate(..., mode='bilinear') call sites
+// (78 of them, e.g. reference models/ddrnet.py:233-236 BilateralFusion,
+// ddrnet.py:275-289 DAPPM, modules.py:150-153 PPM) and the
+// "upsample + add (+relu)" feature-fusion pattern that follows most of them.
+//
+// Layouts: any strided 4-D tensor. Channels-last bf16 tensors whose channel
+// count is a multiple of 8 take a 16-byte vector path (one thread = 8
+// channels of one pixel), everything else a scalar path walking the output in
+// memory order. Backward is a gather (each input pixel sums the output pixels
+// that read it) so no float atomics are issued.
+#include "rtseg_common.h"
+#include "rtseg_launch.h"
+
+namespace rtseg {
+
+struct Shape4 { int n, c, h, w; int64_t sn, sc, sh, sw; };
+
+__device__ __forceinline__ int64_t off4(const Shape4& s, int n, int c, int h, int w) {
+  return n * s.sn + c * s.sc + h * s.sh + w * s.sw;
+}
+
+// ------------------------------- forward -----------------------------------
+template <typename T, int ACT, bool SKIP>
+__global__ void __launch_bounds__(256) interp_fwd_scalar(
+    const T* __restrict__ x, Shape4 xs, const T* __restrict__ skip, Shape4 ks,
+    T* __restrict__ y, Shape4 ys, LinMap mh, LinMap mw) {
+  const int64_t total = static_cast<int64_t>(ys.n) * ys.c * ys.h * ys.w;
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    int ox = static_cast<int>(i % ys.w);
+    int64_t t = i / ys.w;
+    int oy = static_cast<int>(t % ys.h);
+    t /= ys.h;
+    int c = static_cast<int>(t % ys.c);
+    int n = static_cast<int>(t / ys.c);
+    int y0, y1, x0, x1; float ly, lx;
+    mh.map(oy, y0, y1, ly);
+    mw.map(ox, x0, x1, lx);
+    const T* b = x + n * xs.sn + c * xs.sc;
+    float v00 = Io<T>::ld(b + y0 * xs.sh + x0 * xs.sw);
+    float v01 = Io<T>::ld(b + y0 * xs.sh + x1 * xs.sw);
+    float v10 = Io<T>::ld(b + y1 * xs.sh + x0 * xs.sw);
+    float v11 = Io<T>::ld(b + y1 * xs.sh + x1 * xs.sw);
+    float v = (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11);
+    if constexpr (SKIP) v += Io<T>::ld(skip + off4(ks, n, c, oy, ox));
+    Io<T>::st(y + off4(ys, n, c, oy, ox), act_fwd<ACT>(v));
+  }
+}
+
+typedef short short8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void unpack8(const short8& v, float* f) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = bf16_to_f32(static_cast<uint16_t>(v[j]));
+}
+
+// Channels-last bf16, C % 8 == 0: one thread = 8 channels of one output pixel.
+template <int ACT, bool SKIP>
+__global__ void __launch_bounds__(256) interp_fwd_cl_bf16(
+    const uint16_t* __restrict__ x, Shape4 xs, const uint16_t* __restrict__ skip, Shape4 ks,
+    uint16_t* __restrict__ y, Shape4 ys, LinMap mh, LinMap mw) {
+  const int cv = ys.c >> 3;
+  const int64_t total = static_cast<int64_t>(ys.n) * ys.h * ys.w * cv;
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    int c8 = static_cast<int>(i % cv);
+    int64_t t = i / cv;
+    int ox = static_cast<int>(t % ys.w);
+    t /= ys.w;
+    int oy = static_cast<int>(t % ys.h);
+    int n = static_cast<int>(t / ys.h);
+    int y0, y1, x0, x1; float ly, lx;
+    mh.map(oy, y0, y1, ly);
+    mw.map(ox, x0, x1, lx);
+    const uint16_t* b = x + n * xs.sn + (c8 << 3);
+    short8 a00 = *reinterpret_cast<const short8*>(b + y0 * xs.sh + x0 * xs.sw);
+    short8 a01 = *reinterpret_cast<const short8*>(b + y0 * xs.sh + x1 * xs.sw);
+    short8 a10 = *reinterpret_cast<const short8*>(b + y1 * xs.sh + x0 * xs.sw);
+    short8 a11 = *reinterpret_cast<const short8*>(b + y1 * xs.sh + x1 * xs.sw);
+    float f00[8], f01[8], f10[8], f11[8], fk[8];
+    unpack8(a00, f00); unpack8(a01, f01); unpack8(a10, f10); unpack8(a11, f11);
+    if constexpr (SKIP) {
+      short8 k = *reinterpret_cast<const short8*>(skip + n * ks.sn + oy * ks.sh + ox * ks.sw + (c8 << 3));
+      unpack8(k, fk);
+    }
+    const float w00 = (1.f - ly) * (1.f - lx), w01 = (1.f - ly) * lx;
+    const float w10 = ly * (1.f - lx), w11 = ly * lx;
+    short8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = w00 * f00[j] + w01 * f01[j] + w10 * f10[j] + w11 * f11[j];
+      if constexpr (SKIP) v += fk[j];
+      o[j] = static_cast<short>(f32_to_bf16(act_fwd<ACT>(v)));
+    }
+    *reinterpret_cast<short8*>(y + n * ys.sn + oy * ys.sh + ox * ys.sw + (c8 << 3)) = o;
+  }
+}
+
+// ------------------------------- backward ----------------------------------
+// grad_x[n,c,iy,ix] = sum_{oy,ox} wy(oy,iy) * wx(ox,ix) * g[n,c,oy,ox]
+template <typename T>
+__global__ void __launch_bounds__(256) interp_bwd_scalar(
+    const T* __restrict__ g, Shape4 gs, T* __restrict__ gx, Shape4 xs, LinMap mh, LinMap mw) {
+  const int64_t total = static_cast<int64_t>(xs.n) * xs.c * xs.h * xs.w;
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    int ix = static_cast<int>(i % xs.w);
+    int64_t t = i / xs.w;
+    int iy = static_cast<int>(t % xs.h);
+    t /= xs.h;
+    int c = static_cast<int>(t % xs.c);
+    int n = static_cast<int>(t / xs.c);
+    int ylo, yhi, xlo, xhi;
+    mh.out_range(iy, gs.h, ylo, yhi);
+    mw.out_range(ix, gs.w, xlo, xhi);
+    const T* gb = g + n * gs.sn + c * gs.sc;
+    float acc = 0.f;
+    for (int oy = ylo; oy <= yhi; ++oy) {
+      float wy = mh.weight(oy, iy);
+      if (wy == 0.f) continue;
+      float row = 0.f;
+      for (int ox = xlo; ox <= xhi; ++ox) {
+        float wx = mw.weight(ox, ix);
+        if (wx != 0.f) row += wx * Io<T>::ld(gb + oy * gs.sh + ox * gs.sw);
+      }
+      acc += wy * row;
+    }
+    Io<T>::st(gx + off4(xs, n, c, iy, ix), acc);
+  }
+}
+
+__global__ void __launch_bounds__(256) interp_bwd_cl_bf16(
+    const uint16_t* __restrict__ g, Shape4 gs, uint16_t* __restrict__ gx, Shape4 xs, LinMap mh,
+    LinMap mw) {
+  const int cv = xs.c >> 3;
+  const int64_t total = static_cast<int64_t>(xs.n) * xs.h * xs.w * cv;
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    int c8 = static_cast<int>(i % cv);
+    int64_t t = i / cv;
+    int ix = static_cast<int>(t % xs.w);
+    t /= xs.w;
+    int iy = static_cast<int>(t % xs.h);
+    int n = static_cast<int>(t / xs.h);
+    int ylo, yhi, xlo, xhi;
+    mh.out_range(iy, gs.h, ylo, yhi);
+    mw.out_range(ix, gs.w, xlo, xhi);
+    const uint16_t* gb = g + n * gs.sn + (c8 << 3);
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    for (int oy = ylo; oy <= yhi; ++oy) {
+      float wy = mh.weight(oy, iy);
+      if (wy == 0.f) continue;
+      for (int ox = xlo; ox <= xhi; ++ox) {
+        float w = wy * mw.weight(ox, ix);
+        if (w == 0.f) continue;
+        float f[8];
+        unpack8(*reinterpret_cast<const short8*>(gb + oy * gs.sh + ox * gs.sw), f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += w * f[j];
+      }
+    }
+    short8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = static_cast<short>(f32_to_bf16(acc[j]));
+    *reinterpret_cast<short8*>(gx + n * xs.sn + iy * xs.sh + ix * xs.sw + (c8 << 3)) = o;
+  }
+}
+
+// g_masked = act'(y) * g (also the gradient of the fused skip input).
+template <typename T, int ACT>
+__global__ void __launch_bounds__(256) act_mask_kernel(const T* __restrict__ g,
+                                                       const T* __restrict__ y,
+                                                       T* __restrict__ out, int64_t n) {
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    Io<T>::st(out + i, act_bwd_from_out<ACT>(Io<T>::ld(g + i), Io<T>::ld(y + i)));
+  }
+}
+
+// ------------------------------- launchers ---------------------------------
+static Shape4 mk(const Tensor4& t) {
+  Shape4 s;
+  s.n = t.n; s.c = t.c; s.h = t.h; s.w = t.w;
+  s.sn = t.sn; s.sc = t.sc; s.sh = t.sh; s.sw = t.sw;
+  return s;
+}
+
+static bool cl_vec_ok(const Tensor4& t) {
+  return t.sc == 1 && (t.c % 8) == 0 && (t.sw % 8) == 0 && (t.sh % 8) == 0 && (t.sn % 8) == 0 &&
+         (reinterpret_cast<uintptr_t>(t.data) % 16) == 0;
+}
+
+template <typename T, int ACT, bool SKIP>
+static void fwd_dispatch(const Tensor4& x, const Tensor4* skip, const Tensor4& y, LinMap mh,
+                         LinMap mw, hipStream_t st) {
+  Shape4 xs = mk(x), ys = mk(y), ks = skip ? mk(*skip) : ys;
+  const T* kp = skip ? static_cast<const T*>(skip->data) : nullptr;
+  if constexpr (sizeof(T) == 2 && !std::is_same<T, _Float16>::value) {
+    if (cl_vec_ok(x) && cl_vec_ok(y) && (!skip || cl_vec_ok(*skip))) {
+      int64_t work = static_cast<int64_t>(y.n) * y.h * y.w * (y.c / 8);
+      interp_fwd_cl_bf16<ACT, SKIP><<<stream_grid(work, 256), 256, 0, st>>>(
+          static_cast<const uint16_t*>(x.data), xs, kp, ks, static_cast<uint16_t*>(y.data), ys, mh, mw);
+      return;
+    }
+  }
+  int64_t work = static_cast<int64_t>(y.n) * y.c * y.h * y.w;
+  interp_fwd_scalar<T, ACT, SKIP><<<stream_grid(work, 256), 256, 0, st>>>(
+      static_cast<const T*>(x.data), xs, kp, ks, static_cast<T*>(y.data), ys, mh, mw);
+}
+
+template <typename T>
+static void fwd_act(const Tensor4& x, const Tensor4* skip, const Tensor4& y, int act, LinMap mh,
+                    LinMap mw, hipStream_t st) {
+  if (skip) {
+    if (act == kActReLU) fwd_dispatch<T, kActReLU, true>(x, skip, y, mh, mw, st);
+    else if (act == kActReLU6) fwd_dispatch<T, kActReLU6, true>(x, skip, y, mh, mw, st);
+    else fwd_dispatch<T, kActNone, true>(x, skip, y, mh, mw, st);
+  } else {
+    if (act == kActReLU) fwd_dispatch<T, kActReLU, false>(x, skip, y, mh, mw, st);
+    else if (act == kActReLU6) fwd_dispatch<T, kActReLU6, false>(x, skip, y, mh, mw, st);
+    else fwd_dispatch<T, kActNone, false>(x, skip, y, mh, mw, st);
+  }
+}
+
+void launch_interp_fwd(const Tensor4& x, const Tensor4* skip, const Tensor4& y, int act,
+                       bool align_corners, hipStream_t st) {
+  LinMap mh = LinMap::make(x.h, y.h, align_corners);
+  LinMap mw = LinMap::make(x.w, y.w, align_corners);
+  switch (x.dtype) {
+    case kF32: fwd_act<float>(x, skip, y, act, mh, mw, st); break;
+    case kBF16: fwd_act<uint16_t>(x, skip, y, act, mh, mw, st); break;
+    default: fwd_act<_Float16>(x, skip, y, act, mh, mw, st); break;
+  }
+}
+
+template <typename T>
+static void bwd_t(const Tensor4& g, const Tensor4& gx, LinMap mh, LinMap mw, hipStream_t st) {
+  Shape4 gs = mk(g), xs = mk(gx);
+  if constexpr (std::is_same<T, uint16_t>::value) {
+    if (cl_vec_ok(g) && cl_vec_ok(gx)) {
+      int64_t work = static_cast<int64_t>(gx.n) * gx.h * gx.w * (gx.c / 8);
+      interp_bwd_cl_bf16<<<stream_grid(work, 256), 256, 0, st>>>(
+          static_cast<const uint16_t*>(g.data), gs, static_cast<uint16_t*>(gx.data), xs, mh, mw);
+      return;
+    }
+  }
+  int64_t work = static_cast<int64_t>(gx.n) * gx.c * gx.h * gx.w;
+  interp_bwd_scalar<T><<<stream_grid(work, 256), 256, 0, st>>>(
+      static_cast<const T*>(g.data), gs, static_cast<T*>(gx.data), xs, mh, mw);
+}
+
+void launch_interp_bwd(const Tensor4& g, const Tensor4& gx, bool align_corners, hipStream_t st) {
+  LinMap mh = LinMap::make(gx.h, g.h, align_corners);
+  LinMap mw = LinMap::make(gx.w, g.w, align_corners);
+  switch (g.dtype) {
+    case kF32: bwd_t<float>(g, gx, mh, mw, st); break;
+    case kBF16: bwd_t<uint16_t>(g, gx, mh, mw, st); break;
+    default: bwd_t<_Float16>(g, gx, mh, mw, st); break;
+  }
+}
+
+void launch_act_mask(const void* g, const void* y, void* out, int64_t n, int dtype, int act,
+                     hipStream_t st) {
+  int grid = stream_grid(n, 256);
+#define RT_MASK(T)                                                                              \
+  if (act == kActReLU6)                                                                         \
+    act_mask_kernel<T, kActReLU6><<<grid, 256, 0, st>>>(static_cast<const T*>(g),               \
+                                                        static_cast<const T*>(y), static_cast<T*>(out), n); \
+  else                                                                                          \
+    act_mask_kernel<T, kActReLU><<<grid, 256, 0, st>>>(static_cast<const T*>(g),                \
+                                                       static_cast<const T*>(y), static_cast<T*>(out), n);
+  if (dtype == kF32) { RT_MASK(float) }
+  else if (dtype == kBF16) { RT_MASK(uint16_t) }
+  else { RT_MASK(_Float16) }
+#undef RT_MASK
+}
+
+}  // namespace rtseg

@@ -1,0 +1,66 @@
+"""Cityscapes fine annotations (parity: reference datasets/cityscapes.py:11-162).
+
+Layout: ``{data_root}/leftImg8bit/{mode}/{city}/*_leftImg8bit.png`` and
+``{data_root}/gtFine/{mode}/{city}/*_gtFine_labelIds.png``.  Masks are mapped
+from label ids to the 19 train ids (255 = ignore) AFTER augmentation, so pad
+value 0 ('unlabeled') becomes ignore exactly like the reference.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+from PIL import Image
+from torch.utils.data import Dataset
+
+from . import transforms as T
+
+# label id -> train id for ids 0..33 (+ 'license plate' id -1 stored last), from
+# the official cityscapesScripts label table.
+_TRAIN_IDS = [255, 255, 255, 255, 255, 255, 255, 0, 1, 255, 255, 2, 3, 4, 255, 255, 255, 5, 255,
+              6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 255, 255, 16, 17, 18, -1]
+CLASS_NAMES = ["road", "sidewalk", "building", "wall", "fence", "pole", "traffic light",
+               "traffic sign", "vegetation", "terrain", "sky", "person", "rider", "car", "truck",
+               "bus", "train", "motorcycle", "bicycle"]
+
+
+def _sample_rng(index: int) -> np.random.Generator:
+    return np.random.default_rng([torch.initial_seed() % (2 ** 63), int(index)])
+
+
+class Cityscapes(Dataset):
+    id_to_train_id = np.array(_TRAIN_IDS)
+    # uint8 lookup (255 for anything unknown) used by encode_target
+    _lut = np.full(256, 255, np.uint8)
+    _lut[:34] = np.array(_TRAIN_IDS[:34], np.int64).clip(0, 255).astype(np.uint8)
+
+    def __init__(self, config, mode="train"):
+        root = os.path.expanduser(config.data_root or config.dataroot or "")
+        img_dir = os.path.join(root, "leftImg8bit", mode)
+        msk_dir = os.path.join(root, "gtFine", mode)
+        if not os.path.isdir(img_dir):
+            raise RuntimeError(f"Image directory: {img_dir} does not exist.")
+        if not os.path.isdir(msk_dir):
+            raise RuntimeError(f"Mask directory: {msk_dir} does not exist.")
+        self.mode = mode
+        self.transform = T.train_transform(config) if mode == "train" else T.val_transform(config)
+        self.images, self.masks = [], []
+        for city in sorted(os.listdir(img_dir)):
+            for name in sorted(os.listdir(os.path.join(img_dir, city))):
+                self.images.append(os.path.join(img_dir, city, name))
+                stem = name.split("_leftImg8bit")[0]
+                self.masks.append(os.path.join(msk_dir, city, f"{stem}_gtFine_labelIds.png"))
+
+    def __len__(self):
+        return len(self.images)
+
+    def __getitem__(self, index):
+        image = np.asarray(Image.open(self.images[index]).convert("RGB"))
+        mask = np.asarray(Image.open(self.masks[index]).convert("L"))
+        image, mask = self.transform(image, mask, _sample_rng(index))
+        return T.to_tensor(image), torch.from_numpy(self.encode_target(mask).astype(np.int64))
+
+    @classmethod
+    def encode_target(cls, mask):
+        return cls._lut[np.asarray(mask, dtype=np.uint8)]

@@ -1,0 +1,151 @@
+"""Building blocks shared by the model zoo.
+
+Parity target: reference models/modules.py (conv3x3/conv1x1 :7-15,
+channel_shuffle :18-32, DSConvBNAct :36-42, DWConvBNAct :46-59, PWConvBNAct
+:63-69, ConvBNAct :73-85, DeConvBNAct :89-108, Activation :111-131,
+PyramidPoolingModule :134-158, SegHead :161-166).
+
+The module trees (and therefore ``state_dict`` keys such as ``<m>.0.weight``,
+``<m>.1.running_mean``, ``<m>.2.activation.weight``, ``<m>.up_conv.0.weight``)
+are kept identical to the reference so checkpoints interchange.  What differs
+is the execution: resize/fusion points call the HIP kernels in
+:mod:`..ops`, and ``ConvBNAct`` accepts ``groups`` (the reference lacks it, which
+breaks RegSeg -- SURVEY A.1 #8).
+"""
+from __future__ import annotations
+
+from typing import Sequence, Union
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+
+IntOrPair = Union[int, Sequence[int]]
+
+
+def _same_padding(kernel_size: IntOrPair, dilation: int = 1):
+    """'same' padding for odd kernels (int or (kh, kw)), scaled by dilation."""
+    if isinstance(kernel_size, (list, tuple)):
+        return tuple((k - 1) // 2 * dilation for k in kernel_size)
+    return (kernel_size - 1) // 2 * dilation
+
+
+def conv3x3(in_channels, out_channels, stride=1, bias=False):
+    return nn.Conv2d(in_channels, out_channels, 3, stride, 1, bias=bias)
+
+
+def conv1x1(in_channels, out_channels, stride=1, bias=False):
+    return nn.Conv2d(in_channels, out_channels, 1, stride, 0, bias=bias)
+
+
+def channel_shuffle(x: torch.Tensor, groups: int = 2) -> torch.Tensor:
+    """ShuffleNet channel shuffle: [N, g*k, H, W] -> interleave the g groups."""
+    n, c, h, w = x.shape
+    return x.reshape(n, groups, c // groups, h, w).transpose(1, 2).reshape(n, c, h, w)
+
+
+_ACTIVATIONS = {
+    "relu": nn.ReLU, "relu6": nn.ReLU6, "leakyrelu": nn.LeakyReLU, "prelu": nn.PReLU,
+    "celu": nn.CELU, "elu": nn.ELU, "hardswish": nn.Hardswish, "hardtanh": nn.Hardtanh,
+    "gelu": nn.GELU, "glu": nn.GLU, "selu": nn.SELU, "silu": nn.SiLU, "sigmoid": nn.Sigmoid,
+    "softmax": nn.Softmax, "tanh": nn.Tanh, "none": nn.Identity,
+}
+
+
+class Activation(nn.Module):
+    """Named activation; the wrapped module lives at ``.activation`` (checkpoint ABI)."""
+
+    def __init__(self, act_type: str, **kwargs):
+        super().__init__()
+        key = act_type.lower()
+        if key not in _ACTIVATIONS:
+            raise NotImplementedError(f"Unsupport activation type: {act_type}")
+        self.act_type = key
+        self.activation = _ACTIVATIONS[key](**kwargs)
+
+    def forward(self, x):
+        return self.activation(x)
+
+
+class ConvBNAct(nn.Sequential):
+    """Conv2d -> BatchNorm2d -> Activation, children ``0 / 1 / 2``."""
+
+    def __init__(self, in_channels, out_channels, kernel_size: IntOrPair = 3, stride=1,
+                 dilation=1, bias=False, act_type="relu", groups=1, **kwargs):
+        conv = nn.Conv2d(in_channels, out_channels, kernel_size, stride,
+                         _same_padding(kernel_size, dilation), dilation, groups=groups, bias=bias)
+        super().__init__(conv, nn.BatchNorm2d(out_channels), Activation(act_type, **kwargs))
+
+
+class DWConvBNAct(nn.Sequential):
+    """Depth-wise conv (channel multiplier = out/in allowed) -> BN -> act."""
+
+    def __init__(self, in_channels, out_channels, kernel_size: IntOrPair, stride=1, dilation=1,
+                 act_type="relu", **kwargs):
+        conv = nn.Conv2d(in_channels, out_channels, kernel_size, stride,
+                         _same_padding(kernel_size, dilation), dilation=dilation,
+                         groups=in_channels, bias=False)
+        super().__init__(conv, nn.BatchNorm2d(out_channels), Activation(act_type, **kwargs))
+
+
+class PWConvBNAct(nn.Sequential):
+    """1x1 conv (bias by default) -> BN -> act."""
+
+    def __init__(self, in_channels, out_channels, act_type="relu", bias=True, **kwargs):
+        super().__init__(nn.Conv2d(in_channels, out_channels, 1, bias=bias),
+                         nn.BatchNorm2d(out_channels), Activation(act_type, **kwargs))
+
+
+class DSConvBNAct(nn.Sequential):
+    """Depth-wise separable: DWConvBNAct (children ``0``) + PWConvBNAct (``1``)."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, dilation=1,
+                 act_type="relu", **kwargs):
+        super().__init__(
+            DWConvBNAct(in_channels, in_channels, kernel_size, stride, dilation, act_type, **kwargs),
+            PWConvBNAct(in_channels, out_channels, act_type, **kwargs))
+
+
+class DeConvBNAct(nn.Module):
+    """Exact x`scale_factor` transposed-conv upsample -> BN -> act (``up_conv.{0,1,2}``)."""
+
+    def __init__(self, in_channels, out_channels, scale_factor=2, kernel_size=None, padding=None,
+                 act_type="relu", **kwargs):
+        super().__init__()
+        k = 2 * scale_factor - 1 if kernel_size is None else kernel_size
+        p = (k - 1) // 2 if padding is None else padding
+        self.up_conv = nn.Sequential(
+            nn.ConvTranspose2d(in_channels, out_channels, kernel_size=k, stride=scale_factor,
+                               padding=p, output_padding=scale_factor - 1),
+            nn.BatchNorm2d(out_channels),
+            Activation(act_type, **kwargs))
+
+    def forward(self, x):
+        return self.up_conv(x)
+
+
+class PyramidPoolingModule(nn.Module):
+    """PSP pooling: 4 adaptive-average branches (1x1 conv, C/4) resized back and concatenated."""
+
+    def __init__(self, in_channels, out_channels, act_type, pool_sizes=(1, 2, 4, 6), bias=False):
+        super().__init__()
+        if len(pool_sizes) != 4:
+            raise AssertionError("Length of pool size should be 4.\n")
+        hid = in_channels // 4
+        for i, ps in enumerate(pool_sizes, start=1):
+            setattr(self, f"stage{i}", nn.Sequential(nn.AdaptiveAvgPool2d(ps), conv1x1(in_channels, hid)))
+        self.conv = PWConvBNAct(2 * in_channels, out_channels, act_type=act_type, bias=bias)
+
+    def forward(self, x):
+        hw = x.shape[2:]
+        feats = [x] + [ops.interpolate(getattr(self, f"stage{i}")(x), hw, True) for i in range(1, 5)]
+        return self.conv(torch.cat(feats, dim=1))
+
+
+class SegHead(nn.Sequential):
+    """3x3 ConvBNAct (-> hid) + 1x1 classifier."""
+
+    def __init__(self, in_channels, num_class, act_type, hid_channels=128):
+        super().__init__(ConvBNAct(in_channels, hid_channels, 3, act_type=act_type),
+                         conv1x1(hid_channels, num_class))

@@ -1,0 +1,19 @@
+"""Hand-written HIP/CDNA4 operators and their autograd wrappers.
+
+Every public op dispatches to the in-tree HIP extension for GPU tensors and to
+an equivalent PyTorch formulation for CPU tensors (see ``_ext.py``).
+"""
+from ._ext import load, use_hip, hip_disabled, library_path
+from .interp import (interpolate, final_upsample, defer_final_upsample, DeferredLogits,
+                     materialize)
+from .seg_loss import (seg_cross_entropy, seg_cross_entropy_reference, MODE_OHEM, MODE_MEAN,
+                       MODE_SUM)
+from .kd import kd_kl_div, kd_kl_div_reference
+from .confmat import confusion_matrix, confusion_matrix_reference
+
+__all__ = [
+    "load", "use_hip", "hip_disabled", "library_path",
+    "interpolate", "final_upsample", "defer_final_upsample", "DeferredLogits", "materialize",
+    "seg_cross_entropy", "seg_cross_entropy_reference", "MODE_OHEM", "MODE_MEAN", "MODE_SUM",
+    "kd_kl_div", "kd_kl_div_reference", "confusion_matrix", "confusion_matrix_reference",
+]

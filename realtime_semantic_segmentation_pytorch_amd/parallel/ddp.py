@@ -1,0 +1,127 @@
+"""Distributed runtime: one process per GPU, RCCL over xGMI (parity: reference
+utils/parallel.py:7-53).
+
+* ``set_device`` -- reads ``RANK / LOCAL_RANK / WORLD_SIZE`` (torchrun env://),
+  pins the HIP device and initialises the process group: backend ``nccl``
+  (= RCCL on ROCm) for GPUs, ``gloo`` for CPU runs/tests.
+* ``parallel_model`` -- SyncBatchNorm conversion (GPU only) and DDP with
+  gradient buckets sized for MI355X: with 288 GB HBM the whole gradient of the
+  largest zoo model (DDRNet-23: 84 MiB fp32) fits in one or two buckets, so the
+  default bucket is 100 MiB -> ~1 large all-reduce per step that RCCL can split
+  across all 7 xGMI links, overlapped with the tail of backward.  Buckets are
+  views of the gradients (``gradient_as_bucket_view``), BN buffers are not
+  re-broadcast every forward when SyncBN already makes them identical.
+* single-process multi-GPU ``nn.DataParallel`` is deliberately not recreated:
+  non-DDP runs use one device ("DP" row).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+from torch.nn.parallel import DistributedDataParallel as DDP
+
+
+def is_parallel(model) -> bool:
+    return isinstance(model, (nn.parallel.DataParallel, nn.parallel.DistributedDataParallel))
+
+
+def de_parallel(model):
+    return model.module if is_parallel(model) else model
+
+
+def dist_env():
+    """(rank, local_rank, world_size) from the launcher environment (-1 when absent)."""
+    return (int(os.getenv("RANK", -1)), int(os.getenv("LOCAL_RANK", -1)),
+            int(os.getenv("WORLD_SIZE", 1)))
+
+
+def is_dist() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
+def get_rank() -> int:
+    return dist.get_rank() if is_dist() else 0
+
+
+def get_world_size() -> int:
+    return dist.get_world_size() if is_dist() else 1
+
+
+def barrier():
+    if is_dist():
+        if dist.get_backend() == "nccl" and torch.cuda.is_available():
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
+
+
+def set_device(config, local_rank=None):
+    """Select the device and (under torchrun) join the process group."""
+    rank, lrank, world = dist_env()
+    if local_rank is None:
+        local_rank = lrank
+    want = getattr(config, "device", None)
+    use_cuda = torch.cuda.is_available() and want != "cpu"
+    if config.DDP:
+        if use_cuda:
+            torch.cuda.set_device(local_rank)
+            device = torch.device("cuda", local_rank)
+            backend = "nccl"
+        else:
+            device = torch.device("cpu")
+            backend = "gloo"
+        if not is_dist():
+            kw = dict(backend=backend, init_method="env://",
+                      timeout=datetime.timedelta(minutes=int(os.getenv("RTSEG_PG_TIMEOUT_MIN", 30))))
+            if backend == "nccl":
+                kw["device_id"] = device
+            dist.init_process_group(**kw)
+        config.gpu_num = dist.get_world_size()
+        config.global_rank = dist.get_rank()
+    else:
+        device = torch.device("cuda", 0) if use_cuda else torch.device("cpu")
+        if use_cuda:
+            torch.cuda.set_device(0)
+        config.gpu_num = 1  # reference: device_count (0 on CPU -> broken)
+        config.global_rank = 0
+    config.num_workers = int(config.base_workers)  # per rank
+    return device
+
+
+def parallel_model(config, model, rank, device):
+    if not config.DDP:
+        return model.to(device)
+    sync = bool(config.synBN) and device.type == "cuda"
+    if sync:
+        model = nn.SyncBatchNorm.convert_sync_batchnorm(model)
+    model = model.to(device)
+    kw = dict(bucket_cap_mb=int(getattr(config, "ddp_bucket_mb", 100)),
+              gradient_as_bucket_view=True,
+              broadcast_buffers=not sync,
+              static_graph=bool(getattr(config, "ddp_static_graph", False)))
+    if device.type == "cuda":
+        kw.update(device_ids=[device.index], output_device=device.index)
+    return DDP(model, **kw)
+
+
+def destroy_ddp_process(config):
+    if config.DDP and is_dist():
+        dist.destroy_process_group()
+
+
+def sampler_set_epoch(config, loader, cur_epochs):
+    sampler = getattr(loader, "sampler", None)
+    if config.DDP and hasattr(sampler, "set_epoch"):
+        sampler.set_epoch(cur_epochs)
+
+
+def all_reduce_mean(t: torch.Tensor) -> torch.Tensor:
+    if get_world_size() > 1:
+        t = t.clone()
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        t /= get_world_size()
+    return t

@@ -1,0 +1,138 @@
+"""Numerics of the HIP kernels vs plain-PyTorch fp32 references (run on MI355X)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from realtime_semantic_segmentation_pytorch_amd import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _lib_loaded():
+    assert ops.load(), "HIP extension must load on the GPU box"
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cl", [False, True])
+@pytest.mark.parametrize("align", [True, False])
+@pytest.mark.parametrize("shape,size", [((2, 16, 7, 9), (28, 36)), ((1, 24, 16, 32), (128, 256)),
+                                        ((2, 8, 32, 64), (16, 32)), ((1, 16, 1, 1), (16, 32))])
+def test_interp_fwd_bwd(dtype, cl, align, shape, size):
+    _lib_loaded()
+    torch.manual_seed(0)
+    x = torch.randn(shape, device=DEV, dtype=dtype)
+    if cl:
+        x = x.contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    y = ops.interpolate(x, size, align)
+    xr = x.detach().float().requires_grad_(True)
+    yr = F.interpolate(xr, size, mode="bilinear", align_corners=align)
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+    g = torch.randn_like(yr)
+    y.backward(g.to(dtype))
+    yr.backward(g)
+    gtol = 1e-4 if dtype == torch.float32 else 5e-2
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=gtol * max(1.0, xr.grad.abs().max().item()), rtol=gtol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("act", [None, "relu"])
+def test_interp_skip_act(dtype, act):
+    _lib_loaded()
+    torch.manual_seed(1)
+    x = torch.randn(2, 32, 16, 32, device=DEV, dtype=dtype).contiguous(memory_format=torch.channels_last)
+    s = torch.randn(2, 32, 64, 128, device=DEV, dtype=dtype).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    s.requires_grad_(True)
+    y = ops.interpolate(x, (64, 128), True, skip=s, act=act)
+    xr = x.detach().float().requires_grad_(True)
+    sr = s.detach().float().requires_grad_(True)
+    yr = F.interpolate(xr, (64, 128), mode="bilinear", align_corners=True) + sr
+    if act == "relu":
+        yr = F.relu(yr)
+    tol = 1e-5 if dtype == torch.float32 else 3e-2
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+    g = torch.randn_like(yr)
+    y.backward(g.to(dtype))
+    yr.backward(g)
+    gtol = 1e-4 if dtype == torch.float32 else 6e-2
+    torch.testing.assert_close(s.grad.float(), sr.grad, atol=gtol, rtol=gtol)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=gtol * xr.grad.abs().max().item(), rtol=gtol)
+
+
+def _labels(n, h, w, c, ignore_frac=0.1, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    lab = torch.randint(0, c, (n, h, w), generator=g)
+    lab[torch.rand((n, h, w), generator=g) < ignore_frac] = 255
+    return lab.to(DEV)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("scale_logits", [0.1, 3.0])  # small logits -> top-k branch; large -> threshold
+@pytest.mark.parametrize("hw,lhw", [((16, 32), (128, 256)), ((32, 64), (32, 64)), ((9, 13), (70, 100))])
+def test_ohem_loss_fused(dtype, scale_logits, hw, lhw):
+    _lib_loaded()
+    torch.manual_seed(2)
+    n, c = 2, 19
+    logits = (torch.randn(n, c, *hw, device=DEV) * scale_logits).to(dtype)
+    logits = logits.contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    labels = _labels(n, *lhw, c)
+    loss = ops.seg_cross_entropy(logits, labels, mode=ops.MODE_OHEM, ohem_thrs=0.7)
+    lr_ = logits.detach().float().requires_grad_(True)
+    ref = ops.seg_cross_entropy_reference(lr_, labels.cpu().to(DEV), mode=ops.MODE_OHEM, ohem_thrs=0.7)
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    torch.testing.assert_close(loss, ref, atol=tol, rtol=tol)
+    loss.backward()
+    ref.backward()
+    gmax = lr_.grad.abs().max().item()
+    torch.testing.assert_close(logits.grad.float(), lr_.grad, atol=max(1e-7, 2e-2 * gmax), rtol=5e-2)
+
+
+@pytest.mark.parametrize("weighted", [False, True])
+@pytest.mark.parametrize("mode", [1, 2])
+def test_ce_loss_modes(weighted, mode):
+    _lib_loaded()
+    torch.manual_seed(3)
+    n, c = 2, 19
+    logits = torch.randn(n, c, 16, 32, device=DEV, requires_grad=True)
+    labels = _labels(n, 128, 256, c, seed=4)
+    w = torch.rand(c, device=DEV) + 0.5 if weighted else None
+    loss = ops.seg_cross_entropy(logits, labels, mode=mode, class_weight=w)
+    lr_ = logits.detach().clone().requires_grad_(True)
+    ref = ops.seg_cross_entropy_reference(lr_, labels, mode=mode, class_weight=w)
+    torch.testing.assert_close(loss, ref, atol=1e-4, rtol=1e-4)
+    loss.backward()
+    ref.backward()
+    torch.testing.assert_close(logits.grad, lr_.grad, atol=1e-6 + 1e-3 * lr_.grad.abs().max().item(), rtol=1e-3)
+
+
+def test_aux_loss_nearest_labels():
+    _lib_loaded()
+    torch.manual_seed(5)
+    logits = torch.randn(2, 19, 16, 32, device=DEV, requires_grad=True)
+    labels = _labels(2, 128, 256, 19, seed=6)
+    loss = ops.seg_cross_entropy(logits, labels, resize_logits=False)
+    lr_ = logits.detach().clone().requires_grad_(True)
+    ref = ops.seg_cross_entropy_reference(lr_, labels, resize_logits=False)
+    torch.testing.assert_close(loss, ref, atol=1e-4, rtol=1e-4)
+    loss.backward()
+    ref.backward()
+    torch.testing.assert_close(logits.grad, lr_.grad, atol=1e-6 + 1e-3 * lr_.grad.abs().max().item(), rtol=1e-3)
+
+
+def test_loss_no_host_sync():
+    """The fused loss must not synchronise with the host (graph-capturable)."""
+    _lib_loaded()
+    logits = torch.randn(2, 19, 16, 32, device=DEV, requires_grad=True)
+    labels = _labels(2, 128, 256, 19)
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        loss = ops.seg_cross_entropy(logits, labels)
+        loss.backward()
+    finally:
+        torch.cuda.set_sync_debug_mode("default")
+    assert math.isfinite(float(loss))
