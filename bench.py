@@ -24,6 +24,13 @@ import os
 import sys
 import time
 
+# MIOpen's exhaustive find (cudnn.benchmark) also times the reference "naive"
+# convolution solvers, which take tens of seconds per shape at 1024x2048; they
+# are never the winner, so keep them out of the search.
+for _k in ("MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_FWD", "MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_BWD",
+           "MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_WRW"):
+    os.environ.setdefault(_k, "0")
+
 import torch
 import torch.distributed as dist
 
@@ -46,6 +53,8 @@ def parse():
     p.add_argument("--no-fused-loss", action="store_true")
     p.add_argument("--nchw", action="store_true")
     p.add_argument("--profile-steps", type=int, default=0)
+    p.add_argument("--no-cudnn-benchmark", action="store_true",
+                   help="use MIOpen immediate-mode heuristics instead of find")
     return p.parse_args()
 
 
@@ -112,7 +121,7 @@ def main():
     from realtime_semantic_segmentation_pytorch_amd.datasets import DeviceBatches
     from realtime_semantic_segmentation_pytorch_amd.parallel import de_parallel
 
-    torch.backends.cudnn.benchmark = True
+    torch.backends.cudnn.benchmark = not a.no_cudnn_benchmark
     cfg = make_config(a, world)
     ops.load()
     trainer = SegTrainer(cfg)

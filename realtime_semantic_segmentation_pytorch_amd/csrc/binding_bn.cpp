@@ -1,0 +1,168 @@
+// torch.library registration of the fused BatchNorm(+residual)+activation ops.
+#include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <torch/library.h>
+
+#include "rtseg_launch.h"
+#include "rtseg_ops.h"
+
+namespace rtseg {
+namespace {
+
+int64_t rows_of(const at::Tensor& x) { return x.numel() / x.size(1); }
+
+void check_cl(const at::Tensor& x, const char* what) {
+  TORCH_CHECK(x.is_cuda(), "rtseg.bn: ", what, " must be on the GPU");
+  TORCH_CHECK(x.dim() == 4 || x.dim() == 2, "rtseg.bn: ", what, " must be 4-D (or [M,C])");
+  if (x.dim() == 4) {
+    TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "rtseg.bn: ", what, " must be channels_last contiguous");
+  } else {
+    TORCH_CHECK(x.is_contiguous(), "rtseg.bn: ", what, " must be contiguous");
+  }
+  const int64_t C = x.size(1);
+  const int v = x.scalar_type() == at::kFloat ? 4 : 8;
+  TORCH_CHECK(C % v == 0 && C / v <= 256, "rtseg.bn: channel count ", C, " unsupported");
+}
+
+const float* fptr(const std::optional<at::Tensor>& t) {
+  return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr;
+}
+float* fptr_mut(const std::optional<at::Tensor>& t) {
+  return t.has_value() && t->defined() ? const_cast<float*>(t->data_ptr<float>()) : nullptr;
+}
+
+at::Tensor bn_stats(const at::Tensor& x) {
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  check_cl(x, "x");
+  const int C = static_cast<int>(x.size(1));
+  at::Tensor sums = at::empty({2 * C + 1}, x.options().dtype(at::kDouble));
+  launch_bn_stats(x.data_ptr(), dtype_code(x), rows_of(x), C, sums.data_ptr<double>(), cur_stream());
+  return sums;
+}
+
+std::tuple<at::Tensor, at::Tensor> bn_finalize(const at::Tensor& sums,
+                                               const std::optional<at::Tensor>& w,
+                                               const std::optional<at::Tensor>& b,
+                                               const std::optional<at::Tensor>& rmean,
+                                               const std::optional<at::Tensor>& rvar,
+                                               const std::optional<at::Tensor>& nbt,
+                                               double momentum, double eps) {
+  c10::hip::HIPGuardMasqueradingAsCUDA g(sums.device());
+  const int C = static_cast<int>((sums.numel() - 1) / 2);
+  auto f32 = sums.options().dtype(at::kFloat);
+  at::Tensor mi = at::empty({2 * C}, f32), ss = at::empty({2 * C}, f32);
+  int64_t* nb = nbt.has_value() && nbt->defined() ? nbt->data_ptr<int64_t>() : nullptr;
+  launch_bn_finalize(sums.data_ptr<double>(), C, fptr(w), fptr(b), fptr_mut(rmean), fptr_mut(rvar),
+                     nb, static_cast<float>(momentum), static_cast<float>(eps),
+                     mi.data_ptr<float>(), ss.data_ptr<float>(), cur_stream());
+  return {mi, ss};
+}
+
+std::tuple<at::Tensor, at::Tensor> bn_eval_coeffs(const std::optional<at::Tensor>& w,
+                                                  const std::optional<at::Tensor>& b,
+                                                  const at::Tensor& rmean, const at::Tensor& rvar,
+                                                  double eps) {
+  c10::hip::HIPGuardMasqueradingAsCUDA g(rmean.device());
+  const int C = static_cast<int>(rmean.numel());
+  auto f32 = rmean.options().dtype(at::kFloat);
+  at::Tensor mi = at::empty({2 * C}, f32), ss = at::empty({2 * C}, f32);
+  launch_bn_eval_coeffs(C, fptr(w), fptr(b), rmean.data_ptr<float>(), rvar.data_ptr<float>(),
+                        static_cast<float>(eps), mi.data_ptr<float>(), ss.data_ptr<float>(),
+                        cur_stream());
+  return {mi, ss};
+}
+
+at::Tensor bn_apply(const at::Tensor& x, const at::Tensor& scale_shift,
+                    const std::optional<at::Tensor>& res, int64_t act) {
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  check_cl(x, "x");
+  const void* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    check_cl(*res, "residual");
+    TORCH_CHECK(res->sizes() == x.sizes() && res->scalar_type() == x.scalar_type(),
+                "rtseg.bn_apply: residual mismatch");
+    rp = res->data_ptr();
+  }
+  at::Tensor y = at::empty_like(x);
+  launch_bn_apply(x.data_ptr(), rp, scale_shift.data_ptr<float>(), y.data_ptr(), dtype_code(x),
+                  rows_of(x), static_cast<int>(x.size(1)), static_cast<int>(act), cur_stream());
+  return y;
+}
+
+at::Tensor bn_bwd_reduce(const at::Tensor& dy, const at::Tensor& x, const std::optional<at::Tensor>& y,
+                         const at::Tensor& mean_invstd, const at::Tensor& scale_shift, int64_t act,
+                         int64_t mask) {
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  check_cl(x, "x");
+  check_cl(dy, "grad");
+  const void* yp = nullptr;
+  if (y.has_value() && y->defined()) { check_cl(*y, "y"); yp = y->data_ptr(); }
+  TORCH_CHECK(mask != 1 || yp, "rtseg.bn_bwd: mask-from-y needs y");
+  const int C = static_cast<int>(x.size(1));
+  at::Tensor sums = at::empty({2 * C}, x.options().dtype(at::kDouble));
+  launch_bn_bwd_reduce(dy.data_ptr(), x.data_ptr(), yp, mean_invstd.data_ptr<float>(),
+                       scale_shift.data_ptr<float>(), dtype_code(x), rows_of(x), C,
+                       static_cast<int>(act), static_cast<int>(mask), sums.data_ptr<double>(),
+                       cur_stream());
+  return sums;
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_bwd_apply(
+    const at::Tensor& dy, const at::Tensor& x, const std::optional<at::Tensor>& y,
+    const at::Tensor& bsums, const std::optional<at::Tensor>& fwd_sums,
+    const at::Tensor& mean_invstd, const at::Tensor& scale_shift,
+    const std::optional<at::Tensor>& w, int64_t act, int64_t mask, bool want_dres,
+    bool batch_stats, bool want_dw) {
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  check_cl(x, "x");
+  check_cl(dy, "grad");
+  const void* yp = nullptr;
+  if (y.has_value() && y->defined()) yp = y->data_ptr();
+  const int C = static_cast<int>(x.size(1));
+  auto f32 = x.options().dtype(at::kFloat);
+  at::Tensor k = at::empty({3 * C}, f32);
+  at::Tensor dw, db;
+  if (want_dw) { dw = at::empty({C}, f32); db = at::empty({C}, f32); }
+  const double* cnt = nullptr;
+  if (fwd_sums.has_value() && fwd_sums->defined()) cnt = fwd_sums->data_ptr<double>() + 2 * C;
+  TORCH_CHECK(!batch_stats || cnt, "rtseg.bn_bwd: batch statistics need the forward count");
+  launch_bn_bwd_finalize(bsums.data_ptr<double>(), cnt, C, fptr(w), mean_invstd.data_ptr<float>(),
+                         batch_stats ? 1 : 0, k.data_ptr<float>(),
+                         want_dw ? dw.data_ptr<float>() : nullptr,
+                         want_dw ? db.data_ptr<float>() : nullptr, cur_stream());
+  at::Tensor dx = at::empty_like(x);
+  at::Tensor dres;
+  if (want_dres) dres = at::empty_like(x);
+  launch_bn_bwd_apply(dy.data_ptr(), x.data_ptr(), yp, mean_invstd.data_ptr<float>(),
+                      scale_shift.data_ptr<float>(), k.data_ptr<float>(), dx.data_ptr(),
+                      want_dres ? dres.data_ptr() : nullptr, dtype_code(x), rows_of(x), C,
+                      static_cast<int>(act), static_cast<int>(mask), cur_stream());
+  return {dx, dres, dw, db};
+}
+
+}  // namespace
+}  // namespace rtseg
+
+TORCH_LIBRARY_FRAGMENT(rtseg, m) {
+  m.def("bn_stats(Tensor x) -> Tensor");
+  m.def("bn_finalize(Tensor sums, Tensor? weight, Tensor? bias, Tensor(a!)? running_mean, "
+        "Tensor(b!)? running_var, Tensor(c!)? num_batches_tracked, float momentum, float eps) -> (Tensor, Tensor)");
+  m.def("bn_eval_coeffs(Tensor? weight, Tensor? bias, Tensor running_mean, Tensor running_var, "
+        "float eps) -> (Tensor, Tensor)");
+  m.def("bn_apply(Tensor x, Tensor scale_shift, Tensor? residual, int act) -> Tensor");
+  m.def("bn_bwd_reduce(Tensor grad, Tensor x, Tensor? y, Tensor mean_invstd, Tensor scale_shift, "
+        "int act, int mask) -> Tensor");
+  m.def("bn_bwd_apply(Tensor grad, Tensor x, Tensor? y, Tensor bsums, Tensor? fwd_sums, "
+        "Tensor mean_invstd, Tensor scale_shift, Tensor? weight, int act, int mask, bool want_dres, "
+        "bool batch_stats, bool want_dw) -> (Tensor, Tensor, Tensor, Tensor)");
+}
+
+TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
+  m.impl("bn_stats", &rtseg::bn_stats);
+  m.impl("bn_finalize", &rtseg::bn_finalize);
+  m.impl("bn_eval_coeffs", &rtseg::bn_eval_coeffs);
+  m.impl("bn_apply", &rtseg::bn_apply);
+  m.impl("bn_bwd_reduce", &rtseg::bn_bwd_reduce);
+  m.impl("bn_bwd_apply", &rtseg::bn_bwd_apply);
+}

@@ -48,4 +48,25 @@ void launch_seg_loss_fwd(const SegLossArgs& a, hipStream_t st);
 void launch_seg_loss_bwd(const SegLossArgs& a, const float* grad_out, const Tensor4& grad_logits,
                          hipStream_t st);
 
+// ---- bn_act.hip --------------------------------------------------------------
+// x is [M, C] row-major (channels-last). sums: [2C+1] fp64 (sum, sumsq, count).
+void launch_bn_stats(const void* x, int dtype, int64_t M, int C, double* sums, hipStream_t st);
+void launch_bn_finalize(const double* sums, int C, const float* w, const float* b, float* rmean,
+                        float* rvar, int64_t* nbt, float momentum, float eps, float* mean_invstd,
+                        float* scale_shift, hipStream_t st);
+void launch_bn_eval_coeffs(int C, const float* w, const float* b, const float* rmean,
+                           const float* rvar, float eps, float* mean_invstd, float* scale_shift,
+                           hipStream_t st);
+void launch_bn_apply(const void* x, const void* res, const float* scale_shift, void* y, int dtype,
+                     int64_t M, int C, int act, hipStream_t st);
+void launch_bn_bwd_reduce(const void* dy, const void* x, const void* y, const float* mean_invstd,
+                          const float* scale_shift, int dtype, int64_t M, int C, int act, int mask,
+                          double* sums, hipStream_t st);
+void launch_bn_bwd_finalize(const double* sums, const double* count_ptr, int C, const float* w,
+                            const float* mean_invstd, int batch_stats, float* kcoef, float* dw,
+                            float* db, hipStream_t st);
+void launch_bn_bwd_apply(const void* dy, const void* x, const void* y, const float* mean_invstd,
+                         const float* scale_shift, const float* kcoef, void* dx, void* dres,
+                         int dtype, int64_t M, int C, int act, int mask, hipStream_t st);
+
 }  // namespace rtseg

@@ -148,7 +148,8 @@ class RB(nn.Module):
 
     def forward(self, x):
         shortcut = self.conv_down(x) if self.downsample else x
-        return self.act(self.conv2(self.conv1(x)) + shortcut)
+        # relu(BN(conv2(.)) + shortcut) as one fused BN/residual/activation kernel
+        return self.conv2(self.conv1(x), residual=shortcut, act=self.act)
 
 
 class RBB(nn.Module):
@@ -166,7 +167,7 @@ class RBB(nn.Module):
 
     def forward(self, x):
         shortcut = self.conv_down(x) if self.downsample else x
-        return self.act(self.conv3(self.conv2(self.conv1(x))) + shortcut)
+        return self.conv3(self.conv2(self.conv1(x)), residual=shortcut, act=self.act)
 
 
 class BilateralFusion(nn.Module):
@@ -179,7 +180,7 @@ class BilateralFusion(nn.Module):
         self.act = Activation(act_type)
 
     def forward(self, x_low, x_high):
-        new_low = self.act(x_low + self.conv_high(x_high))
+        new_low = self.conv_high(x_high, residual=x_low, act=self.act)
         new_high = _resize_add_act(self.conv_low(x_low), x_high.shape[2:], x_high, self.act)
         return new_low, new_high
 

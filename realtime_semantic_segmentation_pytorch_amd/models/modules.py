@@ -68,7 +68,32 @@ class Activation(nn.Module):
         return self.activation(x)
 
 
-class ConvBNAct(nn.Sequential):
+class _FusedTail:
+    """Mixin for ``Sequential(conv, bn, act)`` blocks: BN + (residual) + activation
+    run as one fused HIP op (``ops.bn_act``) on channels-last GPU activations.
+
+    ``forward(x, residual=None, act=None)`` computes
+    ``act(own_act(bn(conv(x))) + residual)``; with a residual the block's own
+    activation must be the identity (the reference's residual blocks are built
+    that way: ``conv2`` of ``RB`` uses ``act_type='none'``).
+    """
+
+    def forward(self, x, residual=None, act=None):
+        conv, bn, own = self[0], self[1], self[2]
+        y = conv(x)
+        if residual is None:
+            return ops.bn_act(y, bn, own, act_module=own)
+        own_code = ops.bn_act_code(own)
+        if own_code != 0:  # own activation is not identity: apply it before the add
+            y = ops.bn_act(y, bn, own, act_module=own)
+            y = y + residual
+            return act(y) if act is not None else y
+        post = act if act is not None else "none"
+        return ops.bn_act(y, bn, post, residual=residual,
+                          act_module=act if isinstance(act, nn.Module) else None)
+
+
+class ConvBNAct(_FusedTail, nn.Sequential):
     """Conv2d -> BatchNorm2d -> Activation, children ``0 / 1 / 2``."""
 
     def __init__(self, in_channels, out_channels, kernel_size: IntOrPair = 3, stride=1,
@@ -78,7 +103,7 @@ class ConvBNAct(nn.Sequential):
         super().__init__(conv, nn.BatchNorm2d(out_channels), Activation(act_type, **kwargs))
 
 
-class DWConvBNAct(nn.Sequential):
+class DWConvBNAct(_FusedTail, nn.Sequential):
     """Depth-wise conv (channel multiplier = out/in allowed) -> BN -> act."""
 
     def __init__(self, in_channels, out_channels, kernel_size: IntOrPair, stride=1, dilation=1,
@@ -89,7 +114,7 @@ class DWConvBNAct(nn.Sequential):
         super().__init__(conv, nn.BatchNorm2d(out_channels), Activation(act_type, **kwargs))
 
 
-class PWConvBNAct(nn.Sequential):
+class PWConvBNAct(_FusedTail, nn.Sequential):
     """1x1 conv (bias by default) -> BN -> act."""
 
     def __init__(self, in_channels, out_channels, act_type="relu", bias=True, **kwargs):
@@ -115,7 +140,7 @@ class DeConvBNAct(nn.Module):
         super().__init__()
         k = 2 * scale_factor - 1 if kernel_size is None else kernel_size
         p = (k - 1) // 2 if padding is None else padding
-        self.up_conv = nn.Sequential(
+        self.up_conv = _FusedSequential(
             nn.ConvTranspose2d(in_channels, out_channels, kernel_size=k, stride=scale_factor,
                                padding=p, output_padding=scale_factor - 1),
             nn.BatchNorm2d(out_channels),
@@ -123,6 +148,10 @@ class DeConvBNAct(nn.Module):
 
     def forward(self, x):
         return self.up_conv(x)
+
+
+class _FusedSequential(_FusedTail, nn.Sequential):
+    pass
 
 
 class PyramidPoolingModule(nn.Module):

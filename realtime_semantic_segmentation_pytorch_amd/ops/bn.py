@@ -1,0 +1,144 @@
+"""Fused BatchNorm (+ residual) + activation, with SyncBN over RCCL (HIP ``bn_act.hip``).
+
+``bn_act(x, bn, act, residual)`` computes ``act(BN(x) + residual)`` for a
+``nn.BatchNorm2d`` / ``nn.SyncBatchNorm`` module ``bn`` (its running stats and
+``num_batches_tracked`` are updated exactly like PyTorch's).  GPU fast path
+conditions: channels-last activations, C a multiple of 8 (4 for fp32) and
+<= 2048, activation in {none, relu, relu6}, ``momentum`` not None; anything
+else runs the stock PyTorch modules.
+
+SyncBN: per-channel (sum, sum of squares, count) are produced in fp64 by one
+reduction kernel and summed across ranks with ONE ``all_reduce`` of 2C+1
+doubles (backward: one all-reduce of 2C doubles) on the current stream -- the
+reference's SyncBatchNorm all-gathers mean/invstd/count instead.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from ._ext import use_hip, ops
+
+ACT_NONE, ACT_RELU, ACT_RELU6 = 0, 1, 2
+MASK_NONE, MASK_FROM_Y, MASK_FROM_X = 0, 1, 2
+
+
+def act_code(act) -> Optional[int]:
+    """Activation module/str -> fused code, or None when it cannot be fused."""
+    if act is None:
+        return ACT_NONE
+    if isinstance(act, str):
+        return {"none": ACT_NONE, "relu": ACT_RELU, "relu6": ACT_RELU6}.get(act.lower())
+    inner = getattr(act, "activation", act)  # models.modules.Activation wrapper
+    if isinstance(inner, nn.Identity):
+        return ACT_NONE
+    if isinstance(inner, nn.ReLU6):
+        return ACT_RELU6
+    if isinstance(inner, nn.ReLU):
+        return ACT_RELU
+    if isinstance(inner, nn.Hardtanh) and inner.min_val == 0.0 and inner.max_val == 6.0:
+        return ACT_RELU6
+    return None
+
+
+def _sync_group(bn):
+    if not isinstance(bn, nn.SyncBatchNorm):
+        return None
+    if not (dist.is_available() and dist.is_initialized()):
+        return None
+    pg = bn.process_group or dist.group.WORLD
+    return pg if dist.get_world_size(pg) > 1 else None
+
+
+class _BNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, bn, act, use_batch_stats, pg):
+        if use_batch_stats:
+            sums = ops().bn_stats(x)
+            if pg is not None:
+                dist.all_reduce(sums, group=pg)
+            track = bn.track_running_stats and bn.training and bn.running_mean is not None
+            mi, ss = ops().bn_finalize(
+                sums, weight, bias, bn.running_mean if track else None,
+                bn.running_var if track else None, bn.num_batches_tracked if track else None,
+                float(bn.momentum), float(bn.eps))
+        else:
+            sums = None
+            mi, ss = ops().bn_eval_coeffs(weight, bias, bn.running_mean, bn.running_var, float(bn.eps))
+        y = ops().bn_apply(x, ss, residual, act)
+        if act == ACT_NONE:
+            mask = MASK_NONE
+        elif residual is None:
+            mask = MASK_FROM_X
+        else:
+            mask = MASK_FROM_Y
+        ctx.act, ctx.mask, ctx.pg = act, mask, pg
+        ctx.batch_stats = use_batch_stats
+        ctx.has_res = residual is not None
+        ctx.has_w = weight is not None
+        ctx.save_for_backward(x, y if mask == MASK_FROM_Y else None, mi, ss, sums, weight)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, mi, ss, sums, weight = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last) if dy.dim() == 4 else dy.contiguous()
+        bsums = ops().bn_bwd_reduce(dy, x, y, mi, ss, ctx.act, ctx.mask)
+        if ctx.pg is not None:
+            dist.all_reduce(bsums, group=ctx.pg)
+        want_dres = ctx.has_res and ctx.needs_input_grad[3]
+        want_dw = ctx.has_w and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
+        dx, dres, dw, db = ops().bn_bwd_apply(dy, x, y, bsums, sums, mi, ss, weight, ctx.act,
+                                              ctx.mask, want_dres, ctx.batch_stats, want_dw)
+        return (dx, dw if want_dw else None, db if want_dw else None,
+                dres if want_dres else None, None, None, None, None)
+
+
+def fused_ok(x: torch.Tensor, bn, act) -> bool:
+    if not isinstance(bn, (nn.BatchNorm2d, nn.SyncBatchNorm)) or x.dim() != 4:
+        return False
+    if act is None or bn.momentum is None:
+        return False
+    if x.dtype not in (torch.float32, torch.bfloat16, torch.float16):
+        return False
+    c = x.shape[1]
+    v = 4 if x.dtype == torch.float32 else 8
+    if c % v or c // v > 256 or x.numel() == 0:
+        return False
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        return False
+    use_batch = bn.training or not bn.track_running_stats or bn.running_mean is None
+    if not use_batch and bn.running_var is None:
+        return False
+    return bn.affine or bn.weight is None
+
+
+def bn_act(x: torch.Tensor, bn, act=None, residual: Optional[torch.Tensor] = None,
+           act_module: Optional[nn.Module] = None) -> torch.Tensor:
+    """``act(bn(x) + residual)``; ``act`` is a fused-activation code or module/str."""
+    code = act if isinstance(act, int) else act_code(act)
+    if use_hip(x) and code is not None and fused_ok(x, bn, code) and (
+            residual is None or (residual.shape == x.shape
+                                 and residual.is_contiguous(memory_format=torch.channels_last))):
+        if residual is not None and residual.dtype != x.dtype:
+            residual = residual.to(x.dtype)
+        use_batch = bn.training or not bn.track_running_stats or bn.running_mean is None
+        pg = _sync_group(bn) if use_batch else None
+        return _BNActFn.apply(x, bn.weight, bn.bias, residual, bn, code, use_batch, pg)
+    y = bn(x)
+    if residual is not None:
+        y = y + residual
+    if act_module is not None:
+        return act_module(y)
+    if code == ACT_RELU:
+        return torch.relu(y)
+    if code == ACT_RELU6:
+        return torch.nn.functional.relu6(y)
+    if code == ACT_NONE:
+        return y
+    if callable(act):
+        return act(y)
+    raise ValueError(f"unsupported activation {act!r}")

@@ -1,0 +1,111 @@
+"""Fused BatchNorm(+residual)+activation HIP kernels vs PyTorch fp32 BatchNorm."""
+import copy
+
+import pytest
+import torch
+import torch.nn as nn
+
+from realtime_semantic_segmentation_pytorch_amd import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _ref(x, bn, act, res):
+    y = bn(x)
+    if res is not None:
+        y = y + res
+    if act == "relu":
+        y = torch.relu(y)
+    elif act == "relu6":
+        y = torch.nn.functional.relu6(y)
+    return y
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("act", ["none", "relu", "relu6"])
+@pytest.mark.parametrize("with_res", [False, True])
+@pytest.mark.parametrize("shape", [(2, 64, 17, 33), (3, 256, 8, 8), (1, 1024, 4, 6), (4, 16, 32, 32)])
+def test_bn_act_train(dtype, act, with_res, shape):
+    assert ops.load()
+    torch.manual_seed(0)
+    c = shape[1]
+    bn = nn.BatchNorm2d(c).to(DEV)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    bn_ref = copy.deepcopy(bn)
+    x = (torch.randn(shape, device=DEV) * 2 + 0.5).to(dtype).contiguous(memory_format=torch.channels_last)
+    res = (torch.randn(shape, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+           if with_res else None)
+    x.requires_grad_(True)
+    if res is not None:
+        res.requires_grad_(True)
+    y = ops.bn_act(x, bn, act, residual=res)
+    xr = x.detach().float().requires_grad_(True)
+    rr = res.detach().float().requires_grad_(True) if res is not None else None
+    yr = _ref(xr, bn_ref, act, rr)
+    if act != "none":  # compare with the kernel's own activation mask (bf16 rounding at 0 / 6)
+        lo = y.detach().float() > 0
+        yr = torch.where(lo | (yr <= 0), yr, torch.zeros_like(yr)) if act == "relu" else yr
+    tol = 1e-4 if dtype == torch.float32 else 3e-2
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+    torch.testing.assert_close(bn.running_mean, bn_ref.running_mean, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(bn.running_var, bn_ref.running_var, atol=1e-3, rtol=1e-3)
+    assert int(bn.num_batches_tracked) == int(bn_ref.num_batches_tracked) == 1
+    g = torch.randn(shape, device=DEV)
+    y.backward(g.to(dtype).contiguous(memory_format=torch.channels_last))
+    yr.backward(g)
+    gt = 2e-3 if dtype == torch.float32 else 6e-2
+    scale = xr.grad.abs().max().item()
+    if dtype == torch.float32 or act == "none":
+        torch.testing.assert_close(x.grad.float(), xr.grad, atol=gt * scale, rtol=gt)
+    else:  # bf16 mask flips near the kinks: compare the bulk
+        bad = ((x.grad.float() - xr.grad).abs() > gt * scale + gt * xr.grad.abs()).float().mean()
+        assert bad < 2e-3
+    torch.testing.assert_close(bn.weight.grad, bn_ref.weight.grad,
+                               atol=gt * bn_ref.weight.grad.abs().max().item(), rtol=gt)
+    torch.testing.assert_close(bn.bias.grad, bn_ref.bias.grad,
+                               atol=gt * bn_ref.bias.grad.abs().max().item(), rtol=gt)
+    if res is not None:
+        torch.testing.assert_close(res.grad.float(), rr.grad, atol=gt, rtol=gt)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_bn_act_eval(dtype):
+    assert ops.load()
+    torch.manual_seed(1)
+    bn = nn.BatchNorm2d(32).to(DEV)
+    with torch.no_grad():
+        bn.running_mean.uniform_(-1, 1)
+        bn.running_var.uniform_(0.5, 2)
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    bn.eval()
+    x = torch.randn(2, 32, 9, 11, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    y = ops.bn_act(x, bn, "relu")
+    yr = torch.relu(bn(x.float()))
+    tol = 1e-5 if dtype == torch.float32 else 3e-2
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+
+
+def test_convbnact_module_fused_matches_unfused():
+    """ConvBNAct / RB forward+backward: fused GPU path == stock modules (fp32)."""
+    from realtime_semantic_segmentation_pytorch_amd.models.ddrnet import RB
+
+    assert ops.load()
+    torch.manual_seed(2)
+    blk = RB(32, 64, 2).to(DEV).to(memory_format=torch.channels_last)
+    ref = copy.deepcopy(blk)
+    x = torch.randn(2, 32, 24, 40, device=DEV).contiguous(memory_format=torch.channels_last)
+    y = blk(x)
+    # reference: plain module math
+    s = ref.conv_down[1](ref.conv_down[0](x))
+    h = ref.conv1[2](ref.conv1[1](ref.conv1[0](x)))
+    yr = torch.relu(ref.conv2[1](ref.conv2[0](h)) + s)
+    torch.testing.assert_close(y, yr, atol=1e-4, rtol=1e-4)
+    y.sum().backward()
+    yr.sum().backward()
+    for (n, p), (_, q) in zip(blk.named_parameters(), ref.named_parameters()):
+        torch.testing.assert_close(p.grad, q.grad, atol=2e-3 * q.grad.abs().max().item() + 1e-6,
+                                   rtol=2e-3, msg=n)
