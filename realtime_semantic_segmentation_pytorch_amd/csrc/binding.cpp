@@ -125,6 +125,9 @@ static std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> seg_loss_fwd(
   at::Tensor pix_lse = at::empty({logits.size(0), out_h, out_w}, f32);
   at::Tensor stats = at::empty({32}, logits.options().dtype(at::kDouble));
   at::Tensor hist = at::empty({3 * 2048}, logits.options().dtype(at::kInt));
+  at::Tensor slab = at::empty({static_cast<int64_t>(seg_loss_fwd_blocks(a)) * 5},
+                              logits.options().dtype(at::kDouble));
+  a.slab = slab.data_ptr<double>();
   a.pix_loss = pix_loss.data_ptr<float>();
   a.pix_lse = pix_lse.data_ptr<float>();
   a.stats = stats.data_ptr<double>();

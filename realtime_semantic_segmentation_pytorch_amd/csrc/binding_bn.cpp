@@ -1,4 +1,9 @@
 // torch.library registration of the fused BatchNorm(+residual)+activation ops.
+//
+// Non-synchronised BN runs as three launches forward (stats slab, fused
+// finalize, apply) and three backward (reduce slab, finalize, apply), each op
+// below issuing its kernels back to back on the current stream.  The SyncBN
+// variants stop after producing fp64 sums so the caller can all-reduce them.
 #include <ATen/ATen.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <torch/library.h>
@@ -31,16 +36,54 @@ const float* fptr(const std::optional<at::Tensor>& t) {
 float* fptr_mut(const std::optional<at::Tensor>& t) {
   return t.has_value() && t->defined() ? const_cast<float*>(t->data_ptr<float>()) : nullptr;
 }
+int64_t* nbt_ptr(const std::optional<at::Tensor>& t) {
+  return t.has_value() && t->defined() ? t->data_ptr<int64_t>() : nullptr;
+}
 
-at::Tensor bn_stats(const at::Tensor& x) {
+at::Tensor stats_slab(const at::Tensor& x, int& G) {
+  const int C = static_cast<int>(x.size(1));
+  const int64_t M = rows_of(x);
+  G = bn_partial_grid(M, C, dtype_code(x));
+  at::Tensor part = at::empty({G, 2 * C}, x.options().dtype(at::kFloat));
+  launch_bn_stats(x.data_ptr(), dtype_code(x), M, C, part.data_ptr<float>(), G, cur_stream());
+  return part;
+}
+
+// forward, single device: -> (mean_invstd[2C], scale_shift[2C], sums[2C+1])
+std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_stats_finalize(
+    const at::Tensor& x, const std::optional<at::Tensor>& w, const std::optional<at::Tensor>& b,
+    const std::optional<at::Tensor>& rmean, const std::optional<at::Tensor>& rvar,
+    const std::optional<at::Tensor>& nbt, double momentum, double eps) {
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   check_cl(x, "x");
   const int C = static_cast<int>(x.size(1));
+  int G = 0;
+  at::Tensor part = stats_slab(x, G);
+  auto f32 = x.options().dtype(at::kFloat);
+  at::Tensor mi = at::empty({2 * C}, f32), ss = at::empty({2 * C}, f32);
   at::Tensor sums = at::empty({2 * C + 1}, x.options().dtype(at::kDouble));
-  launch_bn_stats(x.data_ptr(), dtype_code(x), rows_of(x), C, sums.data_ptr<double>(), cur_stream());
+  launch_bn_finalize_partials(part.data_ptr<float>(), G, C, static_cast<double>(rows_of(x)),
+                              fptr(w), fptr(b), fptr_mut(rmean), fptr_mut(rvar), nbt_ptr(nbt),
+                              static_cast<float>(momentum), static_cast<float>(eps),
+                              mi.data_ptr<float>(), ss.data_ptr<float>(), sums.data_ptr<double>(),
+                              cur_stream());
+  return {mi, ss, sums};
+}
+
+// forward, SyncBN step 1: -> sums[2C+1] (to be all-reduced)
+at::Tensor bn_stats_sums(const at::Tensor& x) {
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  check_cl(x, "x");
+  const int C = static_cast<int>(x.size(1));
+  int G = 0;
+  at::Tensor part = stats_slab(x, G);
+  at::Tensor sums = at::empty({2 * C + 1}, x.options().dtype(at::kDouble));
+  launch_bn_slab_to_sums(part.data_ptr<float>(), G, C, static_cast<double>(rows_of(x)),
+                         sums.data_ptr<double>(), cur_stream());
   return sums;
 }
 
+// forward, SyncBN step 2
 std::tuple<at::Tensor, at::Tensor> bn_finalize(const at::Tensor& sums,
                                                const std::optional<at::Tensor>& w,
                                                const std::optional<at::Tensor>& b,
@@ -52,9 +95,8 @@ std::tuple<at::Tensor, at::Tensor> bn_finalize(const at::Tensor& sums,
   const int C = static_cast<int>((sums.numel() - 1) / 2);
   auto f32 = sums.options().dtype(at::kFloat);
   at::Tensor mi = at::empty({2 * C}, f32), ss = at::empty({2 * C}, f32);
-  int64_t* nb = nbt.has_value() && nbt->defined() ? nbt->data_ptr<int64_t>() : nullptr;
   launch_bn_finalize(sums.data_ptr<double>(), C, fptr(w), fptr(b), fptr_mut(rmean), fptr_mut(rvar),
-                     nb, static_cast<float>(momentum), static_cast<float>(eps),
+                     nbt_ptr(nbt), static_cast<float>(momentum), static_cast<float>(eps),
                      mi.data_ptr<float>(), ss.data_ptr<float>(), cur_stream());
   return {mi, ss};
 }
@@ -90,54 +132,73 @@ at::Tensor bn_apply(const at::Tensor& x, const at::Tensor& scale_shift,
   return y;
 }
 
-at::Tensor bn_bwd_reduce(const at::Tensor& dy, const at::Tensor& x, const std::optional<at::Tensor>& y,
-                         const at::Tensor& mean_invstd, const at::Tensor& scale_shift, int64_t act,
-                         int64_t mask) {
-  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
-  check_cl(x, "x");
-  check_cl(dy, "grad");
+const void* opt_y(const std::optional<at::Tensor>& y, int64_t mask) {
   const void* yp = nullptr;
   if (y.has_value() && y->defined()) { check_cl(*y, "y"); yp = y->data_ptr(); }
   TORCH_CHECK(mask != 1 || yp, "rtseg.bn_bwd: mask-from-y needs y");
-  const int C = static_cast<int>(x.size(1));
-  at::Tensor sums = at::empty({2 * C}, x.options().dtype(at::kDouble));
-  launch_bn_bwd_reduce(dy.data_ptr(), x.data_ptr(), yp, mean_invstd.data_ptr<float>(),
-                       scale_shift.data_ptr<float>(), dtype_code(x), rows_of(x), C,
-                       static_cast<int>(act), static_cast<int>(mask), sums.data_ptr<double>(),
-                       cur_stream());
-  return sums;
+  return yp;
 }
 
-std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_bwd_apply(
-    const at::Tensor& dy, const at::Tensor& x, const std::optional<at::Tensor>& y,
-    const at::Tensor& bsums, const std::optional<at::Tensor>& fwd_sums,
-    const at::Tensor& mean_invstd, const at::Tensor& scale_shift,
-    const std::optional<at::Tensor>& w, int64_t act, int64_t mask, bool want_dres,
-    bool batch_stats, bool want_dw) {
+at::Tensor bwd_slab(const at::Tensor& dy, const at::Tensor& x, const void* yp, const at::Tensor& mi,
+                    const at::Tensor& ss, int64_t act, int64_t mask, int& G) {
+  const int C = static_cast<int>(x.size(1));
+  const int64_t M = rows_of(x);
+  G = bn_partial_grid(M, C, dtype_code(x));
+  at::Tensor part = at::empty({G, 2 * C}, x.options().dtype(at::kFloat));
+  launch_bn_bwd_reduce(dy.data_ptr(), x.data_ptr(), yp, mi.data_ptr<float>(), ss.data_ptr<float>(),
+                       dtype_code(x), M, C, static_cast<int>(act), static_cast<int>(mask),
+                       part.data_ptr<float>(), G, cur_stream());
+  return part;
+}
+
+// backward, SyncBN step 1: -> bsums[2C] (to be all-reduced)
+at::Tensor bn_bwd_sums(const at::Tensor& dy, const at::Tensor& x, const std::optional<at::Tensor>& y,
+                       const at::Tensor& mi, const at::Tensor& ss, int64_t act, int64_t mask) {
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   check_cl(x, "x");
   check_cl(dy, "grad");
-  const void* yp = nullptr;
-  if (y.has_value() && y->defined()) yp = y->data_ptr();
+  int G = 0;
+  at::Tensor part = bwd_slab(dy, x, opt_y(y, mask), mi, ss, act, mask, G);
+  const int C = static_cast<int>(x.size(1));
+  at::Tensor bsums = at::empty({2 * C}, x.options().dtype(at::kDouble));
+  launch_bn_slab_to_sums(part.data_ptr<float>(), G, C, -1.0, bsums.data_ptr<double>(), cur_stream());
+  return bsums;
+}
+
+// backward: reduce (unless bsums given) + finalize + apply -> (dx, dres, dw, db)
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_backward(
+    const at::Tensor& dy, const at::Tensor& x, const std::optional<at::Tensor>& y,
+    const std::optional<at::Tensor>& bsums, const std::optional<at::Tensor>& fwd_sums,
+    const at::Tensor& mi, const at::Tensor& ss, const std::optional<at::Tensor>& w, int64_t act,
+    int64_t mask, bool want_dres, bool batch_stats, bool want_dw) {
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  check_cl(x, "x");
+  check_cl(dy, "grad");
+  const void* yp = opt_y(y, mask);
   const int C = static_cast<int>(x.size(1));
   auto f32 = x.options().dtype(at::kFloat);
+  at::Tensor part;
+  int G = 0;
+  const double* sums_p = nullptr;
+  if (bsums.has_value() && bsums->defined()) sums_p = bsums->data_ptr<double>();
+  else part = bwd_slab(dy, x, yp, mi, ss, act, mask, G);
   at::Tensor k = at::empty({3 * C}, f32);
   at::Tensor dw, db;
   if (want_dw) { dw = at::empty({C}, f32); db = at::empty({C}, f32); }
   const double* cnt = nullptr;
   if (fwd_sums.has_value() && fwd_sums->defined()) cnt = fwd_sums->data_ptr<double>() + 2 * C;
   TORCH_CHECK(!batch_stats || cnt, "rtseg.bn_bwd: batch statistics need the forward count");
-  launch_bn_bwd_finalize(bsums.data_ptr<double>(), cnt, C, fptr(w), mean_invstd.data_ptr<float>(),
-                         batch_stats ? 1 : 0, k.data_ptr<float>(),
+  launch_bn_bwd_finalize(part.defined() ? part.data_ptr<float>() : nullptr, G, sums_p, cnt, C,
+                         fptr(w), mi.data_ptr<float>(), batch_stats ? 1 : 0, k.data_ptr<float>(),
                          want_dw ? dw.data_ptr<float>() : nullptr,
                          want_dw ? db.data_ptr<float>() : nullptr, cur_stream());
   at::Tensor dx = at::empty_like(x);
   at::Tensor dres;
   if (want_dres) dres = at::empty_like(x);
-  launch_bn_bwd_apply(dy.data_ptr(), x.data_ptr(), yp, mean_invstd.data_ptr<float>(),
-                      scale_shift.data_ptr<float>(), k.data_ptr<float>(), dx.data_ptr(),
-                      want_dres ? dres.data_ptr() : nullptr, dtype_code(x), rows_of(x), C,
-                      static_cast<int>(act), static_cast<int>(mask), cur_stream());
+  launch_bn_bwd_apply(dy.data_ptr(), x.data_ptr(), yp, mi.data_ptr<float>(), ss.data_ptr<float>(),
+                      k.data_ptr<float>(), dx.data_ptr(), want_dres ? dres.data_ptr() : nullptr,
+                      dtype_code(x), rows_of(x), C, static_cast<int>(act), static_cast<int>(mask),
+                      cur_stream());
   return {dx, dres, dw, db};
 }
 
@@ -145,24 +206,28 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_bwd_apply(
 }  // namespace rtseg
 
 TORCH_LIBRARY_FRAGMENT(rtseg, m) {
-  m.def("bn_stats(Tensor x) -> Tensor");
+  m.def("bn_stats_finalize(Tensor x, Tensor? weight, Tensor? bias, Tensor(a!)? running_mean, "
+        "Tensor(b!)? running_var, Tensor(c!)? num_batches_tracked, float momentum, float eps) "
+        "-> (Tensor, Tensor, Tensor)");
+  m.def("bn_stats_sums(Tensor x) -> Tensor");
   m.def("bn_finalize(Tensor sums, Tensor? weight, Tensor? bias, Tensor(a!)? running_mean, "
         "Tensor(b!)? running_var, Tensor(c!)? num_batches_tracked, float momentum, float eps) -> (Tensor, Tensor)");
   m.def("bn_eval_coeffs(Tensor? weight, Tensor? bias, Tensor running_mean, Tensor running_var, "
         "float eps) -> (Tensor, Tensor)");
   m.def("bn_apply(Tensor x, Tensor scale_shift, Tensor? residual, int act) -> Tensor");
-  m.def("bn_bwd_reduce(Tensor grad, Tensor x, Tensor? y, Tensor mean_invstd, Tensor scale_shift, "
+  m.def("bn_bwd_sums(Tensor grad, Tensor x, Tensor? y, Tensor mean_invstd, Tensor scale_shift, "
         "int act, int mask) -> Tensor");
-  m.def("bn_bwd_apply(Tensor grad, Tensor x, Tensor? y, Tensor bsums, Tensor? fwd_sums, "
+  m.def("bn_backward(Tensor grad, Tensor x, Tensor? y, Tensor? bsums, Tensor? fwd_sums, "
         "Tensor mean_invstd, Tensor scale_shift, Tensor? weight, int act, int mask, bool want_dres, "
         "bool batch_stats, bool want_dw) -> (Tensor, Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
-  m.impl("bn_stats", &rtseg::bn_stats);
+  m.impl("bn_stats_finalize", &rtseg::bn_stats_finalize);
+  m.impl("bn_stats_sums", &rtseg::bn_stats_sums);
   m.impl("bn_finalize", &rtseg::bn_finalize);
   m.impl("bn_eval_coeffs", &rtseg::bn_eval_coeffs);
   m.impl("bn_apply", &rtseg::bn_apply);
-  m.impl("bn_bwd_reduce", &rtseg::bn_bwd_reduce);
-  m.impl("bn_bwd_apply", &rtseg::bn_bwd_apply);
+  m.impl("bn_bwd_sums", &rtseg::bn_bwd_sums);
+  m.impl("bn_backward", &rtseg::bn_backward);
 }

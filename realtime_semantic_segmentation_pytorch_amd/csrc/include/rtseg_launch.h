@@ -37,20 +37,30 @@ struct SegLossArgs {
   float* pix_loss;       // [N, out_h, out_w] fp32 workspace
   float* pix_lse;        // [N, out_h, out_w] fp32 workspace (log-sum-exp per pixel)
   double* stats;         // kSegStats device scalars, see seg_loss.hip
+  double* slab;          // [seg_loss_fwd_blocks, 5] per-tile partial statistics
   unsigned* hist;        // 3 x 2048 radix-select histogram workspace
   float* acc;            // [N, C, h, w] fp32 backward accumulator (upsample path)
   int mode;              // 0 = OHEM, 1 = weighted mean CE, 2 = sum CE
   float ohem_thresh;     // -log(p)
   float* out_loss;       // scalar
 };
+int seg_loss_fwd_blocks(const SegLossArgs& a);
 void launch_seg_loss_fwd(const SegLossArgs& a, hipStream_t st);
 // grad_logits (fp32, layout of grad tensor given) = grad_scale * d loss / d logits
 void launch_seg_loss_bwd(const SegLossArgs& a, const float* grad_out, const Tensor4& grad_logits,
                          hipStream_t st);
 
 // ---- bn_act.hip --------------------------------------------------------------
-// x is [M, C] row-major (channels-last). sums: [2C+1] fp64 (sum, sumsq, count).
-void launch_bn_stats(const void* x, int dtype, int64_t M, int C, double* sums, hipStream_t st);
+// x is [M, C] row-major (channels-last). Partial slabs are [G, 2C] fp32
+// (G = bn_partial_grid); sums are [2C+1] fp64 (sum, second moment, count).
+int bn_partial_grid(int64_t M, int C, int dtype);
+void launch_bn_stats(const void* x, int dtype, int64_t M, int C, float* part, int G, hipStream_t st);
+void launch_bn_finalize_partials(const float* part, int G, int C, double count, const float* w,
+                                 const float* b, float* rmean, float* rvar, int64_t* nbt,
+                                 float momentum, float eps, float* mean_invstd, float* scale_shift,
+                                 double* sums_out, hipStream_t st);
+void launch_bn_slab_to_sums(const float* part, int G, int C, double count, double* sums,
+                            hipStream_t st);
 void launch_bn_finalize(const double* sums, int C, const float* w, const float* b, float* rmean,
                         float* rvar, int64_t* nbt, float momentum, float eps, float* mean_invstd,
                         float* scale_shift, hipStream_t st);
@@ -61,10 +71,10 @@ void launch_bn_apply(const void* x, const void* res, const float* scale_shift, v
                      int64_t M, int C, int act, hipStream_t st);
 void launch_bn_bwd_reduce(const void* dy, const void* x, const void* y, const float* mean_invstd,
                           const float* scale_shift, int dtype, int64_t M, int C, int act, int mask,
-                          double* sums, hipStream_t st);
-void launch_bn_bwd_finalize(const double* sums, const double* count_ptr, int C, const float* w,
-                            const float* mean_invstd, int batch_stats, float* kcoef, float* dw,
-                            float* db, hipStream_t st);
+                          float* part, int G, hipStream_t st);
+void launch_bn_bwd_finalize(const float* part, int G, const double* sums, const double* count_ptr,
+                            int C, const float* w, const float* mean_invstd, int batch_stats,
+                            float* kcoef, float* dw, float* db, hipStream_t st);
 void launch_bn_bwd_apply(const void* dy, const void* x, const void* y, const float* mean_invstd,
                          const float* scale_shift, const float* kcoef, void* dx, void* dres,
                          int dtype, int64_t M, int C, int act, int mask, hipStream_t st);

@@ -8,10 +8,13 @@
 // relu-backward).
 //
 // Layout: x is [M, C] row-major (M = N*H*W, i.e. NHWC / channels_last). One
-// thread owns a 16-byte channel vector (8 bf16/fp16 or 4 fp32) and walks rows;
-// per-channel partial sums are reduced in LDS and added to fp64 accumulators
-// with one atomic per channel per block, so the cross-rank SyncBN reduction is
-// a single all-reduce of [2, C] doubles (done by the caller on RCCL).
+// thread owns a 16-byte channel vector (8 bf16/fp16 or 4 fp32) and walks a
+// contiguous row range of its block with 4 independent loads in flight; each
+// block writes its per-channel partial sums to a [G, 2C] fp32 slab (no atomics,
+// no memset, deterministic), and a finalize kernel reduces the slab in fp64 and
+// produces mean/invstd, the folded scale/shift and the running-stat update in
+// the same launch.  For SyncBN the slab is reduced to [2C+1] fp64 sums that the
+// caller all-reduces over RCCL before finalizing.
 //
 // Backward "mask modes": the activation derivative is recomputed instead of
 // stored -- from the pre-activation x*scale+shift when there is no residual
@@ -72,50 +75,168 @@ __device__ __forceinline__ float act_grad_pre(float g, float z) {  // from pre-a
   else return g;
 }
 
+// ----------------------------------------------------------- geometry -------
+// Channel-vector / row layout of a block of 256 threads.
+struct RowGeo {
+  int cv, rpi, my_cv, my_r;
+  __device__ __forceinline__ RowGeo(int C, int V) {
+    cv = C / V;
+    rpi = 256 / cv;
+    my_cv = threadIdx.x % cv;
+    my_r = threadIdx.x / cv;
+  }
+};
+
+// Block-contiguous row range, a multiple of rpi rows.
+__device__ __forceinline__ void block_rows(int64_t M, int rpi, int64_t& r0, int64_t& r1) {
+  int64_t per = (M + gridDim.x - 1) / gridDim.x;
+  per = (per + rpi - 1) / rpi * rpi;
+  r0 = static_cast<int64_t>(blockIdx.x) * per;
+  r1 = r0 + per < M ? r0 + per : M;
+}
+
+// Write this thread's V partial pairs to LDS, reduce over the rpi row-slots and
+// store one [2C] slab row per block.
+template <int V>
+__device__ __forceinline__ void block_partials_out(const float* s, const float* q, const RowGeo& g,
+                                                   int C, float* sm, float* __restrict__ part) {
+  float* ss = sm;
+  float* qq = sm + g.rpi * C;
+  if (g.my_r < g.rpi) {
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      ss[g.my_r * C + g.my_cv * V + j] = s[j];
+      qq[g.my_r * C + g.my_cv * V + j] = q[j];
+    }
+  }
+  __syncthreads();
+  float* out = part + static_cast<int64_t>(blockIdx.x) * 2 * C;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < g.rpi; ++r) { a += ss[r * C + c]; b += qq[r * C + c]; }
+    out[c] = a;
+    out[C + c] = b;
+  }
+}
+
 // --------------------------------------------------------------- stats ------
-// sums[0:C] += sum x, sums[C:2C] += sum x^2
 template <typename T>
 __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, int64_t M, int C,
-                                                       double* __restrict__ sums) {
+                                                       float* __restrict__ part) {
   constexpr int V = Vec<T>::N;
-  extern __shared__ __attribute__((aligned(16))) float sm[];  // [rows_per_iter][C] x 2
-  const int cv = C / V;
-  const int rpi = blockDim.x / cv;  // rows per iteration
-  const int t = threadIdx.x;
-  const int my_cv = t % cv;
-  const int my_r = t / cv;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const RowGeo g(C, V);
   float s[V], q[V];
 #pragma unroll
   for (int j = 0; j < V; ++j) { s[j] = 0.f; q[j] = 0.f; }
-  if (my_r < rpi) {
-    for (int64_t r = static_cast<int64_t>(blockIdx.x) * rpi + my_r; r < M;
-         r += static_cast<int64_t>(gridDim.x) * rpi) {
+  if (g.my_r < g.rpi) {
+    int64_t r0, r1;
+    block_rows(M, g.rpi, r0, r1);
+    const T* base = x + g.my_cv * V;
+    int64_t r = r0 + g.my_r;
+    const int64_t step = static_cast<int64_t>(g.rpi) * C;
+    for (; r + 3 * g.rpi < r1; r += 4 * g.rpi) {  // 4 independent 16-B loads in flight
+      float f0[V], f1[V], f2[V], f3[V];
+      const T* p = base + r * C;
+      Vec<T>::load(p, f0); Vec<T>::load(p + step, f1);
+      Vec<T>::load(p + 2 * step, f2); Vec<T>::load(p + 3 * step, f3);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        s[j] += (f0[j] + f1[j]) + (f2[j] + f3[j]);
+        q[j] += (f0[j] * f0[j] + f1[j] * f1[j]) + (f2[j] * f2[j] + f3[j] * f3[j]);
+      }
+    }
+    for (; r < r1; r += g.rpi) {
       float f[V];
-      Vec<T>::load(x + r * C + my_cv * V, f);
+      Vec<T>::load(base + r * C, f);
 #pragma unroll
       for (int j = 0; j < V; ++j) { s[j] += f[j]; q[j] += f[j] * f[j]; }
     }
   }
-  float* ss = sm;
-  float* qq = sm + rpi * C;
-  if (my_r < rpi) {
-#pragma unroll
-    for (int j = 0; j < V; ++j) {
-      ss[my_r * C + my_cv * V + j] = s[j];
-      qq[my_r * C + my_cv * V + j] = q[j];
-    }
-  }
-  __syncthreads();
-  for (int c = t; c < C; c += blockDim.x) {
-    double a = 0.0, b = 0.0;
-    for (int r = 0; r < rpi; ++r) { a += ss[r * C + c]; b += qq[r * C + c]; }
-    atomicAdd(sums + c, a);
-    atomicAdd(sums + C + c, b);
-  }
-  if (blockIdx.x == 0 && t == 0) atomicAdd(sums + 2 * C, static_cast<double>(M));
+  block_partials_out<V>(s, q, g, C, sm, part);
 }
 
-// One thread per channel: batch mean/invstd, affine scale/shift, running stats.
+// Slab [G][2C] -> fp64 per-channel totals for 64 channels per block (4 waves
+// split the slab rows).  Result in red[0..63] (sum) / red[64..127] (second).
+__device__ __forceinline__ void reduce_slab64(const float* __restrict__ part, int G, int C, int c,
+                                              double* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    for (int gi = w; gi < G; gi += 4) {
+      a += part[static_cast<int64_t>(gi) * 2 * C + c];
+      b += part[static_cast<int64_t>(gi) * 2 * C + C + c];
+    }
+  }
+  red[w * 128 + lane] = a;
+  red[w * 128 + 64 + lane] = b;
+  __syncthreads();
+  if (w == 0) {
+    double ta = 0.0, tb = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { ta += red[k * 128 + lane]; tb += red[k * 128 + 64 + lane]; }
+    red[lane] = ta;
+    red[64 + lane] = tb;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void finalize_channel(int c, int C, double sum, double sumsq,
+                                                 double count, const float* w, const float* b,
+                                                 float* rmean, float* rvar, float momentum,
+                                                 float eps, float* mean_invstd, float* scale_shift) {
+  const double mean = sum / count;
+  double var = sumsq / count - mean * mean;
+  if (var < 0) var = 0;
+  const float invstd = static_cast<float>(1.0 / sqrt(var + static_cast<double>(eps)));
+  const float sc = (w ? w[c] : 1.f) * invstd;
+  mean_invstd[c] = static_cast<float>(mean);
+  mean_invstd[C + c] = invstd;
+  scale_shift[c] = sc;
+  scale_shift[C + c] = (b ? b[c] : 0.f) - static_cast<float>(mean) * sc;
+  if (rmean) {
+    const double unbiased = count > 1 ? var * count / (count - 1) : var;
+    rmean[c] = (1.f - momentum) * rmean[c] + momentum * static_cast<float>(mean);
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * static_cast<float>(unbiased);
+  }
+}
+
+// Fused: slab reduce + finalize (+ sums[2C+1] for the backward's count).
+__global__ void __launch_bounds__(256) bn_finalize_partials_kernel(
+    const float* __restrict__ part, int G, int C, double count, const float* __restrict__ w,
+    const float* __restrict__ b, float* __restrict__ rmean, float* __restrict__ rvar,
+    int64_t* __restrict__ nbt, float momentum, float eps, float* __restrict__ mean_invstd,
+    float* __restrict__ scale_shift, double* __restrict__ sums_out) {
+  __shared__ double red[4 * 128];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  reduce_slab64(part, G, C, c, red);
+  if (threadIdx.x < 64 && c < C) {
+    const double sum = red[threadIdx.x], sumsq = red[64 + threadIdx.x];
+    if (sums_out) { sums_out[c] = sum; sums_out[C + c] = sumsq; }
+    finalize_channel(c, C, sum, sumsq, count, w, b, rmean, rvar, momentum, eps, mean_invstd,
+                     scale_shift);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (nbt) nbt[0] += 1;
+    if (sums_out) sums_out[2 * C] = count;
+  }
+}
+
+// SyncBN path, step 1: slab -> fp64 [2C+1] sums (all-reduced by the caller).
+__global__ void __launch_bounds__(256) bn_slab_to_sums_kernel(const float* __restrict__ part, int G,
+                                                              int C, double count,
+                                                              double* __restrict__ sums) {
+  __shared__ double red[4 * 128];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  reduce_slab64(part, G, C, c, red);
+  if (threadIdx.x < 64 && c < C) {
+    sums[c] = red[threadIdx.x];
+    sums[C + c] = red[64 + threadIdx.x];
+  }
+  if (count >= 0 && blockIdx.x == 0 && threadIdx.x == 0) sums[2 * C] = count;
+}
+
+// SyncBN path, step 2: finalize from the all-reduced sums.
 __global__ void bn_finalize_kernel(const double* __restrict__ sums, int C,
                                    const float* __restrict__ w, const float* __restrict__ b,
                                    float* __restrict__ rmean, float* __restrict__ rvar,
@@ -124,23 +245,8 @@ __global__ void bn_finalize_kernel(const double* __restrict__ sums, int C,
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c == 0 && nbt) nbt[0] += 1;
   if (c >= C) return;
-  const double count = sums[2 * C];
-  const double mean = sums[c] / count;
-  double var = sums[C + c] / count - mean * mean;
-  if (var < 0) var = 0;
-  const float invstd = static_cast<float>(1.0 / sqrt(var + static_cast<double>(eps)));
-  const float wc = w ? w[c] : 1.f;
-  const float bc = b ? b[c] : 0.f;
-  const float sc = wc * invstd;
-  mean_invstd[c] = static_cast<float>(mean);
-  mean_invstd[C + c] = invstd;
-  scale_shift[c] = sc;
-  scale_shift[C + c] = bc - static_cast<float>(mean) * sc;
-  if (rmean) {
-    const double unbiased = count > 1 ? var * count / (count - 1) : var;
-    rmean[c] = (1.f - momentum) * rmean[c] + momentum * static_cast<float>(mean);
-    rvar[c] = (1.f - momentum) * rvar[c] + momentum * static_cast<float>(unbiased);
-  }
+  finalize_channel(c, C, sums[c], sums[C + c], sums[2 * C], w, b, rmean, rvar, momentum, eps,
+                   mean_invstd, scale_shift);
 }
 
 // Eval mode: scale/shift from running statistics.
@@ -160,6 +266,25 @@ __global__ void bn_eval_coeffs_kernel(int C, const float* __restrict__ w, const 
 
 // --------------------------------------------------------------- apply ------
 template <typename T, int ACT, bool RES>
+__device__ __forceinline__ void apply_one(const T* __restrict__ x, const T* __restrict__ res,
+                                          const float* coef, T* __restrict__ y, int64_t i, int cv,
+                                          int C) {
+  constexpr int V = Vec<T>::N;
+  const int c0 = static_cast<int>(i % cv) * V;
+  const int64_t off = (i / cv) * C + c0;
+  float f[V], r[V];
+  Vec<T>::load(x + off, f);
+  if constexpr (RES) Vec<T>::load(res + off, r);
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    float z = f[j] * coef[c0 + j] + coef[C + c0 + j];
+    if constexpr (RES) z += r[j];
+    f[j] = act_fwd<ACT>(z);
+  }
+  Vec<T>::store(y + off, f);
+}
+
+template <typename T, int ACT, bool RES>
 __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x,
                                                        const T* __restrict__ res,
                                                        const float* __restrict__ scale_shift,
@@ -170,21 +295,13 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x,
   __syncthreads();
   const int cv = C / V;
   const int64_t total = M * cv;
-  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < total;
-       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    const int c0 = static_cast<int>(i % cv) * V;
-    const int64_t off = (i / cv) * C + c0;
-    float f[V], r[V];
-    Vec<T>::load(x + off, f);
-    if constexpr (RES) Vec<T>::load(res + off, r);
-#pragma unroll
-    for (int j = 0; j < V; ++j) {
-      float z = f[j] * coef[c0 + j] + coef[C + c0 + j];
-      if constexpr (RES) z += r[j];
-      f[j] = act_fwd<ACT>(z);
-    }
-    Vec<T>::store(y + off, f);
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  for (; i + stride < total; i += 2 * stride) {  // two vectors in flight per thread
+    apply_one<T, ACT, RES>(x, res, coef, y, i, cv, C);
+    apply_one<T, ACT, RES>(x, res, coef, y, i + stride, cv, C);
   }
+  if (i < total) apply_one<T, ACT, RES>(x, res, coef, y, i, cv, C);
 }
 
 // ----------------------------------------------------------- backward -------
@@ -205,64 +322,60 @@ __device__ __forceinline__ void load_g(const T* dy, const T* x, const T* y, cons
   }
 }
 
-// sums[0:C] += sum g, sums[C:2C] += sum g * (x - mean)
+// slab[G][0:C] = sum g, slab[G][C:2C] = sum g * (x - mean)
 template <typename T, int ACT, int MASK>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y,
     const float* __restrict__ mean_invstd, const float* __restrict__ scale_shift, int64_t M, int C,
-    double* __restrict__ sums) {
+    float* __restrict__ part) {
   constexpr int V = Vec<T>::N;
   extern __shared__ __attribute__((aligned(16))) float sm[];  // coef[2C] | mean[C] | partials
   float* coef = sm;
   float* mu = sm + 2 * C;
-  const int cv = C / V;
-  const int rpi = blockDim.x / cv;
-  float* ss = sm + 3 * C;
-  float* qq = ss + rpi * C;
   for (int c = threadIdx.x; c < 2 * C; c += blockDim.x) coef[c] = scale_shift[c];
   for (int c = threadIdx.x; c < C; c += blockDim.x) mu[c] = mean_invstd[c];
   __syncthreads();
-  const int t = threadIdx.x;
-  const int my_cv = t % cv, my_r = t / cv, c0 = my_cv * V;
+  const RowGeo g(C, V);
+  const int c0 = g.my_cv * V;
   float s[V], q[V];
 #pragma unroll
   for (int j = 0; j < V; ++j) { s[j] = 0.f; q[j] = 0.f; }
-  if (my_r < rpi) {
-    for (int64_t r = static_cast<int64_t>(blockIdx.x) * rpi + my_r; r < M;
-         r += static_cast<int64_t>(gridDim.x) * rpi) {
-      float g[V], xv[V];
-      load_g<T, ACT, MASK>(dy, x, y, coef, C, r * C + c0, c0, g, xv);
+  if (g.my_r < g.rpi) {
+    int64_t r0, r1;
+    block_rows(M, g.rpi, r0, r1);
+    float m[V];
 #pragma unroll
-      for (int j = 0; j < V; ++j) { s[j] += g[j]; q[j] += g[j] * (xv[j] - mu[c0 + j]); }
+    for (int j = 0; j < V; ++j) m[j] = mu[c0 + j];
+    int64_t r = r0 + g.my_r;
+    for (; r + g.rpi < r1; r += 2 * g.rpi) {  // two rows (4-6 loads) in flight
+      float ga[V], xa[V], gb[V], xb[V];
+      load_g<T, ACT, MASK>(dy, x, y, coef, C, r * C + c0, c0, ga, xa);
+      load_g<T, ACT, MASK>(dy, x, y, coef, C, (r + g.rpi) * C + c0, c0, gb, xb);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        s[j] += ga[j] + gb[j];
+        q[j] += ga[j] * (xa[j] - m[j]) + gb[j] * (xb[j] - m[j]);
+      }
     }
+    if (r < r1) {
+      float ga[V], xa[V];
+      load_g<T, ACT, MASK>(dy, x, y, coef, C, r * C + c0, c0, ga, xa);
 #pragma unroll
-    for (int j = 0; j < V; ++j) { ss[my_r * C + c0 + j] = s[j]; qq[my_r * C + c0 + j] = q[j]; }
+      for (int j = 0; j < V; ++j) { s[j] += ga[j]; q[j] += ga[j] * (xa[j] - m[j]); }
+    }
   }
-  __syncthreads();
-  for (int c = t; c < C; c += blockDim.x) {
-    double a = 0.0, b = 0.0;
-    for (int r = 0; r < rpi; ++r) { a += ss[r * C + c]; b += qq[r * C + c]; }
-    atomicAdd(sums + c, a);
-    atomicAdd(sums + C + c, b);
-  }
+  __syncthreads();  // coef/mu region is reused below only after every thread is done
+  block_partials_out<V>(s, q, g, C, sm + 3 * C, part);
 }
 
-// Per channel: dx coefficients (k1, k2, k3) and the parameter gradients.
-__global__ void bn_bwd_finalize_kernel(const double* __restrict__ sums,
-                                       const double* __restrict__ count_ptr, int C,
-                                       const float* __restrict__ w,
-                                       const float* __restrict__ mean_invstd, int batch_stats,
-                                       float* __restrict__ kcoef, float* __restrict__ dw,
-                                       float* __restrict__ db) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+__device__ __forceinline__ void bwd_finalize_channel(int c, int C, double sg, double sgx,
+                                                     double count, const float* w,
+                                                     const float* mean_invstd, int batch_stats,
+                                                     float* kcoef, float* dw, float* db) {
   const float invstd = mean_invstd[C + c];
-  const double sg = sums[c], sgx = sums[C + c];
-  const double count = count_ptr ? *count_ptr : 1.0;
   if (dw) dw[c] = static_cast<float>(sgx * invstd);
   if (db) db[c] = static_cast<float>(sg);
-  const float wc = w ? w[c] : 1.f;
-  kcoef[c] = wc * invstd;
+  kcoef[c] = (w ? w[c] : 1.f) * invstd;
   if (batch_stats) {
     kcoef[C + c] = static_cast<float>(sg / count);
     kcoef[2 * C + c] = static_cast<float>(sgx / count) * invstd * invstd;
@@ -270,6 +383,41 @@ __global__ void bn_bwd_finalize_kernel(const double* __restrict__ sums,
     kcoef[C + c] = 0.f;
     kcoef[2 * C + c] = 0.f;
   }
+}
+
+// Slab (or already-reduced sums, SyncBN) -> dx coefficients + parameter grads.
+__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(
+    const float* __restrict__ part, int G, const double* __restrict__ sums,
+    const double* __restrict__ count_ptr, int C, const float* __restrict__ w,
+    const float* __restrict__ mean_invstd, int batch_stats, float* __restrict__ kcoef,
+    float* __restrict__ dw, float* __restrict__ db) {
+  __shared__ double red[4 * 128];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  if (!sums) reduce_slab64(part, G, C, c, red);
+  if (threadIdx.x < 64 && c < C) {
+    const double sg = sums ? sums[c] : red[threadIdx.x];
+    const double sgx = sums ? sums[C + c] : red[64 + threadIdx.x];
+    const double count = count_ptr ? *count_ptr : 1.0;
+    bwd_finalize_channel(c, C, sg, sgx, count, w, mean_invstd, batch_stats, kcoef, dw, db);
+  }
+}
+
+template <typename T, int ACT, int MASK, bool DRES>
+__device__ __forceinline__ void bwd_apply_one(const T* dy, const T* x, const T* y, const float* coef,
+                                              const float* mu, const float* k, T* dx, T* dres,
+                                              int64_t i, int cv, int C) {
+  constexpr int V = Vec<T>::N;
+  const int c0 = static_cast<int>(i % cv) * V;
+  const int64_t off = (i / cv) * C + c0;
+  float g[V], xv[V], o[V];
+  load_g<T, ACT, MASK>(dy, x, y, coef, C, off, c0, g, xv);
+  if constexpr (DRES) Vec<T>::store(dres + off, g);
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    const int c = c0 + j;
+    o[j] = k[c] * (g[j] - k[C + c] - (xv[j] - mu[c]) * k[2 * C + c]);
+  }
+  Vec<T>::store(dx + off, o);
 }
 
 template <typename T, int ACT, int MASK, bool DRES>
@@ -288,43 +436,51 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
   __syncthreads();
   const int cv = C / V;
   const int64_t total = M * cv;
-  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < total;
-       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    const int c0 = static_cast<int>(i % cv) * V;
-    const int64_t off = (i / cv) * C + c0;
-    float g[V], xv[V], o[V];
-    load_g<T, ACT, MASK>(dy, x, y, coef, C, off, c0, g, xv);
-    if constexpr (DRES) Vec<T>::store(dres + off, g);
-#pragma unroll
-    for (int j = 0; j < V; ++j) {
-      const int c = c0 + j;
-      o[j] = k[c] * (g[j] - k[C + c] - (xv[j] - mu[c]) * k[2 * C + c]);
-    }
-    Vec<T>::store(dx + off, o);
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  for (; i + stride < total; i += 2 * stride) {
+    bwd_apply_one<T, ACT, MASK, DRES>(dy, x, y, coef, mu, k, dx, dres, i, cv, C);
+    bwd_apply_one<T, ACT, MASK, DRES>(dy, x, y, coef, mu, k, dx, dres, i + stride, cv, C);
   }
+  if (i < total) bwd_apply_one<T, ACT, MASK, DRES>(dy, x, y, coef, mu, k, dx, dres, i, cv, C);
 }
 
 // ------------------------------------------------------------ launchers -----
-static int reduce_grid(int64_t M, int rpi) {
-  int64_t g = (M + rpi * 64 - 1) / (rpi * 64);  // >= 64 rows per thread-row
+int bn_partial_grid(int64_t M, int C, int dtype) {
+  const int V = dtype == kF32 ? 4 : 8;
+  const int rpi = 256 / (C / V);
+  int64_t g = (M + static_cast<int64_t>(rpi) * 32 - 1) / (static_cast<int64_t>(rpi) * 32);
   if (g > 1024) g = 1024;
   if (g < 1) g = 1;
   return static_cast<int>(g);
 }
 
 template <typename T>
-static void stats_t(const void* x, int64_t M, int C, double* sums, hipStream_t st) {
-  const int cv = C / Vec<T>::N;
-  const int rpi = 256 / cv;
+static void stats_t(const void* x, int64_t M, int C, float* part, int G, hipStream_t st) {
+  const int rpi = 256 / (C / Vec<T>::N);
   const size_t lds = sizeof(float) * 2 * rpi * C;
-  bn_stats_kernel<T><<<reduce_grid(M, rpi), 256, lds, st>>>(static_cast<const T*>(x), M, C, sums);
+  bn_stats_kernel<T><<<G, 256, lds, st>>>(static_cast<const T*>(x), M, C, part);
 }
 
-void launch_bn_stats(const void* x, int dtype, int64_t M, int C, double* sums, hipStream_t st) {
-  hipMemsetAsync(sums, 0, sizeof(double) * (2 * C + 1), st);
-  if (dtype == kF32) stats_t<float>(x, M, C, sums, st);
-  else if (dtype == kBF16) stats_t<uint16_t>(x, M, C, sums, st);
-  else stats_t<_Float16>(x, M, C, sums, st);
+void launch_bn_stats(const void* x, int dtype, int64_t M, int C, float* part, int G,
+                     hipStream_t st) {
+  if (dtype == kF32) stats_t<float>(x, M, C, part, G, st);
+  else if (dtype == kBF16) stats_t<uint16_t>(x, M, C, part, G, st);
+  else stats_t<_Float16>(x, M, C, part, G, st);
+}
+
+void launch_bn_finalize_partials(const float* part, int G, int C, double count, const float* w,
+                                 const float* b, float* rmean, float* rvar, int64_t* nbt,
+                                 float momentum, float eps, float* mean_invstd, float* scale_shift,
+                                 double* sums_out, hipStream_t st) {
+  bn_finalize_partials_kernel<<<(C + 63) / 64, 256, 0, st>>>(part, G, C, count, w, b, rmean, rvar,
+                                                             nbt, momentum, eps, mean_invstd,
+                                                             scale_shift, sums_out);
+}
+
+void launch_bn_slab_to_sums(const float* part, int G, int C, double count, double* sums,
+                            hipStream_t st) {
+  bn_slab_to_sums_kernel<<<(C + 63) / 64, 256, 0, st>>>(part, G, C, count, sums);
 }
 
 void launch_bn_finalize(const double* sums, int C, const float* w, const float* b,
@@ -341,12 +497,20 @@ void launch_bn_eval_coeffs(int C, const float* w, const float* b, const float* r
                                                          scale_shift);
 }
 
+static int apply_grid(int64_t work) {
+  int64_t g = (work + 511) / 512;  // two vectors per thread
+  const int64_t cap = 256 * 8;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return static_cast<int>(g);
+}
+
 template <typename T, int ACT>
 static void apply_t(const void* x, const void* res, const float* ss, void* y, int64_t M, int C,
                     hipStream_t st) {
   const int64_t work = M * (C / Vec<T>::N);
   const size_t lds = sizeof(float) * 2 * C;
-  const int grid = stream_grid(work, 256);
+  const int grid = apply_grid(work);
   if (res)
     bn_apply_kernel<T, ACT, true><<<grid, 256, lds, st>>>(
         static_cast<const T*>(x), static_cast<const T*>(res), ss, static_cast<T*>(y), M, C);
@@ -372,13 +536,12 @@ void launch_bn_apply(const void* x, const void* res, const float* scale_shift, v
 
 template <typename T, int ACT, int MASK>
 static void bwd_reduce_t(const void* dy, const void* x, const void* y, const float* mi,
-                         const float* ss, int64_t M, int C, double* sums, hipStream_t st) {
-  const int cv = C / Vec<T>::N;
-  const int rpi = 256 / cv;
+                         const float* ss, int64_t M, int C, float* part, int G, hipStream_t st) {
+  const int rpi = 256 / (C / Vec<T>::N);
   const size_t lds = sizeof(float) * (3 * C + 2 * rpi * C);
-  bn_bwd_reduce_kernel<T, ACT, MASK><<<reduce_grid(M, rpi), 256, lds, st>>>(
+  bn_bwd_reduce_kernel<T, ACT, MASK><<<G, 256, lds, st>>>(
       static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(y), mi, ss, M, C,
-      sums);
+      part);
 }
 
 template <typename T, int ACT, int MASK, bool DRES>
@@ -387,7 +550,7 @@ static void bwd_apply_t(const void* dy, const void* x, const void* y, const floa
                         hipStream_t st) {
   const int64_t work = M * (C / Vec<T>::N);
   const size_t lds = sizeof(float) * 6 * C;
-  bn_bwd_apply_kernel<T, ACT, MASK, DRES><<<stream_grid(work, 256), 256, lds, st>>>(
+  bn_bwd_apply_kernel<T, ACT, MASK, DRES><<<apply_grid(work), 256, lds, st>>>(
       static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(y), mi, ss, k,
       static_cast<T*>(dx), static_cast<T*>(dres), M, C);
 }
@@ -406,25 +569,24 @@ static void bwd_apply_t(const void* dy, const void* x, const void* y, const floa
 
 template <typename T>
 static void bwd_reduce_dispatch(const void* dy, const void* x, const void* y, const float* mi,
-                                const float* ss, int64_t M, int C, int act, int mask,
-                                double* sums, hipStream_t st) {
-  RT_ACT_MASK_DISPATCH(bwd_reduce_t, dy, x, y, mi, ss, M, C, sums, st);
+                                const float* ss, int64_t M, int C, int act, int mask, float* part,
+                                int G, hipStream_t st) {
+  RT_ACT_MASK_DISPATCH(bwd_reduce_t, dy, x, y, mi, ss, M, C, part, G, st);
 }
 
 void launch_bn_bwd_reduce(const void* dy, const void* x, const void* y, const float* mean_invstd,
                           const float* scale_shift, int dtype, int64_t M, int C, int act, int mask,
-                          double* sums, hipStream_t st) {
-  hipMemsetAsync(sums, 0, sizeof(double) * 2 * C, st);
-  if (dtype == kF32) bwd_reduce_dispatch<float>(dy, x, y, mean_invstd, scale_shift, M, C, act, mask, sums, st);
-  else if (dtype == kBF16) bwd_reduce_dispatch<uint16_t>(dy, x, y, mean_invstd, scale_shift, M, C, act, mask, sums, st);
-  else bwd_reduce_dispatch<_Float16>(dy, x, y, mean_invstd, scale_shift, M, C, act, mask, sums, st);
+                          float* part, int G, hipStream_t st) {
+  if (dtype == kF32) bwd_reduce_dispatch<float>(dy, x, y, mean_invstd, scale_shift, M, C, act, mask, part, G, st);
+  else if (dtype == kBF16) bwd_reduce_dispatch<uint16_t>(dy, x, y, mean_invstd, scale_shift, M, C, act, mask, part, G, st);
+  else bwd_reduce_dispatch<_Float16>(dy, x, y, mean_invstd, scale_shift, M, C, act, mask, part, G, st);
 }
 
-void launch_bn_bwd_finalize(const double* sums, const double* count_ptr, int C, const float* w,
-                            const float* mean_invstd, int batch_stats, float* kcoef, float* dw,
-                            float* db, hipStream_t st) {
-  bn_bwd_finalize_kernel<<<(C + 255) / 256, 256, 0, st>>>(sums, count_ptr, C, w, mean_invstd,
-                                                          batch_stats, kcoef, dw, db);
+void launch_bn_bwd_finalize(const float* part, int G, const double* sums, const double* count_ptr,
+                            int C, const float* w, const float* mean_invstd, int batch_stats,
+                            float* kcoef, float* dw, float* db, hipStream_t st) {
+  bn_bwd_finalize_kernel<<<(C + 63) / 64, 256, 0, st>>>(part, G, sums, count_ptr, C, w,
+                                                        mean_invstd, batch_stats, kcoef, dw, db);
 }
 
 template <typename T, int ACT, int MASK>

@@ -52,90 +52,152 @@ __device__ __forceinline__ int64_t label_at(const int64_t* __restrict__ labels, 
   return labels[(static_cast<int64_t>(n) * g.lh + ly) * g.lw + lx];
 }
 
-// Interpolated logit of class c at output pixel given precomputed taps.
-template <typename T>
-struct Taps {
-  const T* p00; const T* p01; const T* p10; const T* p11;
-  float w00, w01, w10, w11;
-  int64_t sc;
-  __device__ __forceinline__ float at(int c) const {
-    const int64_t o = c * sc;
-    return w00 * Io<T>::ld(p00 + o) + w01 * Io<T>::ld(p01 + o) + w10 * Io<T>::ld(p10 + o) +
-           w11 * Io<T>::ld(p11 + o);
-  }
+// ------------------------------- tiles -------------------------------------
+// A block owns a TH x TW tile of output pixels.  The low-resolution logits
+// under the tile's bounding box are staged once into LDS as fp32 [BH][BW][CP]
+// (CP = C rounded up to odd -> conflict-free strided reads), then vertically
+// interpolated to the tile's TH rows, V[TH][BW][CP]; every pixel then needs
+// only 2 LDS reads per class.  Identity geometry (aux heads) reads L directly.
+struct TileGeo {
+  int n, oy0, ox0, oy1, ox1, by0, bx0, BH, BW, CP;
+  bool ident_h, ident_w;
 };
 
-template <typename T>
-__device__ __forceinline__ Taps<T> make_taps(const T* __restrict__ x, const LossGeo& g, int n,
-                                             int oy, int ox) {
-  int y0, y1, x0, x1; float ly, lx;
-  g.mh.map(oy, y0, y1, ly);
-  g.mw.map(ox, x0, x1, lx);
-  Taps<T> t;
-  const T* b = x + n * g.sn;
-  t.p00 = b + y0 * g.sh + x0 * g.sw; t.p01 = b + y0 * g.sh + x1 * g.sw;
-  t.p10 = b + y1 * g.sh + x0 * g.sw; t.p11 = b + y1 * g.sh + x1 * g.sw;
-  t.w00 = (1.f - ly) * (1.f - lx); t.w01 = (1.f - ly) * lx;
-  t.w10 = ly * (1.f - lx); t.w11 = ly * lx;
-  t.sc = g.sc;
+template <int TH, int TW>
+__device__ __forceinline__ TileGeo tile_geo(const LossGeo& g) {
+  TileGeo t;
+  const int tiles_x = (g.ow + TW - 1) / TW;
+  const int tiles_y = (g.oh + TH - 1) / TH;
+  const int bid = blockIdx.x;
+  const int tx = bid % tiles_x;
+  const int ty = (bid / tiles_x) % tiles_y;
+  t.n = bid / (tiles_x * tiles_y);
+  t.oy0 = ty * TH; t.ox0 = tx * TW;
+  t.oy1 = min(t.oy0 + TH, g.oh) - 1; t.ox1 = min(t.ox0 + TW, g.ow) - 1;
+  int a0, a1; float l;
+  g.mh.map(t.oy0, a0, a1, l); t.by0 = a0;
+  g.mh.map(t.oy1, a0, a1, l); const int by1 = a1;
+  g.mw.map(t.ox0, a0, a1, l); t.bx0 = a0;
+  g.mw.map(t.ox1, a0, a1, l); const int bx1 = a1;
+  t.BH = by1 - t.by0 + 1; t.BW = bx1 - t.bx0 + 1;
+  t.CP = g.c | 1;
+  t.ident_h = g.oh == g.h; t.ident_w = g.ow == g.w;
   return t;
 }
 
+template <typename T, int TH>
+__device__ __forceinline__ const float* stage_logits(const T* __restrict__ x, const LossGeo& g,
+                                                     const TileGeo& t, float* L, float* V) {
+  const int C = g.c;
+  const int total = t.BH * t.BW * C;
+  const T* base = x + t.n * g.sn + t.by0 * g.sh + t.bx0 * g.sw;
+  for (int e = threadIdx.x; e < total; e += blockDim.x) {
+    const int c = e % C;
+    const int j = (e / C) % t.BW;
+    const int i = e / (C * t.BW);
+    L[(i * t.BW + j) * t.CP + c] = Io<T>::ld(base + c * g.sc + i * g.sh + j * g.sw);
+  }
+  __syncthreads();
+  if (t.ident_h) return L;  // rows already at output resolution
+  const int vt = TH * t.BW * C;
+  for (int e = threadIdx.x; e < vt; e += blockDim.x) {
+    const int c = e % C;
+    const int j = (e / C) % t.BW;
+    const int r = e / (C * t.BW);
+    const int oy = min(t.oy0 + r, t.oy1);
+    int y0, y1; float ly;
+    g.mh.map(oy, y0, y1, ly);
+    V[(r * t.BW + j) * t.CP + c] = (1.f - ly) * L[((y0 - t.by0) * t.BW + j) * t.CP + c] +
+                                   ly * L[((y1 - t.by0) * t.BW + j) * t.CP + c];
+  }
+  __syncthreads();
+  return V;
+}
+
+// pointers to the two horizontal taps of output pixel (r, ox) inside the staged rows
+__device__ __forceinline__ void pixel_taps(const LossGeo& g, const TileGeo& t, const float* rows,
+                                           int r, int ox, const float*& pa, const float*& pb,
+                                           float& lx) {
+  const int rr = t.ident_h ? (t.oy0 + r - t.by0) : r;
+  int x0, x1;
+  g.mw.map(ox, x0, x1, lx);
+  pa = rows + (rr * t.BW + (x0 - t.bx0)) * t.CP;
+  pb = rows + (rr * t.BW + (x1 - t.bx0)) * t.CP;
+}
+
 // ------------------------------- forward -----------------------------------
-template <typename T>
-__global__ void __launch_bounds__(256) seg_ce_fwd_kernel(
+enum : int { SL_VALID = 0, SL_HCNT, SL_HSUM, SL_WLOSS, SL_WSUM, SL_N };
+
+template <typename T, int TH, int TW>
+__global__ void __launch_bounds__(256) seg_ce_fwd_tile(
     const T* __restrict__ x, LossGeo g, const int64_t* __restrict__ labels, int ignore,
     const float* __restrict__ cw, float thresh, float* __restrict__ pix_loss,
-    float* __restrict__ pix_lse, double* __restrict__ stats) {
+    float* __restrict__ pix_lse, double* __restrict__ slab) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
   __shared__ double red[4];
-  const int64_t total = static_cast<int64_t>(g.n) * g.oh * g.ow;
-  double valid = 0, hard_cnt = 0, hard_sum = 0, wloss = 0, wsum = 0;
-  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < total;
-       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    int ox = static_cast<int>(i % g.ow);
-    int64_t t = i / g.ow;
-    int oy = static_cast<int>(t % g.oh);
-    int n = static_cast<int>(t / g.oh);
-    Taps<T> tp = make_taps(x, g, n, oy, ox);
-    int64_t y = label_at(labels, g, n, oy, ox);
+  const TileGeo t = tile_geo<TH, TW>(g);
+  float* L = sm;
+  float* V = sm + t.BH * t.BW * t.CP;
+  const float* rows = stage_logits<T, TH>(x, g, t, L, V);
+  float acc[SL_N] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int p = threadIdx.x; p < TH * TW; p += blockDim.x) {
+    const int r = p / TW, oy = t.oy0 + r, ox = t.ox0 + p % TW;
+    if (oy > t.oy1 || ox > t.ox1) continue;
+    const float *pa, *pb; float lx;
+    pixel_taps(g, t, rows, r, ox, pa, pb, lx);
+    const int64_t y = label_at(labels, g, t.n, oy, ox);
     float m = -INFINITY, s = 0.f, zy = 0.f;
     for (int c = 0; c < g.c; ++c) {
-      float z = tp.at(c);
+      const float z = (1.f - lx) * pa[c] + lx * pb[c];
       if (c == y) zy = z;
       if (z > m) { s = s * __expf(m - z) + 1.f; m = z; }
       else s += __expf(z - m);
     }
-    float lse = m + __logf(s);
+    const float lse = m + __logf(s);
     float l = 0.f;
-    bool ok = (y != ignore) && y >= 0 && y < g.c;
-    if (ok) {
+    if (y != ignore && y >= 0 && y < g.c) {
       l = fmaxf(lse - zy, 0.f);
-      float w = cw ? cw[y] : 1.f;
-      valid += 1.0;
-      wloss += static_cast<double>(w) * l;
-      wsum += w;
+      const float w = cw ? cw[y] : 1.f;
+      acc[SL_VALID] += 1.f;
+      acc[SL_WLOSS] += w * l;
+      acc[SL_WSUM] += w;
     }
-    if (l > thresh) { hard_cnt += 1.0; hard_sum += l; }
-    pix_loss[i] = l;
-    pix_lse[i] = lse;
+    if (l > thresh) { acc[SL_HCNT] += 1.f; acc[SL_HSUM] += l; }
+    const int64_t pi = (static_cast<int64_t>(t.n) * g.oh + oy) * g.ow + ox;
+    pix_loss[pi] = l;
+    pix_lse[pi] = lse;
   }
-  double vals[5] = {valid, hard_cnt, hard_sum, wloss, wsum};
-  const int slots[5] = {S_VALID, S_HARD_CNT, S_HARD_SUM, S_WLOSS, S_WSUM};
 #pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    double r = block_sum(vals[k], red);
-    if (threadIdx.x == 0 && r != 0.0) atomicAdd(stats + slots[k], r);
+  for (int k = 0; k < SL_N; ++k) {
+    const double v = block_sum(static_cast<double>(acc[k]), red);
+    if (threadIdx.x == 0) slab[static_cast<int64_t>(blockIdx.x) * SL_N + k] = v;
   }
 }
 
-// Decide the branch (threshold vs top-k) on device.
-__global__ void seg_finalize1(double* stats, int mode, float thresh, float* out_loss) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// One block: reduce the per-tile slab, then decide threshold vs top-k on device.
+__global__ void __launch_bounds__(1024) seg_finalize1(const double* __restrict__ slab, int nblk,
+                                                      double* stats, int mode, float thresh,
+                                                      float* out_loss) {
+  __shared__ double red[16];
+  double tot[SL_N];
+#pragma unroll
+  for (int k = 0; k < SL_N; ++k) {
+    double v = 0.0;
+    for (int i = threadIdx.x; i < nblk; i += blockDim.x) v += slab[static_cast<int64_t>(i) * SL_N + k];
+    tot[k] = block_sum(v, red);
+  }
+  if (threadIdx.x != 0) return;
+  for (int k = S_VALID; k < S_NSTATS; ++k) stats[k] = 0.0;
+  stats[S_VALID] = tot[SL_VALID];
+  stats[S_HARD_CNT] = tot[SL_HCNT];
+  stats[S_HARD_SUM] = tot[SL_HSUM];
+  stats[S_WLOSS] = tot[SL_WLOSS];
+  stats[S_WSUM] = tot[SL_WSUM];
   if (mode == MODE_OHEM) {
-    double n_min = floor(stats[S_VALID] / 16.0);
-    double hc = stats[S_HARD_CNT];
+    const double n_min = floor(stats[S_VALID] / 16.0);
+    const double hc = stats[S_HARD_CNT];
     if (hc >= n_min) {
-      double v = hc > 0 ? stats[S_HARD_SUM] / hc : 0.0;
+      const double v = hc > 0 ? stats[S_HARD_SUM] / hc : 0.0;
       stats[S_LOSS] = v;
       stats[S_SEL_T] = thresh;
       stats[S_SEL_A] = hc > 0 ? 1.0 / hc : 0.0;
@@ -149,8 +211,8 @@ __global__ void seg_finalize1(double* stats, int mode, float thresh, float* out_
       stats[S_PREFIX] = 0.0;
     }
   } else {
-    double ws = stats[S_WSUM];
-    double v = (mode == MODE_MEAN) ? (ws > 0 ? stats[S_WLOSS] / ws : 0.0) : stats[S_WLOSS];
+    const double ws = stats[S_WSUM];
+    const double v = (mode == MODE_MEAN) ? (ws > 0 ? stats[S_WLOSS] / ws : 0.0) : stats[S_WLOSS];
     stats[S_LOSS] = v;
     stats[S_SEL_A] = (mode == MODE_MEAN) ? (ws > 0 ? 1.0 / ws : 0.0) : 1.0;
     stats[S_FLAG_TOPK] = 0.0;
@@ -310,98 +372,84 @@ __global__ void __launch_bounds__(256) seg_ce_bwd_identity(
   }
 }
 
-// Upsampled geometry: block = TH x TW output pixels. G tile -> LDS, row pass,
-// column pass, atomics into the fp32 low-res gradient.
-template <typename T, int TH, int TW, int CMAX>
-__global__ void __launch_bounds__(256) seg_ce_bwd_upsample(
+// Upsampled geometry: stage logits (as in the forward), per-pixel softmax
+// gradient tile G[C][TH][TW] in LDS, transpose of the bilinear map as a row
+// pass then a column pass, fp32 atomics only for the tile's bounding box cells.
+template <typename T, int TH, int TW>
+__global__ void __launch_bounds__(256) seg_ce_bwd_tile(
     const T* __restrict__ x, LossGeo g, const int64_t* __restrict__ labels, int ignore,
     const float* __restrict__ cw, const float* __restrict__ pix_loss,
     const float* __restrict__ pix_lse, const double* __restrict__ stats, int mode,
-    const float* __restrict__ grad_out, float* __restrict__ gacc, int bw_max, int bh_max) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* Gt = smem;                       // [C][TH][TW]
-  float* R = smem + g.c * TH * TW;        // [C][TH][bw_max]
-  const int tiles_x = (g.ow + TW - 1) / TW;
-  const int tiles_y = (g.oh + TH - 1) / TH;
-  const int bid = blockIdx.x;
-  const int tx = bid % tiles_x;
-  const int ty = (bid / tiles_x) % tiles_y;
-  const int n = bid / (tiles_x * tiles_y);
-  const int oy0 = ty * TH, ox0 = tx * TW;
-  const int oy1 = min(oy0 + TH, g.oh) - 1, ox1 = min(ox0 + TW, g.ow) - 1;
-  const SelRule r = load_rule(stats, mode);
+    const float* __restrict__ grad_out, float* __restrict__ gacc) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const TileGeo t = tile_geo<TH, TW>(g);
+  const int C = g.c;
+  float* L = sm;
+  float* V = L + t.BH * t.BW * t.CP;
+  float* Gt = V + TH * t.BW * t.CP;   // [C][TH][TW]
+  float* R = Gt + C * TH * TW;         // [C][TH][BW]
+  const float* rows = stage_logits<T, TH>(x, g, t, L, V);
+  const SelRule rule = load_rule(stats, mode);
   const float go = *grad_out;
-
-  // low-res bounding box of this tile
-  int a0, a1, b0, b1; float l_;
-  g.mh.map(oy0, a0, a1, l_);
-  int by0 = a0;
-  g.mh.map(oy1, a0, a1, l_);
-  int by1 = a1;
-  g.mw.map(ox0, b0, b1, l_);
-  int bx0 = b0;
-  g.mw.map(ox1, b0, b1, l_);
-  int bx1 = b1;
-  const int BH = by1 - by0 + 1, BW = bx1 - bx0 + 1;
-
-  // 1) per-pixel softmax gradient into LDS
   for (int p = threadIdx.x; p < TH * TW; p += blockDim.x) {
-    int r_ = p / TW, c_ = p % TW;
-    int oy = oy0 + r_, ox = ox0 + c_;
+    const int r = p / TW, oy = t.oy0 + r, ox = t.ox0 + p % TW;
     float* gp = Gt + p;
-    if (oy > oy1 || ox > ox1) {
-      for (int c = 0; c < g.c; ++c) gp[c * TH * TW] = 0.f;
-      continue;
+    float w = 0.f;
+    int64_t y = -1;
+    int64_t pi = 0;
+    if (oy <= t.oy1 && ox <= t.ox1) {
+      pi = (static_cast<int64_t>(t.n) * g.oh + oy) * g.ow + ox;
+      y = label_at(labels, g, t.n, oy, ox);
+      w = pixel_weight(rule, pix_loss[pi], y, ignore, C, cw) * go;
     }
-    int64_t pi = (static_cast<int64_t>(n) * g.oh + oy) * g.ow + ox;
-    int64_t y = label_at(labels, g, n, oy, ox);
-    float w = pixel_weight(r, pix_loss[pi], y, ignore, g.c, cw) * go;
     if (w == 0.f) {
-      for (int c = 0; c < g.c; ++c) gp[c * TH * TW] = 0.f;
+      for (int c = 0; c < C; ++c) gp[c * TH * TW] = 0.f;
       continue;
     }
-    Taps<T> tp = make_taps(x, g, n, oy, ox);
+    const float *pa, *pb; float lx;
+    pixel_taps(g, t, rows, r, ox, pa, pb, lx);
     const float lse = pix_lse[pi];
-    for (int c = 0; c < g.c; ++c) {
-      float z = tp.at(c);
+    for (int c = 0; c < C; ++c) {
+      const float z = (1.f - lx) * pa[c] + lx * pb[c];
       gp[c * TH * TW] = w * (__expf(z - lse) - (c == y ? 1.f : 0.f));
     }
   }
   __syncthreads();
-  // 2) row pass: R[c][r][j] = sum_ox wx(ox, bx0+j) * G[c][r][ox]
-  for (int e = threadIdx.x; e < g.c * TH * BW; e += blockDim.x) {
-    int j = e % BW;
-    int r_ = (e / BW) % TH;
-    int c = e / (BW * TH);
-    int ix = bx0 + j;
+  // row pass: R[c][r][j] = sum_ox wx(ox, bx0+j) * G[c][r][ox]
+  const int BW = t.BW, BH = t.BH;
+  for (int e = threadIdx.x; e < C * TH * BW; e += blockDim.x) {
+    const int j = e % BW;
+    const int r = (e / BW) % TH;
+    const int c = e / (BW * TH);
+    const int ix = t.bx0 + j;
     int lo, hi;
     g.mw.out_range(ix, g.ow, lo, hi);
-    lo = max(lo, ox0); hi = min(hi, ox1);
+    lo = max(lo, t.ox0); hi = min(hi, t.ox1);
+    const float* row = Gt + (c * TH + r) * TW - t.ox0;
     float s = 0.f;
-    const float* row = Gt + (c * TH + r_) * TW - ox0;
     for (int ox = lo; ox <= hi; ++ox) {
-      float w = g.mw.weight(ox, ix);
-      if (w != 0.f) s += w * row[ox];
+      const float wx = g.mw.weight(ox, ix);
+      if (wx != 0.f) s += wx * row[ox];
     }
-    R[(c * TH + r_) * bw_max + j] = s;
+    R[(c * TH + r) * BW + j] = s;
   }
   __syncthreads();
-  // 3) column pass + global accumulate
-  for (int e = threadIdx.x; e < g.c * BH * BW; e += blockDim.x) {
-    int j = e % BW;
-    int i = (e / BW) % BH;
-    int c = e / (BW * BH);
-    int iy = by0 + i;
+  // column pass + global accumulate (neighbouring tiles share border cells)
+  for (int e = threadIdx.x; e < C * BH * BW; e += blockDim.x) {
+    const int j = e % BW;
+    const int i = (e / BW) % BH;
+    const int c = e / (BW * BH);
+    const int iy = t.by0 + i;
     int lo, hi;
     g.mh.out_range(iy, g.oh, lo, hi);
-    lo = max(lo, oy0); hi = min(hi, oy1);
+    lo = max(lo, t.oy0); hi = min(hi, t.oy1);
     float s = 0.f;
     for (int oy = lo; oy <= hi; ++oy) {
-      float w = g.mh.weight(oy, iy);
-      if (w != 0.f) s += w * R[(c * TH + (oy - oy0)) * bw_max + j];
+      const float wy = g.mh.weight(oy, iy);
+      if (wy != 0.f) s += wy * R[(c * TH + (oy - t.oy0)) * BW + j];
     }
     if (s != 0.f)
-      atomicAdd(gacc + ((static_cast<int64_t>(n) * g.c + c) * g.h + iy) * g.w + (bx0 + j), s);
+      atomicAdd(gacc + ((static_cast<int64_t>(t.n) * C + c) * g.h + iy) * g.w + (t.bx0 + j), s);
   }
 }
 
@@ -437,19 +485,58 @@ static LossGeo make_geo(const SegLossArgs& a) {
   return g;
 }
 
+// Tile shape: wide tiles for the usual <= 32 classes, smaller ones otherwise
+// so the staged logits / gradient tile stay within LDS.
+static bool big_tile(const LossGeo& g) { return g.c <= 32; }
+
+template <int TH, int TW>
+static int tiles_of(const LossGeo& g) {
+  return ((g.oh + TH - 1) / TH) * ((g.ow + TW - 1) / TW) * g.n;
+}
+
+template <int TH, int TW>
+static size_t stage_floats(const LossGeo& g) {
+  const int bh = static_cast<int>((TH - 1) * g.mh.scale) + 3;
+  const int bw = static_cast<int>((TW - 1) * g.mw.scale) + 3;
+  const int cp = g.c | 1;
+  return static_cast<size_t>(bh) * bw * cp + static_cast<size_t>(TH) * bw * cp;
+}
+
+template <typename K>
+static void allow_lds(K kernel, size_t bytes) {
+  if (bytes > 64 * 1024)
+    hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes));
+}
+
+int seg_loss_fwd_blocks(const SegLossArgs& a) {
+  LossGeo g = make_geo(a);
+  return big_tile(g) ? tiles_of<8, 64>(g) : tiles_of<4, 32>(g);
+}
+
+template <typename T, int TH, int TW>
+static void fwd_tile(const SegLossArgs& a, const LossGeo& g, hipStream_t st) {
+  const size_t lds = sizeof(float) * stage_floats<TH, TW>(g);
+  auto k = seg_ce_fwd_tile<T, TH, TW>;
+  allow_lds(k, lds);
+  const int nblk = tiles_of<TH, TW>(g);
+  k<<<nblk, 256, lds, st>>>(static_cast<const T*>(a.logits.data), g, a.labels, a.ignore_index,
+                            a.class_weight, a.ohem_thresh, a.pix_loss, a.pix_lse, a.slab);
+  seg_finalize1<<<1, 1024, 0, st>>>(a.slab, nblk, a.stats, a.mode, a.ohem_thresh, a.out_loss);
+}
+
 template <typename T>
 static void fwd_t(const SegLossArgs& a, const LossGeo& g, hipStream_t st) {
   const int64_t total = static_cast<int64_t>(g.n) * g.oh * g.ow;
-  hipMemsetAsync(a.stats, 0, sizeof(double) * S_NSTATS, st);
-  seg_ce_fwd_kernel<T><<<stream_grid(total, 256), 256, 0, st>>>(
-      static_cast<const T*>(a.logits.data), g, a.labels, a.ignore_index, a.class_weight,
-      a.ohem_thresh, a.pix_loss, a.pix_lse, a.stats);
-  seg_finalize1<<<1, 64, 0, st>>>(a.stats, a.mode, a.ohem_thresh, a.out_loss);
+  if (big_tile(g)) fwd_tile<T, 8, 64>(a, g, st);
+  else fwd_tile<T, 4, 32>(a, g, st);
   if (a.mode != MODE_OHEM) return;
+  // top-k fallback (every kernel exits at once when the threshold branch was taken)
   hipMemsetAsync(a.hist, 0, sizeof(unsigned) * 3 * 2048, st);
   const int shifts[3] = {21, 10, 0};
   const int bits[3] = {11, 11, 10};
-  const int grid = stream_grid(total, 256);
+  int grid = static_cast<int>((total + 4095) / 4096);
+  grid = grid < 1 ? 1 : (grid > 512 ? 512 : grid);
   for (int p = 0; p < 3; ++p) {
     radix_hist_kernel<<<grid, 256, 0, st>>>(a.pix_loss, total, a.stats, a.hist + p * 2048,
                                             shifts[p], bits[p], p);
@@ -468,6 +555,19 @@ void launch_seg_loss_fwd(const SegLossArgs& a, hipStream_t st) {
   }
 }
 
+template <typename T, int TH, int TW>
+static void bwd_tile(const SegLossArgs& a, const LossGeo& g, const float* grad_out,
+                     hipStream_t st) {
+  const int bw = static_cast<int>((TW - 1) * g.mw.scale) + 3;
+  const size_t lds = sizeof(float) * (stage_floats<TH, TW>(g) + static_cast<size_t>(g.c) * TH * TW +
+                                      static_cast<size_t>(g.c) * TH * bw);
+  auto k = seg_ce_bwd_tile<T, TH, TW>;
+  allow_lds(k, lds);
+  k<<<tiles_of<TH, TW>(g), 256, lds, st>>>(
+      static_cast<const T*>(a.logits.data), g, a.labels, a.ignore_index, a.class_weight,
+      a.pix_loss, a.pix_lse, a.stats, a.mode, grad_out, a.acc);
+}
+
 template <typename T, typename G>
 static void bwd_t(const SegLossArgs& a, const LossGeo& g, const float* grad_out,
                   const Tensor4& gl, hipStream_t st) {
@@ -479,20 +579,12 @@ static void bwd_t(const SegLossArgs& a, const LossGeo& g, const float* grad_out,
         grad_out, static_cast<G*>(gl.data), gl.sn, gl.sc, gl.sh, gl.sw);
     return;
   }
-  float* acc = a.acc;
   const int64_t nacc = static_cast<int64_t>(g.n) * g.c * g.h * g.w;
-  hipMemsetAsync(acc, 0, sizeof(float) * nacc, st);
-  constexpr int TH = 8, TW = 64;
-  const int bw_max = static_cast<int>(TW * g.mw.scale) + 4;
-  const int bh_max = static_cast<int>(TH * g.mh.scale) + 4;
-  const size_t lds = sizeof(float) * (static_cast<size_t>(g.c) * TH * TW +
-                                      static_cast<size_t>(g.c) * TH * bw_max);
-  const int tiles = ((g.oh + TH - 1) / TH) * ((g.ow + TW - 1) / TW) * g.n;
-  seg_ce_bwd_upsample<T, TH, TW, 32><<<tiles, 256, lds, st>>>(
-      x, g, a.labels, a.ignore_index, a.class_weight, a.pix_loss, a.pix_lse, a.stats, a.mode,
-      grad_out, acc, bw_max, bh_max);
+  hipMemsetAsync(a.acc, 0, sizeof(float) * nacc, st);
+  if (big_tile(g)) bwd_tile<T, 8, 64>(a, g, grad_out, st);
+  else bwd_tile<T, 4, 32>(a, g, grad_out, st);
   cast_out_kernel<G><<<stream_grid(nacc, 256), 256, 0, st>>>(
-      acc, g.n, g.c, g.h, g.w, static_cast<G*>(gl.data), gl.sn, gl.sc, gl.sh, gl.sw);
+      a.acc, g.n, g.c, g.h, g.w, static_cast<G*>(gl.data), gl.sn, gl.sc, gl.sh, gl.sw);
 }
 
 void launch_seg_loss_bwd(const SegLossArgs& a, const float* grad_out, const Tensor4& gl,

@@ -57,14 +57,18 @@ class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, bn, act, use_batch_stats, pg):
         if use_batch_stats:
-            sums = ops().bn_stats(x)
-            if pg is not None:
-                dist.all_reduce(sums, group=pg)
             track = bn.track_running_stats and bn.training and bn.running_mean is not None
-            mi, ss = ops().bn_finalize(
-                sums, weight, bias, bn.running_mean if track else None,
-                bn.running_var if track else None, bn.num_batches_tracked if track else None,
-                float(bn.momentum), float(bn.eps))
+            rm = bn.running_mean if track else None
+            rv = bn.running_var if track else None
+            nb = bn.num_batches_tracked if track else None
+            if pg is None:
+                mi, ss, sums = ops().bn_stats_finalize(x, weight, bias, rm, rv, nb,
+                                                       float(bn.momentum), float(bn.eps))
+            else:  # SyncBN: one all-reduce of (sum, sumsq, count) in fp64 over RCCL
+                sums = ops().bn_stats_sums(x)
+                dist.all_reduce(sums, group=pg)
+                mi, ss = ops().bn_finalize(sums, weight, bias, rm, rv, nb, float(bn.momentum),
+                                           float(bn.eps))
         else:
             sums = None
             mi, ss = ops().bn_eval_coeffs(weight, bias, bn.running_mean, bn.running_var, float(bn.eps))
@@ -86,13 +90,14 @@ class _BNActFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, y, mi, ss, sums, weight = ctx.saved_tensors
         dy = dy.contiguous(memory_format=torch.channels_last) if dy.dim() == 4 else dy.contiguous()
-        bsums = ops().bn_bwd_reduce(dy, x, y, mi, ss, ctx.act, ctx.mask)
+        bsums = None
         if ctx.pg is not None:
+            bsums = ops().bn_bwd_sums(dy, x, y, mi, ss, ctx.act, ctx.mask)
             dist.all_reduce(bsums, group=ctx.pg)
         want_dres = ctx.has_res and ctx.needs_input_grad[3]
         want_dw = ctx.has_w and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
-        dx, dres, dw, db = ops().bn_bwd_apply(dy, x, y, bsums, sums, mi, ss, weight, ctx.act,
-                                              ctx.mask, want_dres, ctx.batch_stats, want_dw)
+        dx, dres, dw, db = ops().bn_backward(dy, x, y, bsums, sums, mi, ss, weight, ctx.act,
+                                             ctx.mask, want_dres, ctx.batch_stats, want_dw)
         return (dx, dw if want_dw else None, db if want_dw else None,
                 dres if want_dres else None, None, None, None, None)
 
