@@ -66,17 +66,22 @@ class SegTrainer(BaseTrainer):
         cfg = self.config
         extras = {}
         defer = bool(getattr(cfg, "fused_loss", True)) and not cfg.use_detail_head
+        # uint8 label maps: the fused loss kernels read them ~4x per step (main/aux x fwd/bwd)
+        labels = masks
+        if (masks.is_cuda and masks.dtype == torch.int64 and cfg.num_class <= 255
+                and 0 <= cfg.ignore_index <= 255):
+            labels = masks.to(torch.uint8)
         with self._autocast(), ops.defer_final_upsample(defer):
             if cfg.use_aux:
                 preds, preds_aux = self.model(images, is_training=True)
-                loss = self.loss_fn(preds, masks)
+                loss = self.loss_fn(preds, labels)
                 if cfg.aux_coef is None:
                     cfg.aux_coef = [1.0] * len(preds_aux)
                 coefs = cfg.aux_coef if isinstance(cfg.aux_coef, (list, tuple)) else [cfg.aux_coef]
                 if len(coefs) != len(preds_aux):
                     raise ValueError("Auxiliary loss coefficient length does not match.")
                 for coef, aux in zip(coefs, preds_aux):
-                    loss = loss + float(coef) * self.loss_fn.aux(aux, masks)
+                    loss = loss + float(coef) * self.loss_fn.aux(aux, labels)
             elif cfg.use_detail_head:
                 detail_gt = self.laplacian_conv(masks.unsqueeze(1).float())
                 detail_gt = de_parallel(self.model).detail_conv(detail_gt)
@@ -85,11 +90,11 @@ class SegTrainer(BaseTrainer):
                 preds_detail = F.interpolate(preds_detail, detail_gt.shape[2:], mode="bilinear",
                                              align_corners=True)
                 loss_detail = self.detail_loss_fn(preds_detail.float(), detail_gt.float())
-                loss = self.loss_fn(preds, masks) + cfg.detail_loss_coef * loss_detail
+                loss = self.loss_fn(preds, labels) + cfg.detail_loss_coef * loss_detail
                 extras["loss_detail"] = loss_detail
             else:
                 preds = self.model(images)
-                loss = self.loss_fn(preds, masks)
+                loss = self.loss_fn(preds, labels)
             if cfg.kd_training:
                 with torch.no_grad(), ops.defer_final_upsample(False):
                     teacher_preds = self.teacher_model(images)

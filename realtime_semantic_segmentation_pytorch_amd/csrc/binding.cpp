@@ -92,12 +92,14 @@ static at::Tensor act_mask(const at::Tensor& g, const at::Tensor& y, int64_t act
 static SegLossArgs loss_args(const at::Tensor& logits, const at::Tensor& labels, int64_t out_h,
                              int64_t out_w, bool align, int64_t ignore,
                              const std::optional<at::Tensor>& cw, int64_t mode, double thresh) {
-  TORCH_CHECK(labels.dim() == 3 && labels.scalar_type() == at::kLong && labels.is_contiguous(),
-              "rtseg.seg_loss: labels must be contiguous int64 [N,H,W]");
+  TORCH_CHECK(labels.dim() == 3 && labels.is_contiguous() &&
+                  (labels.scalar_type() == at::kLong || labels.scalar_type() == at::kByte),
+              "rtseg.seg_loss: labels must be contiguous int64 or uint8 [N,H,W]");
   TORCH_CHECK(labels.size(0) == logits.size(0), "rtseg.seg_loss: batch mismatch");
   SegLossArgs a{};
   a.logits = view4(logits);
-  a.labels = labels.data_ptr<int64_t>();
+  a.labels = labels.data_ptr();
+  a.label_bytes = labels.scalar_type() == at::kByte ? 1 : 8;
   a.lh = static_cast<int>(labels.size(1));
   a.lw = static_cast<int>(labels.size(2));
   a.out_h = static_cast<int>(out_h);

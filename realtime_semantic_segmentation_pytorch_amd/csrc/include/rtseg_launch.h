@@ -28,7 +28,8 @@ void launch_act_mask(const void* g, const void* y, void* out, int64_t n, int dty
 // resized) labels, plus OHEM / mean selection entirely on device.
 struct SegLossArgs {
   Tensor4 logits;        // [N, C, h, w] (any strides)
-  const int64_t* labels; // [N, LH, LW] contiguous
+  const void* labels;    // [N, LH, LW] contiguous, int64 or uint8
+  int label_bytes;       // 8 or 1
   int lh, lw;
   int out_h, out_w;      // loss is evaluated on this grid (== label grid normally)
   bool align_corners;

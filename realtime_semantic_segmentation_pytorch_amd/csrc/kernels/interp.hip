@@ -50,6 +50,35 @@ __global__ void __launch_bounds__(256) interp_fwd_scalar(
   }
 }
 
+// Channels-last output with a channel count that is not a multiple of 8 (e.g.
+// 19-class logits): walk the output in NHWC order so stores stay coalesced.
+template <typename T, int ACT, bool SKIP>
+__global__ void __launch_bounds__(256) interp_fwd_cl_scalar(
+    const T* __restrict__ x, Shape4 xs, const T* __restrict__ skip, Shape4 ks,
+    T* __restrict__ y, Shape4 ys, LinMap mh, LinMap mw) {
+  const int64_t total = static_cast<int64_t>(ys.n) * ys.c * ys.h * ys.w;
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    int c = static_cast<int>(i % ys.c);
+    int64_t t = i / ys.c;
+    int ox = static_cast<int>(t % ys.w);
+    t /= ys.w;
+    int oy = static_cast<int>(t % ys.h);
+    int n = static_cast<int>(t / ys.h);
+    int y0, y1, x0, x1; float ly, lx;
+    mh.map(oy, y0, y1, ly);
+    mw.map(ox, x0, x1, lx);
+    const T* b = x + n * xs.sn + c * xs.sc;
+    float v00 = Io<T>::ld(b + y0 * xs.sh + x0 * xs.sw);
+    float v01 = Io<T>::ld(b + y0 * xs.sh + x1 * xs.sw);
+    float v10 = Io<T>::ld(b + y1 * xs.sh + x0 * xs.sw);
+    float v11 = Io<T>::ld(b + y1 * xs.sh + x1 * xs.sw);
+    float v = (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11);
+    if constexpr (SKIP) v += Io<T>::ld(skip + off4(ks, n, c, oy, ox));
+    Io<T>::st(y + off4(ys, n, c, oy, ox), act_fwd<ACT>(v));
+  }
+}
+
 typedef short short8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ void unpack8(const short8& v, float* f) {
@@ -209,6 +238,11 @@ static void fwd_dispatch(const Tensor4& x, const Tensor4* skip, const Tensor4& y
     }
   }
   int64_t work = static_cast<int64_t>(y.n) * y.c * y.h * y.w;
+  if (y.sc == 1 && y.c > 1) {
+    interp_fwd_cl_scalar<T, ACT, SKIP><<<stream_grid(work, 256), 256, 0, st>>>(
+        static_cast<const T*>(x.data), xs, kp, ks, static_cast<T*>(y.data), ys, mh, mw);
+    return;
+  }
   interp_fwd_scalar<T, ACT, SKIP><<<stream_grid(work, 256), 256, 0, st>>>(
       static_cast<const T*>(x.data), xs, kp, ks, static_cast<T*>(y.data), ys, mh, mw);
 }

@@ -43,13 +43,15 @@ struct LossGeo {
   int lh, lw, oh, ow;
   LinMap mh, mw;
   float lab_sy, lab_sx;  // nearest label remap scales (label = floor(o * s))
+  const int64_t* lab64;  // labels: int64 (torch.long) ...
+  const uint8_t* lab8;   // ... or uint8 (8x less label traffic); exactly one is set
 };
 
-__device__ __forceinline__ int64_t label_at(const int64_t* __restrict__ labels, const LossGeo& g,
-                                            int n, int oy, int ox) {
+__device__ __forceinline__ int64_t label_at(const LossGeo& g, int n, int oy, int ox) {
   int ly = (g.lh == g.oh) ? oy : min(static_cast<int>(floorf(oy * g.lab_sy)), g.lh - 1);
   int lx = (g.lw == g.ow) ? ox : min(static_cast<int>(floorf(ox * g.lab_sx)), g.lw - 1);
-  return labels[(static_cast<int64_t>(n) * g.lh + ly) * g.lw + lx];
+  const int64_t i = (static_cast<int64_t>(n) * g.lh + ly) * g.lw + lx;
+  return g.lab8 ? static_cast<int64_t>(g.lab8[i]) : g.lab64[i];
 }
 
 // ------------------------------- tiles -------------------------------------
@@ -128,9 +130,43 @@ __device__ __forceinline__ void pixel_taps(const LossGeo& g, const TileGeo& t, c
 // ------------------------------- forward -----------------------------------
 enum : int { SL_VALID = 0, SL_HCNT, SL_HSUM, SL_WLOSS, SL_WSUM, SL_N };
 
-template <typename T, int TH, int TW>
+// Log-sum-exp of the interpolated logits of one pixel. NC > 0: class count known
+// at compile time -> logits held in registers, max then sum (no divergence);
+// NC == 0: runtime class count, online (single pass) formulation.
+template <int NC>
+__device__ __forceinline__ float pixel_lse(const float* pa, const float* pb, float lx, int C,
+                                           int64_t y, float& zy) {
+  if constexpr (NC > 0) {
+    float z[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) z[c] = pa[c] + lx * (pb[c] - pa[c]);
+    float m = z[0];
+#pragma unroll
+    for (int c = 1; c < NC; ++c) m = fmaxf(m, z[c]);
+    float s = 0.f;
+    zy = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      s += __expf(z[c] - m);
+      zy = (c == y) ? z[c] : zy;
+    }
+    return m + __logf(s);
+  } else {
+    float m = -INFINITY, s = 0.f;
+    zy = 0.f;
+    for (int c = 0; c < C; ++c) {
+      const float z = pa[c] + lx * (pb[c] - pa[c]);
+      if (c == y) zy = z;
+      if (z > m) { s = s * __expf(m - z) + 1.f; m = z; }
+      else s += __expf(z - m);
+    }
+    return m + __logf(s);
+  }
+}
+
+template <typename T, int TH, int TW, int NC>
 __global__ void __launch_bounds__(256) seg_ce_fwd_tile(
-    const T* __restrict__ x, LossGeo g, const int64_t* __restrict__ labels, int ignore,
+    const T* __restrict__ x, LossGeo g, int ignore,
     const float* __restrict__ cw, float thresh, float* __restrict__ pix_loss,
     float* __restrict__ pix_lse, double* __restrict__ slab) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -145,15 +181,9 @@ __global__ void __launch_bounds__(256) seg_ce_fwd_tile(
     if (oy > t.oy1 || ox > t.ox1) continue;
     const float *pa, *pb; float lx;
     pixel_taps(g, t, rows, r, ox, pa, pb, lx);
-    const int64_t y = label_at(labels, g, t.n, oy, ox);
-    float m = -INFINITY, s = 0.f, zy = 0.f;
-    for (int c = 0; c < g.c; ++c) {
-      const float z = (1.f - lx) * pa[c] + lx * pb[c];
-      if (c == y) zy = z;
-      if (z > m) { s = s * __expf(m - z) + 1.f; m = z; }
-      else s += __expf(z - m);
-    }
-    const float lse = m + __logf(s);
+    const int64_t y = label_at(g, t.n, oy, ox);
+    float zy;
+    const float lse = pixel_lse<NC>(pa, pb, lx, g.c, y, zy);
     float l = 0.f;
     if (y != ignore && y >= 0 && y < g.c) {
       l = fmaxf(lse - zy, 0.f);
@@ -341,7 +371,7 @@ __device__ __forceinline__ float pixel_weight(const SelRule& r, float l, int64_t
 // Identity geometry (loss grid == logit grid): gradient written per pixel.
 template <typename T, typename G>
 __global__ void __launch_bounds__(256) seg_ce_bwd_identity(
-    const T* __restrict__ x, LossGeo g, const int64_t* __restrict__ labels, int ignore,
+    const T* __restrict__ x, LossGeo g, int ignore,
     const float* __restrict__ cw, const float* __restrict__ pix_loss,
     const float* __restrict__ pix_lse, const double* __restrict__ stats, int mode,
     const float* __restrict__ grad_out, G* __restrict__ gx, int64_t gsn, int64_t gsc,
@@ -355,7 +385,7 @@ __global__ void __launch_bounds__(256) seg_ce_bwd_identity(
     int64_t t = i / g.ow;
     int oy = static_cast<int>(t % g.oh);
     int n = static_cast<int>(t / g.oh);
-    int64_t y = label_at(labels, g, n, oy, ox);
+    int64_t y = label_at(g, n, oy, ox);
     float w = pixel_weight(r, pix_loss[i], y, ignore, g.c, cw) * go;
     G* o = gx + n * gsn + oy * gsh + ox * gsw;
     if (w == 0.f) {
@@ -373,83 +403,114 @@ __global__ void __launch_bounds__(256) seg_ce_bwd_identity(
 }
 
 // Upsampled geometry: stage logits (as in the forward), per-pixel softmax
-// gradient tile G[C][TH][TW] in LDS, transpose of the bilinear map as a row
-// pass then a column pass, fp32 atomics only for the tile's bounding box cells.
-template <typename T, int TH, int TW>
+// gradient tile G[C][TH][TW] in LDS, then the transpose of the bilinear map:
+// a row scan per (class, row) and a column scan per (class, low-res column),
+// both driven by per-tile tap tables (taps are monotone in the output index,
+// so each scan carries just two running sums).  fp32 atomics only for the
+// tile's bounding-box cells (shared with neighbouring tiles).
+template <typename T, int TH, int TW, int NC>
 __global__ void __launch_bounds__(256) seg_ce_bwd_tile(
-    const T* __restrict__ x, LossGeo g, const int64_t* __restrict__ labels, int ignore,
+    const T* __restrict__ x, LossGeo g, int ignore,
     const float* __restrict__ cw, const float* __restrict__ pix_loss,
     const float* __restrict__ pix_lse, const double* __restrict__ stats, int mode,
     const float* __restrict__ grad_out, float* __restrict__ gacc) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
+  __shared__ int tj0[TW], tj1[TW], ti0[TH], ti1[TH];
+  __shared__ float tlx[TW], tly[TH];
   const TileGeo t = tile_geo<TH, TW>(g);
-  const int C = g.c;
+  const int C = NC > 0 ? NC : g.c;
   float* L = sm;
   float* V = L + t.BH * t.BW * t.CP;
-  float* Gt = V + TH * t.BW * t.CP;   // [C][TH][TW]
-  float* R = Gt + C * TH * TW;         // [C][TH][BW]
-  const float* rows = stage_logits<T, TH>(x, g, t, L, V);
+  constexpr int GR = TW + 1;           // padded G row: conflict-free row scans
+  constexpr int GS = TH * GR;          // G class stride
+  const int BW = t.BW;
+  const int RS = BW | 1;               // padded R row
+  float* Gt = V + TH * t.BW * t.CP;    // [C][TH][TW + 1]
+  float* R = Gt + C * GS;              // [C][TH][RS]
+  for (int k = threadIdx.x; k < TW; k += blockDim.x) {
+    int a0, a1; float l;
+    g.mw.map(min(t.ox0 + k, t.ox1), a0, a1, l);
+    tj0[k] = a0 - t.bx0; tj1[k] = a1 - t.bx0; tlx[k] = l;
+  }
+  for (int k = threadIdx.x; k < TH; k += blockDim.x) {
+    int a0, a1; float l;
+    g.mh.map(min(t.oy0 + k, t.oy1), a0, a1, l);
+    ti0[k] = a0 - t.by0; ti1[k] = a1 - t.by0; tly[k] = l;
+  }
+  for (int e = threadIdx.x; e < C * TH * RS; e += blockDim.x) R[e] = 0.f;
+  const float* rows = stage_logits<T, TH>(x, g, t, L, V);  // has __syncthreads
   const SelRule rule = load_rule(stats, mode);
   const float go = *grad_out;
   for (int p = threadIdx.x; p < TH * TW; p += blockDim.x) {
     const int r = p / TW, oy = t.oy0 + r, ox = t.ox0 + p % TW;
-    float* gp = Gt + p;
+    float* gp = Gt + r * GR + p % TW;
     float w = 0.f;
     int64_t y = -1;
     int64_t pi = 0;
     if (oy <= t.oy1 && ox <= t.ox1) {
       pi = (static_cast<int64_t>(t.n) * g.oh + oy) * g.ow + ox;
-      y = label_at(labels, g, t.n, oy, ox);
+      y = label_at(g, t.n, oy, ox);
       w = pixel_weight(rule, pix_loss[pi], y, ignore, C, cw) * go;
     }
     if (w == 0.f) {
-      for (int c = 0; c < C; ++c) gp[c * TH * TW] = 0.f;
+      for (int c = 0; c < C; ++c) gp[c * GS] = 0.f;
       continue;
     }
     const float *pa, *pb; float lx;
     pixel_taps(g, t, rows, r, ox, pa, pb, lx);
     const float lse = pix_lse[pi];
-    for (int c = 0; c < C; ++c) {
-      const float z = (1.f - lx) * pa[c] + lx * pb[c];
-      gp[c * TH * TW] = w * (__expf(z - lse) - (c == y ? 1.f : 0.f));
+    if constexpr (NC > 0) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const float z = pa[c] + lx * (pb[c] - pa[c]);
+        gp[c * GS] = w * (__expf(z - lse) - (c == y ? 1.f : 0.f));
+      }
+    } else {
+      for (int c = 0; c < C; ++c) {
+        const float z = pa[c] + lx * (pb[c] - pa[c]);
+        gp[c * GS] = w * (__expf(z - lse) - (c == y ? 1.f : 0.f));
+      }
     }
   }
   __syncthreads();
-  // row pass: R[c][r][j] = sum_ox wx(ox, bx0+j) * G[c][r][ox]
-  const int BW = t.BW, BH = t.BH;
-  for (int e = threadIdx.x; e < C * TH * BW; e += blockDim.x) {
-    const int j = e % BW;
-    const int r = (e / BW) % TH;
-    const int c = e / (BW * TH);
-    const int ix = t.bx0 + j;
-    int lo, hi;
-    g.mw.out_range(ix, g.ow, lo, hi);
-    lo = max(lo, t.ox0); hi = min(hi, t.ox1);
-    const float* row = Gt + (c * TH + r) * TW - t.ox0;
-    float s = 0.f;
-    for (int ox = lo; ox <= hi; ++ox) {
-      const float wx = g.mw.weight(ox, ix);
-      if (wx != 0.f) s += wx * row[ox];
+  const int nx = t.ox1 - t.ox0 + 1, ny = t.oy1 - t.oy0 + 1;
+  // row scan: R[c][r][j] = sum_k wx(k, j) * G[c][r][k]
+  for (int cr = threadIdx.x; cr < C * TH; cr += blockDim.x) {
+    const int c = cr / TH, r = cr % TH;
+    if (r >= ny) continue;
+    float* Rr = R + (c * TH + r) * RS;
+    const float* gr = Gt + c * GS + r * GR;
+    int jc = tj0[0];
+    float a = 0.f, b = 0.f;  // running sums for columns jc and jc + 1
+    for (int k = 0; k < nx; ++k) {
+      const int j0 = tj0[k];
+      while (jc < j0) { Rr[jc] += a; a = b; b = 0.f; ++jc; }
+      const float v = gr[k];
+      if (tj1[k] == j0) a += v;
+      else { const float l = tlx[k]; a += (1.f - l) * v; b += l * v; }
     }
-    R[(c * TH + r) * BW + j] = s;
+    Rr[jc] += a;
+    if (jc + 1 < BW) Rr[jc + 1] += b;
   }
   __syncthreads();
-  // column pass + global accumulate (neighbouring tiles share border cells)
-  for (int e = threadIdx.x; e < C * BH * BW; e += blockDim.x) {
-    const int j = e % BW;
-    const int i = (e / BW) % BH;
-    const int c = e / (BW * BH);
-    const int iy = t.by0 + i;
-    int lo, hi;
-    g.mh.out_range(iy, g.oh, lo, hi);
-    lo = max(lo, t.oy0); hi = min(hi, t.oy1);
-    float s = 0.f;
-    for (int oy = lo; oy <= hi; ++oy) {
-      const float wy = g.mh.weight(oy, iy);
-      if (wy != 0.f) s += wy * R[(c * TH + (oy - t.oy0)) * BW + j];
+  // column scan + global accumulate
+  for (int cj = threadIdx.x; cj < C * BW; cj += blockDim.x) {
+    const int c = cj / BW, j = cj % BW;
+    float* dst = gacc + ((static_cast<int64_t>(t.n) * C + c) * g.h + t.by0) * g.w + (t.bx0 + j);
+    int ic = ti0[0];
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < ny; ++r) {
+      const int i0 = ti0[r];
+      while (ic < i0) {
+        if (a != 0.f) atomicAdd(dst + static_cast<int64_t>(ic) * g.w, a);
+        a = b; b = 0.f; ++ic;
+      }
+      const float v = R[(c * TH + r) * RS + j];
+      if (ti1[r] == i0) a += v;
+      else { const float l = tly[r]; a += (1.f - l) * v; b += l * v; }
     }
-    if (s != 0.f)
-      atomicAdd(gacc + ((static_cast<int64_t>(t.n) * C + c) * g.h + iy) * g.w + (t.bx0 + j), s);
+    if (a != 0.f) atomicAdd(dst + static_cast<int64_t>(ic) * g.w, a);
+    if (b != 0.f && ic + 1 < t.BH) atomicAdd(dst + static_cast<int64_t>(ic + 1) * g.w, b);
   }
 }
 
@@ -482,6 +543,8 @@ static LossGeo make_geo(const SegLossArgs& a) {
   g.mw = LinMap::make(g.w, g.ow, a.align_corners);
   g.lab_sy = static_cast<float>(a.lh) / static_cast<float>(a.out_h);
   g.lab_sx = static_cast<float>(a.lw) / static_cast<float>(a.out_w);
+  g.lab64 = a.label_bytes == 1 ? nullptr : static_cast<const int64_t*>(a.labels);
+  g.lab8 = a.label_bytes == 1 ? static_cast<const uint8_t*>(a.labels) : nullptr;
   return g;
 }
 
@@ -511,16 +574,16 @@ static void allow_lds(K kernel, size_t bytes) {
 
 int seg_loss_fwd_blocks(const SegLossArgs& a) {
   LossGeo g = make_geo(a);
-  return big_tile(g) ? tiles_of<8, 64>(g) : tiles_of<4, 32>(g);
+  return big_tile(g) ? tiles_of<16, 64>(g) : tiles_of<4, 32>(g);
 }
 
-template <typename T, int TH, int TW>
+template <typename T, int TH, int TW, int NC>
 static void fwd_tile(const SegLossArgs& a, const LossGeo& g, hipStream_t st) {
   const size_t lds = sizeof(float) * stage_floats<TH, TW>(g);
-  auto k = seg_ce_fwd_tile<T, TH, TW>;
+  auto k = seg_ce_fwd_tile<T, TH, TW, NC>;
   allow_lds(k, lds);
   const int nblk = tiles_of<TH, TW>(g);
-  k<<<nblk, 256, lds, st>>>(static_cast<const T*>(a.logits.data), g, a.labels, a.ignore_index,
+  k<<<nblk, 256, lds, st>>>(static_cast<const T*>(a.logits.data), g, a.ignore_index,
                             a.class_weight, a.ohem_thresh, a.pix_loss, a.pix_lse, a.slab);
   seg_finalize1<<<1, 1024, 0, st>>>(a.slab, nblk, a.stats, a.mode, a.ohem_thresh, a.out_loss);
 }
@@ -528,8 +591,9 @@ static void fwd_tile(const SegLossArgs& a, const LossGeo& g, hipStream_t st) {
 template <typename T>
 static void fwd_t(const SegLossArgs& a, const LossGeo& g, hipStream_t st) {
   const int64_t total = static_cast<int64_t>(g.n) * g.oh * g.ow;
-  if (big_tile(g)) fwd_tile<T, 8, 64>(a, g, st);
-  else fwd_tile<T, 4, 32>(a, g, st);
+  if (g.c == 19) fwd_tile<T, 16, 64, 19>(a, g, st);  // Cityscapes: classes in registers
+  else if (big_tile(g)) fwd_tile<T, 16, 64, 0>(a, g, st);
+  else fwd_tile<T, 4, 32, 0>(a, g, st);
   if (a.mode != MODE_OHEM) return;
   // top-k fallback (every kernel exits at once when the threshold branch was taken)
   hipMemsetAsync(a.hist, 0, sizeof(unsigned) * 3 * 2048, st);
@@ -555,16 +619,16 @@ void launch_seg_loss_fwd(const SegLossArgs& a, hipStream_t st) {
   }
 }
 
-template <typename T, int TH, int TW>
+template <typename T, int TH, int TW, int NC>
 static void bwd_tile(const SegLossArgs& a, const LossGeo& g, const float* grad_out,
                      hipStream_t st) {
   const int bw = static_cast<int>((TW - 1) * g.mw.scale) + 3;
-  const size_t lds = sizeof(float) * (stage_floats<TH, TW>(g) + static_cast<size_t>(g.c) * TH * TW +
-                                      static_cast<size_t>(g.c) * TH * bw);
-  auto k = seg_ce_bwd_tile<T, TH, TW>;
+  const size_t lds = sizeof(float) * (stage_floats<TH, TW>(g) + static_cast<size_t>(g.c) * TH * (TW + 1) +
+                                      static_cast<size_t>(g.c) * TH * (bw | 1));
+  auto k = seg_ce_bwd_tile<T, TH, TW, NC>;
   allow_lds(k, lds);
   k<<<tiles_of<TH, TW>(g), 256, lds, st>>>(
-      static_cast<const T*>(a.logits.data), g, a.labels, a.ignore_index, a.class_weight,
+      static_cast<const T*>(a.logits.data), g, a.ignore_index, a.class_weight,
       a.pix_loss, a.pix_lse, a.stats, a.mode, grad_out, a.acc);
 }
 
@@ -575,14 +639,15 @@ static void bwd_t(const SegLossArgs& a, const LossGeo& g, const float* grad_out,
   if (g.oh == g.h && g.ow == g.w) {
     const int64_t total = static_cast<int64_t>(g.n) * g.oh * g.ow;
     seg_ce_bwd_identity<T, G><<<stream_grid(total, 256), 256, 0, st>>>(
-        x, g, a.labels, a.ignore_index, a.class_weight, a.pix_loss, a.pix_lse, a.stats, a.mode,
+        x, g, a.ignore_index, a.class_weight, a.pix_loss, a.pix_lse, a.stats, a.mode,
         grad_out, static_cast<G*>(gl.data), gl.sn, gl.sc, gl.sh, gl.sw);
     return;
   }
   const int64_t nacc = static_cast<int64_t>(g.n) * g.c * g.h * g.w;
   hipMemsetAsync(a.acc, 0, sizeof(float) * nacc, st);
-  if (big_tile(g)) bwd_tile<T, 8, 64>(a, g, grad_out, st);
-  else bwd_tile<T, 4, 32>(a, g, grad_out, st);
+  if (g.c == 19) bwd_tile<T, 8, 64, 19>(a, g, grad_out, st);
+  else if (big_tile(g)) bwd_tile<T, 8, 64, 0>(a, g, grad_out, st);
+  else bwd_tile<T, 4, 32, 0>(a, g, grad_out, st);
   cast_out_kernel<G><<<stream_grid(nacc, 256), 256, 0, st>>>(
       a.acc, g.n, g.c, g.h, g.w, static_cast<G*>(gl.data), gl.sn, gl.sc, gl.sh, gl.sw);
 }

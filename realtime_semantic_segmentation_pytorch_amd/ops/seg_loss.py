@@ -50,13 +50,12 @@ def _resize_labels_nearest(labels: torch.Tensor, size) -> torch.Tensor:
 def _fused_ok(logits: torch.Tensor, out_hw) -> bool:
     c = logits.shape[1]
     h, w = logits.shape[2], logits.shape[3]
+    if c > 256:
+        return False
     if (h, w) == tuple(out_hw):
         return True
-    # upsample path keeps the class tile in LDS (see seg_loss.hip): C * 8 * (64 + bw) * 4 B
-    if h > out_hw[0] or w > out_hw[1]:
-        return False
-    bw = int(64 * (w - 1) / max(out_hw[1] - 1, 1)) + 4
-    return c * 8 * (64 + bw) * 4 <= 64 * 1024
+    # upsample only: the backward keeps a [C, TH, TW] gradient tile in LDS (seg_loss.hip)
+    return h <= out_hw[0] and w <= out_hw[1]
 
 
 def seg_cross_entropy(logits: torch.Tensor, labels: torch.Tensor, *, mode: int = MODE_OHEM,
@@ -73,7 +72,8 @@ def seg_cross_entropy(logits: torch.Tensor, labels: torch.Tensor, *, mode: int =
     """
     if labels.dim() == 4:
         labels = labels.squeeze(1)
-    labels = labels.long()
+    if labels.dtype not in (torch.int64, torch.uint8):
+        labels = labels.long()
     if out_size is None:
         out_size = tuple(labels.shape[-2:]) if resize_logits else tuple(logits.shape[-2:])
     out_size = (int(out_size[0]), int(out_size[1]))
@@ -89,7 +89,7 @@ def seg_cross_entropy(logits: torch.Tensor, labels: torch.Tensor, *, mode: int =
         cw = class_weight.float().contiguous() if class_weight is not None else None
         return _SegLossFn.apply(logits, labels.contiguous(), out_size[0], out_size[1],
                                 bool(align_corners), int(ignore_index), cw, int(mode), thresh)
-    return seg_cross_entropy_reference(logits, labels, mode=mode, ohem_thrs=ohem_thrs,
+    return seg_cross_entropy_reference(logits, labels.long(), mode=mode, ohem_thrs=ohem_thrs,
                                        ignore_index=ignore_index, class_weight=class_weight,
                                        out_size=out_size, align_corners=align_corners,
                                        resize_logits=resize_logits)

@@ -113,8 +113,10 @@ def test_ce_loss_modes(weighted, mode):
 
 
 @pytest.mark.parametrize("c,hw,lhw,cl", [(40, (12, 20), (96, 160), True), (40, (24, 40), (24, 40), False),
-                                         (19, (16, 32), (128, 256), False), (7, (5, 300), (40, 2400), True)])
-def test_loss_class_counts_layouts(c, hw, lhw, cl):
+                                         (19, (16, 32), (128, 256), False), (7, (5, 300), (40, 2400), True),
+                                         (150, (16, 16), (64, 64), True)])
+@pytest.mark.parametrize("u8", [False, True])
+def test_loss_class_counts_layouts(c, hw, lhw, cl, u8):
     _lib_loaded()
     torch.manual_seed(7)
     logits = torch.randn(2, c, *hw, device=DEV) * 2
@@ -122,7 +124,7 @@ def test_loss_class_counts_layouts(c, hw, lhw, cl):
         logits = logits.contiguous(memory_format=torch.channels_last)
     logits.requires_grad_(True)
     labels = _labels(2, *lhw, c, seed=8)
-    loss = ops.seg_cross_entropy(logits, labels)
+    loss = ops.seg_cross_entropy(logits, labels.to(torch.uint8) if u8 else labels)
     lr_ = logits.detach().clone().requires_grad_(True)
     ref = ops.seg_cross_entropy_reference(lr_, labels)
     torch.testing.assert_close(loss, ref, atol=1e-4, rtol=1e-4)

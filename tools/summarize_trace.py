@@ -21,7 +21,7 @@ from summarize_kernel_stats import family  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
-    ap.add_argument("--marker", default="seg_ce_fwd_kernel")
+    ap.add_argument("--marker", default="seg_ce_fwd")
     ap.add_argument("--per-step", type=int, default=2)
     ap.add_argument("--skip", type=int, default=3)
     ap.add_argument("--top", type=int, default=45)
