@@ -153,9 +153,12 @@ static at::Tensor seg_loss_bwd(const at::Tensor& grad, const at::Tensor& logits,
   at::Tensor gl = at::empty(logits.sizes(), logits.options().memory_format(logits.suggest_memory_format()));
   at::Tensor acc;
   if (!(out_h == logits.size(2) && out_w == logits.size(3))) {
-    acc = at::empty({logits.size(0), logits.size(1), logits.size(2), logits.size(3)},
-                    logits.options().dtype(at::kFloat));
+    acc = at::empty_like(gl, gl.options().dtype(at::kFloat));
+    TORCH_CHECK(acc.strides() == gl.strides() && gl.is_non_overlapping_and_dense(),
+                "rtseg.seg_loss_bwd: accumulator layout mismatch");
     a.acc = acc.data_ptr<float>();
+    a.acc_sn = acc.stride(0); a.acc_sc = acc.stride(1);
+    a.acc_sh = acc.stride(2); a.acc_sw = acc.stride(3);
   }
   launch_seg_loss_bwd(a, g32.data_ptr<float>(), view4(gl), cur_stream());
   return gl;

@@ -40,7 +40,8 @@ struct SegLossArgs {
   double* stats;         // kSegStats device scalars, see seg_loss.hip
   double* slab;          // [seg_loss_fwd_blocks, 5] per-tile partial statistics
   unsigned* hist;        // 3 x 2048 radix-select histogram workspace
-  float* acc;            // [N, C, h, w] fp32 backward accumulator (upsample path)
+  float* acc;            // fp32 backward accumulator (upsample path), strides of the gradient
+  int64_t acc_sn, acc_sc, acc_sh, acc_sw;
   int mode;              // 0 = OHEM, 1 = weighted mean CE, 2 = sum CE
   float ohem_thresh;     // -log(p)
   float* out_loss;       // scalar

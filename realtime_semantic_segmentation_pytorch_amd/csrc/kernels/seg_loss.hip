@@ -413,7 +413,8 @@ __global__ void __launch_bounds__(256) seg_ce_bwd_tile(
     const T* __restrict__ x, LossGeo g, int ignore,
     const float* __restrict__ cw, const float* __restrict__ pix_loss,
     const float* __restrict__ pix_lse, const double* __restrict__ stats, int mode,
-    const float* __restrict__ grad_out, float* __restrict__ gacc) {
+    const float* __restrict__ grad_out, float* __restrict__ gacc, int64_t asn, int64_t asc,
+    int64_t ash, int64_t asw) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   __shared__ int tj0[TW], tj1[TW], ti0[TH], ti1[TH];
   __shared__ float tlx[TW], tly[TH];
@@ -496,41 +497,31 @@ __global__ void __launch_bounds__(256) seg_ce_bwd_tile(
   // column scan + global accumulate
   for (int cj = threadIdx.x; cj < C * BW; cj += blockDim.x) {
     const int c = cj / BW, j = cj % BW;
-    float* dst = gacc + ((static_cast<int64_t>(t.n) * C + c) * g.h + t.by0) * g.w + (t.bx0 + j);
+    float* dst = gacc + t.n * asn + c * asc + t.by0 * ash + (t.bx0 + j) * asw;
     int ic = ti0[0];
     float a = 0.f, b = 0.f;
     for (int r = 0; r < ny; ++r) {
       const int i0 = ti0[r];
       while (ic < i0) {
-        if (a != 0.f) atomicAdd(dst + static_cast<int64_t>(ic) * g.w, a);
+        if (a != 0.f) atomicAdd(dst + static_cast<int64_t>(ic) * ash, a);
         a = b; b = 0.f; ++ic;
       }
       const float v = R[(c * TH + r) * RS + j];
       if (ti1[r] == i0) a += v;
       else { const float l = tly[r]; a += (1.f - l) * v; b += l * v; }
     }
-    if (a != 0.f) atomicAdd(dst + static_cast<int64_t>(ic) * g.w, a);
-    if (b != 0.f && ic + 1 < t.BH) atomicAdd(dst + static_cast<int64_t>(ic + 1) * g.w, b);
+    if (a != 0.f) atomicAdd(dst + static_cast<int64_t>(ic) * ash, a);
+    if (b != 0.f && ic + 1 < t.BH) atomicAdd(dst + static_cast<int64_t>(ic + 1) * ash, b);
   }
 }
 
-// fp32 [N,C,h,w] accumulator -> gradient tensor of any layout/dtype
+// fp32 accumulator (same strides as the gradient tensor) -> gradient dtype
 template <typename G>
-__global__ void __launch_bounds__(256) cast_out_kernel(const float* __restrict__ acc, int N, int C,
-                                                       int H, int W, G* __restrict__ out,
-                                                       int64_t sn, int64_t sc, int64_t sh,
-                                                       int64_t sw) {
-  const int64_t total = static_cast<int64_t>(N) * C * H * W;
-  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < total;
-       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    int x = static_cast<int>(i % W);
-    int64_t t = i / W;
-    int y = static_cast<int>(t % H);
-    t /= H;
-    int c = static_cast<int>(t % C);
-    int n = static_cast<int>(t / C);
-    Io<G>::st(out + n * sn + c * sc + y * sh + x * sw, acc[i]);
-  }
+__global__ void __launch_bounds__(256) cast_out_kernel(const float* __restrict__ acc,
+                                                       G* __restrict__ out, int64_t n) {
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    Io<G>::st(out + i, acc[i]);
 }
 
 // ------------------------------- launchers ---------------------------------
@@ -550,8 +541,6 @@ static LossGeo make_geo(const SegLossArgs& a) {
 
 // Tile shape: wide tiles for the usual <= 32 classes, smaller ones otherwise
 // so the staged logits / gradient tile stay within LDS.
-static bool big_tile(const LossGeo& g) { return g.c <= 32; }
-
 template <int TH, int TW>
 static int tiles_of(const LossGeo& g) {
   return ((g.oh + TH - 1) / TH) * ((g.ow + TW - 1) / TW) * g.n;
@@ -562,7 +551,16 @@ static size_t stage_floats(const LossGeo& g) {
   const int bh = static_cast<int>((TH - 1) * g.mh.scale) + 3;
   const int bw = static_cast<int>((TW - 1) * g.mw.scale) + 3;
   const int cp = g.c | 1;
-  return static_cast<size_t>(bh) * bw * cp + static_cast<size_t>(TH) * bw * cp;
+  const size_t v = g.oh == g.h ? 0 : static_cast<size_t>(TH) * bw * cp;  // no V rows on identity
+  return static_cast<size_t>(bh) * bw * cp + v;
+}
+
+// Tile shape per geometry: 16x64 for upsampled main heads, 8x64 for identity
+// (aux heads: the staged logits cover the whole tile), 4x32 beyond 32 classes.
+enum TileKind { kTile16x64 = 0, kTile8x64 = 1, kTile4x32 = 2 };
+static TileKind tile_kind(const LossGeo& g) {
+  if (g.c > 32) return kTile4x32;
+  return (g.oh == g.h) ? kTile8x64 : kTile16x64;
 }
 
 template <typename K>
@@ -574,7 +572,11 @@ static void allow_lds(K kernel, size_t bytes) {
 
 int seg_loss_fwd_blocks(const SegLossArgs& a) {
   LossGeo g = make_geo(a);
-  return big_tile(g) ? tiles_of<16, 64>(g) : tiles_of<4, 32>(g);
+  switch (tile_kind(g)) {
+    case kTile16x64: return tiles_of<16, 64>(g);
+    case kTile8x64: return tiles_of<8, 64>(g);
+    default: return tiles_of<4, 32>(g);
+  }
 }
 
 template <typename T, int TH, int TW, int NC>
@@ -591,9 +593,16 @@ static void fwd_tile(const SegLossArgs& a, const LossGeo& g, hipStream_t st) {
 template <typename T>
 static void fwd_t(const SegLossArgs& a, const LossGeo& g, hipStream_t st) {
   const int64_t total = static_cast<int64_t>(g.n) * g.oh * g.ow;
-  if (g.c == 19) fwd_tile<T, 16, 64, 19>(a, g, st);  // Cityscapes: classes in registers
-  else if (big_tile(g)) fwd_tile<T, 16, 64, 0>(a, g, st);
-  else fwd_tile<T, 4, 32, 0>(a, g, st);
+  const TileKind tk = tile_kind(g);
+  if (tk == kTile16x64) {
+    if (g.c == 19) fwd_tile<T, 16, 64, 19>(a, g, st);  // Cityscapes: classes in registers
+    else fwd_tile<T, 16, 64, 0>(a, g, st);
+  } else if (tk == kTile8x64) {
+    if (g.c == 19) fwd_tile<T, 8, 64, 19>(a, g, st);
+    else fwd_tile<T, 8, 64, 0>(a, g, st);
+  } else {
+    fwd_tile<T, 4, 32, 0>(a, g, st);
+  }
   if (a.mode != MODE_OHEM) return;
   // top-k fallback (every kernel exits at once when the threshold branch was taken)
   hipMemsetAsync(a.hist, 0, sizeof(unsigned) * 3 * 2048, st);
@@ -629,7 +638,8 @@ static void bwd_tile(const SegLossArgs& a, const LossGeo& g, const float* grad_o
   allow_lds(k, lds);
   k<<<tiles_of<TH, TW>(g), 256, lds, st>>>(
       static_cast<const T*>(a.logits.data), g, a.ignore_index, a.class_weight,
-      a.pix_loss, a.pix_lse, a.stats, a.mode, grad_out, a.acc);
+      a.pix_loss, a.pix_lse, a.stats, a.mode, grad_out, a.acc, a.acc_sn, a.acc_sc, a.acc_sh,
+      a.acc_sw);
 }
 
 template <typename T, typename G>
@@ -646,10 +656,9 @@ static void bwd_t(const SegLossArgs& a, const LossGeo& g, const float* grad_out,
   const int64_t nacc = static_cast<int64_t>(g.n) * g.c * g.h * g.w;
   hipMemsetAsync(a.acc, 0, sizeof(float) * nacc, st);
   if (g.c == 19) bwd_tile<T, 8, 64, 19>(a, g, grad_out, st);
-  else if (big_tile(g)) bwd_tile<T, 8, 64, 0>(a, g, grad_out, st);
+  else if (g.c <= 32) bwd_tile<T, 8, 64, 0>(a, g, grad_out, st);
   else bwd_tile<T, 4, 32, 0>(a, g, grad_out, st);
-  cast_out_kernel<G><<<stream_grid(nacc, 256), 256, 0, st>>>(
-      a.acc, g.n, g.c, g.h, g.w, static_cast<G*>(gl.data), gl.sn, gl.sc, gl.sh, gl.sw);
+  cast_out_kernel<G><<<stream_grid(nacc, 256), 256, 0, st>>>(a.acc, static_cast<G*>(gl.data), nacc);
 }
 
 void launch_seg_loss_bwd(const SegLossArgs& a, const float* grad_out, const Tensor4& gl,

@@ -178,3 +178,39 @@ class SegHead(nn.Sequential):
     def __init__(self, in_channels, num_class, act_type, hid_channels=128):
         super().__init__(ConvBNAct(in_channels, hid_channels, 3, act_type=act_type),
                          conv1x1(hid_channels, num_class))
+
+
+def pooled_conv_bn_act(block: nn.Sequential, pooled: torch.Tensor, spatial: int) -> torch.Tensor:
+    """``block`` (Sequential conv1x1, BN, act) applied to ``pooled`` [N, C, 1, 1]
+    *as if* it had been broadcast to ``spatial`` = H*W positions first.
+
+    The reference attention modules (bisenetv1.py:76-88 ARM, stdc.py via ARM,
+    canet/regseg SE variants) do ``pool(x).expand_as(x)`` and then run a 1x1
+    conv + BatchNorm over the full H x W map.  Every position holds the same
+    vector, so conv and BN batch statistics equal those of the N pooled
+    vectors; only BN's *unbiased* running-variance factor uses the expanded
+    count N*H*W.  This evaluates the block on the N vectors (H*W times less
+    work) with that exact factor, and returns [N, C, 1, 1] for a broadcast
+    multiply -- forward values and gradients identical to the reference.
+    """
+    conv, bn, act = block[0], block[1], block[2]
+    y = conv(pooled)
+    out_dtype = y.dtype
+    if bn.training or not bn.track_running_stats or bn.running_mean is None:
+        y32 = y.float()
+        mean = y32.mean(dim=(0, 2, 3))
+        var = y32.var(dim=(0, 2, 3), unbiased=False)
+        if bn.training and bn.track_running_stats and bn.running_mean is not None:
+            with torch.no_grad():
+                count = y.shape[0] * spatial
+                mom = bn.momentum if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked + 1)
+                bn.running_mean.mul_(1 - mom).add_(mean.detach(), alpha=mom)
+                bn.running_var.mul_(1 - mom).add_(var.detach() * count / max(count - 1, 1), alpha=mom)
+                bn.num_batches_tracked.add_(1)
+        inv = torch.rsqrt(var + bn.eps)
+        y = (y32 - mean[None, :, None, None]) * inv[None, :, None, None]
+        if bn.affine:
+            y = y * bn.weight[None, :, None, None] + bn.bias[None, :, None, None]
+    else:
+        y = bn(y)
+    return act(y).to(out_dtype)
