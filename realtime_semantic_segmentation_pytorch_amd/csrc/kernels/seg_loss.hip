@@ -87,30 +87,40 @@ __device__ __forceinline__ TileGeo tile_geo(const LossGeo& g) {
   return t;
 }
 
-template <typename T, int TH>
+template <typename T, int TH, int NC>
 __device__ __forceinline__ const float* stage_logits(const T* __restrict__ x, const LossGeo& g,
-                                                     const TileGeo& t, float* L, float* V) {
-  const int C = g.c;
-  const int total = t.BH * t.BW * C;
+                                                     const TileGeo& t, float* L, float* V,
+                                                     bool want_v = true) {
+  const int C = NC > 0 ? NC : g.c;
   const T* base = x + t.n * g.sn + t.by0 * g.sh + t.bx0 * g.sw;
-  for (int e = threadIdx.x; e < total; e += blockDim.x) {
-    const int c = e % C;
-    const int j = (e / C) % t.BW;
-    const int i = e / (C * t.BW);
-    L[(i * t.BW + j) * t.CP + c] = Io<T>::ld(base + c * g.sc + i * g.sh + j * g.sw);
+  // one thread per bounding-box pixel, classes innermost (contiguous in NHWC)
+  for (int e = threadIdx.x; e < t.BH * t.BW; e += blockDim.x) {
+    const int i = e / t.BW, j = e - (e / t.BW) * t.BW;
+    const T* src = base + i * g.sh + j * g.sw;
+    float* dst = L + e * t.CP;
+    if constexpr (NC > 0) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) dst[c] = Io<T>::ld(src + c * g.sc);
+    } else {
+      for (int c = 0; c < C; ++c) dst[c] = Io<T>::ld(src + c * g.sc);
+    }
   }
   __syncthreads();
-  if (t.ident_h) return L;  // rows already at output resolution
-  const int vt = TH * t.BW * C;
-  for (int e = threadIdx.x; e < vt; e += blockDim.x) {
-    const int c = e % C;
-    const int j = (e / C) % t.BW;
-    const int r = e / (C * t.BW);
-    const int oy = min(t.oy0 + r, t.oy1);
+  if (t.ident_h || !want_v) return L;  // rows already at output resolution / caller uses L taps
+  // vertical interpolation to the tile's TH output rows: one thread per (row, column)
+  for (int e = threadIdx.x; e < TH * t.BW; e += blockDim.x) {
+    const int r = e / t.BW, j = e - (e / t.BW) * t.BW;
     int y0, y1; float ly;
-    g.mh.map(oy, y0, y1, ly);
-    V[(r * t.BW + j) * t.CP + c] = (1.f - ly) * L[((y0 - t.by0) * t.BW + j) * t.CP + c] +
-                                   ly * L[((y1 - t.by0) * t.BW + j) * t.CP + c];
+    g.mh.map(min(t.oy0 + r, t.oy1), y0, y1, ly);
+    const float* a0 = L + ((y0 - t.by0) * t.BW + j) * t.CP;
+    const float* a1 = L + ((y1 - t.by0) * t.BW + j) * t.CP;
+    float* dst = V + e * t.CP;
+    if constexpr (NC > 0) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) dst[c] = a0[c] + ly * (a1[c] - a0[c]);
+    } else {
+      for (int c = 0; c < C; ++c) dst[c] = a0[c] + ly * (a1[c] - a0[c]);
+    }
   }
   __syncthreads();
   return V;
@@ -174,7 +184,7 @@ __global__ void __launch_bounds__(256) seg_ce_fwd_tile(
   const TileGeo t = tile_geo<TH, TW>(g);
   float* L = sm;
   float* V = sm + t.BH * t.BW * t.CP;
-  const float* rows = stage_logits<T, TH>(x, g, t, L, V);
+  const float* rows = stage_logits<T, TH, NC>(x, g, t, L, V);
   float acc[SL_N] = {0.f, 0.f, 0.f, 0.f, 0.f};
   for (int p = threadIdx.x; p < TH * TW; p += blockDim.x) {
     const int r = p / TW, oy = t.oy0 + r, ox = t.ox0 + p % TW;
@@ -402,12 +412,16 @@ __global__ void __launch_bounds__(256) seg_ce_bwd_identity(
   }
 }
 
-// Upsampled geometry: stage logits (as in the forward), per-pixel softmax
-// gradient tile G[C][TH][TW] in LDS, then the transpose of the bilinear map:
-// a row scan per (class, row) and a column scan per (class, low-res column),
-// both driven by per-tile tap tables (taps are monotone in the output index,
-// so each scan carries just two running sums).  fp32 atomics only for the
-// tile's bounding-box cells (shared with neighbouring tiles).
+// Upsampled geometry.  The gradient w.r.t. low-res logit (c, i, j) is
+//   sum_{oy, ox} wy(oy, i) * wx(ox, j) * G_c(oy, ox),
+//   G_c = w_pixel * (softmax_c - [c == label]).
+// Pass 1: one thread per (output row r, low-res column j) walks the ~1/scale
+// output pixels whose horizontal taps include j, recomputes G for each (every
+// pixel is visited by its two columns) and accumulates wx * G in registers ->
+// R[c][r][j] in LDS.  Pass 2: one thread per (class, low-res column) folds the
+// rows with wy and issues fp32 atomics only for the tile's bounding-box cells
+// (shared with neighbouring tiles).  No [C, TH, TW] gradient tile, so LDS stays
+// small and occupancy high.
 template <typename T, int TH, int TW, int NC>
 __global__ void __launch_bounds__(256) seg_ce_bwd_tile(
     const T* __restrict__ x, LossGeo g, int ignore,
@@ -416,98 +430,98 @@ __global__ void __launch_bounds__(256) seg_ce_bwd_tile(
     const float* __restrict__ grad_out, float* __restrict__ gacc, int64_t asn, int64_t asc,
     int64_t ash, int64_t asw) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  __shared__ int tj0[TW], tj1[TW], ti0[TH], ti1[TH];
+  __shared__ int tx0[TW], tx1[TW], ty0[TH], ty1[TH], jlo[TW + 4], jhi[TW + 4];  // BW <= TW + 2
   __shared__ float tlx[TW], tly[TH];
   const TileGeo t = tile_geo<TH, TW>(g);
   const int C = NC > 0 ? NC : g.c;
-  float* L = sm;
-  float* V = L + t.BH * t.BW * t.CP;
-  constexpr int GR = TW + 1;           // padded G row: conflict-free row scans
-  constexpr int GS = TH * GR;          // G class stride
-  const int BW = t.BW;
-  const int RS = BW | 1;               // padded R row
-  float* Gt = V + TH * t.BW * t.CP;    // [C][TH][TW + 1]
-  float* R = Gt + C * GS;              // [C][TH][RS]
+  const int BW = t.BW, RS = BW | 1;
+  const int nx = t.ox1 - t.ox0 + 1, ny = t.oy1 - t.oy0 + 1;
+  float* L = sm;                          // [BH][BW][CP]
+  float* R = L + t.BH * t.BW * t.CP;      // [C][TH][RS]
   for (int k = threadIdx.x; k < TW; k += blockDim.x) {
     int a0, a1; float l;
     g.mw.map(min(t.ox0 + k, t.ox1), a0, a1, l);
-    tj0[k] = a0 - t.bx0; tj1[k] = a1 - t.bx0; tlx[k] = l;
+    tx0[k] = a0 - t.bx0; tx1[k] = a1 - t.bx0; tlx[k] = l;
   }
   for (int k = threadIdx.x; k < TH; k += blockDim.x) {
     int a0, a1; float l;
     g.mh.map(min(t.oy0 + k, t.oy1), a0, a1, l);
-    ti0[k] = a0 - t.by0; ti1[k] = a1 - t.by0; tly[k] = l;
+    ty0[k] = a0 - t.by0; ty1[k] = a1 - t.by0; tly[k] = l;
   }
-  for (int e = threadIdx.x; e < C * TH * RS; e += blockDim.x) R[e] = 0.f;
-  const float* rows = stage_logits<T, TH>(x, g, t, L, V);  // has __syncthreads
+  stage_logits<T, TH, NC>(x, g, t, L, nullptr, false);  // syncs: tables visible too
+  // ox range of each low-res column (taps are monotone in ox)
+  for (int j = threadIdx.x; j < BW; j += blockDim.x) {
+    int lo = nx, hi = -1;
+    for (int k = 0; k < nx; ++k)
+      if (tx0[k] == j || tx1[k] == j) { lo = min(lo, k); hi = k; }
+    jlo[j] = lo; jhi[j] = hi;
+  }
+  __syncthreads();
   const SelRule rule = load_rule(stats, mode);
   const float go = *grad_out;
-  for (int p = threadIdx.x; p < TH * TW; p += blockDim.x) {
-    const int r = p / TW, oy = t.oy0 + r, ox = t.ox0 + p % TW;
-    float* gp = Gt + r * GR + p % TW;
-    float w = 0.f;
-    int64_t y = -1;
-    int64_t pi = 0;
-    if (oy <= t.oy1 && ox <= t.ox1) {
-      pi = (static_cast<int64_t>(t.n) * g.oh + oy) * g.ow + ox;
-      y = label_at(g, t.n, oy, ox);
-      w = pixel_weight(rule, pix_loss[pi], y, ignore, C, cw) * go;
-    }
-    if (w == 0.f) {
-      for (int c = 0; c < C; ++c) gp[c * GS] = 0.f;
-      continue;
-    }
-    const float *pa, *pb; float lx;
-    pixel_taps(g, t, rows, r, ox, pa, pb, lx);
-    const float lse = pix_lse[pi];
+  for (int rj = threadIdx.x; rj < TH * BW; rj += blockDim.x) {
+    const int r = rj / BW, j = rj - (rj / BW) * BW;
+    float* Rc = R + r * RS + j;
+    float acc[NC > 0 ? NC : 1];
     if constexpr (NC > 0) {
 #pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        const float z = pa[c] + lx * (pb[c] - pa[c]);
-        gp[c * GS] = w * (__expf(z - lse) - (c == y ? 1.f : 0.f));
-      }
+      for (int c = 0; c < NC; ++c) acc[c] = 0.f;
     } else {
-      for (int c = 0; c < C; ++c) {
-        const float z = pa[c] + lx * (pb[c] - pa[c]);
-        gp[c * GS] = w * (__expf(z - lse) - (c == y ? 1.f : 0.f));
+      for (int c = 0; c < C; ++c) Rc[c * TH * RS] = 0.f;
+    }
+    if (r < ny) {
+      const int oy = t.oy0 + r;
+      const float ly = tly[r];
+      const float* row0 = L + ty0[r] * t.BW * t.CP;
+      const float* row1 = L + ty1[r] * t.BW * t.CP;
+      const int64_t prow = (static_cast<int64_t>(t.n) * g.oh + oy) * g.ow + t.ox0;
+      for (int k = jlo[j]; k <= jhi[j]; ++k) {
+        const float lx = tlx[k];
+        const float wx = (tx0[k] == j ? 1.f - lx : 0.f) + (tx1[k] == j ? lx : 0.f);
+        const int64_t y = label_at(g, t.n, oy, t.ox0 + k);
+        const float w = wx * pixel_weight(rule, pix_loss[prow + k], y, ignore, C, cw) * go;
+        if (w == 0.f) continue;
+        const float lse = pix_lse[prow + k];
+        const float* p00 = row0 + tx0[k] * t.CP;
+        const float* p01 = row0 + tx1[k] * t.CP;
+        const float* p10 = row1 + tx0[k] * t.CP;
+        const float* p11 = row1 + tx1[k] * t.CP;
+        const float w00 = (1.f - ly) * (1.f - lx), w01 = (1.f - ly) * lx;
+        const float w10 = ly * (1.f - lx), w11 = ly * lx;
+        if constexpr (NC > 0) {
+#pragma unroll
+          for (int c = 0; c < NC; ++c) {
+            const float z = w00 * p00[c] + w01 * p01[c] + w10 * p10[c] + w11 * p11[c];
+            acc[c] += w * (__expf(z - lse) - (c == y ? 1.f : 0.f));
+          }
+        } else {
+          for (int c = 0; c < C; ++c) {
+            const float z = w00 * p00[c] + w01 * p01[c] + w10 * p10[c] + w11 * p11[c];
+            Rc[c * TH * RS] += w * (__expf(z - lse) - (c == y ? 1.f : 0.f));
+          }
+        }
       }
     }
-  }
-  __syncthreads();
-  const int nx = t.ox1 - t.ox0 + 1, ny = t.oy1 - t.oy0 + 1;
-  // row scan: R[c][r][j] = sum_k wx(k, j) * G[c][r][k]
-  for (int cr = threadIdx.x; cr < C * TH; cr += blockDim.x) {
-    const int c = cr / TH, r = cr % TH;
-    if (r >= ny) continue;
-    float* Rr = R + (c * TH + r) * RS;
-    const float* gr = Gt + c * GS + r * GR;
-    int jc = tj0[0];
-    float a = 0.f, b = 0.f;  // running sums for columns jc and jc + 1
-    for (int k = 0; k < nx; ++k) {
-      const int j0 = tj0[k];
-      while (jc < j0) { Rr[jc] += a; a = b; b = 0.f; ++jc; }
-      const float v = gr[k];
-      if (tj1[k] == j0) a += v;
-      else { const float l = tlx[k]; a += (1.f - l) * v; b += l * v; }
+    if constexpr (NC > 0) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) Rc[c * TH * RS] = acc[c];
     }
-    Rr[jc] += a;
-    if (jc + 1 < BW) Rr[jc + 1] += b;
   }
   __syncthreads();
-  // column scan + global accumulate
+  // column pass: fold output rows onto low-res rows, accumulate globally
   for (int cj = threadIdx.x; cj < C * BW; cj += blockDim.x) {
-    const int c = cj / BW, j = cj % BW;
+    const int c = cj / BW, j = cj - (cj / BW) * BW;
     float* dst = gacc + t.n * asn + c * asc + t.by0 * ash + (t.bx0 + j) * asw;
-    int ic = ti0[0];
+    int ic = ty0[0];
     float a = 0.f, b = 0.f;
     for (int r = 0; r < ny; ++r) {
-      const int i0 = ti0[r];
+      const int i0 = ty0[r];
       while (ic < i0) {
         if (a != 0.f) atomicAdd(dst + static_cast<int64_t>(ic) * ash, a);
         a = b; b = 0.f; ++ic;
       }
       const float v = R[(c * TH + r) * RS + j];
-      if (ti1[r] == i0) a += v;
+      if (ty1[r] == i0) a += v;
       else { const float l = tly[r]; a += (1.f - l) * v; b += l * v; }
     }
     if (a != 0.f) atomicAdd(dst + static_cast<int64_t>(ic) * ash, a);
@@ -631,8 +645,9 @@ void launch_seg_loss_fwd(const SegLossArgs& a, hipStream_t st) {
 template <typename T, int TH, int TW, int NC>
 static void bwd_tile(const SegLossArgs& a, const LossGeo& g, const float* grad_out,
                      hipStream_t st) {
+  const int bh = static_cast<int>((TH - 1) * g.mh.scale) + 3;
   const int bw = static_cast<int>((TW - 1) * g.mw.scale) + 3;
-  const size_t lds = sizeof(float) * (stage_floats<TH, TW>(g) + static_cast<size_t>(g.c) * TH * (TW + 1) +
+  const size_t lds = sizeof(float) * (static_cast<size_t>(bh) * bw * (g.c | 1) +
                                       static_cast<size_t>(g.c) * TH * (bw | 1));
   auto k = seg_ce_bwd_tile<T, TH, TW, NC>;
   allow_lds(k, lds);
@@ -655,8 +670,8 @@ static void bwd_t(const SegLossArgs& a, const LossGeo& g, const float* grad_out,
   }
   const int64_t nacc = static_cast<int64_t>(g.n) * g.c * g.h * g.w;
   hipMemsetAsync(a.acc, 0, sizeof(float) * nacc, st);
-  if (g.c == 19) bwd_tile<T, 8, 64, 19>(a, g, grad_out, st);
-  else if (g.c <= 32) bwd_tile<T, 8, 64, 0>(a, g, grad_out, st);
+  if (g.c == 19) bwd_tile<T, 16, 128, 19>(a, g, grad_out, st);
+  else if (g.c <= 32) bwd_tile<T, 16, 128, 0>(a, g, grad_out, st);
   else bwd_tile<T, 4, 32, 0>(a, g, grad_out, st);
   cast_out_kernel<G><<<stream_grid(nacc, 256), 256, 0, st>>>(a.acc, static_cast<G*>(gl.data), nacc);
 }
