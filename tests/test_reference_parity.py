@@ -68,6 +68,11 @@ CASES = [
     ("bisenetv2", "bisenetv2", "BiSeNetv2", dict(use_aux=True), (128, 256)),
     ("stdc", "stdc", "STDC", dict(encoder_type="stdc1", use_aux=True), (128, 256)),
     ("stdc", "stdc", "STDC", dict(encoder_type="stdc2", use_detail_head=True), (128, 256)),
+    # the reference mutates a default list for espnet-a: always pass a fresh one
+    ("espnet", "espnet", "ESPNet", dict(arch_type="espnet-a", block_channel=[16, 64, 128]), (128, 256)),
+    ("espnet", "espnet", "ESPNet", dict(arch_type="espnet-b", block_channel=[16, 64, 128]), (128, 256)),
+    ("espnet", "espnet", "ESPNet", dict(arch_type="espnet-c", block_channel=[16, 64, 128]), (128, 256)),
+    ("dfanet", "dfanet", "DFANet", dict(backbone_type="XceptionB", use_extra_backbone=False), (128, 256)),
 ]
 
 
@@ -75,7 +80,7 @@ def _extra_cases():
     """Every other model registered in both zoos (constructed with defaults)."""
     from realtime_semantic_segmentation_pytorch_amd.models import MODEL_HUB
 
-    done = {c[0] for c in CASES}
+    done = {c[0] for c in CASES if c[0] not in ("espnet", "dfanet")}
     out = []
     for key, (mod, cls) in MODEL_HUB.items():
         if key in done:
