@@ -146,3 +146,33 @@ def test_state_dict_and_outputs_match_reference(key, mod, cls, kw, hw):
     assert len(ro) == len(oo)
     for a, b in zip(ro, oo):
         torch.testing.assert_close(b, a, atol=5e-4, rtol=5e-4)
+
+
+def test_regseg_matches_reference_with_groups_fix():
+    """Reference RegSeg passes ``groups`` to a ConvBNAct that lacks it (SURVEY A.1
+    #8).  Patch the reference module's ConvBNAct with the intended grouped conv
+    and check our (working) RegSeg against it."""
+    rmod = ref_module("regseg")
+    base = rmod.ConvBNAct
+
+    class GroupedConvBNAct(base):
+        def __init__(self, *args, groups=1, **kwargs):
+            super().__init__(*args, **kwargs)
+            if groups != 1:
+                c = self[0]
+                self[0] = torch.nn.Conv2d(c.in_channels, c.out_channels, c.kernel_size, c.stride, c.padding,
+                                          c.dilation, groups=groups, bias=c.bias is not None)
+
+    rmod.ConvBNAct = GroupedConvBNAct
+    try:
+        torch.manual_seed(0)
+        ref = rmod.RegSeg(num_class=19)
+    finally:
+        rmod.ConvBNAct = base
+    ours = model_class("regseg")(num_class=19)
+    ours.load_state_dict(ref.state_dict(), strict=True)
+    x = torch.randn(2, 3, 128, 256)
+    for train in (False, True):
+        ref.train(train), ours.train(train)
+        with torch.no_grad():
+            torch.testing.assert_close(ours(x), ref(x), atol=5e-4, rtol=5e-4)
