@@ -73,6 +73,7 @@ CASES = [
     ("espnet", "espnet", "ESPNet", dict(arch_type="espnet-b", block_channel=[16, 64, 128]), (128, 256)),
     ("espnet", "espnet", "ESPNet", dict(arch_type="espnet-c", block_channel=[16, 64, 128]), (128, 256)),
     ("dfanet", "dfanet", "DFANet", dict(backbone_type="XceptionB", use_extra_backbone=False), (128, 256)),
+    ("lite_hrnet", "lite_hrnet", "LiteHRNet", dict(arch_type="litehrnet30"), (128, 256)),
 ]
 
 
@@ -80,7 +81,7 @@ def _extra_cases():
     """Every other model registered in both zoos (constructed with defaults)."""
     from realtime_semantic_segmentation_pytorch_amd.models import MODEL_HUB
 
-    done = {c[0] for c in CASES if c[0] not in ("espnet", "dfanet")}
+    done = {c[0] for c in CASES if c[0] not in ("espnet", "dfanet", "lite_hrnet")}
     out = []
     for key, (mod, cls) in MODEL_HUB.items():
         if key in done:
