@@ -1,0 +1,132 @@
+"""Whole-zoo training-path tests.
+
+CPU: every registered model runs a train step through the trainer's path
+(deferred final upsample -> fused-loss formulation -> backward) and the deferred
+logits materialise to exactly the model's normal output.
+
+GPU: every model in fp32 channels-last runs forward + loss + backward once on
+the HIP kernels and once with ``RTSEG_DISABLE_HIP=1`` (PyTorch formulation of
+the same ops); outputs, loss and all parameter gradients must agree.  A second
+GPU test runs the production configuration (bf16 autocast, channels-last, OHEM)
+and checks for finite loss/gradients.
+"""
+import copy
+
+import pytest
+import torch
+
+from realtime_semantic_segmentation_pytorch_amd import ops
+from realtime_semantic_segmentation_pytorch_amd.configs import BaseConfig
+from realtime_semantic_segmentation_pytorch_amd.core.loss import SegCELoss
+from realtime_semantic_segmentation_pytorch_amd.models import (AUX_MODELS, DETAIL_HEAD_MODELS, MODEL_HUB,
+                                                               get_model)
+from realtime_semantic_segmentation_pytorch_amd.ops.interp import DeferredLogits
+
+KEYS = sorted(MODEL_HUB)
+HW = (128, 256)
+
+
+def _model(key, use_aux=False):
+    c = BaseConfig()
+    c.model, c.num_class = key, 19
+    c.use_aux = use_aux and key in AUX_MODELS
+    c.use_detail_head = False
+    torch.manual_seed(0)
+    return get_model(c)
+
+
+def _main(out):
+    return out[0] if isinstance(out, (tuple, list)) else out
+
+
+def _forward(m, x):
+    kw = {"is_training": True} if m.training else {}
+    return m(x, **kw)
+
+
+@pytest.mark.parametrize("key", KEYS)
+def test_train_step_with_deferred_upsample_cpu(key):
+    m = _model(key, use_aux=True).train()
+    x = torch.randn(2, 3, *HW)
+    labels = torch.randint(0, 19, (2, *HW))
+    loss_fn = SegCELoss(ops.MODE_OHEM, 0.7)
+    with ops.defer_final_upsample():
+        out = _forward(m, x)
+    main = _main(out)
+    assert main.shape == (2, 19, *HW)
+    loss = loss_fn(main, labels)
+    if isinstance(out, (tuple, list)) and len(out) > 1:
+        for a in out[1] if isinstance(out[1], (list, tuple)) else [out[1]]:
+            loss = loss + loss_fn.aux(a, labels)
+    loss.backward()
+    assert torch.isfinite(loss)
+    grads = [p.grad for p in m.parameters() if p.requires_grad]
+    assert sum(g is not None for g in grads) >= 0.9 * len(grads)
+    assert all(torch.isfinite(g).all() for g in grads if g is not None)
+
+
+@pytest.mark.parametrize("key", KEYS)
+def test_deferred_logits_materialize_to_model_output_cpu(key):
+    m = _model(key).eval()
+    x = torch.randn(1, 3, *HW)
+    ref = _main(m(x))
+    with ops.defer_final_upsample():
+        out = _main(m(x))
+    got = out.materialize() if isinstance(out, DeferredLogits) else out
+    torch.testing.assert_close(got, ref, atol=1e-5, rtol=1e-5)
+
+
+def _run_gpu(m, x, labels, disable_hip, monkeypatch):
+    if disable_hip:
+        monkeypatch.setenv("RTSEG_DISABLE_HIP", "1")
+    else:
+        monkeypatch.delenv("RTSEG_DISABLE_HIP", raising=False)
+    torch.manual_seed(123)
+    with ops.defer_final_upsample():
+        out = _main(_forward(m, x))
+    loss = SegCELoss(ops.MODE_MEAN)(out, labels)
+    loss.backward()
+    full = out.materialize() if isinstance(out, DeferredLogits) else out
+    grads = {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
+    monkeypatch.delenv("RTSEG_DISABLE_HIP", raising=False)
+    return full.detach(), loss.detach(), grads
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-6)).item()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key", KEYS)
+def test_zoo_hip_matches_torch_path_gpu(key, monkeypatch):
+    base = _model(key).cuda().to(memory_format=torch.channels_last).train()
+    x = torch.randn(2, 3, *HW, device="cuda").contiguous(memory_format=torch.channels_last)
+    labels = torch.randint(0, 19, (2, *HW), device="cuda")
+    y_h, l_h, g_h = _run_gpu(copy.deepcopy(base), x, labels, False, monkeypatch)
+    y_t, l_t, g_t = _run_gpu(copy.deepcopy(base), x, labels, True, monkeypatch)
+    assert _rel(y_h, y_t) < 1e-3
+    assert abs(l_h.item() - l_t.item()) <= 1e-3 * abs(l_t.item()) + 1e-5
+    assert g_h.keys() == g_t.keys()
+    total_h = torch.cat([g.flatten().float() for g in g_h.values()])
+    total_t = torch.cat([g.flatten().float() for g in g_t.values()])
+    assert _rel(total_h, total_t) < 5e-3
+    bad = [n for n in g_t if _rel(g_h[n], g_t[n]) > 5e-2 and g_t[n].norm() > 1e-4 * total_t.norm()]
+    assert not bad, bad[:5]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key", KEYS)
+def test_zoo_bf16_channels_last_train_step_gpu(key):
+    m = _model(key, use_aux=True).cuda().to(memory_format=torch.channels_last).train()
+    x = torch.randn(2, 3, *HW, device="cuda").contiguous(memory_format=torch.channels_last)
+    labels = torch.randint(0, 19, (2, *HW), device="cuda", dtype=torch.uint8)
+    loss_fn = SegCELoss(ops.MODE_OHEM, 0.7)
+    with torch.autocast("cuda", dtype=torch.bfloat16), ops.defer_final_upsample():
+        out = _forward(m, x)
+        loss = loss_fn(_main(out), labels)
+        if isinstance(out, (tuple, list)) and len(out) > 1:
+            for a in out[1] if isinstance(out[1], (list, tuple)) else [out[1]]:
+                loss = loss + loss_fn.aux(a, labels)
+    loss.backward()
+    assert torch.isfinite(loss)
+    assert all(torch.isfinite(p.grad).all() for p in m.parameters() if p.grad is not None)
