@@ -1,0 +1,86 @@
+"""SMP-compatible encoder/decoder models (config.model='smp') and the KD teacher (CPU).
+
+segmentation_models_pytorch is not installed, so parity with real SMP is
+"parity unpinned"; these tests pin the module layout we rely on (SMP key
+prefixes, parameter counts of well-known SMP configurations, output shapes,
+encoder strides / dilation rule) and the teacher-loading path.
+"""
+import os
+
+import pytest
+import torch
+
+from realtime_semantic_segmentation_pytorch_amd import ops
+from realtime_semantic_segmentation_pytorch_amd.configs import BaseConfig
+from realtime_semantic_segmentation_pytorch_amd.models import get_model, get_teacher_model
+from realtime_semantic_segmentation_pytorch_amd.models.smp import DECODER_HUB, build_smp_model, get_encoder
+
+# parameter counts (M) of SMP models with ResNet-18 encoders and 19 classes
+PARAMS_R18 = {"deeplabv3": 15.904, "deeplabv3p": 12.334, "fpn": 13.050, "linknet": 11.664, "manet": 21.678,
+              "pan": 11.373, "pspnet": 11.413, "unet": 14.331, "unetpp": 15.973}
+
+
+@pytest.mark.parametrize("decoder", sorted(DECODER_HUB))
+def test_smp_decoder_shapes_keys_params(decoder):
+    m = build_smp_model(decoder, "resnet18", None, 19)
+    n = sum(p.numel() for p in m.parameters()) / 1e6
+    assert abs(n - PARAMS_R18[decoder]) < 1e-3
+    keys = list(m.state_dict())
+    assert keys[0] == "encoder.conv1.weight" and keys[-1] == "segmentation_head.0.bias"
+    assert all(k.split(".")[0] in ("encoder", "decoder", "segmentation_head") for k in keys)
+    x = torch.randn(2, 3, 128, 128)  # PAN's pyramid needs >= 128 px
+    m.train()
+    y = m(x)
+    assert y.shape == (2, 19, 128, 128)
+    y.float().mean().backward()
+    m.eval()
+    with torch.no_grad():
+        assert m(x).shape == (2, 19, 128, 128)
+
+
+def test_smp_deferred_head_matches_full_output():
+    m = build_smp_model("deeplabv3p", "resnet18", None, 19).eval()
+    x = torch.randn(1, 3, 64, 128)
+    ref = m(x)
+    with ops.defer_final_upsample():
+        d = m(x)
+    assert isinstance(d, ops.DeferredLogits) and tuple(d.logits.shape[2:]) == (16, 32)
+    torch.testing.assert_close(d.materialize(), ref, atol=1e-5, rtol=1e-5)
+
+
+def test_encoder_strides_and_smp_dilation_rule():
+    e = get_encoder("resnet50", depth=5, output_stride=8)
+    feats = e(torch.randn(1, 3, 64, 64))
+    assert [f.shape[1] for f in feats] == [3, 64, 256, 512, 1024, 2048]
+    assert [f.shape[2] for f in feats] == [64, 32, 16, 8, 8, 8]
+    # SMP rule: EVERY conv of a dilated stage gets the stage's rate (not torchvision's first-block rule)
+    assert e.layer3[0].conv2.dilation == (2, 2) and e.layer4[0].conv2.dilation == (4, 4)
+    assert e.layer4[0].downsample[0].stride == (1, 1)
+    m = get_encoder("mobilenet_v2", depth=5)
+    assert [f.shape[1] for f in m(torch.randn(1, 3, 64, 64))] == [3, 16, 24, 32, 96, 1280]
+
+
+def test_unsupported_encoders_raise():
+    with pytest.raises(NotImplementedError):
+        get_encoder("mit_b0")
+    with pytest.raises(ValueError):
+        build_smp_model("unetpp", "mit_b0", None, 19)
+    with pytest.raises(ValueError):
+        build_smp_model("nope", "resnet18", None, 19)
+
+
+def test_get_model_smp_and_teacher_roundtrip(tmp_path):
+    c = BaseConfig()
+    c.model, c.encoder, c.decoder, c.encoder_weights, c.num_class = "smp", "resnet18", "unet", None, 19
+    c.use_aux = c.use_detail_head = False
+    assert get_model(c).__class__.__name__ == "Unet"
+    # teacher: {'state_dict': smp_state} checkpoint, loaded with weights_only=True
+    t = build_smp_model("deeplabv3p", "resnet18", None, 19)
+    path = os.path.join(tmp_path, "teacher.pth")
+    torch.save({"state_dict": t.state_dict()}, path)
+    c.kd_training, c.teacher_ckpt, c.teacher_encoder, c.teacher_decoder = True, path, "resnet18", "deeplabv3p"
+    teacher = get_teacher_model(c, torch.device("cpu"))
+    assert not teacher.training
+    assert all(not p.requires_grad for p in teacher.parameters())
+    for k, v in t.state_dict().items():
+        assert torch.equal(teacher.state_dict()[k], v)
