@@ -1,0 +1,71 @@
+"""Graph-captured inference engine (the MI355X-native replacement for the
+reference's eager ``model(input)`` loop in tools/test_speed.py:26-60).
+
+A segmentation forward at batch 1 is a few hundred small kernels; launched
+eagerly from Python the host becomes the bottleneck.  ``InferenceEngine``
+puts the model in eval / channels-last / (bf16) form, warms it up on a side
+stream (MIOpen solver selection happens here), then captures ONE forward into
+a HIP graph (``torch.cuda.CUDAGraph`` is hipGraph on ROCm) with static
+input/output buffers.  ``engine(x)`` is a device copy into the static input +
+one graph launch.  All rtseg HIP ops are capture-safe (no host syncs, stream-
+ordered, caching-allocator memory).
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+
+
+class InferenceEngine:
+    def __init__(self, model: nn.Module, input_shape: Sequence[int], dtype: torch.dtype = torch.bfloat16,
+                 channels_last: bool = True, use_graph: bool = True, warmup: int = 3,
+                 device: Optional[torch.device] = None):
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.dtype = dtype
+        self.channels_last = channels_last
+        self.model = model.eval().to(self.device)
+        if channels_last:
+            self.model = self.model.to(memory_format=torch.channels_last)
+        self.autocast = dtype in (torch.bfloat16, torch.float16)
+        fmt = torch.channels_last if channels_last else torch.contiguous_format
+        self.static_in = torch.zeros(*input_shape, device=self.device).contiguous(memory_format=fmt)
+        self.graph = None
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(max(1, warmup)):
+                out = self._forward(self.static_in)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        self.static_out = out
+        if use_graph:
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self.static_out = self._forward(self.static_in)
+            torch.cuda.synchronize(self.device)
+
+    @torch.no_grad()
+    def _forward(self, x):
+        with torch.autocast("cuda", dtype=self.dtype, enabled=self.autocast):
+            out = self.model(x)
+        if isinstance(out, (tuple, list)):
+            out = out[0]
+        return ops.materialize(out)
+
+    @torch.no_grad()
+    def __call__(self, x: torch.Tensor) -> torch.Tensor:
+        if self.graph is None:
+            return self._forward(x.to(self.device, non_blocking=True).contiguous(
+                memory_format=torch.channels_last if self.channels_last else torch.contiguous_format))
+        self.static_in.copy_(x, non_blocking=True)
+        self.graph.replay()
+        return self.static_out
+
+    @torch.no_grad()
+    def predict(self, x: torch.Tensor) -> torch.Tensor:
+        """Class-index map [N, H, W] (argmax over classes)."""
+        return self(x).argmax(dim=1)

@@ -84,3 +84,18 @@ def test_get_model_smp_and_teacher_roundtrip(tmp_path):
     assert all(not p.requires_grad for p in teacher.parameters())
     for k, v in t.state_dict().items():
         assert torch.equal(teacher.state_dict()[k], v)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("decoder", sorted(DECODER_HUB))
+def test_smp_bf16_train_step_gpu(decoder):
+    from realtime_semantic_segmentation_pytorch_amd.core.loss import SegCELoss
+
+    m = build_smp_model(decoder, "resnet18", None, 19).cuda().to(memory_format=torch.channels_last).train()
+    x = torch.randn(2, 3, 128, 256, device="cuda").contiguous(memory_format=torch.channels_last)
+    labels = torch.randint(0, 19, (2, 128, 256), device="cuda", dtype=torch.uint8)
+    with torch.autocast("cuda", dtype=torch.bfloat16), ops.defer_final_upsample():
+        loss = SegCELoss(ops.MODE_OHEM, 0.7)(m(x), labels)
+    loss.backward()
+    assert torch.isfinite(loss)
+    assert all(torch.isfinite(p.grad).all() for p in m.parameters() if p.grad is not None)
