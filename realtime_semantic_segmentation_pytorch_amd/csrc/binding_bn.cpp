@@ -26,8 +26,10 @@ void check_cl(const at::Tensor& x, const char* what) {
     TORCH_CHECK(x.is_contiguous(), "rtseg.bn: ", what, " must be contiguous");
   }
   const int64_t C = x.size(1);
-  const int v = x.scalar_type() == at::kFloat ? 4 : 8;
-  TORCH_CHECK(C % v == 0 && C / v <= 256, "rtseg.bn: channel count ", C, " unsupported");
+  TORCH_CHECK(C <= (1 << 20) && bn_vec_width(dtype_code(x), static_cast<int>(C)) > 0,
+              "rtseg.bn: channel count ", C, " unsupported for ", x.scalar_type());
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "rtseg.bn: ", what,
+              " must be 16-byte aligned");
 }
 
 const float* fptr(const std::optional<at::Tensor>& t) {

@@ -26,45 +26,41 @@ namespace rtseg {
 
 enum MaskMode : int { kMaskNone = 0, kMaskFromY = 1, kMaskFromX = 2 };
 
-template <typename T> struct Vec;
-template <> struct Vec<uint16_t> {  // bf16
-  static constexpr int N = 8;
-  typedef short raw __attribute__((ext_vector_type(8)));
-  __device__ __forceinline__ static void load(const uint16_t* p, float* f) {
-    raw v = *reinterpret_cast<const raw*>(p);
+// V-element channel vector of T: 16-byte vectors on the fast path (8 bf16/fp16 or
+// 4 fp32); narrower widths (down to one element) serve channel counts that are
+// not multiples of the full width (e.g. 12, 19, 35 channels in the zoo).
+template <int BYTES> struct RawT;
+template <> struct RawT<2> { typedef uint16_t type; };
+template <> struct RawT<4> { typedef uint32_t type; };
+template <> struct RawT<8> { typedef uint2 type; };
+template <> struct RawT<16> { typedef uint4 type; };
+
+template <typename T> __device__ __forceinline__ float to_f(T v);
+template <> __device__ __forceinline__ float to_f<float>(float v) { return v; }
+template <> __device__ __forceinline__ float to_f<uint16_t>(uint16_t v) { return bf16_to_f32(v); }
+template <> __device__ __forceinline__ float to_f<_Float16>(_Float16 v) { return static_cast<float>(v); }
+template <typename T> __device__ __forceinline__ T from_f(float v);
+template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
+template <> __device__ __forceinline__ uint16_t from_f<uint16_t>(float v) { return f32_to_bf16(v); }
+template <> __device__ __forceinline__ _Float16 from_f<_Float16>(float v) { return static_cast<_Float16>(v); }
+
+template <typename T, int V>
+struct VecIO {
+  typedef typename RawT<V * sizeof(T)>::type raw;
+  __device__ __forceinline__ static void load(const T* p, float* f) {
+    raw r = *reinterpret_cast<const raw*>(p);
+    T e[V];
+    __builtin_memcpy(e, &r, sizeof(raw));
 #pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = bf16_to_f32(static_cast<uint16_t>(v[j]));
+    for (int j = 0; j < V; ++j) f[j] = to_f<T>(e[j]);
   }
-  __device__ __forceinline__ static void store(uint16_t* p, const float* f) {
-    raw v;
+  __device__ __forceinline__ static void store(T* p, const float* f) {
+    T e[V];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = static_cast<short>(f32_to_bf16(f[j]));
-    *reinterpret_cast<raw*>(p) = v;
-  }
-};
-template <> struct Vec<_Float16> {
-  static constexpr int N = 8;
-  typedef _Float16 raw __attribute__((ext_vector_type(8)));
-  __device__ __forceinline__ static void load(const _Float16* p, float* f) {
-    raw v = *reinterpret_cast<const raw*>(p);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = static_cast<float>(v[j]);
-  }
-  __device__ __forceinline__ static void store(_Float16* p, const float* f) {
-    raw v;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = static_cast<_Float16>(f[j]);
-    *reinterpret_cast<raw*>(p) = v;
-  }
-};
-template <> struct Vec<float> {
-  static constexpr int N = 4;
-  __device__ __forceinline__ static void load(const float* p, float* f) {
-    float4 v = *reinterpret_cast<const float4*>(p);
-    f[0] = v.x; f[1] = v.y; f[2] = v.z; f[3] = v.w;
-  }
-  __device__ __forceinline__ static void store(float* p, const float* f) {
-    *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
+    for (int j = 0; j < V; ++j) e[j] = from_f<T>(f[j]);
+    raw r;
+    __builtin_memcpy(&r, e, sizeof(raw));
+    *reinterpret_cast<raw*>(p) = r;
   }
 };
 
@@ -120,10 +116,9 @@ __device__ __forceinline__ void block_partials_out(const float* s, const float* 
 }
 
 // --------------------------------------------------------------- stats ------
-template <typename T>
+template <typename T, int V>
 __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, int64_t M, int C,
                                                        float* __restrict__ part) {
-  constexpr int V = Vec<T>::N;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const RowGeo g(C, V);
   float s[V], q[V];
@@ -138,8 +133,8 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, 
     for (; r + 3 * g.rpi < r1; r += 4 * g.rpi) {  // 4 independent 16-B loads in flight
       float f0[V], f1[V], f2[V], f3[V];
       const T* p = base + r * C;
-      Vec<T>::load(p, f0); Vec<T>::load(p + step, f1);
-      Vec<T>::load(p + 2 * step, f2); Vec<T>::load(p + 3 * step, f3);
+      VecIO<T, V>::load(p, f0); VecIO<T, V>::load(p + step, f1);
+      VecIO<T, V>::load(p + 2 * step, f2); VecIO<T, V>::load(p + 3 * step, f3);
 #pragma unroll
       for (int j = 0; j < V; ++j) {
         s[j] += (f0[j] + f1[j]) + (f2[j] + f3[j]);
@@ -148,7 +143,7 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, 
     }
     for (; r < r1; r += g.rpi) {
       float f[V];
-      Vec<T>::load(base + r * C, f);
+      VecIO<T, V>::load(base + r * C, f);
 #pragma unroll
       for (int j = 0; j < V; ++j) { s[j] += f[j]; q[j] += f[j] * f[j]; }
     }
@@ -275,31 +270,29 @@ __global__ void bn_eval_coeffs_kernel(int C, const float* __restrict__ w, const 
 }
 
 // --------------------------------------------------------------- apply ------
-template <typename T, int ACT, bool RES>
+template <typename T, int V, int ACT, bool RES>
 __device__ __forceinline__ void apply_one(const T* __restrict__ x, const T* __restrict__ res,
                                           const float* coef, T* __restrict__ y, int64_t i, int cv,
                                           int C) {
-  constexpr int V = Vec<T>::N;
   const int c0 = static_cast<int>(i % cv) * V;
   const int64_t off = (i / cv) * C + c0;
   float f[V], r[V];
-  Vec<T>::load(x + off, f);
-  if constexpr (RES) Vec<T>::load(res + off, r);
+  VecIO<T, V>::load(x + off, f);
+  if constexpr (RES) VecIO<T, V>::load(res + off, r);
 #pragma unroll
   for (int j = 0; j < V; ++j) {
     float z = f[j] * coef[c0 + j] + coef[C + c0 + j];
     if constexpr (RES) z += r[j];
     f[j] = act_fwd<ACT>(z);
   }
-  Vec<T>::store(y + off, f);
+  VecIO<T, V>::store(y + off, f);
 }
 
-template <typename T, int ACT, bool RES>
+template <typename T, int V, int ACT, bool RES>
 __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x,
                                                        const T* __restrict__ res,
                                                        const float* __restrict__ scale_shift,
                                                        T* __restrict__ y, int64_t M, int C) {
-  constexpr int V = Vec<T>::N;
   extern __shared__ __attribute__((aligned(16))) float coef[];  // [2][C]
   for (int c = threadIdx.x; c < 2 * C; c += blockDim.x) coef[c] = scale_shift[c];
   __syncthreads();
@@ -308,22 +301,21 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x,
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
   for (; i + stride < total; i += 2 * stride) {  // two vectors in flight per thread
-    apply_one<T, ACT, RES>(x, res, coef, y, i, cv, C);
-    apply_one<T, ACT, RES>(x, res, coef, y, i + stride, cv, C);
+    apply_one<T, V, ACT, RES>(x, res, coef, y, i, cv, C);
+    apply_one<T, V, ACT, RES>(x, res, coef, y, i + stride, cv, C);
   }
-  if (i < total) apply_one<T, ACT, RES>(x, res, coef, y, i, cv, C);
+  if (i < total) apply_one<T, V, ACT, RES>(x, res, coef, y, i, cv, C);
 }
 
 // ----------------------------------------------------------- backward -------
-template <typename T, int ACT, int MASK>
+template <typename T, int V, int ACT, int MASK>
 __device__ __forceinline__ void load_g(const T* dy, const T* x, const T* y, const float* coef, int C,
                                        int64_t off, int c0, float* g, float* xv) {
-  constexpr int V = Vec<T>::N;
-  Vec<T>::load(dy + off, g);
-  Vec<T>::load(x + off, xv);
+  VecIO<T, V>::load(dy + off, g);
+  VecIO<T, V>::load(x + off, xv);
   if constexpr (MASK == kMaskFromY) {
     float yv[V];
-    Vec<T>::load(y + off, yv);
+    VecIO<T, V>::load(y + off, yv);
 #pragma unroll
     for (int j = 0; j < V; ++j) g[j] = act_bwd_from_out<ACT>(g[j], yv[j]);
   } else if constexpr (MASK == kMaskFromX) {
@@ -333,12 +325,11 @@ __device__ __forceinline__ void load_g(const T* dy, const T* x, const T* y, cons
 }
 
 // slab[G][0:C] = sum g, slab[G][C:2C] = sum g * (x - mean)
-template <typename T, int ACT, int MASK>
+template <typename T, int V, int ACT, int MASK>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y,
     const float* __restrict__ mean_invstd, const float* __restrict__ scale_shift, int64_t M, int C,
     float* __restrict__ part) {
-  constexpr int V = Vec<T>::N;
   extern __shared__ __attribute__((aligned(16))) float sm[];  // coef[2C] | mean[C] | partials
   float* coef = sm;
   float* mu = sm + 2 * C;
@@ -359,8 +350,8 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     int64_t r = r0 + g.my_r;
     for (; r + g.rpi < r1; r += 2 * g.rpi) {  // two rows (4-6 loads) in flight
       float ga[V], xa[V], gb[V], xb[V];
-      load_g<T, ACT, MASK>(dy, x, y, coef, C, r * C + c0, c0, ga, xa);
-      load_g<T, ACT, MASK>(dy, x, y, coef, C, (r + g.rpi) * C + c0, c0, gb, xb);
+      load_g<T, V, ACT, MASK>(dy, x, y, coef, C, r * C + c0, c0, ga, xa);
+      load_g<T, V, ACT, MASK>(dy, x, y, coef, C, (r + g.rpi) * C + c0, c0, gb, xb);
 #pragma unroll
       for (int j = 0; j < V; ++j) {
         s[j] += ga[j] + gb[j];
@@ -369,7 +360,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     }
     if (r < r1) {
       float ga[V], xa[V];
-      load_g<T, ACT, MASK>(dy, x, y, coef, C, r * C + c0, c0, ga, xa);
+      load_g<T, V, ACT, MASK>(dy, x, y, coef, C, r * C + c0, c0, ga, xa);
 #pragma unroll
       for (int j = 0; j < V; ++j) { s[j] += ga[j]; q[j] += ga[j] * (xa[j] - m[j]); }
     }
@@ -412,30 +403,28 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(
   }
 }
 
-template <typename T, int ACT, int MASK, bool DRES>
+template <typename T, int V, int ACT, int MASK, bool DRES>
 __device__ __forceinline__ void bwd_apply_one(const T* dy, const T* x, const T* y, const float* coef,
                                               const float* mu, const float* k, T* dx, T* dres,
                                               int64_t i, int cv, int C) {
-  constexpr int V = Vec<T>::N;
   const int c0 = static_cast<int>(i % cv) * V;
   const int64_t off = (i / cv) * C + c0;
   float g[V], xv[V], o[V];
-  load_g<T, ACT, MASK>(dy, x, y, coef, C, off, c0, g, xv);
-  if constexpr (DRES) Vec<T>::store(dres + off, g);
+  load_g<T, V, ACT, MASK>(dy, x, y, coef, C, off, c0, g, xv);
+  if constexpr (DRES) VecIO<T, V>::store(dres + off, g);
 #pragma unroll
   for (int j = 0; j < V; ++j) {
     const int c = c0 + j;
     o[j] = k[c] * (g[j] - k[C + c] - (xv[j] - mu[c]) * k[2 * C + c]);
   }
-  Vec<T>::store(dx + off, o);
+  VecIO<T, V>::store(dx + off, o);
 }
 
-template <typename T, int ACT, int MASK, bool DRES>
+template <typename T, int V, int ACT, int MASK, bool DRES>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
     const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y,
     const float* __restrict__ mean_invstd, const float* __restrict__ scale_shift,
     const float* __restrict__ kcoef, T* __restrict__ dx, T* __restrict__ dres, int64_t M, int C) {
-  constexpr int V = Vec<T>::N;
   extern __shared__ __attribute__((aligned(16))) float sm[];  // coef[2C] | mu[C] | k[3C]
   float* coef = sm;
   float* mu = sm + 2 * C;
@@ -449,15 +438,24 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
   for (; i + stride < total; i += 2 * stride) {
-    bwd_apply_one<T, ACT, MASK, DRES>(dy, x, y, coef, mu, k, dx, dres, i, cv, C);
-    bwd_apply_one<T, ACT, MASK, DRES>(dy, x, y, coef, mu, k, dx, dres, i + stride, cv, C);
+    bwd_apply_one<T, V, ACT, MASK, DRES>(dy, x, y, coef, mu, k, dx, dres, i, cv, C);
+    bwd_apply_one<T, V, ACT, MASK, DRES>(dy, x, y, coef, mu, k, dx, dres, i + stride, cv, C);
   }
-  if (i < total) bwd_apply_one<T, ACT, MASK, DRES>(dy, x, y, coef, mu, k, dx, dres, i, cv, C);
+  if (i < total) bwd_apply_one<T, V, ACT, MASK, DRES>(dy, x, y, coef, mu, k, dx, dres, i, cv, C);
 }
 
 // ------------------------------------------------------------ launchers -----
+// Channel-vector width: the widest of {16 B, 8 B, 4 B, 1 element} that divides C
+// with at most 256 vectors per row (fp16 keeps the 16-byte path only).
+int bn_vec_width(int dtype, int C) {
+  if (dtype == kF16) return (C % 8 == 0 && C / 8 <= 256) ? 8 : 0;
+  for (int v = dtype == kF32 ? 4 : 8; v >= 1; v >>= 1)
+    if (C % v == 0 && C / v <= 256) return v;
+  return 0;
+}
+
 int bn_partial_grid(int64_t M, int C, int dtype) {
-  const int V = dtype == kF32 ? 4 : 8;
+  const int V = bn_vec_width(dtype, C);
   const int rpi = 256 / (C / V);
   int64_t g = (M + static_cast<int64_t>(rpi) * 32 - 1) / (static_cast<int64_t>(rpi) * 32);
   if (g > 512) g = 512;
@@ -465,18 +463,31 @@ int bn_partial_grid(int64_t M, int C, int dtype) {
   return static_cast<int>(g);
 }
 
-template <typename T>
-static void stats_t(const void* x, int64_t M, int C, float* part, int G, hipStream_t st) {
-  const int rpi = 256 / (C / Vec<T>::N);
-  const size_t lds = sizeof(float) * 2 * rpi * C;
-  bn_stats_kernel<T><<<G, 256, lds, st>>>(static_cast<const T*>(x), M, C, part);
+// Calls F.template operator()<T, V>() for the (dtype, width) of this layer.
+template <typename F>
+static void with_tv(int dtype, int C, F&& f) {
+  const int v = bn_vec_width(dtype, C);
+  if (dtype == kF32) {
+    if (v == 4) f.template operator()<float, 4>();
+    else if (v == 2) f.template operator()<float, 2>();
+    else f.template operator()<float, 1>();
+  } else if (dtype == kBF16) {
+    if (v == 8) f.template operator()<uint16_t, 8>();
+    else if (v == 4) f.template operator()<uint16_t, 4>();
+    else if (v == 2) f.template operator()<uint16_t, 2>();
+    else f.template operator()<uint16_t, 1>();
+  } else {
+    f.template operator()<_Float16, 8>();
+  }
 }
 
 void launch_bn_stats(const void* x, int dtype, int64_t M, int C, float* part, int G,
                      hipStream_t st) {
-  if (dtype == kF32) stats_t<float>(x, M, C, part, G, st);
-  else if (dtype == kBF16) stats_t<uint16_t>(x, M, C, part, G, st);
-  else stats_t<_Float16>(x, M, C, part, G, st);
+  with_tv(dtype, C, [&]<typename T, int V>() {
+    const int rpi = 256 / (C / V);
+    const size_t lds = sizeof(float) * 2 * rpi * C;
+    bn_stats_kernel<T, V><<<G, 256, lds, st>>>(static_cast<const T*>(x), M, C, part);
+  });
 }
 
 void launch_bn_finalize_partials(const float* part, int G, int C, double count, const float* w,
@@ -515,81 +526,68 @@ static int apply_grid(int64_t work) {
   return static_cast<int>(g);
 }
 
-template <typename T, int ACT>
+template <typename T, int V, int ACT>
 static void apply_t(const void* x, const void* res, const float* ss, void* y, int64_t M, int C,
                     hipStream_t st) {
-  const int64_t work = M * (C / Vec<T>::N);
+  const int64_t work = M * (C / V);
   const size_t lds = sizeof(float) * 2 * C;
   const int grid = apply_grid(work);
   if (res)
-    bn_apply_kernel<T, ACT, true><<<grid, 256, lds, st>>>(
+    bn_apply_kernel<T, V, ACT, true><<<grid, 256, lds, st>>>(
         static_cast<const T*>(x), static_cast<const T*>(res), ss, static_cast<T*>(y), M, C);
   else
-    bn_apply_kernel<T, ACT, false><<<grid, 256, lds, st>>>(
+    bn_apply_kernel<T, V, ACT, false><<<grid, 256, lds, st>>>(
         static_cast<const T*>(x), nullptr, ss, static_cast<T*>(y), M, C);
-}
-
-template <typename T>
-static void apply_act(const void* x, const void* res, const float* ss, void* y, int64_t M, int C,
-                      int act, hipStream_t st) {
-  if (act == kActReLU) apply_t<T, kActReLU>(x, res, ss, y, M, C, st);
-  else if (act == kActReLU6) apply_t<T, kActReLU6>(x, res, ss, y, M, C, st);
-  else apply_t<T, kActNone>(x, res, ss, y, M, C, st);
 }
 
 void launch_bn_apply(const void* x, const void* res, const float* scale_shift, void* y, int dtype,
                      int64_t M, int C, int act, hipStream_t st) {
-  if (dtype == kF32) apply_act<float>(x, res, scale_shift, y, M, C, act, st);
-  else if (dtype == kBF16) apply_act<uint16_t>(x, res, scale_shift, y, M, C, act, st);
-  else apply_act<_Float16>(x, res, scale_shift, y, M, C, act, st);
+  with_tv(dtype, C, [&]<typename T, int V>() {
+    if (act == kActReLU) apply_t<T, V, kActReLU>(x, res, scale_shift, y, M, C, st);
+    else if (act == kActReLU6) apply_t<T, V, kActReLU6>(x, res, scale_shift, y, M, C, st);
+    else apply_t<T, V, kActNone>(x, res, scale_shift, y, M, C, st);
+  });
 }
 
-template <typename T, int ACT, int MASK>
+template <typename T, int V, int ACT, int MASK>
 static void bwd_reduce_t(const void* dy, const void* x, const void* y, const float* mi,
                          const float* ss, int64_t M, int C, float* part, int G, hipStream_t st) {
-  const int rpi = 256 / (C / Vec<T>::N);
+  const int rpi = 256 / (C / V);
   const size_t lds = sizeof(float) * (3 * C + 2 * rpi * C);
-  bn_bwd_reduce_kernel<T, ACT, MASK><<<G, 256, lds, st>>>(
+  bn_bwd_reduce_kernel<T, V, ACT, MASK><<<G, 256, lds, st>>>(
       static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(y), mi, ss, M, C,
       part);
 }
 
-template <typename T, int ACT, int MASK, bool DRES>
+template <typename T, int V, int ACT, int MASK, bool DRES>
 static void bwd_apply_t(const void* dy, const void* x, const void* y, const float* mi,
                         const float* ss, const float* k, void* dx, void* dres, int64_t M, int C,
                         hipStream_t st) {
-  const int64_t work = M * (C / Vec<T>::N);
+  const int64_t work = M * (C / V);
   const size_t lds = sizeof(float) * 6 * C;
-  bn_bwd_apply_kernel<T, ACT, MASK, DRES><<<apply_grid(work), 256, lds, st>>>(
+  bn_bwd_apply_kernel<T, V, ACT, MASK, DRES><<<apply_grid(work), 256, lds, st>>>(
       static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(y), mi, ss, k,
       static_cast<T*>(dx), static_cast<T*>(dres), M, C);
 }
 
 #define RT_ACT_MASK_DISPATCH(FN, ...)                                                   \
   do {                                                                                  \
-    if (act == kActNone) FN<T, kActNone, kMaskNone>(__VA_ARGS__);                       \
+    if (act == kActNone) FN<T, V, kActNone, kMaskNone>(__VA_ARGS__);                    \
     else if (act == kActReLU) {                                                         \
-      if (mask == kMaskFromY) FN<T, kActReLU, kMaskFromY>(__VA_ARGS__);                 \
-      else FN<T, kActReLU, kMaskFromX>(__VA_ARGS__);                                    \
+      if (mask == kMaskFromY) FN<T, V, kActReLU, kMaskFromY>(__VA_ARGS__);              \
+      else FN<T, V, kActReLU, kMaskFromX>(__VA_ARGS__);                                 \
     } else {                                                                            \
-      if (mask == kMaskFromY) FN<T, kActReLU6, kMaskFromY>(__VA_ARGS__);                \
-      else FN<T, kActReLU6, kMaskFromX>(__VA_ARGS__);                                   \
+      if (mask == kMaskFromY) FN<T, V, kActReLU6, kMaskFromY>(__VA_ARGS__);             \
+      else FN<T, V, kActReLU6, kMaskFromX>(__VA_ARGS__);                                \
     }                                                                                   \
   } while (0)
-
-template <typename T>
-static void bwd_reduce_dispatch(const void* dy, const void* x, const void* y, const float* mi,
-                                const float* ss, int64_t M, int C, int act, int mask, float* part,
-                                int G, hipStream_t st) {
-  RT_ACT_MASK_DISPATCH(bwd_reduce_t, dy, x, y, mi, ss, M, C, part, G, st);
-}
 
 void launch_bn_bwd_reduce(const void* dy, const void* x, const void* y, const float* mean_invstd,
                           const float* scale_shift, int dtype, int64_t M, int C, int act, int mask,
                           float* part, int G, hipStream_t st) {
-  if (dtype == kF32) bwd_reduce_dispatch<float>(dy, x, y, mean_invstd, scale_shift, M, C, act, mask, part, G, st);
-  else if (dtype == kBF16) bwd_reduce_dispatch<uint16_t>(dy, x, y, mean_invstd, scale_shift, M, C, act, mask, part, G, st);
-  else bwd_reduce_dispatch<_Float16>(dy, x, y, mean_invstd, scale_shift, M, C, act, mask, part, G, st);
+  with_tv(dtype, C, [&]<typename T, int V>() {
+    RT_ACT_MASK_DISPATCH(bwd_reduce_t, dy, x, y, mean_invstd, scale_shift, M, C, part, G, st);
+  });
 }
 
 void launch_bn_bwd_finalize(const float* part, int G, const double* sums, const double* count_ptr,
@@ -599,27 +597,21 @@ void launch_bn_bwd_finalize(const float* part, int G, const double* sums, const 
                                                         mean_invstd, batch_stats, kcoef, dw, db);
 }
 
-template <typename T, int ACT, int MASK>
+template <typename T, int V, int ACT, int MASK>
 static void bwd_apply_res(const void* dy, const void* x, const void* y, const float* mi,
                           const float* ss, const float* k, void* dx, void* dres, int64_t M, int C,
                           hipStream_t st) {
-  if (dres) bwd_apply_t<T, ACT, MASK, true>(dy, x, y, mi, ss, k, dx, dres, M, C, st);
-  else bwd_apply_t<T, ACT, MASK, false>(dy, x, y, mi, ss, k, dx, dres, M, C, st);
-}
-
-template <typename T>
-static void bwd_apply_dispatch(const void* dy, const void* x, const void* y, const float* mi,
-                               const float* ss, const float* k, void* dx, void* dres, int64_t M,
-                               int C, int act, int mask, hipStream_t st) {
-  RT_ACT_MASK_DISPATCH(bwd_apply_res, dy, x, y, mi, ss, k, dx, dres, M, C, st);
+  if (dres) bwd_apply_t<T, V, ACT, MASK, true>(dy, x, y, mi, ss, k, dx, dres, M, C, st);
+  else bwd_apply_t<T, V, ACT, MASK, false>(dy, x, y, mi, ss, k, dx, dres, M, C, st);
 }
 
 void launch_bn_bwd_apply(const void* dy, const void* x, const void* y, const float* mean_invstd,
                          const float* scale_shift, const float* kcoef, void* dx, void* dres,
                          int dtype, int64_t M, int C, int act, int mask, hipStream_t st) {
-  if (dtype == kF32) bwd_apply_dispatch<float>(dy, x, y, mean_invstd, scale_shift, kcoef, dx, dres, M, C, act, mask, st);
-  else if (dtype == kBF16) bwd_apply_dispatch<uint16_t>(dy, x, y, mean_invstd, scale_shift, kcoef, dx, dres, M, C, act, mask, st);
-  else bwd_apply_dispatch<_Float16>(dy, x, y, mean_invstd, scale_shift, kcoef, dx, dres, M, C, act, mask, st);
+  with_tv(dtype, C, [&]<typename T, int V>() {
+    RT_ACT_MASK_DISPATCH(bwd_apply_res, dy, x, y, mean_invstd, scale_shift, kcoef, dx, dres, M, C,
+                         st);
+  });
 }
 
 }  // namespace rtseg

@@ -64,6 +64,14 @@ def _variant_kwargs(config, key):
 
 
 def get_model(config):
+    """Build the configured model; every BatchNorm2d is routed through the fused HIP
+    kernels (``ops.convert_batchnorm``; checkpoint-compatible)."""
+    from .. import ops
+
+    return ops.convert_batchnorm(_build_model(config))
+
+
+def _build_model(config):
     key = config.model
     if key == "smp":
         from .smp import build_smp_model
@@ -92,7 +100,10 @@ def get_teacher_model(config, device):
 
     if config.teacher_decoder not in DECODER_HUB:
         raise ValueError(f"Unsupported teacher decoder type: {config.teacher_decoder}")
-    model = build_smp_model(config.teacher_decoder, config.teacher_encoder, None, config.num_class)
+    from .. import ops
+
+    model = ops.convert_batchnorm(build_smp_model(config.teacher_decoder, config.teacher_encoder, None,
+                                                  config.num_class))
     ckpt_path = config.teacher_ckpt
     if ckpt_path:
         if not os.path.isfile(ckpt_path):

@@ -45,7 +45,7 @@ class ASPPPooling(nn.Sequential):
                          nn.BatchNorm2d(out_channels), nn.ReLU())
 
     def forward(self, x):
-        y = self[3](self[2](self[1](x.mean(dim=(2, 3), keepdim=True))))
+        y = ops.bn_act(self[1](x.mean(dim=(2, 3), keepdim=True)), self[2], "relu")
         return y.expand(-1, -1, x.shape[2], x.shape[3])
 
 

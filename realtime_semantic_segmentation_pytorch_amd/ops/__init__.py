@@ -9,7 +9,8 @@ from .interp import (interpolate, final_upsample, defer_final_upsample, Deferred
 from .seg_loss import (seg_cross_entropy, seg_cross_entropy_reference, MODE_OHEM, MODE_MEAN,
                        MODE_SUM)
 from .kd import kd_kl_div, kd_kl_div_reference
-from .bn import bn_act, act_code as bn_act_code, fused_ok as bn_fused_ok
+from .bn import (bn_act, act_code as bn_act_code, fused_ok as bn_fused_ok, convert_batchnorm,
+                 FusedBatchNorm2d, FusedSyncBatchNorm)
 from .confmat import confusion_matrix, confusion_matrix_reference
 
 __all__ = [
@@ -17,5 +18,5 @@ __all__ = [
     "interpolate", "final_upsample", "defer_final_upsample", "DeferredLogits", "materialize",
     "seg_cross_entropy", "seg_cross_entropy_reference", "MODE_OHEM", "MODE_MEAN", "MODE_SUM",
     "kd_kl_div", "kd_kl_div_reference", "confusion_matrix", "confusion_matrix_reference",
-    "bn_act", "bn_act_code", "bn_fused_ok",
+    "bn_act", "bn_act_code", "bn_fused_ok", "convert_batchnorm", "FusedBatchNorm2d", "FusedSyncBatchNorm",
 ]

@@ -3,8 +3,9 @@
 ``bn_act(x, bn, act, residual)`` computes ``act(BN(x) + residual)`` for a
 ``nn.BatchNorm2d`` / ``nn.SyncBatchNorm`` module ``bn`` (its running stats and
 ``num_batches_tracked`` are updated exactly like PyTorch's).  GPU fast path
-conditions: channels-last activations, C a multiple of 8 (4 for fp32) and
-<= 2048, activation in {none, relu, relu6}, ``momentum`` not None; anything
+conditions: channels-last activations, any C whose widest dividing channel
+vector (16/8/4 bytes or one element) leaves <= 256 vectors per row,
+activation in {none, relu, relu6}, ``momentum`` not None; anything
 else runs the stock PyTorch modules.
 
 SyncBN: per-channel (sum, sum of squares, count) are produced in fp64 by one
@@ -89,7 +90,7 @@ class _BNActFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, y, mi, ss, sums, weight = ctx.saved_tensors
-        dy = dy.contiguous(memory_format=torch.channels_last) if dy.dim() == 4 else dy.contiguous()
+        dy = _aligned_cl(dy)
         bsums = None
         if ctx.pg is not None:
             bsums = ops().bn_bwd_sums(dy, x, y, mi, ss, ctx.act, ctx.mask)
@@ -102,6 +103,24 @@ class _BNActFn(torch.autograd.Function):
                 dres if want_dres else None, None, None, None, None)
 
 
+def vec_width(dtype: torch.dtype, c: int) -> int:
+    """Channel-vector width the HIP kernels use (mirror of ``bn_vec_width``); 0 = unsupported."""
+    if dtype == torch.float16:
+        return 8 if c % 8 == 0 and c // 8 <= 256 else 0
+    v = 4 if dtype == torch.float32 else 8
+    while v >= 1:
+        if c % v == 0 and c // v <= 256:
+            return v
+        v //= 2
+    return 0
+
+
+def _aligned_cl(t: torch.Tensor) -> torch.Tensor:
+    t = t.contiguous(memory_format=torch.channels_last) if t.dim() == 4 else t.contiguous()
+    return t if t.data_ptr() % 16 == 0 else t.clone(memory_format=torch.channels_last if t.dim() == 4
+                                                      else torch.contiguous_format)
+
+
 def fused_ok(x: torch.Tensor, bn, act) -> bool:
     if not isinstance(bn, (nn.BatchNorm2d, nn.SyncBatchNorm)) or x.dim() != 4:
         return False
@@ -109,11 +128,9 @@ def fused_ok(x: torch.Tensor, bn, act) -> bool:
         return False
     if x.dtype not in (torch.float32, torch.bfloat16, torch.float16):
         return False
-    c = x.shape[1]
-    v = 4 if x.dtype == torch.float32 else 8
-    if c % v or c // v > 256 or x.numel() == 0:
+    if vec_width(x.dtype, x.shape[1]) == 0 or x.numel() == 0:
         return False
-    if not x.is_contiguous(memory_format=torch.channels_last):
+    if not x.is_contiguous(memory_format=torch.channels_last) or x.data_ptr() % 16:
         return False
     use_batch = bn.training or not bn.track_running_stats or bn.running_mean is None
     if not use_batch and bn.running_var is None:
@@ -127,7 +144,8 @@ def bn_act(x: torch.Tensor, bn, act=None, residual: Optional[torch.Tensor] = Non
     code = act if isinstance(act, int) else act_code(act)
     if use_hip(x) and code is not None and fused_ok(x, bn, code) and (
             residual is None or (residual.shape == x.shape
-                                 and residual.is_contiguous(memory_format=torch.channels_last))):
+                                 and residual.is_contiguous(memory_format=torch.channels_last)
+                                 and residual.data_ptr() % 16 == 0)):
         if residual is not None and residual.dtype != x.dtype:
             residual = residual.to(x.dtype)
         use_batch = bn.training or not bn.track_running_stats or bn.running_mean is None
@@ -147,3 +165,43 @@ def bn_act(x: torch.Tensor, bn, act=None, residual: Optional[torch.Tensor] = Non
     if callable(act):
         return act(y)
     raise ValueError(f"unsupported activation {act!r}")
+
+
+# --------------------------------------------------------------------------
+# Module-level routing: every BatchNorm2d of a model through the fused kernels.
+# --------------------------------------------------------------------------
+class FusedBatchNorm2d(nn.BatchNorm2d):
+    """``nn.BatchNorm2d`` whose forward runs the HIP kernels when possible.
+
+    Models call ``ops.bn_act`` at their conv-BN-act tails; BatchNorms that are
+    used as plain modules (``nn.Sequential(conv, BN, act)`` executed as a
+    Sequential, SMP-style blocks, attention branches on pooled maps) are routed
+    here by :func:`convert_batchnorm`.  Same parameters / buffers / state_dict.
+    """
+
+    def forward(self, x):
+        if use_hip(x) and fused_ok(x, self, ACT_NONE):
+            use_batch = self.training or not self.track_running_stats or self.running_mean is None
+            pg = _sync_group(self) if use_batch else None
+            return _BNActFn.apply(x, self.weight, self.bias, None, self, ACT_NONE, use_batch, pg)
+        return nn.BatchNorm2d.forward(self, x)
+
+
+class FusedSyncBatchNorm(nn.SyncBatchNorm):
+    def forward(self, x):
+        if use_hip(x) and fused_ok(x, self, ACT_NONE):
+            use_batch = self.training or not self.track_running_stats or self.running_mean is None
+            pg = _sync_group(self) if use_batch else None
+            return _BNActFn.apply(x, self.weight, self.bias, None, self, ACT_NONE, use_batch, pg)
+        return nn.SyncBatchNorm.forward(self, x)
+
+
+def convert_batchnorm(model: nn.Module) -> nn.Module:
+    """Swap the class of every BatchNorm2d / SyncBatchNorm in ``model`` to the fused
+    variant (in place; parameters, buffers and checkpoint keys are unchanged)."""
+    for m in model.modules():
+        if type(m) is nn.BatchNorm2d:
+            m.__class__ = FusedBatchNorm2d
+        elif type(m) is nn.SyncBatchNorm:
+            m.__class__ = FusedSyncBatchNorm
+    return model

@@ -65,7 +65,7 @@ def _digest(paths, flags) -> str:
 
 def _kernel_flags():
     return [
-        "-c", "-fPIC", "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-mcode-object-version=5",
+        "-c", "-fPIC", "-O3", "-std=c++20", f"--offload-arch={ARCH}", "-mcode-object-version=5",
         "-ffp-contract=fast", "-munsafe-fp-atomics", "-Wno-unused-result",
         "-I", os.path.join(CSRC, "include"),
     ]

@@ -98,6 +98,8 @@ def parallel_model(config, model, rank, device):
     sync = bool(config.synBN) and device.type == "cuda"
     if sync:
         model = nn.SyncBatchNorm.convert_sync_batchnorm(model)
+        from ..ops import convert_batchnorm
+        convert_batchnorm(model)  # SyncBN -> fused HIP SyncBN (one fp64 all-reduce per layer)
     model = model.to(device)
     kw = dict(bucket_cap_mb=int(getattr(config, "ddp_bucket_mb", 100)),
               gradient_as_bucket_view=True,

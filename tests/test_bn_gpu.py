@@ -25,7 +25,9 @@ def _ref(x, bn, act, res):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("act", ["none", "relu", "relu6"])
 @pytest.mark.parametrize("with_res", [False, True])
-@pytest.mark.parametrize("shape", [(2, 64, 17, 33), (3, 256, 8, 8), (1, 1024, 4, 6), (4, 16, 32, 32)])
+@pytest.mark.parametrize("shape", [(2, 64, 17, 33), (3, 256, 8, 8), (1, 1024, 4, 6), (4, 16, 32, 32),
+                                   (2, 12, 9, 10), (2, 19, 16, 16), (2, 3, 5, 7), (2, 250, 1, 1), (3, 131, 4, 4),
+                                   (2, 36, 8, 8)])
 def test_bn_act_train(dtype, act, with_res, shape):
     assert ops.load()
     torch.manual_seed(0)
@@ -41,6 +43,7 @@ def test_bn_act_train(dtype, act, with_res, shape):
     x.requires_grad_(True)
     if res is not None:
         res.requires_grad_(True)
+    assert ops.bn_fused_ok(x, bn, ops.bn_act_code(act))  # the HIP path, not the fallback
     y = ops.bn_act(x, bn, act, residual=res)
     xr = x.detach().float().requires_grad_(True)
     rr = res.detach().float().requires_grad_(True) if res is not None else None
@@ -109,3 +112,28 @@ def test_convbnact_module_fused_matches_unfused():
     for (n, p), (_, q) in zip(blk.named_parameters(), ref.named_parameters()):
         torch.testing.assert_close(p.grad, q.grad, atol=2e-3 * q.grad.abs().max().item() + 1e-6,
                                    rtol=2e-3, msg=n)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(2, 256, 1, 1), (4, 19, 16, 16), (2, 48, 32, 32)])
+def test_fused_batchnorm_module_matches_torch(dtype, shape):
+    """ops.convert_batchnorm routes plain BatchNorm2d modules (e.g. pooled attention
+    branches) through the HIP kernels, train and eval."""
+    torch.manual_seed(0)
+    ref = nn.BatchNorm2d(shape[1]).to(DEV)
+    mod = ops.convert_batchnorm(nn.Sequential(copy.deepcopy(ref)))[0]
+    assert isinstance(mod, ops.FusedBatchNorm2d)
+    x = torch.randn(shape, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    assert ops.bn_fused_ok(x, mod, 0)
+    for train in (True, False):
+        ref.train(train), mod.train(train)
+        xa = x.clone().requires_grad_(True)
+        xb = x.float().clone().requires_grad_(True)
+        ya, yb = mod(xa), ref(xb)
+        tol = 1e-4 if dtype == torch.float32 else 3e-2
+        torch.testing.assert_close(ya.float(), yb, atol=tol, rtol=tol)
+        g = torch.randn(shape, device=DEV)
+        ya.backward(g.to(dtype).contiguous(memory_format=torch.channels_last))
+        yb.backward(g)
+        torch.testing.assert_close(xa.grad.float(), xb.grad, atol=10 * tol, rtol=10 * tol)
+    torch.testing.assert_close(mod.running_mean, ref.running_mean, atol=1e-4, rtol=1e-4)
