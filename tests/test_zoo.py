@@ -99,33 +99,39 @@ def _rel(a, b):
 @pytest.mark.gpu
 @pytest.mark.parametrize("key", KEYS)
 def test_zoo_hip_matches_torch_path_gpu(key, monkeypatch):
-    """Eval forward must agree tightly.  Train-mode fwd/bwd is compared against the
-    run-to-run noise of the torch path itself (MIOpen backward kernels use atomics,
-    and tiny-batch BatchNorm -- e.g. DFANet's FC attention over 2 samples -- amplifies
-    that noise by orders of magnitude)."""
-    base = _model(key).cuda().to(memory_format=torch.channels_last)
-    x = torch.randn(2, 3, *HW, device="cuda").contiguous(memory_format=torch.channels_last)
-    labels = torch.randint(0, 19, (2, *HW), device="cuda")
+    """Eval forward: HIP path == torch path (tight).  Train fwd/bwd: both GPU paths are
+    scored against a CPU fp64 run of the same model -- several zoo models have fp32
+    gradient errors of ~1e-3 on either path (ill-conditioned tiny-batch BatchNorm,
+    MIOpen algorithm choice), so the HIP path must be as accurate as the torch path."""
+    torch.manual_seed(0)
+    cpu = _model(key)
+    for mod in cpu.modules():  # CPU and GPU RNG streams differ: compare without dropout
+        if isinstance(mod, torch.nn.modules.dropout._DropoutNd):
+            mod.p = 0.0
+    x = torch.randn(2, 3, *HW)
+    labels = torch.randint(0, 19, (2, *HW))
+    base = copy.deepcopy(cpu).cuda().to(memory_format=torch.channels_last)
+    xg = x.cuda().contiguous(memory_format=torch.channels_last)
     # eval: deterministic, tight
     ev = copy.deepcopy(base).eval()
     with torch.no_grad():
         monkeypatch.delenv("RTSEG_DISABLE_HIP", raising=False)
-        e_h = _main(ev(x)).float()
+        e_h = _main(ev(xg)).float()
         monkeypatch.setenv("RTSEG_DISABLE_HIP", "1")
-        e_t = _main(ev(x)).float()
+        e_t = _main(ev(xg)).float()
         monkeypatch.delenv("RTSEG_DISABLE_HIP", raising=False)
     assert _rel(e_h, e_t) < 2e-5
-    # train: relative to torch-vs-torch noise
+    # train: accuracy against fp64
+    y_r, l_r, g_r = _run_gpu(copy.deepcopy(cpu).train().double(), x.double(), labels, False, monkeypatch)
     base.train()
-    y_h, l_h, g_h = _run_gpu(copy.deepcopy(base), x, labels, False, monkeypatch)
-    y_t, l_t, g_t = _run_gpu(copy.deepcopy(base), x, labels, True, monkeypatch)
-    y_n, l_n, g_n = _run_gpu(copy.deepcopy(base), x, labels, True, monkeypatch)
-    assert g_h.keys() == g_t.keys()
-    cat = lambda g: torch.cat([v.flatten().float() for v in g.values()])  # noqa: E731
-    noise_y, noise_g = _rel(y_n, y_t), _rel(cat(g_n), cat(g_t))
-    assert _rel(y_h, y_t) <= 5 * noise_y + 1e-4
-    assert abs(l_h.item() - l_t.item()) <= 5 * abs(l_n.item() - l_t.item()) + 1e-4 * abs(l_t.item()) + 1e-6
-    assert _rel(cat(g_h), cat(g_t)) <= 5 * noise_g + 2e-3
+    y_h, l_h, g_h = _run_gpu(copy.deepcopy(base), xg, labels.cuda(), False, monkeypatch)
+    y_t, l_t, g_t = _run_gpu(copy.deepcopy(base), xg, labels.cuda(), True, monkeypatch)
+    assert g_h.keys() == g_t.keys() == g_r.keys()
+    cat = lambda g: torch.cat([g[n].flatten().double().cpu() for n in g_r])  # noqa: E731
+    err = lambda a, b: ((a.double().cpu() - b.double().cpu()).norm() / (b.double().cpu().norm() + 1e-30)).item()  # noqa: E731
+    assert err(y_h, y_r) <= 2 * err(y_t, y_r) + 1e-5
+    assert abs(l_h.item() - l_r.item()) <= 2 * abs(l_t.item() - l_r.item()) + 1e-5 * abs(l_r.item())
+    assert err(cat(g_h), cat(g_r)) <= 2 * err(cat(g_t), cat(g_r)) + 1e-4
 
 
 @pytest.mark.gpu

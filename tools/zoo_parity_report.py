@@ -49,11 +49,15 @@ def main():
         yt, lt, gt = run(copy.deepcopy(base), x, labels, True)
         yt2, lt2, gt2 = run(copy.deepcopy(base), x, labels, True)
         cat = lambda g: torch.cat([v.flatten() for v in g.values()])  # noqa: E731
-        worst = sorted(((rel(gh[n], gt[n]), n) for n in gt), reverse=True)[:4]
+        gmax = max(v.norm().item() for v in gt.values())
+        worst = sorted(((rel(gh[n], gt[n]), n) for n in gt if gt[n].norm() > 1e-3 * gmax), reverse=True)[:4]
         print(f"{key:12s} out {rel(yh, yt):.2e} loss {abs(lh - lt) / abs(lt):.2e} grads {rel(cat(gh), cat(gt)):.2e}"
               f" | noise out {rel(yt2, yt):.2e} grads {rel(cat(gt2), cat(gt)):.2e}", flush=True)
         for e, n in worst:
             print(f"      {e:.2e} {n} |g|={gt[n].norm():.2e} noise {rel(gt2[n], gt[n]):.2e}", flush=True)
+        if os.environ.get("ZOO_VERBOSE"):
+            for n in gt:  # forward order: the deviation starts downstream of the last clean layer
+                print(f"        {rel(gh[n], gt[n]):.2e} (noise {rel(gt2[n], gt[n]):.2e}) {n}", flush=True)
 
 
 if __name__ == "__main__":
