@@ -121,6 +121,7 @@ class BaseConfig:
         self.amp_dtype = "bf16"          # autocast dtype when amp_training: 'bf16' | 'fp16'
         self.channels_last = True        # NHWC activations (MIOpen/HIP kernels prefer it)
         self.fused_loss = True           # fold the final upsample into the HIP loss kernel
+        self.fused_optimizer = True      # HIP multi-tensor optimizer step that also writes the EMA
         self.ddp_bucket_mb = 100         # gradient bucket size for the RCCL all-reduce
         self.ddp_static_graph = True
         self.synthetic_data = False      # device-generated synthetic batches (benchmarks)

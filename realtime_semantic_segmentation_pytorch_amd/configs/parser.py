@@ -46,7 +46,7 @@ _SPEC = [
     # validating
     ("val_bs", int, {}), ("begin_val_epoch", int, {}), ("val_interval", int, {}),
     # testing
-    ("is_testing", "true", {}), ("test_bs", int, {}), ("test_data_folder", str, {}),
+    ("is_testing", "true", {}), ("train", "true", {"dest": "train_mode"}), ("test_bs", int, {}), ("test_data_folder", str, {}),
     ("colormap", str, {"choices": ["cityscapes", "custom"]}), ("save_mask", "false", {}),
     ("blend_prediction", "false", {}), ("blend_alpha", float, {}),
     # loss
@@ -81,6 +81,7 @@ _SPEC = [
     ("no_fused_loss", "true", {"dest": "no_fused_loss"}), ("ddp_bucket_mb", int, {}),
     ("synthetic_data", "true", {}), ("synthetic_len", int, {}), ("max_train_itrs", int, {}),
     ("log_interval", int, {}), ("device", str, {}),
+    ("no_fused_optimizer", "true", {"dest": "no_fused_optimizer"}),
 ]
 
 
@@ -111,6 +112,10 @@ def load_parser(config, argv=None):
             config.channels_last = not v
         elif k == "no_fused_loss":
             config.fused_loss = not v
+        elif k == "no_fused_optimizer":
+            config.fused_optimizer = not v
+        elif k == "train_mode":  # MyConfig defaults to prediction (reference my_config.py:27)
+            config.is_testing = not v
         else:
             setattr(config, k, v)
     return config

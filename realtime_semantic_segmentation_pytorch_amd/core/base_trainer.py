@@ -63,6 +63,9 @@ class BaseTrainer:
             if self._resume_state is not None and self._resume_state.get("ema_state_dict") is not None:
                 self.ema_model.ema.load_state_dict(self._resume_state["ema_state_dict"])
             self._resume_state = None
+            # fp16 GradScaler may skip a step -> keep the EMA out of the optimizer in that mode
+            self.ema_fused = (not self.scaler.is_enabled()) and self.device.type == "cuda" and \
+                self.ema_model.attach(self.optimizer, self.model)
 
     # ------------------------------------------------------------------ run
     def run(self, config):

@@ -108,13 +108,16 @@ class SegTrainer(BaseTrainer):
         self.optimizer.zero_grad(set_to_none=True)
         loss, _, extras = self.compute_loss(images, masks)
         self.scaler.scale(loss).backward()
+        if self.ema_fused:  # the fused optimizer writes the parameter EMAs in its own launch
+            self.optimizer.ema_weight = 1.0 - self.ema_model.decay(self.train_itrs + 1)
         self.scaler.step(self.optimizer)
         self.scaler.update()
         total = getattr(self.scheduler, "total_steps", None)
         if total is None or self.scheduler.last_epoch < total:  # never step OneCycle past its end
             self.scheduler.step()
         self.train_itrs += 1
-        self.ema_model.update(self.model, self.train_itrs)
+        self.ema_model.update(self.model, self.train_itrs,
+                              params_done=self.ema_fused and getattr(self.optimizer, "last_step_fused", False))
         return loss.detach(), extras
 
     # ----------------------------------------------------------------- epoch

@@ -1,0 +1,222 @@
+// torch.library registration of the KD-loss, confusion-matrix and fused
+// optimizer/EMA operators (kernels: kd_metrics.hip, optim.hip).
+#include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <torch/library.h>
+
+#include "rtseg_launch.h"
+#include "rtseg_ops.h"
+
+namespace rtseg {
+
+static void check_pair(const at::Tensor& s, const at::Tensor& t) {
+  TORCH_CHECK(s.dim() == 4 && t.dim() == 4 && s.sizes() == t.sizes(),
+              "rtseg.kd: student/teacher logits must both be [N,C,H,W] of equal shape");
+  TORCH_CHECK(s.scalar_type() == t.scalar_type(), "rtseg.kd: student/teacher dtype mismatch");
+  TORCH_CHECK(s.is_cuda() && t.is_cuda() && s.device() == t.device(), "rtseg.kd: tensors on different devices");
+}
+
+// -> (loss scalar fp32, lse [2, N*H*W] fp32)
+static std::tuple<at::Tensor, at::Tensor> kd_kl_fwd(const at::Tensor& s, const at::Tensor& t, double temperature) {
+  check_pair(s, t);
+  TORCH_CHECK(temperature > 0.0, "rtseg.kd: temperature must be > 0");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(s.device());
+  const int64_t npix = s.size(0) * s.size(2) * s.size(3);
+  auto f32 = s.options().dtype(at::kFloat);
+  at::Tensor loss = at::empty({}, f32);
+  at::Tensor lse = at::empty({2, npix}, f32);
+  at::Tensor part = at::empty({kd_partial_blocks(npix)}, s.options().dtype(at::kDouble));
+  launch_kd_fwd(view4(s), view4(t), static_cast<float>(temperature), lse.data_ptr<float>(),
+                part.data_ptr<double>(), loss.data_ptr<float>(), cur_stream());
+  return {loss, lse};
+}
+
+static at::Tensor kd_kl_bwd(const at::Tensor& grad, const at::Tensor& s, const at::Tensor& t,
+                            const at::Tensor& lse, double temperature) {
+  check_pair(s, t);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(s.device());
+  const int64_t npix = s.size(0) * s.size(2) * s.size(3);
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == 2 * npix,
+              "rtseg.kd_bwd: bad lse workspace");
+  at::Tensor g32 = grad.to(at::kFloat).contiguous();
+  at::Tensor gs = at::empty(s.sizes(), s.options().memory_format(s.suggest_memory_format()));
+  launch_kd_bwd(view4(s), view4(t), view4(gs), static_cast<float>(temperature), lse.data_ptr<float>(),
+                g32.data_ptr<float>(), cur_stream());
+  return gs;
+}
+
+// cm[target, argmax_c x] as int64 [C, C]
+static at::Tensor confmat(const at::Tensor& x, const at::Tensor& target, int64_t num_class, int64_t ignore) {
+  TORCH_CHECK(x.dim() == 4 && x.size(1) == num_class, "rtseg.confmat: logits must be [N, num_class, H, W]");
+  TORCH_CHECK(target.scalar_type() == at::kLong && target.is_contiguous() && target.dim() == 3 &&
+                  target.size(0) == x.size(0) && target.size(1) == x.size(2) && target.size(2) == x.size(3),
+              "rtseg.confmat: target must be contiguous int64 [N, H, W] matching the logits");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  at::Tensor cm = at::zeros({num_class, num_class}, x.options().dtype(at::kLong));
+  launch_confmat(view4(x), target.data_ptr<int64_t>(), static_cast<int>(ignore),
+                 reinterpret_cast<unsigned long long*>(cm.data_ptr<int64_t>()), cur_stream());
+  return cm;
+}
+
+static OptHyper hyper(int64_t mode, double lr, double momentum, double dampening, double weight_decay,
+                      bool nesterov, double beta1, double beta2, double eps, double step_size,
+                      double inv_sqrt_bc2, double grad_scale, double ema_w) {
+  TORCH_CHECK(mode >= 0 && mode <= 2, "rtseg.fused_opt: bad mode");
+  OptHyper h;
+  h.mode = static_cast<int>(mode);
+  h.lr = static_cast<float>(lr);
+  h.momentum = static_cast<float>(momentum);
+  h.dampening = static_cast<float>(dampening);
+  h.weight_decay = static_cast<float>(weight_decay);
+  h.nesterov = nesterov ? 1 : 0;
+  h.beta1 = static_cast<float>(beta1);
+  h.beta2 = static_cast<float>(beta2);
+  h.eps = static_cast<float>(eps);
+  h.step_size = static_cast<float>(step_size);
+  h.inv_sqrt_bc2 = static_cast<float>(inv_sqrt_bc2);
+  h.grad_scale = static_cast<float>(grad_scale);
+  h.ema_w = static_cast<float>(ema_w);
+  return h;
+}
+
+static void check_meta(const at::Tensor& meta, int64_t ntensor, int64_t nblocks) {
+  TORCH_CHECK(meta.is_cuda() && meta.scalar_type() == at::kLong && meta.is_contiguous() &&
+                  meta.numel() == ntensor * kOptMetaFields + 2 * nblocks,
+              "rtseg.fused_opt: malformed tensor table");
+}
+
+static void fused_opt_step(const at::Tensor& meta, int64_t ntensor, int64_t nblocks, int64_t mode, double lr,
+                           double momentum, double dampening, double weight_decay, bool nesterov, double beta1,
+                           double beta2, double eps, double step_size, double inv_sqrt_bc2, double grad_scale,
+                           double ema_w) {
+  check_meta(meta, ntensor, nblocks);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(meta.device());
+  launch_fused_opt(meta.data_ptr<int64_t>(), static_cast<int>(ntensor), static_cast<int>(nblocks),
+                   hyper(mode, lr, momentum, dampening, weight_decay, nesterov, beta1, beta2, eps, step_size,
+                         inv_sqrt_bc2, grad_scale, ema_w),
+                   cur_stream());
+}
+
+static void ema_lerp(const at::Tensor& meta, int64_t ntensor, int64_t nblocks, double w) {
+  check_meta(meta, ntensor, nblocks);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(meta.device());
+  launch_ema_lerp(meta.data_ptr<int64_t>(), static_cast<int>(ntensor), static_cast<int>(nblocks),
+                  static_cast<float>(w), cur_stream());
+}
+
+}  // namespace rtseg
+
+TORCH_LIBRARY_FRAGMENT(rtseg, m) {
+  m.def("kd_kl_fwd(Tensor s, Tensor t, float temperature) -> (Tensor, Tensor)");
+  m.def("kd_kl_bwd(Tensor grad, Tensor s, Tensor t, Tensor lse, float temperature) -> Tensor");
+  m.def("confmat(Tensor x, Tensor target, int num_class, int ignore_index) -> Tensor");
+  m.def("fused_opt_step(Tensor meta, int ntensor, int nblocks, int mode, float lr, float momentum, "
+        "float dampening, float weight_decay, bool nesterov, float beta1, float beta2, float eps, "
+        "float step_size, float inv_sqrt_bc2, float grad_scale, float ema_w) -> ()");
+  m.def("ema_lerp(Tensor meta, int ntensor, int nblocks, float w) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
+  m.impl("kd_kl_fwd", &rtseg::kd_kl_fwd);
+  m.impl("kd_kl_bwd", &rtseg::kd_kl_bwd);
+  m.impl("confmat", &rtseg::confmat);
+  m.impl("fused_opt_step", &rtseg::fused_opt_step);
+  m.impl("ema_lerp", &rtseg::ema_lerp);
+}
+
+// ------------------------------ depth-wise conv (dwconv.hip) -------------------------
+namespace rtseg {
+
+static void check_cl(const at::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.dim() == 4 && t.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "rtseg.dwconv: ", what, " must be a channels-last contiguous 4-D GPU tensor");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "rtseg.dwconv: ", what,
+              " must be 16-byte aligned");
+}
+
+static DwGeom dw_geom(int64_t n, int64_t cin, int64_t h, int64_t w, int64_t cout, int64_t kh, int64_t kw,
+                      int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw) {
+  TORCH_CHECK(cin > 0 && cout % cin == 0, "rtseg.dwconv: out_channels must be a multiple of in_channels");
+  TORCH_CHECK(kh > 0 && kw > 0 && sh > 0 && sw > 0 && dh > 0 && dw > 0 && ph >= 0 && pw >= 0,
+              "rtseg.dwconv: bad geometry");
+  DwGeom g;
+  g.n = static_cast<int>(n); g.cin = static_cast<int>(cin); g.h = static_cast<int>(h); g.w = static_cast<int>(w);
+  g.cout = static_cast<int>(cout); g.mult = static_cast<int>(cout / cin);
+  g.kh = static_cast<int>(kh); g.kw = static_cast<int>(kw); g.sh = static_cast<int>(sh); g.sw = static_cast<int>(sw);
+  g.ph = static_cast<int>(ph); g.pw = static_cast<int>(pw); g.dh = static_cast<int>(dh); g.dw = static_cast<int>(dw);
+  g.ho = static_cast<int>((h + 2 * ph - dh * (kh - 1) - 1) / sh + 1);
+  g.wo = static_cast<int>((w + 2 * pw - dw * (kw - 1) - 1) / sw + 1);
+  TORCH_CHECK(g.ho > 0 && g.wo > 0, "rtseg.dwconv: empty output");
+  return g;
+}
+
+static void check_wt(const at::Tensor& wt, int64_t taps, int64_t cout) {
+  TORCH_CHECK(wt.is_cuda() && wt.scalar_type() == at::kFloat && wt.is_contiguous() && wt.dim() == 2 &&
+                  wt.size(0) == taps && wt.size(1) == cout,
+              "rtseg.dwconv: weights must be tap-major fp32 [KH*KW, Cout]");
+}
+
+static at::Tensor dw_conv_fwd(const at::Tensor& x, const at::Tensor& wt, const std::optional<at::Tensor>& bias,
+                              int64_t cout, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
+                              int64_t dh, int64_t dw) {
+  check_cl(x, "input");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  DwGeom g = dw_geom(x.size(0), x.size(1), x.size(2), x.size(3), cout, kh, kw, sh, sw, ph, pw, dh, dw);
+  check_wt(wt, kh * kw, cout);
+  const float* b = nullptr;
+  if (bias.has_value()) {
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->is_contiguous() && bias->numel() == cout,
+                "rtseg.dwconv: bias must be fp32 [Cout]");
+    b = bias->data_ptr<float>();
+  }
+  at::Tensor y = at::empty({x.size(0), cout, g.ho, g.wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  launch_dw_fwd(g, dtype_code(x), x.data_ptr(), wt.data_ptr<float>(), b, y.data_ptr(), cur_stream());
+  return y;
+}
+
+static at::Tensor dw_conv_dgrad(const at::Tensor& dy, const at::Tensor& wt, int64_t cin, int64_t h, int64_t w,
+                                int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh,
+                                int64_t dw) {
+  check_cl(dy, "grad_output");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  DwGeom g = dw_geom(dy.size(0), cin, h, w, dy.size(1), kh, kw, sh, sw, ph, pw, dh, dw);
+  TORCH_CHECK(g.ho == dy.size(2) && g.wo == dy.size(3), "rtseg.dwconv: grad_output shape mismatch");
+  check_wt(wt, kh * kw, dy.size(1));
+  at::Tensor dx = at::empty({dy.size(0), cin, h, w}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  launch_dw_dgrad(g, dtype_code(dy), dy.data_ptr(), wt.data_ptr<float>(), dx.data_ptr(), cur_stream());
+  return dx;
+}
+
+static at::Tensor dw_conv_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t kh, int64_t kw, int64_t sh,
+                                int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw) {
+  check_cl(dy, "grad_output");
+  check_cl(x, "input");
+  TORCH_CHECK(dy.scalar_type() == x.scalar_type(), "rtseg.dwconv: dtype mismatch");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  DwGeom g = dw_geom(x.size(0), x.size(1), x.size(2), x.size(3), dy.size(1), kh, kw, sh, sw, ph, pw, dh, dw);
+  TORCH_CHECK(g.ho == dy.size(2) && g.wo == dy.size(3) && dy.size(0) == x.size(0),
+              "rtseg.dwconv: grad_output shape mismatch");
+  const DwWgradPlan p = dw_wgrad_plan(g, dtype_code(x));
+  auto f32 = x.options().dtype(at::kFloat);
+  at::Tensor part = at::empty({static_cast<int64_t>(p.slices) * kh * kw * g.cout}, f32);
+  at::Tensor dwt = at::empty({g.cout, 1, kh, kw}, f32);
+  launch_dw_wgrad(g, dtype_code(x), dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(), dwt.data_ptr<float>(),
+                  cur_stream());
+  return dwt;
+}
+
+}  // namespace rtseg
+
+TORCH_LIBRARY_FRAGMENT(rtseg, m) {
+  m.def("dw_conv_fwd(Tensor x, Tensor wt, Tensor? bias, int cout, int kh, int kw, int sh, int sw, int ph, int pw, "
+        "int dh, int dw) -> Tensor");
+  m.def("dw_conv_dgrad(Tensor dy, Tensor wt, int cin, int h, int w, int kh, int kw, int sh, int sw, int ph, "
+        "int pw, int dh, int dw) -> Tensor");
+  m.def("dw_conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw) -> Tensor");
+}
+
+TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
+  m.impl("dw_conv_fwd", &rtseg::dw_conv_fwd);
+  m.impl("dw_conv_dgrad", &rtseg::dw_conv_dgrad);
+  m.impl("dw_conv_wgrad", &rtseg::dw_conv_wgrad);
+}

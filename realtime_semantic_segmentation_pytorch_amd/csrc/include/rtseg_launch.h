@@ -83,4 +83,51 @@ void launch_bn_bwd_apply(const void* dy, const void* x, const void* y, const flo
                          const float* scale_shift, const float* kcoef, void* dx, void* dres,
                          int dtype, int64_t M, int C, int act, int mask, hipStream_t st);
 
+
+// ---- kd_metrics.hip ---------------------------------------------------------
+int kd_partial_blocks(int64_t npix);
+// lse: [2, N*H*W] fp32 (student, teacher log-sum-exp of z/T); part: [kd_partial_blocks] fp64
+void launch_kd_fwd(const Tensor4& s, const Tensor4& t, float temperature, float* lse, double* part,
+                   float* out, hipStream_t st);
+void launch_kd_bwd(const Tensor4& s, const Tensor4& t, const Tensor4& gs, float temperature,
+                   const float* lse, const float* gout, hipStream_t st);
+// cm: [C, C] uint64 (accumulated, caller zeroes), target: [N, H, W] int64 contiguous
+void launch_confmat(const Tensor4& x, const int64_t* target, int ignore, unsigned long long* cm,
+                    hipStream_t st);
+
+// ---- optim.hip --------------------------------------------------------------
+// Tensor table row: {param f32*, grad*, state1 f32*, state2 f32*, ema f32*, numel, grad_is_bf16,
+// first_step}; followed by a [nblocks, 2] (tensor, chunk-start) map.
+constexpr int kOptMetaFields = 8;
+constexpr int64_t kOptChunk = 16384;
+enum OptMode : int { kOptSGD = 0, kOptAdam = 1, kOptAdamW = 2 };
+struct OptHyper {
+  int mode;
+  float lr, momentum, dampening, weight_decay;
+  int nesterov;
+  float beta1, beta2, eps, step_size, inv_sqrt_bc2;
+  float grad_scale;
+  float ema_w;  // 1 - decay (1 => copy)
+};
+void launch_fused_opt(const int64_t* meta, int ntensor, int nblocks, const OptHyper& hp, hipStream_t st);
+void launch_ema_lerp(const int64_t* meta, int ntensor, int nblocks, float w, hipStream_t st);
+
+// ---- dwconv.hip -------------------------------------------------------------
+// Depth-wise conv geometry; activations channels-last, weights tap-major fp32 [KH*KW][Cout].
+struct DwGeom {
+  int n, h, w, cin, cout, mult;  // mult = cout / cin
+  int ho, wo, kh, kw, sh, sw, ph, pw, dh, dw;
+};
+struct DwWgradPlan {
+  int vec, lanes, chunks, tap_groups, slices;
+};
+int dw_vec(int dtype, int c);
+DwWgradPlan dw_wgrad_plan(const DwGeom& g, int dtype);
+void launch_dw_fwd(const DwGeom& g, int dtype, const void* x, const float* wt, const float* bias, void* y,
+                   hipStream_t st);
+void launch_dw_dgrad(const DwGeom& g, int dtype, const void* dy, const float* wt, void* dx, hipStream_t st);
+// part: [slices, KH*KW, Cout] fp32 workspace; dw: [Cout, KH*KW] fp32
+void launch_dw_wgrad(const DwGeom& g, int dtype, const void* dy, const void* x, float* part, float* dw,
+                     hipStream_t st);
+
 }  // namespace rtseg

@@ -1,0 +1,199 @@
+// Knowledge-distillation KL loss and the mIoU confusion matrix for CDNA4 (gfx950).
+//
+// KD (reference core/loss.py:80-88):
+//   loss = T^2 / (N*C*H*W) * sum_{n,h,w} KL( softmax(t/T) || softmax(s/T) )
+// Per pixel  KL = sum_c p_t,c (b_c - a_c) - lse(b) + lse(a),   a = s/T, b = t/T,
+// so the forward needs one max pass and one exp pass over the C logits of both
+// tensors (the second pass hits L1/L2).  The forward stores lse(a), lse(b) per
+// pixel, which makes the backward a single streaming pass:
+//   dL/ds_c = g * T / numel * (exp(a_c - lse_a) - exp(b_c - lse_b)).
+// Partial sums are per block (fp64) and reduced by one finalize block, so the
+// loss is deterministic and never touches the host.
+//
+// Confusion matrix (reference utils/metrics.py:4-7 via torchmetrics
+// JaccardIndex): argmax over C fused with an LDS-private C x C histogram, one
+// global 64-bit atomic per non-empty bin per block.
+#include "rtseg_common.h"
+#include "rtseg_launch.h"
+
+namespace rtseg {
+
+namespace {
+
+struct PixIdx {
+  int hw, w;
+  __device__ __forceinline__ void split(int64_t p, int& n, int& h, int& x) const {
+    n = static_cast<int>(p / hw);
+    const int r = static_cast<int>(p - static_cast<int64_t>(n) * hw);
+    h = r / w;
+    x = r - h * w;
+  }
+};
+
+constexpr int kKdBlock = 256;
+
+template <typename T>
+__global__ void __launch_bounds__(kKdBlock) kd_fwd_kernel(Tensor4 s, Tensor4 t, float inv_t,
+                                                          float* lse, double* part) {
+  const T* sp = static_cast<const T*>(s.data);
+  const T* tp = static_cast<const T*>(t.data);
+  const int64_t npix = static_cast<int64_t>(s.n) * s.h * s.w;
+  const PixIdx pi{s.h * s.w, s.w};
+  double acc = 0.0;
+  for (int64_t p = blockIdx.x * static_cast<int64_t>(kKdBlock) + threadIdx.x; p < npix;
+       p += static_cast<int64_t>(gridDim.x) * kKdBlock) {
+    int n, h, x;
+    pi.split(p, n, h, x);
+    const int64_t so = n * s.sn + h * s.sh + x * s.sw;
+    const int64_t to = n * t.sn + h * t.sh + x * t.sw;
+    float ma = -INFINITY, mb = -INFINITY;
+    for (int c = 0; c < s.c; ++c) {
+      ma = fmaxf(ma, Io<T>::ld(sp + so + c * s.sc) * inv_t);
+      mb = fmaxf(mb, Io<T>::ld(tp + to + c * t.sc) * inv_t);
+    }
+    float za = 0.f, zb = 0.f, cross = 0.f;
+    for (int c = 0; c < s.c; ++c) {
+      const float a = Io<T>::ld(sp + so + c * s.sc) * inv_t;
+      const float b = Io<T>::ld(tp + to + c * t.sc) * inv_t;
+      za += __expf(a - ma);
+      const float eb = __expf(b - mb);
+      zb += eb;
+      cross += eb * (b - a);
+    }
+    const float la = ma + __logf(za), lb = mb + __logf(zb);
+    lse[p] = la;
+    lse[npix + p] = lb;
+    acc += static_cast<double>(cross / zb - lb + la);
+  }
+  __shared__ double red[kKdBlock / kWave];
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = acc;
+}
+
+__global__ void __launch_bounds__(kKdBlock) kd_finalize_kernel(const double* part, int nparts, double scale,
+                                                               float* out) {
+  double v = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += kKdBlock) v += part[i];
+  __shared__ double red[kKdBlock / kWave];
+  v = block_sum(v, red);
+  if (threadIdx.x == 0) *out = static_cast<float>(v * scale);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kKdBlock) kd_bwd_kernel(Tensor4 s, Tensor4 t, Tensor4 gs, float inv_t,
+                                                          const float* lse, const float* gout,
+                                                          float coef) {
+  const T* sp = static_cast<const T*>(s.data);
+  const T* tp = static_cast<const T*>(t.data);
+  T* gp = static_cast<T*>(gs.data);
+  const int64_t npix = static_cast<int64_t>(s.n) * s.h * s.w;
+  const PixIdx pi{s.h * s.w, s.w};
+  const float k = *gout * coef;
+  for (int64_t p = blockIdx.x * static_cast<int64_t>(kKdBlock) + threadIdx.x; p < npix;
+       p += static_cast<int64_t>(gridDim.x) * kKdBlock) {
+    int n, h, x;
+    pi.split(p, n, h, x);
+    const int64_t so = n * s.sn + h * s.sh + x * s.sw;
+    const int64_t to = n * t.sn + h * t.sh + x * t.sw;
+    const int64_t go = n * gs.sn + h * gs.sh + x * gs.sw;
+    const float la = lse[p], lb = lse[npix + p];
+    for (int c = 0; c < s.c; ++c) {
+      const float a = Io<T>::ld(sp + so + c * s.sc) * inv_t;
+      const float b = Io<T>::ld(tp + to + c * t.sc) * inv_t;
+      Io<T>::st(gp + go + c * gs.sc, k * (__expf(a - la) - __expf(b - lb)));
+    }
+  }
+}
+
+// ---- confusion matrix ---------------------------------------------------------
+constexpr int kCmBlock = 256;
+
+template <typename T, bool LDS>
+__global__ void __launch_bounds__(kCmBlock) confmat_kernel(Tensor4 x, const int64_t* target, int ignore,
+                                                           unsigned long long* cm) {
+  extern __shared__ unsigned hist[];
+  const int C = x.c;
+  if constexpr (LDS) {
+    for (int i = threadIdx.x; i < C * C; i += kCmBlock) hist[i] = 0u;
+    __syncthreads();
+  }
+  const T* xp = static_cast<const T*>(x.data);
+  const int64_t npix = static_cast<int64_t>(x.n) * x.h * x.w;
+  const PixIdx pi{x.h * x.w, x.w};
+  for (int64_t p = blockIdx.x * static_cast<int64_t>(kCmBlock) + threadIdx.x; p < npix;
+       p += static_cast<int64_t>(gridDim.x) * kCmBlock) {
+    const int64_t lbl = target[p];
+    if (lbl == ignore || lbl < 0 || lbl >= C) continue;
+    int n, h, w;
+    pi.split(p, n, h, w);
+    const T* q = xp + n * x.sn + h * x.sh + w * x.sw;
+    float best = Io<T>::ld(q);
+    int arg = 0;
+    for (int c = 1; c < C; ++c) {
+      const float v = Io<T>::ld(q + c * x.sc);
+      if (v > best || (v != v && best == best)) { best = v; arg = c; }  // NaN wins, like torch.argmax
+    }
+    const int bin = static_cast<int>(lbl) * C + arg;
+    if constexpr (LDS) atomicAdd(&hist[bin], 1u);
+    else atomicAdd(&cm[bin], 1ull);
+  }
+  if constexpr (LDS) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < C * C; i += kCmBlock) {
+      const unsigned v = hist[i];
+      if (v) atomicAdd(&cm[i], static_cast<unsigned long long>(v));
+    }
+  }
+}
+
+template <typename F>
+void by_dtype(int dtype, F&& f) {
+  if (dtype == kF32) f(float{});
+  else if (dtype == kBF16) f(uint16_t{});
+  else f(_Float16{});
+}
+
+}  // namespace
+
+int kd_partial_blocks(int64_t npix) { return stream_grid(npix, kKdBlock); }
+
+void launch_kd_fwd(const Tensor4& s, const Tensor4& t, float temperature, float* lse, double* part,
+                   float* out, hipStream_t st) {
+  const int64_t npix = static_cast<int64_t>(s.n) * s.h * s.w;
+  const int g = kd_partial_blocks(npix);
+  const float inv_t = 1.f / temperature;
+  by_dtype(s.dtype, [&](auto tag) {
+    using T = decltype(tag);
+    kd_fwd_kernel<T><<<g, kKdBlock, 0, st>>>(s, t, inv_t, lse, part);
+  });
+  const double numel = static_cast<double>(npix) * s.c;
+  const double scale = static_cast<double>(temperature) * temperature / numel;
+  kd_finalize_kernel<<<1, kKdBlock, 0, st>>>(part, g, scale, out);
+}
+
+void launch_kd_bwd(const Tensor4& s, const Tensor4& t, const Tensor4& gs, float temperature,
+                   const float* lse, const float* gout, hipStream_t st) {
+  const int64_t npix = static_cast<int64_t>(s.n) * s.h * s.w;
+  const int g = kd_partial_blocks(npix);
+  const double numel = static_cast<double>(npix) * s.c;
+  const float coef = static_cast<float>(static_cast<double>(temperature) / numel);
+  by_dtype(s.dtype, [&](auto tag) {
+    using T = decltype(tag);
+    kd_bwd_kernel<T><<<g, kKdBlock, 0, st>>>(s, t, gs, 1.f / temperature, lse, gout, coef);
+  });
+}
+
+void launch_confmat(const Tensor4& x, const int64_t* target, int ignore, unsigned long long* cm,
+                    hipStream_t st) {
+  const int64_t npix = static_cast<int64_t>(x.n) * x.h * x.w;
+  const int g = stream_grid(npix, kCmBlock);
+  const size_t lds = static_cast<size_t>(x.c) * x.c * sizeof(unsigned);
+  const bool use_lds = lds <= 64 * 1024;
+  by_dtype(x.dtype, [&](auto tag) {
+    using T = decltype(tag);
+    if (use_lds) confmat_kernel<T, true><<<g, kCmBlock, lds, st>>>(x, target, ignore, cm);
+    else confmat_kernel<T, false><<<g, kCmBlock, 0, st>>>(x, target, ignore, cm);
+  });
+}
+
+}  // namespace rtseg

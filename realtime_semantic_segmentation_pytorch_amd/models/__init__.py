@@ -64,11 +64,15 @@ def _variant_kwargs(config, key):
 
 
 def get_model(config):
-    """Build the configured model; every BatchNorm2d is routed through the fused HIP
-    kernels (``ops.convert_batchnorm``; checkpoint-compatible)."""
+    """Build the configured model; every BatchNorm2d and depth-wise conv is routed
+    through the HIP kernels (``ops.convert_batchnorm`` / ``ops.convert_depthwise``;
+    module classes only -- parameters and checkpoint keys are unchanged)."""
     from .. import ops
 
-    return ops.convert_batchnorm(_build_model(config))
+    model = ops.convert_batchnorm(_build_model(config))
+    if getattr(config, "hip_depthwise", True):
+        ops.convert_depthwise(model)
+    return model
 
 
 def _build_model(config):
@@ -102,8 +106,8 @@ def get_teacher_model(config, device):
         raise ValueError(f"Unsupported teacher decoder type: {config.teacher_decoder}")
     from .. import ops
 
-    model = ops.convert_batchnorm(build_smp_model(config.teacher_decoder, config.teacher_encoder, None,
-                                                  config.num_class))
+    model = ops.convert_depthwise(ops.convert_batchnorm(
+        build_smp_model(config.teacher_decoder, config.teacher_encoder, None, config.num_class)))
     ckpt_path = config.teacher_ckpt
     if ckpt_path:
         if not os.path.isfile(ckpt_path):

@@ -2,7 +2,7 @@
 
 ``confusion_matrix(logits[N,C,H,W] | labels[N,H,W], target[N,H,W], C, ignore)``
 returns ``cm[target, pred]`` as int64 ``[C, C]``.  GPU: one HIP kernel fusing the
-class argmax with an LDS-private histogram (``confmat.hip``); CPU: bincount.
+class argmax with an LDS-private histogram (``csrc/kernels/kd_metrics.hip``); CPU: bincount.
 """
 from __future__ import annotations
 
@@ -21,7 +21,7 @@ def confusion_matrix_reference(preds, target, num_class, ignore_index=255):
 
 
 def confusion_matrix(preds, target, num_class, ignore_index=255):
-    if (use_hip(preds) and preds.dim() == 4 and hasattr(ops(), "confmat")
+    if (use_hip(preds) and preds.dim() == 4
             and preds.dtype in (torch.float32, torch.bfloat16, torch.float16)):
         return ops().confmat(preds, target.long().contiguous(), num_class, ignore_index)
     return confusion_matrix_reference(preds, target, num_class, ignore_index)

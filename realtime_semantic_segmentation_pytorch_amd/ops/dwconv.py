@@ -1,0 +1,100 @@
+"""Depth-wise convolution on the HIP kernels of ``csrc/kernels/dwconv.hip``.
+
+Reference: every ``nn.Conv2d(groups=in_channels)`` of the zoo --
+``DWConvBNAct`` (models/modules.py:46-59, incl. BiSeNetV2's x6 channel
+multiplier), the raw depth-wise convs of CGNet / MiniNet / DABNet / FDDWNet,
+asymmetric (k,1)/(1,k) and dilated (up to 17) variants.  MIOpen has
+no fast channels-last depth-wise path, so these run as three hand-written
+kernels (forward, gather-form data gradient, two-stage deterministic weight
+gradient) on NHWC activations with fp32 accumulation and fp32 weights.
+
+``DepthwiseConv2d`` is an ``nn.Conv2d`` (same parameters and state-dict keys)
+whose forward takes the HIP path for channels-last GPU inputs;
+:func:`convert_depthwise` swaps the class of every eligible conv of a model in
+place.  Under autocast the input is cast to the autocast dtype like
+``F.conv2d`` would, while the kernels read the fp32 master weights directly.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ._ext import ops, use_hip
+
+_DTYPES = (torch.float32, torch.bfloat16, torch.float16)
+
+
+def _cl_aligned(t: torch.Tensor) -> torch.Tensor:
+    if not t.is_contiguous(memory_format=torch.channels_last):
+        t = t.contiguous(memory_format=torch.channels_last)
+    if t.data_ptr() % 16:
+        t = t.clone(memory_format=torch.channels_last)
+    return t
+
+
+class _DWConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, geom):
+        cout, kh, kw, sh, sw, ph, pw, dh, dw = geom
+        wt = weight.detach().float().reshape(cout, kh * kw).t().contiguous()
+        b = bias.detach().float().contiguous() if bias is not None else None
+        x = _cl_aligned(x)
+        y = ops().dw_conv_fwd(x, wt, b, cout, kh, kw, sh, sw, ph, pw, dh, dw)
+        ctx.geom = geom
+        ctx.has_bias = bias is not None
+        ctx.wdtype = weight.dtype
+        ctx.save_for_backward(x, wt)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wt = ctx.saved_tensors
+        cout, kh, kw, sh, sw, ph, pw, dh, dw = ctx.geom
+        dy = _cl_aligned(dy.to(x.dtype))
+        dx = dwt = db = None
+        if ctx.needs_input_grad[0]:
+            dx = ops().dw_conv_dgrad(dy, wt, x.shape[1], x.shape[2], x.shape[3], kh, kw, sh, sw, ph, pw, dh, dw)
+        if ctx.needs_input_grad[1]:
+            dwt = ops().dw_conv_wgrad(dy, x, kh, kw, sh, sw, ph, pw, dh, dw).to(ctx.wdtype)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = dy.float().sum((0, 2, 3))
+        return dx, dwt, db, None
+
+
+def depthwise_ok(conv: nn.Conv2d) -> bool:
+    return (isinstance(conv, nn.Conv2d) and conv.groups > 1 and conv.groups == conv.in_channels
+            and conv.out_channels % conv.in_channels == 0 and conv.padding_mode == "zeros"
+            and not isinstance(conv.padding, str))
+
+
+def dw_conv2d(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
+    """``conv(x)`` for a depth-wise ``conv``; HIP kernels for channels-last GPU inputs."""
+    if x.dim() == 4 and use_hip(x) and x.is_contiguous(memory_format=torch.channels_last):
+        dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
+        if dt in _DTYPES and conv.weight.dtype in _DTYPES:
+            kh, kw = conv.kernel_size
+            geom = (conv.out_channels, kh, kw, conv.stride[0], conv.stride[1], conv.padding[0],
+                    conv.padding[1], conv.dilation[0], conv.dilation[1])
+            return _DWConvFn.apply(x.to(dt), conv.weight, conv.bias, geom)
+    return F.conv2d(x, conv.weight, conv.bias, conv.stride, conv.padding, conv.dilation, conv.groups)
+
+
+def dw_conv2d_reference(x, weight, bias, stride, padding, dilation):
+    return F.conv2d(x, weight, bias, stride, padding, dilation, x.shape[1])
+
+
+class DepthwiseConv2d(nn.Conv2d):
+    """``nn.Conv2d(groups=in_channels)`` routed through the HIP depth-wise kernels."""
+
+    def forward(self, x):
+        return dw_conv2d(x, self)
+
+
+def convert_depthwise(model: nn.Module) -> nn.Module:
+    """Swap the class of every eligible depth-wise ``nn.Conv2d`` to :class:`DepthwiseConv2d`
+    (in place; parameters and checkpoint keys unchanged)."""
+    for m in model.modules():
+        if type(m) is nn.Conv2d and depthwise_ok(m):
+            m.__class__ = DepthwiseConv2d
+    return model

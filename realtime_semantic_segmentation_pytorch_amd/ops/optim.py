@@ -1,0 +1,196 @@
+"""Fused optimizer step + model-EMA update (HIP kernel ``csrc/kernels/optim.hip``).
+
+Parity: reference utils/optimizer.py:4-20 (torch SGD / Adam / AdamW) and
+utils/model_ema.py:28-40 (EMA lerp with decay ``itrs / total_itrs`` after every
+optimizer step).  ``FusedSGD`` / ``FusedAdam`` / ``FusedAdamW`` subclass the
+torch optimizers, keep their ``param_groups`` and ``state`` layout (so
+checkpoints, ``OneCycleLR`` momentum/beta cycling and ``GradScaler`` work
+unchanged) and replace ``step()`` on GPU with ONE multi-tensor launch that also
+writes the EMA copy of every parameter when an EMA is attached
+(``attach_ema``).  CPU tensors, sparse/complex grads or ``maximize`` /
+``amsgrad`` configurations fall back to the stock torch step (then the EMA is
+updated separately by ``ModelEmaV2``).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+from torch.optim import SGD, Adam, AdamW
+
+from ._ext import ops, use_hip
+
+MODE_SGD, MODE_ADAM, MODE_ADAMW = 0, 1, 2
+META_FIELDS = 8
+CHUNK = 16384
+
+
+def build_table(rows, device):
+    """rows: [(param, grad, state1|None, state2|None, ema|None, first_step)] -> (meta, ntensor, nblocks)."""
+    meta, bmap = [], []
+    for ti, (p, g, s1, s2, e, first) in enumerate(rows):
+        n = p.numel()
+        meta += [p.data_ptr(), g.data_ptr(), s1.data_ptr() if s1 is not None else 0,
+                 s2.data_ptr() if s2 is not None else 0, e.data_ptr() if e is not None else 0, n,
+                 1 if g.dtype == torch.bfloat16 else 0, 1 if first else 0]
+        for start in range(0, n, CHUNK):
+            bmap += [ti, start]
+    t = torch.tensor(meta + bmap, dtype=torch.int64)
+    if device.type == "cuda":
+        # pinned staging + async copy: rebuilding the table never blocks the host on the GPU queue
+        t = t.pin_memory().to(device, non_blocking=True)
+    return t, len(rows), len(bmap) // 2
+
+
+def _dense_ok(p) -> bool:
+    g = p.grad
+    return (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and g is not None
+            and not g.is_sparse and g.is_contiguous() and g.dtype in (torch.float32, torch.bfloat16)
+            and g.shape == p.shape)
+
+
+class _FusedMixin:
+    """Shared machinery: tensor-table cache, EMA attachment, fallback policy."""
+
+    _mode = MODE_SGD
+
+    def _fused_init(self):
+        self._ema_of = {}          # param -> EMA tensor
+        self.ema_weight = None     # 1 - decay for the NEXT step (set by the trainer); None => no fused EMA
+        self._tables = {}
+        self.last_step_fused = False
+
+    def attach_ema(self, pairs):
+        """pairs: iterable of (model_param, ema_tensor) of identical shape/dtype."""
+        self._ema_of = {p: e for p, e in pairs}
+        self._tables = {}
+
+    def _can_fuse(self, group) -> bool:
+        if group.get("maximize", False) or group.get("differentiable", False):
+            return False
+        if group.get("amsgrad", False) or group.get("capturable", False):
+            return False
+        ps = [p for p in group["params"] if p.grad is not None]
+        return bool(ps) and all(_dense_ok(p) for p in ps) and use_hip(ps[0])
+
+    def _launch(self, slot, rows, hp):
+        key = tuple((r[0].data_ptr(), r[1].data_ptr(), r[5], r[4] is not None) for r in rows)
+        cache = self._tables
+        if cache.get(slot, (None,))[0] != key:
+            cache[slot] = (key, build_table(rows, rows[0][0].device))
+        meta, nt, nb = cache[slot][1]
+        ops().fused_opt_step(meta, nt, nb, self._mode, *hp)
+
+
+class FusedSGD(_FusedMixin, SGD):
+    _mode = MODE_SGD
+
+    def __init__(self, params, **kw):
+        super().__init__(params, **kw)
+        self._fused_init()
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        if not all(self._can_fuse(g) for g in self.param_groups if any(p.grad is not None for p in g["params"])):
+            self.last_step_fused = False
+            return super().step(closure)
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        ema_w = self.ema_weight
+        for gi, group in enumerate(self.param_groups):
+            mom = float(group["momentum"])
+            rows = []
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                st = self.state[p]
+                first = False
+                buf = None
+                if mom != 0.0:
+                    buf = st.get("momentum_buffer")
+                    if buf is None:
+                        buf = st["momentum_buffer"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                        first = True
+                rows.append((p, p.grad, buf, None, self._ema_of.get(p) if ema_w is not None else None, first))
+            if not rows:
+                continue
+            lr = float(group["lr"])
+            hp = (lr, mom, float(group["dampening"]), float(group["weight_decay"]), bool(group["nesterov"]),
+                  0.0, 0.0, 0.0, 0.0, 0.0, 1.0, float(ema_w) if ema_w is not None else 0.0)
+            self._launch(gi, rows, hp)
+        self.last_step_fused = ema_w is not None and bool(self._ema_of)
+        return loss
+
+
+class _FusedAdamBase(_FusedMixin):
+    @torch.no_grad()
+    def step(self, closure=None):
+        if not all(self._can_fuse(g) for g in self.param_groups if any(p.grad is not None for p in g["params"])):
+            self.last_step_fused = False
+            return super().step(closure)
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        ema_w = self.ema_weight
+        for gi, group in enumerate(self.param_groups):
+            beta1, beta2 = (float(b) for b in group["betas"])
+            by_step = {}
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["step"] += 1
+                by_step.setdefault(float(st["step"]), []).append(
+                    (p, p.grad, st["exp_avg"], st["exp_avg_sq"],
+                     self._ema_of.get(p) if ema_w is not None else None, False))
+            lr = float(group["lr"])
+            # normally one bucket; several only after loading a hand-assembled state
+            for steps, rows in by_step.items():
+                bc1 = 1.0 - beta1 ** steps
+                bc2 = 1.0 - beta2 ** steps
+                hp = (lr, 0.0, 0.0, float(group["weight_decay"]), False, beta1, beta2, float(group["eps"]),
+                      lr / bc1, 1.0 / math.sqrt(bc2), 1.0, float(ema_w) if ema_w is not None else 0.0)
+                self._launch((gi, steps), rows, hp)
+        self.last_step_fused = ema_w is not None and bool(self._ema_of)
+        return loss
+
+
+class FusedAdam(_FusedAdamBase, Adam):
+    _mode = MODE_ADAM
+
+    def __init__(self, params, **kw):
+        super().__init__(params, **kw)
+        self._fused_init()
+
+
+class FusedAdamW(_FusedAdamBase, AdamW):
+    _mode = MODE_ADAMW
+
+    def __init__(self, params, **kw):
+        super().__init__(params, **kw)
+        self._fused_init()
+
+
+_EMA_TABLES: dict = {}
+
+
+def ema_lerp_(pairs, weight: float):
+    """e <- lerp(e, src, weight) over [(src, e)] fp32 CUDA tensors in one launch (BN running stats)."""
+    rows = [(s, s, None, None, e, False) for s, e in pairs]
+    if not rows:
+        return
+    key = tuple((r[0].data_ptr(), r[4].data_ptr()) for r in rows)
+    tab = _EMA_TABLES.get(key)
+    if tab is None:
+        if len(_EMA_TABLES) > 16:
+            _EMA_TABLES.clear()
+        tab = _EMA_TABLES[key] = build_table(rows, rows[0][0].device)
+    meta, nt, nb = tab
+    ops().ema_lerp(meta, nt, nb, float(weight))

@@ -1,0 +1,78 @@
+"""Depth-wise conv HIP kernels (fwd / dgrad / wgrad) vs F.conv2d in fp32."""
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from realtime_semantic_segmentation_pytorch_amd import ops
+from realtime_semantic_segmentation_pytorch_amd.ops.dwconv import DepthwiseConv2d
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+# (cin, mult, kernel, stride, dilation, hw)
+GEOMS = [
+    (32, 1, (3, 3), 1, 1, (17, 23)),
+    (32, 1, (3, 3), 2, 1, (32, 48)),
+    (16, 6, (3, 3), 2, 1, (20, 30)),    # BiSeNetV2 gather-expansion x6
+    (24, 1, (3, 1), 1, 2, (15, 9)),     # asymmetric dilated
+    (24, 1, (1, 5), 1, 1, (8, 20)),
+    (12, 1, (3, 3), 1, 17, (40, 40)),   # large dilation (FDDWNet / LEDNet)
+    (3, 1, (3, 3), 1, 1, (9, 11)),      # odd channel count -> scalar vectors
+    (40, 2, (5, 5), 1, 1, (12, 14)),    # 25 taps -> several wgrad tap groups
+    (64, 1, (3, 3), 1, 1, (64, 128)),
+]
+
+
+@pytest.fixture(autouse=True)
+def _lib():
+    assert ops.load(), "HIP extension must load on the GPU box"
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("bias", [False, True])
+@pytest.mark.parametrize("geom", GEOMS)
+def test_dwconv_fwd_bwd(dtype, bias, geom):
+    cin, mult, k, s, d, hw = geom
+    torch.manual_seed(0)
+    pad = tuple((kk - 1) // 2 * d for kk in k)
+    conv = nn.Conv2d(cin, cin * mult, k, s, pad, d, groups=cin, bias=bias).to(DEV)
+    ref = nn.Conv2d(cin, cin * mult, k, s, pad, d, groups=cin, bias=bias).to(DEV)
+    ref.load_state_dict(conv.state_dict())
+    conv.__class__ = DepthwiseConv2d
+    x = torch.randn(2, cin, *hw, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    y = conv(x)
+    assert y.dtype == dtype and y.is_contiguous(memory_format=torch.channels_last)
+    xr = x.detach().float().requires_grad_(True)
+    yr = ref(xr)
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    torch.testing.assert_close(y.float(), yr, atol=tol * max(1.0, yr.abs().max().item()), rtol=tol)
+    g = torch.randn_like(yr)
+    y.backward(g.to(dtype))
+    yr.backward(g)
+    gt = 1e-4 if dtype == torch.float32 else 3e-2
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=gt * max(1.0, xr.grad.abs().max().item()), rtol=gt)
+    torch.testing.assert_close(conv.weight.grad, ref.weight.grad,
+                               atol=gt * max(1.0, ref.weight.grad.abs().max().item()), rtol=gt)
+    if bias:
+        torch.testing.assert_close(conv.bias.grad, ref.bias.grad,
+                                   atol=gt * max(1.0, ref.bias.grad.abs().max().item()), rtol=gt)
+
+
+def test_dwconv_autocast_module():
+    from realtime_semantic_segmentation_pytorch_amd.models.modules import DWConvBNAct
+
+    torch.manual_seed(0)
+    blk = DWConvBNAct(32, 32, 3, 1, 1, "relu").to(DEV)
+    ops.convert_depthwise(blk)
+    assert isinstance(blk[0], DepthwiseConv2d)
+    x = torch.randn(4, 32, 24, 40, device=DEV).contiguous(memory_format=torch.channels_last)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = blk(x)
+    assert y.dtype == torch.bfloat16
+    y.float().sum().backward()
+    assert blk[0].weight.grad is not None and blk[0].weight.grad.dtype == torch.float32
+    with torch.no_grad():
+        yr = F.relu(blk[1](F.conv2d(x, blk[0].weight, None, 1, 1, 1, 32)))
+    torch.testing.assert_close(y.float(), yr, atol=5e-2, rtol=5e-2)

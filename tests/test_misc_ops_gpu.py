@@ -1,0 +1,125 @@
+"""KD KL loss, confusion matrix and fused optimizer+EMA HIP kernels vs PyTorch fp32 references."""
+import copy
+
+import pytest
+import torch
+import torch.nn as nn
+
+from realtime_semantic_segmentation_pytorch_amd import ops
+from realtime_semantic_segmentation_pytorch_amd.ops.optim import FusedAdam, FusedAdamW, FusedSGD
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True)
+def _lib():
+    assert ops.load(), "HIP extension must load on the GPU box"
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cl", [False, True])
+@pytest.mark.parametrize("shape,temp", [((2, 19, 32, 64), 4.0), ((1, 7, 9, 13), 1.0), ((3, 40, 5, 6), 2.5)])
+def test_kd_kl_fwd_bwd(dtype, cl, shape, temp):
+    torch.manual_seed(0)
+    s = (torch.randn(shape, device=DEV) * 3).to(dtype)
+    t = (torch.randn(shape, device=DEV) * 3).to(dtype)
+    if cl:
+        s = s.contiguous(memory_format=torch.channels_last)
+        t = t.contiguous(memory_format=torch.channels_last)
+    s.requires_grad_(True)
+    loss = ops.kd_kl_div(s, t, temp)
+    sr = s.detach().float().requires_grad_(True)
+    ref = ops.kd_kl_div_reference(sr, t.float(), temp)
+    torch.testing.assert_close(loss.float(), ref, rtol=1e-4, atol=1e-6)
+    loss.backward(torch.tensor(0.7, device=DEV))
+    ref.backward(torch.tensor(0.7, device=DEV))
+    scale = sr.grad.abs().max().item()
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    torch.testing.assert_close(s.grad.float(), sr.grad, atol=tol * scale, rtol=tol)
+    if cl:
+        assert s.grad.is_contiguous(memory_format=torch.channels_last)
+
+
+def test_kd_no_host_sync():
+    s = torch.randn(2, 19, 16, 32, device=DEV, requires_grad=True)
+    t = torch.randn(2, 19, 16, 32, device=DEV)
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        loss = ops.kd_kl_div(s, t, 4.0)
+        loss.backward()
+    finally:
+        torch.cuda.set_sync_debug_mode("default")
+    assert torch.isfinite(loss).item()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cl", [False, True])
+@pytest.mark.parametrize("c", [19, 3, 150])
+def test_confmat(dtype, cl, c):
+    torch.manual_seed(1)
+    x = torch.randn(2, c, 33, 47, device=DEV).to(dtype)
+    if cl:
+        x = x.contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, c, (2, 33, 47), device=DEV)
+    y[:, ::5] = 255
+    cm = ops.confusion_matrix(x, y, c, 255)
+    ref = ops.confusion_matrix_reference(x.float().cpu(), y.cpu(), c, 255)
+    assert cm.dtype == torch.int64
+    torch.testing.assert_close(cm.cpu(), ref)
+
+
+def _model():
+    torch.manual_seed(0)
+    return nn.Sequential(nn.Conv2d(3, 16, 3, bias=False), nn.BatchNorm2d(16), nn.ReLU(),
+                         nn.Conv2d(16, 40000 // 16, 1), nn.Flatten(), nn.Linear(2500 * 4, 3)).to(DEV)
+
+
+@pytest.mark.parametrize("kind", ["sgd", "sgd_nesterov", "adam", "adamw"])
+def test_fused_optimizer_matches_torch(kind):
+    m_ref = _model()
+    m_fus = copy.deepcopy(m_ref)
+    ema = copy.deepcopy(m_fus)
+    ema_ref = copy.deepcopy(m_ref)
+    if kind.startswith("sgd"):
+        kw = dict(lr=0.05, momentum=0.9, weight_decay=1e-4, nesterov=kind == "sgd_nesterov")
+        o_ref, o_fus = torch.optim.SGD(m_ref.parameters(), **kw), FusedSGD(m_fus.parameters(), **kw)
+    elif kind == "adam":
+        o_ref, o_fus = torch.optim.Adam(m_ref.parameters(), lr=1e-3), FusedAdam(m_fus.parameters(), lr=1e-3)
+    else:
+        kw = dict(lr=1e-3, weight_decay=0.01)
+        o_ref, o_fus = torch.optim.AdamW(m_ref.parameters(), **kw), FusedAdamW(m_fus.parameters(), **kw)
+    pairs = [(p, e.data) for p, e in zip(m_fus.parameters(), ema.parameters())]
+    o_fus.attach_ema(pairs)
+    x = torch.randn(4, 3, 4, 4, device=DEV)
+    for it in range(1, 5):
+        for m, o in ((m_ref, o_ref), (m_fus, o_fus)):
+            o.zero_grad()
+            m(x).square().mean().backward()
+        decay = it / 10
+        o_fus.ema_weight = 1.0 - decay
+        o_ref.step()
+        o_fus.step()
+        assert o_fus.last_step_fused
+        with torch.no_grad():
+            for e, p in zip(ema_ref.parameters(), m_ref.parameters()):
+                e.lerp_(p, 1.0 - decay)
+    for a, b in zip(m_ref.parameters(), m_fus.parameters()):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+    for a, b in zip(ema_ref.parameters(), ema.parameters()):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+    # state layout is torch's: a torch optimizer can resume from the fused one's state dict
+    sd = o_fus.state_dict()
+    o2 = type(o_ref)(m_fus.parameters(), lr=1e-3)
+    o2.load_state_dict(sd)
+
+
+def test_ema_lerp_buffers():
+    from realtime_semantic_segmentation_pytorch_amd.ops.optim import ema_lerp_
+
+    src = [torch.randn(n, device=DEV) for n in (5, 70000, 1)]
+    ema = [torch.randn_like(s) for s in src]
+    ref = [e.clone().lerp_(s, 0.3) for e, s in zip(ema, src)]
+    ema_lerp_(list(zip(src, ema)), 0.3)
+    for a, b in zip(ema, ref):
+        torch.testing.assert_close(a, b)
