@@ -31,10 +31,15 @@ for _k in ("MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_FWD", "MIOPEN_DEBUG_CONV_DIRECT_
            "MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_WRW"):
     os.environ.setdefault(_k, "0")
 
+_ROOT = os.path.dirname(os.path.abspath(__file__))
+# MIOpen find results (solver choice per conv shape on gfx950) persist in-tree, so a fresh
+# box reuses them instead of re-benchmarking every solver during warm-up.
+os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(_ROOT, "miopen_db"))
+
 import torch
 import torch.distributed as dist
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, _ROOT)
 
 from realtime_semantic_segmentation_pytorch_amd.configs import BaseConfig  # noqa: E402
 
@@ -44,10 +49,12 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--batch", type=int, default=8, help="images per GPU per step")
+    p.add_argument("--batch", type=int, default=32, help="images per GPU per step (288 GB HBM: 27 GB at 32)")
     p.add_argument("--height", type=int, default=1024)
     p.add_argument("--width", type=int, default=2048)
-    p.add_argument("--arch", default="DDRNet-23")
+    p.add_argument("--model", default="ddrnet", help="registry key (ddrnet | bisenetv2 | stdc | ...)")
+    p.add_argument("--arch", default="DDRNet-23", help="DDRNet arch_type / STDC+PP-LiteSeg encoder_type")
+    p.add_argument("--detail-head", action="store_true", help="STDC: detail head instead of aux heads")
     p.add_argument("--no-infer", action="store_true", help="skip the inference-FPS measurement")
     p.add_argument("--fp32", action="store_true", help="disable bf16 autocast (diagnostic)")
     p.add_argument("--no-fused-loss", action="store_true")
@@ -62,9 +69,13 @@ def make_config(a, world):
     c = BaseConfig()
     c.dataset = "cityscapes"
     c.num_class = 19
-    c.model = "ddrnet"
-    c.arch_type = a.arch
-    c.use_aux = True
+    c.model = a.model
+    if a.model == "ddrnet":
+        c.arch_type = a.arch
+    elif a.model in ("stdc", "ppliteseg"):
+        c.encoder_type = a.arch if a.arch.startswith("stdc") else "stdc2"
+    c.use_detail_head = bool(a.detail_head)
+    c.use_aux = a.model in ("ddrnet", "bisenetv2", "icnet", "stdc") and not a.detail_head
     c.loss_type = "ohem"
     c.optimizer_type = "sgd"
     c.train_bs = a.batch
@@ -89,25 +100,45 @@ def make_config(a, world):
 
 
 @torch.no_grad()
-def infer_fps(model, h, w, dtype, channels_last, iters=30, warm=10):
-    model.eval()
+def infer_fps(model, h, w, dtype, channels_last, iters=50, warm=10):
+    """tools/test_speed.py protocol (batch 1, eval) on the HIP-graph inference engine."""
+    from realtime_semantic_segmentation_pytorch_amd.utils.inference import InferenceEngine
+
+    eng = InferenceEngine(model, (1, 3, h, w), dtype=dtype, channels_last=channels_last, warmup=warm)
     x = torch.randn(1, 3, h, w, device="cuda")
-    if channels_last:
-        x = x.contiguous(memory_format=torch.channels_last)
-    ctx = torch.autocast("cuda", dtype=dtype, enabled=dtype != torch.float32)
-    with ctx:
-        for _ in range(warm):
-            model(x)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(iters):
-            model(x)
-        torch.cuda.synchronize()
-    return iters / (time.perf_counter() - t0)
+    for _ in range(3):
+        eng(x)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        eng(x)
+    torch.cuda.synchronize()
+    fps = iters / (time.perf_counter() - t0)
+    del eng
+    return fps
+
+
+README_FPS_DDRNET23_SLIM = 233.0  # reference README.md:144 (RTX 2080, fp32, 1024x512, batch 1)
+
+
+def _heartbeat(period=30.0):
+    """stderr line every `period` s (MIOpen find on a fresh box can be silent for minutes)."""
+    import threading
+
+    stop = threading.Event()
+    t0 = time.perf_counter()
+
+    def run():
+        while not stop.wait(period):
+            print(f"[bench] alive {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=run, daemon=True).start()
+    return stop
 
 
 def main():
     a = parse()
+    hb = _heartbeat()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1 and "LOCAL_RANK" not in os.environ:
         raise SystemExit("N>1 must be launched with torchrun (one process per GPU)")
@@ -136,8 +167,13 @@ def main():
         imgs, masks = data.next()
         return trainer.train_step(imgs, masks)
 
-    for _ in range(a.warmup):
+    for i in range(a.warmup):
+        t_w = time.perf_counter()
         step()
+        if rank == 0:
+            torch.cuda.synchronize()
+            print(f"[bench] warm-up step {i + 1}/{a.warmup}: {time.perf_counter() - t_w:.2f} s",
+                  file=sys.stderr, flush=True)
 
     def sync_all():
         torch.cuda.synchronize()
@@ -176,10 +212,21 @@ def main():
              "fused_loss": cfg.fused_loss}
     if rank == 0 and not a.no_infer:
         m = de_parallel(trainer.model)
-        extra["infer_fps_bf16_bs1_1024x2048"] = round(infer_fps(m, a.height, a.width, torch.bfloat16,
-                                                                cfg.channels_last), 2)
-        extra["infer_fps_fp32_bs1_1024x2048"] = round(infer_fps(m, a.height, a.width, torch.float32,
-                                                                cfg.channels_last), 2)
+        tag = f"{a.height}x{a.width}"
+        extra[f"infer_fps_bf16_bs1_{tag}"] = round(infer_fps(m, a.height, a.width, torch.bfloat16,
+                                                             cfg.channels_last), 2)
+        extra[f"infer_fps_fp32_bs1_{tag}"] = round(infer_fps(m, a.height, a.width, torch.float32,
+                                                             cfg.channels_last), 2)
+        if a.model == "ddrnet":
+            # the README's own FPS row: DDRNet-23-slim, 1024x512, fp32, batch 1 (use_aux as in MyConfig)
+            from realtime_semantic_segmentation_pytorch_amd.models import get_model
+
+            sc = make_config(a, world)
+            sc.arch_type = "DDRNet-23-slim"
+            slim = get_model(sc).to(dev)
+            fps = infer_fps(slim, a.height // 2, a.width // 2, torch.float32, cfg.channels_last)
+            extra["ddrnet23slim_fps_fp32_bs1_512x1024"] = round(fps, 2)
+            extra["ddrnet23slim_fps_vs_readme_rtx2080"] = round(fps / README_FPS_DDRNET23_SLIM, 3)
     if dist.is_initialized():
         dist.barrier(device_ids=[dev.index])
     if rank == 0:
@@ -197,12 +244,16 @@ def main():
             "dtype": "fp32" if a.fp32 else "bf16",
             "data": "synthetic (device-resident random 1024x2048 images, blocky 19-class masks, "
                     "random-init weights)",
-            "config": {"model": a.arch, "global_batch": a.batch * world,
+            "config": {"model": a.arch if a.model == "ddrnet" else f"{a.model}-{a.arch}" if a.model in (
+                           "stdc", "ppliteseg") else a.model,
+                       "global_batch": a.batch * world,
                        "seq_len": f"{a.height}x{a.width}", "parallelism": f"dp{world}",
-                       "num_class": 19, "loss": "ohem+aux", "optimizer": "sgd+onecycle+ema"},
+                       "num_class": 19, "loss": "ohem+detail" if a.detail_head else "ohem+aux" if cfg.use_aux else "ohem",
+                       "optimizer": "sgd+onecycle+ema"},
             "extra": extra,
         }
         print(json.dumps(out), flush=True)
+    hb.set()
     if dist.is_initialized():
         dist.destroy_process_group()
 

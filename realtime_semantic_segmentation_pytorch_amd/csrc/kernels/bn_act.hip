@@ -151,8 +151,13 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, 
   block_partials_out<V>(s, q, g, C, sm, part);
 }
 
-// Slab [G][2C] -> fp64 per-channel totals for 64 channels per block (4 waves
-// split the slab rows).  Result in red[0..63] (sum) / red[64..127] (second).
+// Slab [G][2C] -> fp64 per-channel totals for 64 channels per block; kFinWaves
+// waves split the slab rows (16 waves keep the serial load chain per lane at
+// G/16 rows -- these kernels are latency-bound, one block per 64 channels).
+// Result in red[0..63] (sum) / red[64..127] (second).
+constexpr int kFinWaves = 16;
+constexpr int kFinBlock = kFinWaves * 64;
+
 __device__ __forceinline__ void reduce_slab64(const float* __restrict__ part, int G, int C, int c,
                                               double* red) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -161,17 +166,17 @@ __device__ __forceinline__ void reduce_slab64(const float* __restrict__ part, in
     const int64_t rs = 2 * static_cast<int64_t>(C);
     const float* p = part + c;
     int gi = w;
-    for (; gi + 28 < G; gi += 32) {  // 8 rows (16 loads) in flight per thread
+    for (; gi + 7 * kFinWaves < G; gi += 8 * kFinWaves) {  // 8 rows (16 loads) in flight per lane
       float fa[8], fb[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        fa[k] = p[(gi + 4 * k) * rs];
-        fb[k] = p[(gi + 4 * k) * rs + C];
+        fa[k] = p[(gi + kFinWaves * k) * rs];
+        fb[k] = p[(gi + kFinWaves * k) * rs + C];
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k) { a += fa[k]; b += fb[k]; }
     }
-    for (; gi < G; gi += 4) { a += p[gi * rs]; b += p[gi * rs + C]; }
+    for (; gi < G; gi += kFinWaves) { a += p[gi * rs]; b += p[gi * rs + C]; }
   }
   red[w * 128 + lane] = a;
   red[w * 128 + 64 + lane] = b;
@@ -179,7 +184,7 @@ __device__ __forceinline__ void reduce_slab64(const float* __restrict__ part, in
   if (w == 0) {
     double ta = 0.0, tb = 0.0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) { ta += red[k * 128 + lane]; tb += red[k * 128 + 64 + lane]; }
+    for (int k = 0; k < kFinWaves; ++k) { ta += red[k * 128 + lane]; tb += red[k * 128 + 64 + lane]; }
     red[lane] = ta;
     red[64 + lane] = tb;
   }
@@ -207,12 +212,12 @@ __device__ __forceinline__ void finalize_channel(int c, int C, double sum, doubl
 }
 
 // Fused: slab reduce + finalize (+ sums[2C+1] for the backward's count).
-__global__ void __launch_bounds__(256) bn_finalize_partials_kernel(
+__global__ void __launch_bounds__(kFinBlock) bn_finalize_partials_kernel(
     const float* __restrict__ part, int G, int C, double count, const float* __restrict__ w,
     const float* __restrict__ b, float* __restrict__ rmean, float* __restrict__ rvar,
     int64_t* __restrict__ nbt, float momentum, float eps, float* __restrict__ mean_invstd,
     float* __restrict__ scale_shift, double* __restrict__ sums_out) {
-  __shared__ double red[4 * 128];
+  __shared__ double red[kFinWaves * 128];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   reduce_slab64(part, G, C, c, red);
   if (threadIdx.x < 64 && c < C) {
@@ -228,10 +233,10 @@ __global__ void __launch_bounds__(256) bn_finalize_partials_kernel(
 }
 
 // SyncBN path, step 1: slab -> fp64 [2C+1] sums (all-reduced by the caller).
-__global__ void __launch_bounds__(256) bn_slab_to_sums_kernel(const float* __restrict__ part, int G,
+__global__ void __launch_bounds__(kFinBlock) bn_slab_to_sums_kernel(const float* __restrict__ part, int G,
                                                               int C, double count,
                                                               double* __restrict__ sums) {
-  __shared__ double red[4 * 128];
+  __shared__ double red[kFinWaves * 128];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   reduce_slab64(part, G, C, c, red);
   if (threadIdx.x < 64 && c < C) {
@@ -387,12 +392,12 @@ __device__ __forceinline__ void bwd_finalize_channel(int c, int C, double sg, do
 }
 
 // Slab (or already-reduced sums, SyncBN) -> dx coefficients + parameter grads.
-__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(
+__global__ void __launch_bounds__(kFinBlock) bn_bwd_finalize_kernel(
     const float* __restrict__ part, int G, const double* __restrict__ sums,
     const double* __restrict__ count_ptr, int C, const float* __restrict__ w,
     const float* __restrict__ mean_invstd, int batch_stats, float* __restrict__ kcoef,
     float* __restrict__ dw, float* __restrict__ db) {
-  __shared__ double red[4 * 128];
+  __shared__ double red[kFinWaves * 128];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   if (!sums) reduce_slab64(part, G, C, c, red);
   if (threadIdx.x < 64 && c < C) {
@@ -494,14 +499,14 @@ void launch_bn_finalize_partials(const float* part, int G, int C, double count, 
                                  const float* b, float* rmean, float* rvar, int64_t* nbt,
                                  float momentum, float eps, float* mean_invstd, float* scale_shift,
                                  double* sums_out, hipStream_t st) {
-  bn_finalize_partials_kernel<<<(C + 63) / 64, 256, 0, st>>>(part, G, C, count, w, b, rmean, rvar,
+  bn_finalize_partials_kernel<<<(C + 63) / 64, kFinBlock, 0, st>>>(part, G, C, count, w, b, rmean, rvar,
                                                              nbt, momentum, eps, mean_invstd,
                                                              scale_shift, sums_out);
 }
 
 void launch_bn_slab_to_sums(const float* part, int G, int C, double count, double* sums,
                             hipStream_t st) {
-  bn_slab_to_sums_kernel<<<(C + 63) / 64, 256, 0, st>>>(part, G, C, count, sums);
+  bn_slab_to_sums_kernel<<<(C + 63) / 64, kFinBlock, 0, st>>>(part, G, C, count, sums);
 }
 
 void launch_bn_finalize(const double* sums, int C, const float* w, const float* b,
@@ -593,7 +598,7 @@ void launch_bn_bwd_reduce(const void* dy, const void* x, const void* y, const fl
 void launch_bn_bwd_finalize(const float* part, int G, const double* sums, const double* count_ptr,
                             int C, const float* w, const float* mean_invstd, int batch_stats,
                             float* kcoef, float* dw, float* db, hipStream_t st) {
-  bn_bwd_finalize_kernel<<<(C + 63) / 64, 256, 0, st>>>(part, G, sums, count_ptr, C, w,
+  bn_bwd_finalize_kernel<<<(C + 63) / 64, kFinBlock, 0, st>>>(part, G, sums, count_ptr, C, w,
                                                         mean_invstd, batch_stats, kcoef, dw, db);
 }
 

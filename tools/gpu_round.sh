@@ -1,10 +1,11 @@
 #!/bin/bash
-# One GPU-box session: kernel numerics tests, then the headline bench (batch 8 and 16).
+# One GPU-box session: benches (filling the in-tree MIOpen find db), rocprofv3 profiles.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests/test_dwconv_gpu.py tests/test_misc_ops_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/t1.log 2>&1 || { echo TESTFAIL; tail -40 gpurun_out/t1.log; exit 1; }
-tail -3 gpurun_out/t1.log
-timeout -k 10 400 python bench.py --steps 10 --warmup 5 > gpurun_out/b8.log 2>&1 || { echo BENCHFAIL; tail -30 gpurun_out/b8.log; exit 1; }
-grep metric gpurun_out/b8.log
-timeout -k 10 400 python bench.py --steps 10 --warmup 5 --batch 16 --no-infer > gpurun_out/b16.log 2>&1 || { echo BENCH16FAIL; tail -30 gpurun_out/b16.log; exit 1; }
+timeout -k 10 500 python bench.py --steps 10 --warmup 5 --batch 32 --no-infer > gpurun_out/b32.log 2>&1 || { echo BENCHFAIL; tail -30 gpurun_out/b32.log; exit 1; }
+grep metric gpurun_out/b32.log
+timeout -k 10 400 python bench.py --steps 10 --warmup 5 --batch 16 --model bisenetv2 --no-infer > gpurun_out/bis.log 2>&1 || { echo BISFAIL; tail -30 gpurun_out/bis.log; exit 1; }
+grep metric gpurun_out/bis.log
+timeout -k 10 500 python bench.py --steps 10 --warmup 5 --batch 16 > gpurun_out/b16.log 2>&1 || { echo B16FAIL; tail -30 gpurun_out/b16.log; exit 1; }
 grep metric gpurun_out/b16.log
+du -sh miopen_db; ls miopen_db | head; cp -r miopen_db gpurun_out/miopen_db_new
