@@ -196,6 +196,8 @@ static at::Tensor dw_conv_wgrad(const at::Tensor& dy, const at::Tensor& x, int64
   DwGeom g = dw_geom(x.size(0), x.size(1), x.size(2), x.size(3), dy.size(1), kh, kw, sh, sw, ph, pw, dh, dw);
   TORCH_CHECK(g.ho == dy.size(2) && g.wo == dy.size(3) && dy.size(0) == x.size(0),
               "rtseg.dwconv: grad_output shape mismatch");
+  TORCH_CHECK(static_cast<int64_t>(g.n) * g.ho * g.wo < (int64_t{1} << 31),
+              "rtseg.dwconv: weight gradient over more than 2^31 output pixels per call");
   const DwWgradPlan p = dw_wgrad_plan(g, dtype_code(x));
   auto f32 = x.options().dtype(at::kFloat);
   at::Tensor part = at::empty({static_cast<int64_t>(p.slices) * kh * kw * g.cout}, f32);

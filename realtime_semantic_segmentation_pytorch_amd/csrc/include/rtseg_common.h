@@ -57,6 +57,32 @@ __device__ __forceinline__ float act_bwd_from_out(float g, float y) {
   else return g;
 }
 
+// ---- fast unsigned division by a loop-invariant divisor ---------------------
+// q = (umulhi(n, m) + n) >> s  (Granlund-Montgomery, exact for all 32-bit n): a
+// 64-bit `/` or `%` in an index decomposition costs ~100 VALU instructions on
+// CDNA, this costs 3-4, which matters in kernels doing O(10) FMAs per element.
+struct FastDiv {
+  uint32_t d, m, s;
+  __host__ static FastDiv make(uint32_t d) {
+    FastDiv f;
+    f.d = d;
+    uint32_t l = 0;
+    while ((1ull << l) < d) ++l;  // l = ceil(log2 d)
+    f.s = l;
+    f.m = static_cast<uint32_t>(((1ull << 32) * ((1ull << l) - d)) / d + 1);
+    return f;
+  }
+  __device__ __forceinline__ uint32_t div(uint32_t n) const {
+    const uint64_t t = __umulhi(n, m);
+    return static_cast<uint32_t>((t + n) >> s);
+  }
+  __device__ __forceinline__ uint32_t divmod(uint32_t n, uint32_t& r) const {
+    const uint32_t q = div(n);
+    r = n - q * d;
+    return q;
+  }
+};
+
 // ---- wave / block reductions (64-lane waves) ------------------------------
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -119,7 +119,7 @@ struct DwGeom {
   int ho, wo, kh, kw, sh, sw, ph, pw, dh, dw;
 };
 struct DwWgradPlan {
-  int vec, lanes, chunks, tap_groups, slices;
+  int vec, lanes, chunks, nt, tap_groups, slices;  // nt = taps per wgrad thread
 };
 int dw_vec(int dtype, int c);
 DwWgradPlan dw_wgrad_plan(const DwGeom& g, int dtype);
@@ -129,5 +129,22 @@ void launch_dw_dgrad(const DwGeom& g, int dtype, const void* dy, const float* wt
 // part: [slices, KH*KW, Cout] fp32 workspace; dw: [Cout, KH*KW] fp32
 void launch_dw_wgrad(const DwGeom& g, int dtype, const void* dy, const void* x, float* part, float* dw,
                      hipStream_t st);
+
+// ---- conv_mfma.hip ------------------------------------------------------------
+// Implicit-GEMM conv, bf16 NHWC: x [N,H,W,Cin], w [Cout,KH,KW,Cin], y [N,Ho,Wo,Cout].
+// part != nullptr: BN statistics slab [conv_mfma_slabs(g), 2*Cout] fp32 (sum | sum of squares).
+// scale_shift != nullptr: y = act(conv * scale + shift (+ res)) (inference BN epilogue).
+struct ConvGeom {
+  const void* x;
+  const void* w;
+  void* y;
+  float* part;
+  const float* scale_shift;
+  const void* res;
+  int act;
+  int n, h, w_in, cin, ho, wo, cout, kh, kw, sh, sw, ph, pw, dh, dw;
+};
+int conv_mfma_slabs(const ConvGeom& g);
+void launch_conv_mfma(const ConvGeom& g, hipStream_t st);
 
 }  // namespace rtseg

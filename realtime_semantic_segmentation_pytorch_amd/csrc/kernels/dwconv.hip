@@ -29,6 +29,11 @@ namespace rtseg {
 namespace {
 
 constexpr int kDwBlock = 256;
+
+// Divisors of the flattened (pixel, channel-vector) index: channel vectors, width, height.
+struct DwDivs {
+  FastDiv c, w, h;
+};
 constexpr int kMaxTaps = 9;  // taps accumulated per wgrad thread (tap groups cover larger kernels)
 
 template <typename T, int VEC> struct Vec;
@@ -106,95 +111,149 @@ template <> struct Vec<_Float16, 1> {
   __device__ __forceinline__ static void store(_Float16* p, const float* v) { *p = static_cast<_Float16>(v[0]); }
 };
 
+// MT: channel multiplier handled at compile time.  1 = plain depth-wise; 2/3/4/6 =
+// multiplier path where a thread owns VEC *input* channels and the VEC*MT
+// contiguous output channels they feed (BiSeNetV2's x6 gather-expansion: one
+// input vector load + MT output vector stores per tap instead of per-element
+// gathers); 0 = any other multiplier (per-element gather, correctness path).
+
+// VEC consecutive fp32 weights (16-byte vectors when VEC % 4 == 0: the tap-major rows and
+// the channel offsets are multiples of VEC, so those loads are aligned).
+template <int VEC>
+__device__ __forceinline__ void load_wvec(const float* p, float* w) {
+  if constexpr (VEC % 4 == 0) {
+#pragma unroll
+    for (int q = 0; q < VEC / 4; ++q) {
+      const float4 f = reinterpret_cast<const float4*>(p)[q];
+      w[4 * q] = f.x; w[4 * q + 1] = f.y; w[4 * q + 2] = f.z; w[4 * q + 3] = f.w;
+    }
+  } else {
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) w[v] = p[v];
+  }
+}
+
+// Out-of-image taps: every load is issued unconditionally from a clamped (valid)
+// address and the LOADED VALUE is zeroed by a select -- never `ok ? fma(load) : acc`,
+// which hipcc lowers to a branch + s_waitcnt around every single load.
+
 // ---------------------------------------------------------------- forward
-template <typename T, int VEC, bool MULT>
-__global__ void __launch_bounds__(kDwBlock) dw_fwd_kernel(DwGeom g, const T* __restrict__ x,
+template <typename T, int VEC, int MT, int KS>
+__global__ void __launch_bounds__(kDwBlock) dw_fwd_kernel(DwGeom g, DwDivs fd, const T* __restrict__ x,
                                                           const float* __restrict__ wt,
                                                           const float* __restrict__ bias, T* __restrict__ y) {
-  const int cv_n = g.cout / VEC;
-  const int64_t total = static_cast<int64_t>(g.n) * g.ho * g.wo * cv_n;
-  for (int64_t it = blockIdx.x * static_cast<int64_t>(kDwBlock) + threadIdx.x; it < total;
-       it += static_cast<int64_t>(gridDim.x) * kDwBlock) {
-    const int cv = static_cast<int>(it % cv_n);
-    int64_t pix = it / cv_n;
-    const int wo = static_cast<int>(pix % g.wo);
-    pix /= g.wo;
-    const int ho = static_cast<int>(pix % g.ho);
-    const int n = static_cast<int>(pix / g.ho);
-    const int co = cv * VEC;
-    float acc[VEC];
+  constexpr int OV = MT > 1 ? VEC * MT : VEC;  // output channels per thread
+  const int cv_n = MT > 1 ? g.cin / VEC : g.cout / VEC;
+  const uint32_t total = static_cast<uint32_t>(g.n) * g.ho * g.wo * cv_n;  // < 2^31 (host splits)
+  for (uint32_t it = blockIdx.x * kDwBlock + threadIdx.x; it < total; it += gridDim.x * kDwBlock) {
+    uint32_t cvu, wou, hou;
+    const uint32_t pix = fd.c.divmod(it, cvu);
+    const uint32_t r = fd.w.divmod(pix, wou);
+    const int n = static_cast<int>(fd.h.divmod(r, hou));
+    const int cv = static_cast<int>(cvu), wo = static_cast<int>(wou), ho = static_cast<int>(hou);
+    const int co = MT > 1 ? cv * VEC * MT : cv * VEC;  // first output channel
+    const int ci = cv * VEC;                             // first input channel (MT > 1)
+    float acc[OV];
 #pragma unroll
-    for (int v = 0; v < VEC; ++v) acc[v] = bias ? bias[co + v] : 0.f;
+    for (int v = 0; v < OV; ++v) acc[v] = bias ? bias[co + v] : 0.f;
     const int hb = ho * g.sh - g.ph, wb = wo * g.sw - g.pw;
-    for (int i = 0; i < g.kh; ++i) {
-      const int hi = hb + i * g.dh;
-      if (hi < 0 || hi >= g.h) continue;
-      const T* xrow = x + (static_cast<int64_t>(n) * g.h + hi) * g.w * g.cin;
-      for (int j = 0; j < g.kw; ++j) {
-        const int wi = wb + j * g.dw;
-        if (wi < 0 || wi >= g.w) continue;
-        float xv[VEC], wv[VEC];
-        const float* wp = wt + (i * g.kw + j) * g.cout + co;
+    // branch-free tap: clamped (always valid) load, product selected away outside the image
+    auto tap = [&](int i, int j) {
+      const int hi = hb + i * g.dh, wi = wb + j * g.dw;
+      const bool ok = hi >= 0 && hi < g.h && wi >= 0 && wi < g.w;
+      const int hc = min(max(hi, 0), g.h - 1), wc = min(max(wi, 0), g.w - 1);
+      const float* wp = wt + (i * g.kw + j) * g.cout + co;
+      const T* xp = x + ((static_cast<int64_t>(n) * g.h + hc) * g.w + wc) * g.cin;
+      float xv[VEC], wv[OV];
+      load_wvec<OV>(wp, wv);
+      if constexpr (MT == 1) {
+        Vec<T, VEC>::load(xp + co, xv);
+      } else if constexpr (MT > 1) {
+        Vec<T, VEC>::load(xp + ci, xv);
+      } else {
 #pragma unroll
-        for (int v = 0; v < VEC; ++v) wv[v] = wp[v];
-        if constexpr (!MULT) {
-          Vec<T, VEC>::load(xrow + static_cast<int64_t>(wi) * g.cin + co, xv);
-        } else {
-#pragma unroll
-          for (int v = 0; v < VEC; ++v) xv[v] = Io<T>::ld(xrow + static_cast<int64_t>(wi) * g.cin + (co + v) / g.mult);
-        }
-#pragma unroll
-        for (int v = 0; v < VEC; ++v) acc[v] = fmaf(xv[v], wv[v], acc[v]);
+        for (int v = 0; v < VEC; ++v) xv[v] = Io<T>::ld(xp + (co + v) / g.mult);
       }
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) xv[v] = ok ? xv[v] : 0.f;
+#pragma unroll
+      for (int e = 0; e < OV; ++e) acc[e] = fmaf(xv[MT > 1 ? e / MT : e], wv[e], acc[e]);
+    };
+    if constexpr (KS > 0) {
+#pragma unroll
+      for (int i = 0; i < KS; ++i)
+#pragma unroll
+        for (int j = 0; j < KS; ++j) tap(i, j);
+    } else {
+      for (int i = 0; i < g.kh; ++i)
+        for (int j = 0; j < g.kw; ++j) tap(i, j);
     }
-    Vec<T, VEC>::store(y + ((static_cast<int64_t>(n) * g.ho + ho) * g.wo + wo) * g.cout + co, acc);
+    T* yp = y + ((static_cast<int64_t>(n) * g.ho + ho) * g.wo + wo) * g.cout + co;
+#pragma unroll
+    for (int q = 0; q < OV / VEC; ++q) Vec<T, VEC>::store(yp + q * VEC, acc + q * VEC);
   }
 }
 
 // ---------------------------------------------------------------- data grad
-template <typename T, int VEC, bool MULT>
-__global__ void __launch_bounds__(kDwBlock) dw_dgrad_kernel(DwGeom g, const T* __restrict__ dy,
+template <typename T, int VEC, int MT, int KS>
+__global__ void __launch_bounds__(kDwBlock) dw_dgrad_kernel(DwGeom g, DwDivs fd, const T* __restrict__ dy,
                                                             const float* __restrict__ wt, T* __restrict__ dx) {
   const int cv_n = g.cin / VEC;
-  const int64_t total = static_cast<int64_t>(g.n) * g.h * g.w * cv_n;
-  for (int64_t it = blockIdx.x * static_cast<int64_t>(kDwBlock) + threadIdx.x; it < total;
-       it += static_cast<int64_t>(gridDim.x) * kDwBlock) {
-    const int cv = static_cast<int>(it % cv_n);
-    int64_t pix = it / cv_n;
-    const int wi = static_cast<int>(pix % g.w);
-    pix /= g.w;
-    const int hi = static_cast<int>(pix % g.h);
-    const int n = static_cast<int>(pix / g.h);
+  const uint32_t total = static_cast<uint32_t>(g.n) * g.h * g.w * cv_n;  // < 2^31 (host splits)
+  for (uint32_t it = blockIdx.x * kDwBlock + threadIdx.x; it < total; it += gridDim.x * kDwBlock) {
+    uint32_t cvu, wiu, hiu;
+    const uint32_t pix = fd.c.divmod(it, cvu);
+    const uint32_t r = fd.w.divmod(pix, wiu);
+    const int n = static_cast<int>(fd.h.divmod(r, hiu));
+    const int cv = static_cast<int>(cvu), wi = static_cast<int>(wiu), hi = static_cast<int>(hiu);
     const int ci = cv * VEC;
     float acc[VEC];
 #pragma unroll
     for (int v = 0; v < VEC; ++v) acc[v] = 0.f;
-    for (int i = 0; i < g.kh; ++i) {
-      const int hn = hi + g.ph - i * g.dh;
-      if (hn < 0) continue;
-      const int ho = hn / g.sh;
-      if (ho * g.sh != hn || ho >= g.ho) continue;
-      const T* dyrow = dy + (static_cast<int64_t>(n) * g.ho + ho) * g.wo * g.cout;
-      for (int j = 0; j < g.kw; ++j) {
-        const int wn = wi + g.pw - j * g.dw;
-        if (wn < 0) continue;
-        const int wo = wn / g.sw;
-        if (wo * g.sw != wn || wo >= g.wo) continue;
-        const T* dp = dyrow + static_cast<int64_t>(wo) * g.cout;
-        const float* wp = wt + (i * g.kw + j) * g.cout;
-        if constexpr (!MULT) {
-          float dv[VEC];
-          Vec<T, VEC>::load(dp + ci, dv);
+    auto tap = [&](int i, int j) {
+      const int hn = hi + g.ph - i * g.dh, wn = wi + g.pw - j * g.dw;
+      const int ho = hn >= 0 ? hn / g.sh : 0, wo = wn >= 0 ? wn / g.sw : 0;
+      const bool ok = hn >= 0 && wn >= 0 && ho * g.sh == hn && wo * g.sw == wn && ho < g.ho && wo < g.wo;
+      const T* dp = dy + ((static_cast<int64_t>(n) * g.ho + min(ho, g.ho - 1)) * g.wo + min(wo, g.wo - 1)) * g.cout;
+      const float* wp = wt + (i * g.kw + j) * g.cout;
+      if constexpr (MT == 1) {
+        float dv[VEC], wv[VEC];
+        Vec<T, VEC>::load(dp + ci, dv);
+        load_wvec<VEC>(wp + ci, wv);
 #pragma unroll
-          for (int v = 0; v < VEC; ++v) acc[v] = fmaf(dv[v], wp[ci + v], acc[v]);
-        } else {
+        for (int v = 0; v < VEC; ++v) acc[v] = fmaf(ok ? dv[v] : 0.f, wv[v], acc[v]);
+      } else if constexpr (MT > 1) {
+        // the VEC*MT output channels fed by this input vector are contiguous
+        const int c0 = ci * MT;
 #pragma unroll
-          for (int v = 0; v < VEC; ++v) {
-            const int c0 = (ci + v) * g.mult;
-            for (int m = 0; m < g.mult; ++m) acc[v] = fmaf(Io<T>::ld(dp + c0 + m), wp[c0 + m], acc[v]);
+        for (int q = 0; q < MT; ++q) {
+          float dv[VEC], wv[VEC];
+          Vec<T, VEC>::load(dp + c0 + q * VEC, dv);
+          load_wvec<VEC>(wp + c0 + q * VEC, wv);
+#pragma unroll
+          for (int r = 0; r < VEC; ++r) {
+            const int e = q * VEC + r;
+            acc[e / MT] = fmaf(ok ? dv[r] : 0.f, wv[r], acc[e / MT]);
           }
         }
+      } else {
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+          const int c0 = (ci + v) * g.mult;
+          float sv = 0.f;
+          for (int m = 0; m < g.mult; ++m) sv = fmaf(Io<T>::ld(dp + c0 + m), wp[c0 + m], sv);
+          acc[v] = ok ? acc[v] + sv : acc[v];
+        }
       }
+    };
+    if constexpr (KS > 0) {
+#pragma unroll
+      for (int i = 0; i < KS; ++i)
+#pragma unroll
+        for (int j = 0; j < KS; ++j) tap(i, j);
+    } else {
+      for (int i = 0; i < g.kh; ++i)
+        for (int j = 0; j < g.kw; ++j) tap(i, j);
     }
     Vec<T, VEC>::store(dx + ((static_cast<int64_t>(n) * g.h + hi) * g.w + wi) * g.cin + ci, acc);
   }
@@ -205,8 +264,8 @@ __global__ void __launch_bounds__(kDwBlock) dw_dgrad_kernel(DwGeom g, const T* _
 // channel-vector lanes x ROWS pixel rows; each thread accumulates <= kMaxTaps
 // taps x VEC channels over its pixel stride, then the ROWS partials are reduced
 // through LDS and one [taps x VEC] partial per (slice, channel vector) is stored.
-template <typename T, int VEC, bool MULT>
-__global__ void __launch_bounds__(kDwBlock) dw_wgrad_kernel(DwGeom g, const T* __restrict__ dy,
+template <typename T, int VEC, int MT, int NT>
+__global__ void __launch_bounds__(kDwBlock) dw_wgrad_kernel(DwGeom g, DwDivs fd, const T* __restrict__ dy,
                                                             const T* __restrict__ x, float* __restrict__ part,
                                                             int lanes) {
   const int rows = kDwBlock / lanes;
@@ -215,45 +274,55 @@ __global__ void __launch_bounds__(kDwBlock) dw_wgrad_kernel(DwGeom g, const T* _
   const int cv = blockIdx.y * lanes + lane;
   const int cv_n = g.cout / VEC;
   const int taps = g.kh * g.kw;
-  const int t0 = blockIdx.z * kMaxTaps;
-  const int nt = min(kMaxTaps, taps - t0);
+  const int t0 = blockIdx.z * NT;
+  const int nt = min(NT, taps - t0);
   const bool active = cv < cv_n;
   const int co = cv * VEC;
-  float acc[kMaxTaps][VEC];
+  // multiplier: the VEC output channels read input channels base + rel[v], rel in [0, 4)
+  const int mult = MT > 0 ? MT : g.mult;
+  const int base = co / mult;
+  int rel[VEC];
 #pragma unroll
-  for (int t = 0; t < kMaxTaps; ++t)
+  for (int v = 0; v < VEC; ++v) rel[v] = (co + v) / mult - base;
+  float acc[NT][VEC];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int v = 0; v < VEC; ++v) acc[t][v] = 0.f;
-  const int64_t npix = static_cast<int64_t>(g.n) * g.ho * g.wo;
+  const uint32_t npix = static_cast<uint32_t>(g.n) * g.ho * g.wo;
   if (active) {
-    for (int64_t p = static_cast<int64_t>(blockIdx.x) * rows + row; p < npix;
-         p += static_cast<int64_t>(gridDim.x) * rows) {
-      const int wo = static_cast<int>(p % g.wo);
-      const int64_t r = p / g.wo;
-      const int ho = static_cast<int>(r % g.ho);
-      const int n = static_cast<int>(r / g.ho);
+    for (uint32_t p = blockIdx.x * rows + row; p < npix; p += gridDim.x * rows) {
+      uint32_t wou, hou;
+      const uint32_t r = fd.w.divmod(p, wou);
+      const int n = static_cast<int>(fd.h.divmod(r, hou));
+      const int wo = static_cast<int>(wou), ho = static_cast<int>(hou);
       float dv[VEC];
-      Vec<T, VEC>::load(dy + p * g.cout + co, dv);
+      Vec<T, VEC>::load(dy + static_cast<int64_t>(p) * g.cout + co, dv);
       const int hb = ho * g.sh - g.ph, wb = wo * g.sw - g.pw;
+      // Branch-free taps: every load goes to a clamped (valid) address and the product is
+      // selected away for out-of-image / padding taps, so all NT taps' loads issue back to
+      // back instead of one L2 round trip per tap behind a branch.
 #pragma unroll
-      for (int t = 0; t < kMaxTaps; ++t) {
-        if (t < nt) {  // fully unrolled with a block-uniform guard: acc stays in registers
-          const int tap = t0 + t;
-          const int i = tap / g.kw, j = tap - (tap / g.kw) * g.kw;
-          const int hi = hb + i * g.dh, wi = wb + j * g.dw;
-          if (hi >= 0 && hi < g.h && wi >= 0 && wi < g.w) {
-            const T* xp = x + ((static_cast<int64_t>(n) * g.h + hi) * g.w + wi) * g.cin;
-            float xv[VEC];
-            if constexpr (!MULT) {
-              Vec<T, VEC>::load(xp + co, xv);
-            } else {
+      for (int t = 0; t < NT; ++t) {
+        const int tap = t0 + min(t, nt - 1);
+        const int i = tap / g.kw, j = tap - (tap / g.kw) * g.kw;
+        const int hi = hb + i * g.dh, wi = wb + j * g.dw;
+        const bool ok = t < nt && hi >= 0 && hi < g.h && wi >= 0 && wi < g.w;
+        const int hc = min(max(hi, 0), g.h - 1), wc = min(max(wi, 0), g.w - 1);
+        const T* xp = x + ((static_cast<int64_t>(n) * g.h + hc) * g.w + wc) * g.cin;
+        float xv[VEC];
+        if constexpr (MT == 1) {
+          Vec<T, VEC>::load(xp + co, xv);
+        } else {  // <= 4 distinct inputs (mult >= 2, VEC <= 8): 4 scalar loads + selects
+          float xs[4];
 #pragma unroll
-              for (int v = 0; v < VEC; ++v) xv[v] = Io<T>::ld(xp + (co + v) / g.mult);
-            }
+          for (int k = 0; k < 4; ++k) xs[k] = Io<T>::ld(xp + min(base + k, g.cin - 1));
 #pragma unroll
-            for (int v = 0; v < VEC; ++v) acc[t][v] = fmaf(dv[v], xv[v], acc[t][v]);
-          }
+          for (int v = 0; v < VEC; ++v)
+            xv[v] = rel[v] == 0 ? xs[0] : rel[v] == 1 ? xs[1] : rel[v] == 2 ? xs[2] : xs[3];
         }
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) acc[t][v] = fmaf(ok ? xv[v] : 0.f, dv[v], acc[t][v]);
       }
     }
   }
@@ -261,7 +330,7 @@ __global__ void __launch_bounds__(kDwBlock) dw_wgrad_kernel(DwGeom g, const T* _
   __shared__ float red[kDwBlock * 8];
   const int64_t slab = static_cast<int64_t>(blockIdx.x) * taps * g.cout;
 #pragma unroll
-  for (int t = 0; t < kMaxTaps; ++t) {
+  for (int t = 0; t < NT; ++t) {
     if (t < nt) {  // nt is block-uniform, so the barriers below are reached by every thread
       __syncthreads();
 #pragma unroll
@@ -277,37 +346,64 @@ __global__ void __launch_bounds__(kDwBlock) dw_wgrad_kernel(DwGeom g, const T* _
   }
 }
 
-// dw[co][tap] = sum_G part[G][tap][co]   (output in the [Cout, 1, KH, KW] layout)
-__global__ void __launch_bounds__(kDwBlock) dw_wgrad_reduce_kernel(const float* __restrict__ part, int G,
-                                                                   int taps, int cout, float* __restrict__ dw) {
-  const int k = blockIdx.x * kDwBlock + threadIdx.x;  // k = tap * cout + co
-  if (k >= taps * cout) return;
+// dw[co][tap] = sum_G part[G][tap][co]   (output in the [Cout, 1, KH, KW] layout).
+// One block per 64 columns; 16 waves split the G rows (latency-bound reduction).
+constexpr int kRedWaves = 16;
+__global__ void __launch_bounds__(kRedWaves * 64) dw_wgrad_reduce_kernel(const float* __restrict__ part, int G,
+                                                                         int taps, int cout, float* __restrict__ dw) {
+  __shared__ float red[kRedWaves * 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int k = blockIdx.x * 64 + lane;  // k = tap * cout + co
+  const int ncol = taps * cout;
   float s = 0.f;
-  for (int gi = 0; gi < G; ++gi) s += part[static_cast<int64_t>(gi) * taps * cout + k];
-  const int tap = k / cout, co = k - (k / cout) * cout;
-  dw[static_cast<int64_t>(co) * taps + tap] = s;
+  if (k < ncol) {
+    const float* p = part + k;
+    int gi = w;
+    for (; gi + 7 * kRedWaves < G; gi += 8 * kRedWaves) {
+      float f[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) f[u] = p[static_cast<int64_t>(gi + u * kRedWaves) * ncol];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += f[u];
+    }
+    for (; gi < G; gi += kRedWaves) s += p[static_cast<int64_t>(gi) * ncol];
+  }
+  red[w * 64 + lane] = s;
+  __syncthreads();
+  if (w == 0 && k < ncol) {
+    float t = 0.f;
+#pragma unroll
+    for (int u = 0; u < kRedWaves; ++u) t += red[u * 64 + lane];
+    const int tap = k / cout, co = k - (k / cout) * cout;
+    dw[static_cast<int64_t>(co) * taps + tap] = t;
+  }
 }
 
 template <typename F>
-void dw_dispatch(int dtype, int vec, bool mult, F&& f) {
-  auto by_vec = [&](auto tag) {
-    using T = decltype(tag);
-    if (mult) {
-      if (vec == 8) f(T{}, std::integral_constant<int, 8>{}, std::true_type{});
-      else if (vec == 4) f(T{}, std::integral_constant<int, 4>{}, std::true_type{});
-      else if (vec == 2) f(T{}, std::integral_constant<int, 2>{}, std::true_type{});
-      else f(T{}, std::integral_constant<int, 1>{}, std::true_type{});
-    } else {
-      if (vec == 8) f(T{}, std::integral_constant<int, 8>{}, std::false_type{});
-      else if (vec == 4) f(T{}, std::integral_constant<int, 4>{}, std::false_type{});
-      else if (vec == 2) f(T{}, std::integral_constant<int, 2>{}, std::false_type{});
-      else f(T{}, std::integral_constant<int, 1>{}, std::false_type{});
+void dw_dispatch(int dtype, int vec, int mult, F&& f) {
+  auto by_mt = [&](auto t, auto v) {
+    switch (mult) {
+      case 1: f(t, v, std::integral_constant<int, 1>{}); break;
+      case 2: f(t, v, std::integral_constant<int, 2>{}); break;
+      case 3: f(t, v, std::integral_constant<int, 3>{}); break;
+      case 4: f(t, v, std::integral_constant<int, 4>{}); break;
+      case 6: f(t, v, std::integral_constant<int, 6>{}); break;
+      default: f(t, v, std::integral_constant<int, 0>{}); break;
     }
+  };
+  auto by_vec = [&](auto t) {
+    if (vec == 8) by_mt(t, std::integral_constant<int, 8>{});
+    else if (vec == 4) by_mt(t, std::integral_constant<int, 4>{});
+    else if (vec == 2) by_mt(t, std::integral_constant<int, 2>{});
+    else by_mt(t, std::integral_constant<int, 1>{});
   };
   if (dtype == kF32) by_vec(float{});
   else if (dtype == kBF16) by_vec(uint16_t{});
   else by_vec(_Float16{});
 }
+
+// Multiplier as the kernels treat it (see MT above).
+int mt_of(int mult) { return (mult == 1 || mult == 2 || mult == 3 || mult == 4 || mult == 6) ? mult : 0; }
 
 }  // namespace
 
@@ -318,29 +414,64 @@ int dw_vec(int dtype, int c) {
   return 1;
 }
 
-void launch_dw_fwd(const DwGeom& g, int dtype, const void* x, const float* wt, const float* bias, void* y,
-                   hipStream_t st) {
-  const int vec = dw_vec(dtype, g.cout);
-  const bool mult = g.mult != 1;
-  const int64_t items = static_cast<int64_t>(g.n) * g.ho * g.wo * (g.cout / vec);
-  const int grid = stream_grid(items, kDwBlock);
-  dw_dispatch(dtype, vec, mult, [&](auto t, auto v, auto m) {
-    using T = decltype(t);
-    dw_fwd_kernel<T, decltype(v)::value, decltype(m)::value><<<grid, kDwBlock, 0, st>>>(
-        g, static_cast<const T*>(x), wt, bias, static_cast<T*>(y));
-  });
+// The kernels index (pixel, channel-vector) pairs in 32 bits: split the batch so every
+// launch stays below 2^31 items (sub-batches are plain pointer offsets in NHWC).
+static int batch_chunk(int64_t per_image, int n) {
+  const int64_t lim = (int64_t{1} << 31) - 1;
+  int64_t c = per_image > 0 ? lim / per_image : n;
+  if (c < 1) c = 1;
+  return static_cast<int>(c < n ? c : n);
 }
 
-void launch_dw_dgrad(const DwGeom& g, int dtype, const void* dy, const float* wt, void* dx, hipStream_t st) {
-  const int vec = dw_vec(dtype, g.cin);
-  const bool mult = g.mult != 1;
-  const int64_t items = static_cast<int64_t>(g.n) * g.h * g.w * (g.cin / vec);
-  const int grid = stream_grid(items, kDwBlock);
-  dw_dispatch(dtype, vec, mult, [&](auto t, auto v, auto m) {
-    using T = decltype(t);
-    dw_dgrad_kernel<T, decltype(v)::value, decltype(m)::value><<<grid, kDwBlock, 0, st>>>(
-        g, static_cast<const T*>(dy), wt, static_cast<T*>(dx));
-  });
+static int64_t elem_bytes(int dtype) { return dtype == kF32 ? 4 : 2; }
+
+void launch_dw_fwd(const DwGeom& g0, int dtype, const void* x, const float* wt, const float* bias, void* y,
+                   hipStream_t st) {
+  const int mt = mt_of(g0.mult);
+  // MT > 1: vectors over the INPUT channels (each feeds VEC*MT contiguous outputs)
+  const int vec = mt > 1 ? dw_vec(dtype, g0.cin) : dw_vec(dtype, g0.cout);
+  const int cv_n = (mt > 1 ? g0.cin : g0.cout) / vec;
+  const int64_t per_img = static_cast<int64_t>(g0.ho) * g0.wo * cv_n;
+  const int nb = batch_chunk(per_img, g0.n);
+  const int64_t eb = elem_bytes(dtype);
+  for (int n0 = 0; n0 < g0.n; n0 += nb) {
+    DwGeom g = g0;
+    g.n = n0 + nb <= g0.n ? nb : g0.n - n0;
+    const char* xb = static_cast<const char*>(x) + static_cast<int64_t>(n0) * g.h * g.w * g.cin * eb;
+    char* yb = static_cast<char*>(y) + static_cast<int64_t>(n0) * g.ho * g.wo * g.cout * eb;
+    const DwDivs fd{FastDiv::make(cv_n), FastDiv::make(g.wo), FastDiv::make(g.ho)};
+    const int grid = stream_grid(per_img * g.n, kDwBlock);
+    dw_dispatch(dtype, vec, g.mult, [&](auto t, auto v, auto m) {
+      using T = decltype(t);
+      constexpr int V = decltype(v)::value, M = decltype(m)::value;
+      // KS = 0: runtime tap loop.  A fully unrolled 3x3 (KS = 3) measured 4-5x slower on
+      // BiSeNetV2 (it re-loads all 9 taps' weights per output with no latency to hide).
+      dw_fwd_kernel<T, V, M, 0><<<grid, kDwBlock, 0, st>>>(g, fd, reinterpret_cast<const T*>(xb), wt, bias,
+                                                             reinterpret_cast<T*>(yb));
+    });
+  }
+}
+
+void launch_dw_dgrad(const DwGeom& g0, int dtype, const void* dy, const float* wt, void* dx, hipStream_t st) {
+  const int vec = dw_vec(dtype, g0.cin);
+  const int cv_n = g0.cin / vec;
+  const int64_t per_img = static_cast<int64_t>(g0.h) * g0.w * cv_n;
+  const int nb = batch_chunk(per_img, g0.n);
+  const int64_t eb = elem_bytes(dtype);
+  for (int n0 = 0; n0 < g0.n; n0 += nb) {
+    DwGeom g = g0;
+    g.n = n0 + nb <= g0.n ? nb : g0.n - n0;
+    const char* dyb = static_cast<const char*>(dy) + static_cast<int64_t>(n0) * g.ho * g.wo * g.cout * eb;
+    char* dxb = static_cast<char*>(dx) + static_cast<int64_t>(n0) * g.h * g.w * g.cin * eb;
+    const DwDivs fd{FastDiv::make(cv_n), FastDiv::make(g.w), FastDiv::make(g.h)};
+    const int grid = stream_grid(per_img * g.n, kDwBlock);
+    dw_dispatch(dtype, vec, g.mult, [&](auto t, auto v, auto m) {
+      using T = decltype(t);
+      constexpr int V = decltype(v)::value, M = decltype(m)::value;
+      dw_dgrad_kernel<T, V, M, 0><<<grid, kDwBlock, 0, st>>>(g, fd, reinterpret_cast<const T*>(dyb), wt,
+                                                               reinterpret_cast<T*>(dxb));
+    });
+  }
 }
 
 DwWgradPlan dw_wgrad_plan(const DwGeom& g, int dtype) {
@@ -350,11 +481,15 @@ DwWgradPlan dw_wgrad_plan(const DwGeom& g, int dtype) {
   p.lanes = 64;
   while (p.lanes > 1 && p.lanes / 2 >= cv_n) p.lanes /= 2;
   p.chunks = (cv_n + p.lanes - 1) / p.lanes;
-  p.tap_groups = (g.kh * g.kw + kMaxTaps - 1) / kMaxTaps;
+  const int taps = g.kh * g.kw;
+  p.nt = taps <= 3 ? 3 : taps <= 5 ? 5 : kMaxTaps;
+  p.tap_groups = (taps + p.nt - 1) / p.nt;
   const int64_t npix = static_cast<int64_t>(g.n) * g.ho * g.wo;
   const int rows = kDwBlock / p.lanes;
-  // ~4 waves of blocks over 256 CUs, but every block keeps >= 16 pixels per row
-  int64_t G = 2048 / (static_cast<int64_t>(p.chunks) * p.tap_groups);
+  // ~1024 blocks over 256 CUs, <= 512 slabs (the column reduce reads G rows), and
+  // every block keeps >= 16 pixels per row
+  int64_t G = 1024 / (static_cast<int64_t>(p.chunks) * p.tap_groups);
+  if (G > 512) G = 512;
   const int64_t gmax = (npix + static_cast<int64_t>(rows) * 16 - 1) / (static_cast<int64_t>(rows) * 16);
   if (G > gmax) G = gmax;
   if (G < 1) G = 1;
@@ -364,17 +499,25 @@ DwWgradPlan dw_wgrad_plan(const DwGeom& g, int dtype) {
 
 void launch_dw_wgrad(const DwGeom& g, int dtype, const void* dy, const void* x, float* part, float* dw,
                      hipStream_t st) {
+  // pixels are indexed in 32 bits; the binding rejects > 2^31 output pixels per call
   const DwWgradPlan p = dw_wgrad_plan(g, dtype);
-  const bool mult = g.mult != 1;
   dim3 grid(p.slices, p.chunks, p.tap_groups);
-  dw_dispatch(dtype, p.vec, mult, [&](auto t, auto v, auto m) {
+  const DwDivs fd{FastDiv::make(1), FastDiv::make(g.wo), FastDiv::make(g.ho)};
+  dw_dispatch(dtype, p.vec, g.mult, [&](auto t, auto v, auto m) {
     using T = decltype(t);
-    dw_wgrad_kernel<T, decltype(v)::value, decltype(m)::value><<<grid, kDwBlock, 0, st>>>(
-        g, static_cast<const T*>(dy), static_cast<const T*>(x), part, p.lanes);
+    constexpr int V = decltype(v)::value, M = decltype(m)::value;
+    const T* dyp = static_cast<const T*>(dy);
+    const T* xp = static_cast<const T*>(x);
+    if (p.nt == 3)
+      dw_wgrad_kernel<T, V, M, 3><<<grid, kDwBlock, 0, st>>>(g, fd, dyp, xp, part, p.lanes);
+    else if (p.nt == 5)
+      dw_wgrad_kernel<T, V, M, 5><<<grid, kDwBlock, 0, st>>>(g, fd, dyp, xp, part, p.lanes);
+    else
+      dw_wgrad_kernel<T, V, M, kMaxTaps><<<grid, kDwBlock, 0, st>>>(g, fd, dyp, xp, part, p.lanes);
   });
   const int taps = g.kh * g.kw;
-  const int rb = (taps * g.cout + kDwBlock - 1) / kDwBlock;
-  dw_wgrad_reduce_kernel<<<rb, kDwBlock, 0, st>>>(part, p.slices, taps, g.cout, dw);
+  const int rb = (taps * g.cout + 63) / 64;
+  dw_wgrad_reduce_kernel<<<rb, kRedWaves * 64, 0, st>>>(part, p.slices, taps, g.cout, dw);
 }
 
 }  // namespace rtseg

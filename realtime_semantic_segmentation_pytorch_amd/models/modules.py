@@ -80,6 +80,10 @@ class _FusedTail:
 
     def forward(self, x, residual=None, act=None):
         conv, bn, own = self[0], self[1], self[2]
+        if ops.conv_ok(x, conv):
+            y = self._mfma_tail(x, conv, bn, own, residual, act)
+            if y is not None:
+                return y
         y = conv(x)
         if residual is None:
             return ops.bn_act(y, bn, own, act_module=own)
@@ -91,6 +95,31 @@ class _FusedTail:
         post = act if act is not None else "none"
         return ops.bn_act(y, bn, post, residual=residual,
                           act_module=act if isinstance(act, nn.Module) else None)
+
+    @staticmethod
+    def _mfma_tail(x, conv, bn, own, residual, act):
+        """conv on the MFMA kernel with the BN statistics (training) or the whole
+        BN + residual + activation tail (inference) in its epilogue; None -> stock path."""
+        if not isinstance(bn, (nn.BatchNorm2d, nn.SyncBatchNorm)):
+            return None
+        own_code = ops.bn_act_code(own)
+        if residual is None:
+            post = own_code
+        elif own_code == 0:
+            post = ops.bn_act_code(act) if act is not None else 0
+        else:
+            return None
+        if post is None:
+            return None
+        use_batch = bn.training or not bn.track_running_stats or bn.running_mean is None
+        if not use_batch:
+            return ops.conv_bn_act_eval(x, conv, bn, post, residual)
+        r = ops.conv_bn_stats(x, conv)
+        if r is None:
+            return None
+        y, part = r
+        return ops.bn_act(y, bn, post, residual=residual, part=part,
+                          act_module=own if residual is None else (act if isinstance(act, nn.Module) else None))
 
 
 class ConvBNAct(_FusedTail, nn.Sequential):

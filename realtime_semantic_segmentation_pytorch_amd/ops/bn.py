@@ -56,17 +56,22 @@ def _sync_group(bn):
 
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, bn, act, use_batch_stats, pg):
+    def forward(ctx, x, weight, bias, residual, bn, act, use_batch_stats, pg, part=None):
         if use_batch_stats:
             track = bn.track_running_stats and bn.training and bn.running_mean is not None
             rm = bn.running_mean if track else None
             rv = bn.running_var if track else None
             nb = bn.num_batches_tracked if track else None
+            count = float(x.numel() // x.shape[1])
             if pg is None:
-                mi, ss, sums = ops().bn_stats_finalize(x, weight, bias, rm, rv, nb,
-                                                       float(bn.momentum), float(bn.eps))
+                if part is not None:  # statistics already produced by the conv epilogue
+                    mi, ss, sums = ops().bn_finalize_slab(part, weight, bias, rm, rv, nb, float(bn.momentum),
+                                                          float(bn.eps), count)
+                else:
+                    mi, ss, sums = ops().bn_stats_finalize(x, weight, bias, rm, rv, nb,
+                                                           float(bn.momentum), float(bn.eps))
             else:  # SyncBN: one all-reduce of (sum, sumsq, count) in fp64 over RCCL
-                sums = ops().bn_stats_sums(x)
+                sums = ops().bn_slab_sums(part, count) if part is not None else ops().bn_stats_sums(x)
                 dist.all_reduce(sums, group=pg)
                 mi, ss = ops().bn_finalize(sums, weight, bias, rm, rv, nb, float(bn.momentum),
                                            float(bn.eps))
@@ -100,7 +105,7 @@ class _BNActFn(torch.autograd.Function):
         dx, dres, dw, db = ops().bn_backward(dy, x, y, bsums, sums, mi, ss, weight, ctx.act,
                                              ctx.mask, want_dres, ctx.batch_stats, want_dw)
         return (dx, dw if want_dw else None, db if want_dw else None,
-                dres if want_dres else None, None, None, None, None)
+                dres if want_dres else None, None, None, None, None, None)
 
 
 def vec_width(dtype: torch.dtype, c: int) -> int:
@@ -139,8 +144,11 @@ def fused_ok(x: torch.Tensor, bn, act) -> bool:
 
 
 def bn_act(x: torch.Tensor, bn, act=None, residual: Optional[torch.Tensor] = None,
-           act_module: Optional[nn.Module] = None) -> torch.Tensor:
-    """``act(bn(x) + residual)``; ``act`` is a fused-activation code or module/str."""
+           act_module: Optional[nn.Module] = None, part: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``act(bn(x) + residual)``; ``act`` is a fused-activation code or module/str.
+
+    ``part``: BN statistics slab of ``x`` already computed by its producer (the MFMA conv
+    epilogue, ``ops.conv``); used only on the fused batch-statistics path."""
     code = act if isinstance(act, int) else act_code(act)
     if use_hip(x) and code is not None and fused_ok(x, bn, code) and (
             residual is None or (residual.shape == x.shape
@@ -150,7 +158,8 @@ def bn_act(x: torch.Tensor, bn, act=None, residual: Optional[torch.Tensor] = Non
             residual = residual.to(x.dtype)
         use_batch = bn.training or not bn.track_running_stats or bn.running_mean is None
         pg = _sync_group(bn) if use_batch else None
-        return _BNActFn.apply(x, bn.weight, bn.bias, residual, bn, code, use_batch, pg)
+        return _BNActFn.apply(x, bn.weight, bn.bias, residual, bn, code, use_batch, pg,
+                              part if use_batch else None)
     y = bn(x)
     if residual is not None:
         y = y + residual

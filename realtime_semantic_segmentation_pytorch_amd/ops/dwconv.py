@@ -16,6 +16,8 @@ place.  Under autocast the input is cast to the autocast dtype like
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -69,8 +71,10 @@ def depthwise_ok(conv: nn.Conv2d) -> bool:
 
 
 def dw_conv2d(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
-    """``conv(x)`` for a depth-wise ``conv``; HIP kernels for channels-last GPU inputs."""
-    if x.dim() == 4 and use_hip(x) and x.is_contiguous(memory_format=torch.channels_last):
+    """``conv(x)`` for a depth-wise ``conv``; HIP kernels for channels-last GPU inputs
+    (``RTSEG_DWCONV=0`` keeps MIOpen, for A/B comparisons)."""
+    if (x.dim() == 4 and use_hip(x) and x.is_contiguous(memory_format=torch.channels_last)
+            and os.environ.get("RTSEG_DWCONV", "1") != "0"):
         dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
         if dt in _DTYPES and conv.weight.dtype in _DTYPES:
             kh, kw = conv.kernel_size

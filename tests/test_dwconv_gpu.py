@@ -21,6 +21,9 @@ GEOMS = [
     (3, 1, (3, 3), 1, 1, (9, 11)),      # odd channel count -> scalar vectors
     (40, 2, (5, 5), 1, 1, (12, 14)),    # 25 taps -> several wgrad tap groups
     (64, 1, (3, 3), 1, 1, (64, 128)),
+    (8, 5, (3, 3), 1, 1, (10, 12)),     # multiplier without a compiled fast path
+    (8, 3, (3, 3), 2, 1, (13, 17)),
+    (128, 6, (3, 3), 1, 1, (16, 32)),   # BiSeNetV2 stage-5 shape class
 ]
 
 
