@@ -12,10 +12,10 @@
 //    Cin % 64 == 0, else 32); 256 threads = 4 waves in 2x2, each wave a 64 x BN/2
 //    sub-tile of v_mfma_f32_16x16x32_bf16 (BK/32 MFMA K-steps per stage);
 //  * a K-step is one tap and BK consecutive input channels, so every A row is one
-//    contiguous 64/128-byte read (padding taps: the load is still issued from a clamped
-//    address and the VALUE is masked to zero -- no branch around the load);
-//  * register-staged double-buffered LDS: the global loads of step k+1 are in flight
-//    while step k's MFMAs run; one barrier per K-step;
+//    contiguous 64/128-byte read;
+//  * operands go global -> LDS by DMA (global_load_lds_dwordx4, no staging registers)
+//    into a 3-stage ring: steps k+1 and k+2 are in flight while step k's MFMAs run; one
+//    counted vmcnt + raw barrier per K-step; padding taps DMA from a 16-byte zero page;
 //  * LDS holds each 32-wide K sub-tile as rows of 64 B (four 16-byte chunks); chunk q of row r at
 //    q ^ h[(r >> 2) & 3], h = {0, 2, 3, 1}, which makes the ds_read_b128 fragment
 //    reads of the 16x16x32 layout conflict-free (each 16-lane LDS group hits 16
@@ -63,6 +63,40 @@ __device__ __forceinline__ int swz(int r, int q) {
 
 __device__ __forceinline__ bf16x8_t as_frag(uint4 v) { return __builtin_bit_cast(bf16x8_t, v); }
 
+// 16 zero bytes in global memory: the DMA source of padding taps / rows past the edge.
+__device__ uint4 g_zero16[1];
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N <= 8, "vmcnt immediate");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+}
+
+// LDS-DMA issued from inline asm: hipcc's waitcnt pass cannot tell which LDS bytes a
+// __builtin_amdgcn_global_load_lds writes, so it drains vmcnt(0) before every later ds_read
+// (it did, in this kernel) -- which serialises the ring.  Opaque to the compiler, the DMA is
+// ordered by the kernel's own counted vmcnt + barrier instead.  M0 = LDS byte address of the
+// wave's 1 KiB destination (wave-uniform); one wait state between the M0 write and its use.
+__device__ __forceinline__ void glds16(const void* src, uint4* lds_dst) {
+  const uint32_t lds_addr = __builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) void*)lds_dst)));
+  asm volatile(
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %0, off"
+      :
+      : "v"(src), "s"(lds_addr)
+      : "memory", "m0");
+}
+
 __device__ __forceinline__ uint4 mask4(uint4 v, bool ok) {
   const unsigned m = ok ? 0xffffffffu : 0u;
   v.x &= m; v.y &= m; v.z &= m; v.w &= m;
@@ -78,31 +112,39 @@ __device__ __forceinline__ float epi_act(float v, int act) {
 template <int EPI, bool STATS, int BN, int BK>
 __global__ void __launch_bounds__(kCThreads, 2) conv_mfma_kernel(ConvK a) {
   constexpr int QR = BK / 8;                   // 16-byte chunks per tile row
-  constexpr int A_PER = kCBM * QR / kCThreads;  // A chunks staged per thread per K-step
-  constexpr int B_PER = BN * QR / kCThreads;    // B chunks staged per thread per K-step
   constexpr int A_SUB = kCBM * 4;               // chunks of one 32-wide K sub-tile of A
   constexpr int B_SUB = BN * 4;
   constexpr int STAGE = (kCBM + BN) * QR;       // chunks per pipeline stage
   constexpr int WNT = BN / 32;                  // 16-wide N tiles per wave (2x2 waves)
-  static_assert(A_PER >= 1 && B_PER >= 1, "tile too small for 256 threads");
-  __shared__ uint4 lds[2 * STAGE > 2048 ? 2 * STAGE : 2048];  // 2 stages; >= 32 KiB for the epilogue
+  // pipeline stages: 3 keeps two K-steps of DMA in flight across each barrier; the widest tile
+  // (128 x 128 x 64: 32 KiB per stage) uses 2 so that two blocks still fit a CU's LDS
+  constexpr int NST = (BN == 128 && BK == 64) ? 2 : 3;
+  __shared__ uint4 lds[NST * STAGE > 2048 ? NST * STAGE : 2048];  // >= 32 KiB for the epilogue
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int n0 = blockIdx.y * BN;
   const int cch = a.cin / BK;  // K-steps per tap
   const int nk = a.kh * a.kw * cch;
-  const int lq = tid % QR;     // this thread's 16-byte chunk within a row
-  const int lr = tid / QR;     // first row; rows lr + e * (256 / QR)
-  constexpr int RSTEP = kCThreads / QR;
+  // LDS-DMA staging: one global_load_lds_dwordx4 moves 64 lanes x 16 B = 16 rows of one 32-wide
+  // K sub-tile into 1 KiB of LDS at (wave-uniform base + 16 B * lane).  The bank swizzle is
+  // applied on the SOURCE side: lane L fills physical chunk L & 3 of row L >> 2, i.e. it loads
+  // logical K chunk (L & 3) ^ h[(L >> 4) & 3] of that row (h = {0, 2, 3, 1}, see swz()).
+  constexpr int A_INST = (BK / 32) * (kCBM / 16), B_INST = (BK / 32) * (BN / 16);
+  constexpr int A_IW = A_INST / 4, B_IW = B_INST / 4;  // DMA instructions per wave per stage
+  static_assert(A_IW >= 1 && B_IW >= 1, "tile too small for 4 waves");
+  const int lrow = lane >> 2;
+  const int lkc = (lane & 3) ^ ((0x1320 >> (((lane >> 4) & 3) * 4)) & 0xF);
   const int64_t wstride = static_cast<int64_t>(a.kh) * a.kw * a.cin;
 
-  const uint16_t* wrow[B_PER];
-  bool wok[B_PER];
+  const uint16_t* wrow[B_IW];
+  bool wok[B_IW];
 #pragma unroll
-  for (int e = 0; e < B_PER; ++e) {
-    const int co = n0 + lr + RSTEP * e;
+  for (int e = 0; e < B_IW; ++e) {
+    const int I = wid * B_IW + e;
+    const int h = I / (BN / 16), rg = I % (BN / 16);
+    const int co = n0 + 16 * rg + lrow;
     wok[e] = co < a.cout;
-    wrow[e] = a.w + static_cast<int64_t>(min(co, a.cout - 1)) * wstride + lq * 8;
+    wrow[e] = a.w + static_cast<int64_t>(min(co, a.cout - 1)) * wstride + (4 * h + lkc) * 8;
   }
   float csum[WNT], csq[WNT];
 #pragma unroll
@@ -110,19 +152,21 @@ __global__ void __launch_bounds__(kCThreads, 2) conv_mfma_kernel(ConvK a) {
 
   for (int mt = blockIdx.x; mt < a.mtiles; mt += gridDim.x) {
     const int m0 = mt * kCBM;
-    const uint16_t* xbase[A_PER];
-    int hb[A_PER], wb[A_PER];
-    bool rok[A_PER];
+    const uint16_t* xbase[A_IW];
+    int hb[A_IW], wb[A_IW];
+    bool rok[A_IW];
 #pragma unroll
-    for (int e = 0; e < A_PER; ++e) {
-      const int m = m0 + lr + RSTEP * e;
+    for (int e = 0; e < A_IW; ++e) {
+      const int I = wid * A_IW + e;
+      const int h = I / 8, rg = I % 8;
+      const int m = m0 + 16 * rg + lrow;
       rok[e] = m < a.m;
       uint32_t wo_, ho_;
       const uint32_t t = a.fwo.divmod(static_cast<uint32_t>(rok[e] ? m : a.m - 1), wo_);
       const uint32_t n_ = a.fho.divmod(t, ho_);
       hb[e] = static_cast<int>(ho_) * a.sh - a.ph;
       wb[e] = static_cast<int>(wo_) * a.sw - a.pw;
-      xbase[e] = a.x + static_cast<int64_t>(n_) * a.ih * a.iw * a.cin + lq * 8;
+      xbase[e] = a.x + static_cast<int64_t>(n_) * a.ih * a.iw * a.cin + (4 * h + lkc) * 8;
     }
     f32x4_t acc[4][WNT];
 #pragma unroll
@@ -130,42 +174,45 @@ __global__ void __launch_bounds__(kCThreads, 2) conv_mfma_kernel(ConvK a) {
 #pragma unroll
       for (int ni = 0; ni < WNT; ++ni) acc[mi][ni] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    uint4 ra[A_PER], rb[B_PER];
-    auto gload = [&](int kk) {
+    // issue the DMA of K-step kk into stage buffer `buf` (padding taps read the zero page)
+    auto stage = [&](int kk, int buf) {
       const int tap = kk / cch;
       const int c0 = (kk - tap * cch) * BK;
       const int i = tap / a.kw, j = tap - (tap / a.kw) * a.kw;
-#pragma unroll
-      for (int e = 0; e < A_PER; ++e) {
-        const int hi = hb[e] + i * a.dh, wi = wb[e] + j * a.dw;
-        const bool ok = rok[e] && hi >= 0 && hi < a.ih && wi >= 0 && wi < a.iw;
-        const int hc = min(max(hi, 0), a.ih - 1), wc = min(max(wi, 0), a.iw - 1);
-        const uint4 v = *reinterpret_cast<const uint4*>(xbase[e] + (static_cast<int64_t>(hc) * a.iw + wc) * a.cin + c0);
-        ra[e] = mask4(v, ok);
-      }
-#pragma unroll
-      for (int e = 0; e < B_PER; ++e) {
-        const uint4 v = *reinterpret_cast<const uint4*>(wrow[e] + tap * a.cin + c0);
-        rb[e] = mask4(v, wok[e]);
-      }
-    };
-    // chunk lq of a row: K sub-tile lq / 4, chunk lq % 4 inside it
-    auto sstore = [&](int buf) {
       uint4* A = lds + buf * STAGE;
       uint4* B = A + kCBM * QR;
 #pragma unroll
-      for (int e = 0; e < A_PER; ++e) A[(lq >> 2) * A_SUB + swz(lr + RSTEP * e, lq & 3)] = ra[e];
+      for (int e = 0; e < A_IW; ++e) {
+        const int I = wid * A_IW + e;
+        const int hi = hb[e] + i * a.dh, wi = wb[e] + j * a.dw;
+        const bool ok = rok[e] && hi >= 0 && hi < a.ih && wi >= 0 && wi < a.iw;
+        const uint16_t* src = xbase[e] + (static_cast<int64_t>(hi) * a.iw + wi) * a.cin + c0;
+        glds16(ok ? static_cast<const void*>(src) : static_cast<const void*>(g_zero16),
+               A + (I / 8) * A_SUB + (I % 8) * 64);
+      }
 #pragma unroll
-      for (int e = 0; e < B_PER; ++e) B[(lq >> 2) * B_SUB + swz(lr + RSTEP * e, lq & 3)] = rb[e];
+      for (int e = 0; e < B_IW; ++e) {
+        const int I = wid * B_IW + e;
+        const uint16_t* src = wrow[e] + tap * a.cin + c0;
+        glds16(wok[e] ? static_cast<const void*>(src) : static_cast<const void*>(g_zero16),
+               B + (I / (BN / 16)) * B_SUB + (I % (BN / 16)) * 64);
+      }
     };
 
-    gload(0);
-    sstore(0);
-    __syncthreads();
+    // NST-stage ring: DMA of K-steps kk+1 .. kk+NST-1 is in flight while kk computes.  Step kk's
+    // data is published by a COUNTED vmcnt (this wave's DMAs of the younger step may stay
+    // outstanding) + a raw s_barrier -- __syncthreads() would drain every DMA (vmcnt(0)).
+    constexpr int PER = A_IW + B_IW;  // DMA instructions per wave per stage
+#pragma unroll
+    for (int p = 0; p < NST - 1; ++p)
+      if (p < nk) stage(p, p);
     for (int kk = 0; kk < nk; ++kk) {
-      const int cur = kk & 1;
-      if (kk + 1 < nk) gload(kk + 1);
-      const uint4* A = lds + cur * STAGE;
+      if (NST == 3 && kk + 1 < nk) wait_vmcnt<(NST - 2) * PER>();
+      else wait_vmcnt<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // all waves: step kk landed, step kk-1's buffer is free
+      if (kk + NST - 1 < nk) stage(kk + NST - 1, (kk + NST - 1) % NST);
+      const uint4* A = lds + (kk % NST) * STAGE;
       const uint4* B = A + kCBM * QR;
 #pragma unroll
       for (int hs = 0; hs < BK / 32; ++hs) {
@@ -176,15 +223,16 @@ __global__ void __launch_bounds__(kCThreads, 2) conv_mfma_kernel(ConvK a) {
 #pragma unroll
         for (int ni = 0; ni < WNT; ++ni)
           fb[ni] = as_frag(B[hs * B_SUB + swz(wn * (BN / 2) + ni * 16 + (lane & 15), lane >> 4)]);
+        __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
           for (int ni = 0; ni < WNT; ++ni)
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mi], fb[ni], acc[mi][ni], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
       }
-      if (kk + 1 < nk) sstore(cur ^ 1);
-      __syncthreads();
     }
+    __syncthreads();  // every wave's last MFMA operands are read before the LDS is reused
 
     // ---- epilogue: stage this wave's 64 x (BN/2) tile as bf16 rows, then 16-byte stores
     constexpr int WC = BN / 2;  // columns per wave
