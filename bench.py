@@ -55,6 +55,8 @@ def parse():
     p.add_argument("--model", default="ddrnet", help="registry key (ddrnet | bisenetv2 | stdc | ...)")
     p.add_argument("--arch", default="DDRNet-23", help="DDRNet arch_type / STDC+PP-LiteSeg encoder_type")
     p.add_argument("--detail-head", action="store_true", help="STDC: detail head instead of aux heads")
+    p.add_argument("--kd", action="store_true",
+                   help="knowledge distillation from an SMP DeepLabV3+/ResNet-101 teacher (random init)")
     p.add_argument("--no-infer", action="store_true", help="skip the inference-FPS measurement")
     p.add_argument("--fp32", action="store_true", help="disable bf16 autocast (diagnostic)")
     p.add_argument("--no-fused-loss", action="store_true")
@@ -94,6 +96,10 @@ def make_config(a, world):
     c.use_tb = False
     c.load_ckpt = False
     c.save_dir = os.environ.get("RTSEG_BENCH_DIR", "/tmp/rtseg_bench")
+    if a.kd:  # BASELINE config 5: DeepLabv3+/ResNet-101 teacher -> student, Hinton KL (T=4)
+        c.kd_training = True
+        c.teacher_model, c.teacher_encoder, c.teacher_decoder = "smp", "resnet101", "deeplabv3p"
+        c.teacher_random_init = True
     c.is_testing = False
     c.use_ema = True
     return c
@@ -248,7 +254,8 @@ def main():
                            "stdc", "ppliteseg") else a.model,
                        "global_batch": a.batch * world,
                        "seq_len": f"{a.height}x{a.width}", "parallelism": f"dp{world}",
-                       "num_class": 19, "loss": "ohem+detail" if a.detail_head else "ohem+aux" if cfg.use_aux else "ohem",
+                       "num_class": 19, "loss": ("ohem+detail" if a.detail_head else "ohem+aux" if cfg.use_aux else "ohem")
+                       + ("+kd(deeplabv3p-r101)" if a.kd else ""),
                        "optimizer": "sgd+onecycle+ema"},
             "extra": extra,
         }

@@ -65,7 +65,7 @@ class SegTrainer(BaseTrainer):
         """Forward + total loss. Returns (loss, main_preds, extras dict)."""
         cfg = self.config
         extras = {}
-        defer = bool(getattr(cfg, "fused_loss", True)) and not cfg.use_detail_head
+        defer = bool(getattr(cfg, "fused_loss", True))
         # uint8 label maps: the fused loss kernels read them ~4x per step (main/aux x fwd/bwd)
         labels = masks
         if (masks.is_cuda and masks.dtype == torch.int64 and cfg.num_class <= 255

@@ -12,6 +12,7 @@
 #include <torch/library.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 
 #include "rtseg_launch.h"
@@ -72,7 +73,11 @@ static at::Tensor interp_bwd(const at::Tensor& g, int64_t in_h, int64_t in_w, bo
   c10::hip::HIPGuardMasqueradingAsCUDA guard(g.device());
   auto fmt = channels_last ? at::MemoryFormat::ChannelsLast : at::MemoryFormat::Contiguous;
   at::Tensor gx = at::empty({g.size(0), g.size(1), in_h, in_w}, g.options().memory_format(fmt));
-  launch_interp_bwd(view4(g), view4(gx), align_corners, cur_stream());
+  const char* sep_env = std::getenv("RTSEG_INTERP_SEP");  // "0": gather-form kernels only (A/B)
+  const int64_t wsn = (sep_env && sep_env[0] == '0') ? 0 : interp_bwd_ws_elems(view4(g), view4(gx));
+  at::Tensor ws;
+  if (wsn > 0) ws = at::empty({wsn}, g.options().dtype(at::kFloat));
+  launch_interp_bwd(view4(g), view4(gx), align_corners, wsn > 0 ? ws.data_ptr<float>() : nullptr, cur_stream());
   return gx;
 }
 

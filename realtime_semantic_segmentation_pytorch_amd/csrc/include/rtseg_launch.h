@@ -19,7 +19,10 @@ struct Tensor4 {
 // ---- interp.hip -------------------------------------------------------------
 void launch_interp_fwd(const Tensor4& x, const Tensor4* skip, const Tensor4& y, int act,
                        bool align_corners, hipStream_t st);
-void launch_interp_bwd(const Tensor4& g, const Tensor4& gx, bool align_corners, hipStream_t st);
+// ws: fp32 workspace of interp_bwd_ws_elems(g, gx) elements (separable path for large
+// up-scaling), or nullptr when that returns 0
+int64_t interp_bwd_ws_elems(const Tensor4& g, const Tensor4& gx);
+void launch_interp_bwd(const Tensor4& g, const Tensor4& gx, bool align_corners, float* ws, hipStream_t st);
 void launch_act_mask(const void* g, const void* y, void* out, int64_t n, int dtype, int act,
                      hipStream_t st);
 

@@ -200,6 +200,49 @@ __global__ void __launch_bounds__(256) interp_bwd_cl_bf16(
   }
 }
 
+// Separable backward for large up-scaling (e.g. the x8 logits upsample a KD loss or a
+// non-deferred loss materialises): gx = Rh^T . g . Rw as two gathers through an fp32
+// [N, OH, IW, C] workspace -- W-pass then H-pass, ~(2s+1) taps each -- instead of one
+// gather over a (2s+1)^2 window per input element.  Index order is channel-fastest so
+// channels-last gradients are read coalesced; loads are never behind a weight test.
+template <typename T>
+__global__ void __launch_bounds__(256) interp_bwd_sep_w(const T* __restrict__ g, Shape4 gs, float* __restrict__ t,
+                                                        int iw, LinMap mw, FastDiv fc, FastDiv fiw, FastDiv foh,
+                                                        uint32_t total) {
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    uint32_t c, ix, oy;
+    const uint32_t r0 = fc.divmod(i, c);
+    const uint32_t r1 = fiw.divmod(r0, ix);
+    const uint32_t n = foh.divmod(r1, oy);
+    int lo, hi;
+    mw.out_range(static_cast<int>(ix), gs.w, lo, hi);
+    const T* gb = g + static_cast<int64_t>(n) * gs.sn + static_cast<int64_t>(c) * gs.sc +
+                  static_cast<int64_t>(oy) * gs.sh;
+    float acc = 0.f;
+    for (int ox = lo; ox <= hi; ++ox) acc = fmaf(mw.weight(ox, static_cast<int>(ix)), Io<T>::ld(gb + ox * gs.sw), acc);
+    t[i] = acc;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) interp_bwd_sep_h(const float* __restrict__ t, int oh, T* __restrict__ gx,
+                                                        Shape4 xs, LinMap mh, FastDiv fc, FastDiv fiw, FastDiv fih,
+                                                        uint32_t total) {
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    uint32_t c, ix, iy;
+    const uint32_t r0 = fc.divmod(i, c);
+    const uint32_t r1 = fiw.divmod(r0, ix);
+    const uint32_t n = fih.divmod(r1, iy);
+    int lo, hi;
+    mh.out_range(static_cast<int>(iy), oh, lo, hi);
+    const int64_t row = static_cast<int64_t>(xs.w) * xs.c;  // t row stride (IW * C)
+    const float* tb = t + static_cast<int64_t>(n) * oh * row + static_cast<int64_t>(ix) * xs.c + c;
+    float acc = 0.f;
+    for (int oy = lo; oy <= hi; ++oy) acc = fmaf(mh.weight(oy, static_cast<int>(iy)), tb[oy * row], acc);
+    Io<T>::st(gx + off4(xs, static_cast<int>(n), static_cast<int>(c), static_cast<int>(iy), static_cast<int>(ix)), acc);
+  }
+}
+
 // g_masked = act'(y) * g (also the gradient of the fused skip input).
 template <typename T, int ACT>
 __global__ void __launch_bounds__(256) act_mask_kernel(const T* __restrict__ g,
@@ -272,9 +315,27 @@ void launch_interp_fwd(const Tensor4& x, const Tensor4* skip, const Tensor4& y, 
   }
 }
 
+int64_t interp_bwd_ws_elems(const Tensor4& g, const Tensor4& gx) {
+  const bool big = g.h > 2 * gx.h || g.w > 2 * gx.w;
+  const int64_t ws = static_cast<int64_t>(g.n) * g.h * gx.w * gx.c;
+  const int64_t out = static_cast<int64_t>(gx.n) * gx.h * gx.w * gx.c;
+  return (big && ws < (int64_t{1} << 31) && out < (int64_t{1} << 31)) ? ws : 0;
+}
+
 template <typename T>
-static void bwd_t(const Tensor4& g, const Tensor4& gx, LinMap mh, LinMap mw, hipStream_t st) {
+static void bwd_t(const Tensor4& g, const Tensor4& gx, LinMap mh, LinMap mw, float* ws, hipStream_t st) {
   Shape4 gs = mk(g), xs = mk(gx);
+  if (ws != nullptr) {
+    const uint32_t tw = static_cast<uint32_t>(static_cast<int64_t>(g.n) * g.h * gx.w * gx.c);
+    interp_bwd_sep_w<T><<<stream_grid(tw, 256), 256, 0, st>>>(static_cast<const T*>(g.data), gs, ws, gx.w, mw,
+                                                              FastDiv::make(gx.c), FastDiv::make(gx.w),
+                                                              FastDiv::make(g.h), tw);
+    const uint32_t th = static_cast<uint32_t>(static_cast<int64_t>(gx.n) * gx.h * gx.w * gx.c);
+    interp_bwd_sep_h<T><<<stream_grid(th, 256), 256, 0, st>>>(ws, g.h, static_cast<T*>(gx.data), xs, mh,
+                                                              FastDiv::make(gx.c), FastDiv::make(gx.w),
+                                                              FastDiv::make(gx.h), th);
+    return;
+  }
   if constexpr (std::is_same<T, uint16_t>::value) {
     if (cl_vec_ok(g) && cl_vec_ok(gx)) {
       int64_t work = static_cast<int64_t>(gx.n) * gx.h * gx.w * (gx.c / 8);
@@ -288,13 +349,13 @@ static void bwd_t(const Tensor4& g, const Tensor4& gx, LinMap mh, LinMap mw, hip
       static_cast<const T*>(g.data), gs, static_cast<T*>(gx.data), xs, mh, mw);
 }
 
-void launch_interp_bwd(const Tensor4& g, const Tensor4& gx, bool align_corners, hipStream_t st) {
+void launch_interp_bwd(const Tensor4& g, const Tensor4& gx, bool align_corners, float* ws, hipStream_t st) {
   LinMap mh = LinMap::make(gx.h, g.h, align_corners);
   LinMap mw = LinMap::make(gx.w, g.w, align_corners);
   switch (g.dtype) {
-    case kF32: bwd_t<float>(g, gx, mh, mw, st); break;
-    case kBF16: bwd_t<uint16_t>(g, gx, mh, mw, st); break;
-    default: bwd_t<_Float16>(g, gx, mh, mw, st); break;
+    case kF32: bwd_t<float>(g, gx, mh, mw, ws, st); break;
+    case kBF16: bwd_t<uint16_t>(g, gx, mh, mw, ws, st); break;
+    default: bwd_t<_Float16>(g, gx, mh, mw, ws, st); break;
   }
 }
 

@@ -60,8 +60,8 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         identity = x if self.downsample is None else self.downsample(x)
-        out = ops.bn_act(self.conv1(x), self.bn1, "relu")
-        return ops.bn_act(self.conv2(out), self.bn2, "relu", residual=identity)
+        out = ops.conv_bn_act(x, self.conv1, self.bn1, "relu")
+        return ops.conv_bn_act(out, self.conv2, self.bn2, "relu", residual=identity)
 
 
 class Bottleneck(nn.Module):
@@ -81,16 +81,16 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         identity = x if self.downsample is None else self.downsample(x)
-        out = ops.bn_act(self.conv1(x), self.bn1, "relu")
-        out = ops.bn_act(self.conv2(out), self.bn2, "relu")
-        return ops.bn_act(self.conv3(out), self.bn3, "relu", residual=identity)
+        out = ops.conv_bn_act(x, self.conv1, self.bn1, "relu")
+        out = ops.conv_bn_act(out, self.conv2, self.bn2, "relu")
+        return ops.conv_bn_act(out, self.conv3, self.bn3, "relu", residual=identity)
 
 
 class _ConvBN(nn.Sequential):
     """``downsample`` projection: keys ``.0.weight`` / ``.1.*`` (torchvision layout)."""
 
     def forward(self, x):
-        return ops.bn_act(self[0](x), self[1], "none")
+        return ops.conv_bn_act(x, self[0], self[1], "none")
 
 
 class ResNet(nn.Module):
@@ -143,7 +143,7 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def stem(self, x):
-        return self.maxpool(ops.bn_act(self.conv1(x), self.bn1, "relu"))
+        return self.maxpool(ops.conv_bn_act(x, self.conv1, self.bn1, "relu"))
 
     def forward(self, x):
         x1 = self.layer1(self.stem(x))
@@ -162,7 +162,7 @@ class ConvBNReLU6(nn.Sequential):
                          nn.BatchNorm2d(cout), nn.ReLU6(inplace=True))
 
     def forward(self, x):
-        return ops.bn_act(self[0](x), self[1], "relu6")
+        return ops.conv_bn_act(x, self[0], self[1], "relu6")
 
 
 class InvertedResidual(nn.Module):

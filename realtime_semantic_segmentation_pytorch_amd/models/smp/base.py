@@ -37,7 +37,7 @@ class ConvBNReLUSeq(nn.Sequential):
     """Generic ``Sequential(conv-like, BatchNorm2d, ReLU[, extra...])`` with a fused tail."""
 
     def forward(self, x):
-        y = ops.bn_act(self[0](x), self[1], "relu")
+        y = ops.conv_bn_act(x, self[0], self[1], "relu")
         for m in list(self)[3:]:
             y = m(y)
         return y

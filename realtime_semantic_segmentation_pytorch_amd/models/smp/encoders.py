@@ -73,7 +73,7 @@ class ResNetEncoder(_EncoderMixin, ResNet):
                 self.layer2, self.layer3, self.layer4]
 
     def _stage_fns(self):
-        return [lambda x: ops.bn_act(self.conv1(x), self.bn1, "relu"),
+        return [lambda x: ops.conv_bn_act(x, self.conv1, self.bn1, "relu"),
                 lambda x: self.layer1(self.maxpool(x)), self.layer2, self.layer3, self.layer4]
 
 

@@ -25,7 +25,7 @@ class ConvBnRelu(nn.Module):
         self.activation = nn.ReLU(inplace=True)
 
     def forward(self, x):
-        y = ops.bn_act(self.conv(x), self.bn, "relu" if self.add_relu else "none")
+        y = ops.conv_bn_act(x, self.conv, self.bn, "relu" if self.add_relu else "none")
         if self.interpolate:
             y = ops.interpolate(y, (y.shape[2] * 2, y.shape[3] * 2), True)
         return y

@@ -177,6 +177,27 @@ def conv_bn_act_eval(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, act_code: 
     return y
 
 
+def conv_bn_act(x: torch.Tensor, conv: nn.Module, bn: nn.Module, act="none", residual=None, act_module=None):
+    """``act(bn(conv(x)) + residual)`` with the conv on the MFMA kernel when it wins: BN
+    statistics in its epilogue (training) or the whole BN + residual + activation tail
+    (inference).  Any other case is ``conv`` followed by ``ops.bn_act``."""
+    from .bn import act_code, bn_act
+
+    if conv_ok(x, conv) and isinstance(bn, (nn.BatchNorm2d, nn.SyncBatchNorm)):
+        code = act if isinstance(act, int) else act_code(act)
+        if code is not None:
+            use_batch = bn.training or not bn.track_running_stats or bn.running_mean is None
+            if not use_batch:
+                y = conv_bn_act_eval(x, conv, bn, code, residual)
+                if y is not None:
+                    return y
+            else:
+                r = conv_bn_stats(x, conv)
+                if r is not None:
+                    return bn_act(r[0], bn, code, residual=residual, act_module=act_module, part=r[1])
+    return bn_act(conv(x), bn, act, residual=residual, act_module=act_module)
+
+
 def decisions() -> dict:
     """Per-shape autotune outcomes so far (for logs / profiles)."""
     return dict(_DECISIONS)
