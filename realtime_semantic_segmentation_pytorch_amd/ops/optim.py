@@ -42,11 +42,25 @@ def build_table(rows, device):
     return t, len(rows), len(bmap) // 2
 
 
+def _dense(t: torch.Tensor) -> bool:
+    """Non-overlapping and dense (some permutation of a contiguous layout)."""
+    if t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last)):
+        return True
+    expected = 1
+    for st, sz in sorted((st, sz) for sz, st in zip(t.shape, t.stride()) if sz != 1):
+        if st != expected:
+            return False
+        expected *= sz
+    return True
+
+
 def _dense_ok(p) -> bool:
+    """The kernel walks every tensor of a row linearly in MEMORY order, so param, grad, state
+    and EMA only need to be dense with identical strides (channels-last conv weights are fine)."""
     g = p.grad
-    return (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and g is not None
-            and not g.is_sparse and g.is_contiguous() and g.dtype in (torch.float32, torch.bfloat16)
-            and g.shape == p.shape)
+    return (p.is_cuda and p.dtype == torch.float32 and _dense(p) and g is not None
+            and not g.is_sparse and g.dtype in (torch.float32, torch.bfloat16)
+            and g.shape == p.shape and g.stride() == p.stride())
 
 
 class _FusedMixin:
@@ -61,8 +75,8 @@ class _FusedMixin:
         self.last_step_fused = False
 
     def attach_ema(self, pairs):
-        """pairs: iterable of (model_param, ema_tensor) of identical shape/dtype."""
-        self._ema_of = {p: e for p, e in pairs}
+        """pairs: iterable of (model_param, ema_tensor) of identical shape/dtype/strides."""
+        self._ema_of = {p: e for p, e in pairs if e.stride() == p.stride() and e.dtype == p.dtype}
         self._tables = {}
 
     def _can_fuse(self, group) -> bool:
@@ -113,6 +127,8 @@ class FusedSGD(_FusedMixin, SGD):
                     if buf is None:
                         buf = st["momentum_buffer"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                         first = True
+                    elif buf.stride() != p.stride():  # e.g. loaded from a checkpoint in another layout
+                        buf = st["momentum_buffer"] = torch.empty_like(p).copy_(buf)
                 rows.append((p, p.grad, buf, None, self._ema_of.get(p) if ema_w is not None else None, first))
             if not rows:
                 continue
@@ -146,6 +162,9 @@ class _FusedAdamBase(_FusedMixin):
                     st["step"] = torch.tensor(0.0, dtype=torch.float32)
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                for k in ("exp_avg", "exp_avg_sq"):  # checkpoint-loaded state may be in another layout
+                    if st[k].stride() != p.stride():
+                        st[k] = torch.empty_like(p).copy_(st[k])
                 st["step"] += 1
                 by_step.setdefault(float(st["step"]), []).append(
                     (p, p.grad, st["exp_avg"], st["exp_avg_sq"],

@@ -75,9 +75,12 @@ def _model():
                          nn.Conv2d(16, 40000 // 16, 1), nn.Flatten(), nn.Linear(2500 * 4, 3)).to(DEV)
 
 
+@pytest.mark.parametrize("cl", [False, True])
 @pytest.mark.parametrize("kind", ["sgd", "sgd_nesterov", "adam", "adamw"])
-def test_fused_optimizer_matches_torch(kind):
+def test_fused_optimizer_matches_torch(kind, cl):
     m_ref = _model()
+    if cl:  # channels-last conv weights: dense but not contiguous -- the fused kernel must take them
+        m_ref = m_ref.to(memory_format=torch.channels_last)
     m_fus = copy.deepcopy(m_ref)
     ema = copy.deepcopy(m_fus)
     ema_ref = copy.deepcopy(m_ref)
@@ -92,6 +95,8 @@ def test_fused_optimizer_matches_torch(kind):
     pairs = [(p, e.data) for p, e in zip(m_fus.parameters(), ema.parameters())]
     o_fus.attach_ema(pairs)
     x = torch.randn(4, 3, 4, 4, device=DEV)
+    if cl:
+        x = x.contiguous(memory_format=torch.channels_last)
     for it in range(1, 5):
         for m, o in ((m_ref, o_ref), (m_fus, o_fus)):
             o.zero_grad()
