@@ -316,7 +316,10 @@ void launch_interp_fwd(const Tensor4& x, const Tensor4* skip, const Tensor4& y, 
 }
 
 int64_t interp_bwd_ws_elems(const Tensor4& g, const Tensor4& gx) {
-  const bool big = g.h > 2 * gx.h || g.w > 2 * gx.w;
+  // the vectorised channels-last bf16 gather stays faster up to x8 (DDRNet's x2..x8 fusions);
+  // the separable path takes the scalar cases (odd C, e.g. 19-class logits) and larger scales
+  const bool vec = g.dtype == kBF16 && cl_vec_ok(g) && cl_vec_ok(gx);
+  const bool big = vec ? (g.h > 8 * gx.h || g.w > 8 * gx.w) : (g.h > 2 * gx.h || g.w > 2 * gx.w);
   const int64_t ws = static_cast<int64_t>(g.n) * g.h * gx.w * gx.c;
   const int64_t out = static_cast<int64_t>(gx.n) * gx.h * gx.w * gx.c;
   return (big && ws < (int64_t{1} << 31) && out < (int64_t{1} << 31)) ? ws : 0;

@@ -5,10 +5,9 @@ utils/parallel.py:7-53).
   pins the HIP device and initialises the process group: backend ``nccl``
   (= RCCL on ROCm) for GPUs, ``gloo`` for CPU runs/tests.
 * ``parallel_model`` -- SyncBatchNorm conversion (GPU only) and DDP with
-  gradient buckets sized for MI355X: with 288 GB HBM the whole gradient of the
-  largest zoo model (DDRNet-23: 84 MiB fp32) fits in one or two buckets, so the
-  default bucket is 100 MiB -> ~1 large all-reduce per step that RCCL can split
-  across all 7 xGMI links, overlapped with the tail of backward.  Buckets are
+  gradient buckets sized for MI355X: 32 MiB buckets -> DDRNet-23's 84 MiB fp32
+  gradient goes out as ~3 large all-reduces (each big enough for RCCL to spread
+  over all 7 xGMI links) that overlap with the rest of backward.  Buckets are
   views of the gradients (``gradient_as_bucket_view``), BN buffers are not
   re-broadcast every forward when SyncBN already makes them identical.
 * single-process multi-GPU ``nn.DataParallel`` is deliberately not recreated:
@@ -101,7 +100,7 @@ def parallel_model(config, model, rank, device):
         from ..ops import convert_batchnorm
         convert_batchnorm(model)  # SyncBN -> fused HIP SyncBN (one fp64 all-reduce per layer)
     model = model.to(device)
-    kw = dict(bucket_cap_mb=int(getattr(config, "ddp_bucket_mb", 100)),
+    kw = dict(bucket_cap_mb=int(getattr(config, "ddp_bucket_mb", 32)),
               gradient_as_bucket_view=True,
               broadcast_buffers=not sync,
               static_graph=bool(getattr(config, "ddp_static_graph", False)))
