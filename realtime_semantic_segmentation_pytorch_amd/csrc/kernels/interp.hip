@@ -55,27 +55,56 @@ __global__ void __launch_bounds__(256) interp_fwd_scalar(
 template <typename T, int ACT, bool SKIP>
 __global__ void __launch_bounds__(256) interp_fwd_cl_scalar(
     const T* __restrict__ x, Shape4 xs, const T* __restrict__ skip, Shape4 ks,
-    T* __restrict__ y, Shape4 ys, LinMap mh, LinMap mw) {
-  const int64_t total = static_cast<int64_t>(ys.n) * ys.c * ys.h * ys.w;
-  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < total;
-       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    int c = static_cast<int>(i % ys.c);
-    int64_t t = i / ys.c;
-    int ox = static_cast<int>(t % ys.w);
-    t /= ys.w;
-    int oy = static_cast<int>(t % ys.h);
-    int n = static_cast<int>(t / ys.h);
+    T* __restrict__ y, Shape4 ys, LinMap mh, LinMap mw, FastDiv fc, FastDiv fw, FastDiv fh, uint32_t total) {
+  // 32-bit index split by invariant-divisor multiplies: a 64-bit `/` and `%` per element
+  // cost more than the interpolation itself (the x8 logits upsample ran 14x off roofline).
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    uint32_t c, ox, oy;
+    const uint32_t r0 = fc.divmod(i, c);
+    const uint32_t r1 = fw.divmod(r0, ox);
+    const int n = static_cast<int>(fh.divmod(r1, oy));
     int y0, y1, x0, x1; float ly, lx;
-    mh.map(oy, y0, y1, ly);
-    mw.map(ox, x0, x1, lx);
-    const T* b = x + n * xs.sn + c * xs.sc;
+    mh.map(static_cast<int>(oy), y0, y1, ly);
+    mw.map(static_cast<int>(ox), x0, x1, lx);
+    const T* b = x + n * xs.sn + static_cast<int64_t>(c) * xs.sc;
     float v00 = Io<T>::ld(b + y0 * xs.sh + x0 * xs.sw);
     float v01 = Io<T>::ld(b + y0 * xs.sh + x1 * xs.sw);
     float v10 = Io<T>::ld(b + y1 * xs.sh + x0 * xs.sw);
     float v11 = Io<T>::ld(b + y1 * xs.sh + x1 * xs.sw);
     float v = (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11);
-    if constexpr (SKIP) v += Io<T>::ld(skip + off4(ks, n, c, oy, ox));
-    Io<T>::st(y + off4(ys, n, c, oy, ox), act_fwd<ACT>(v));
+    if constexpr (SKIP) v += Io<T>::ld(skip + off4(ks, n, static_cast<int>(c), static_cast<int>(oy), static_cast<int>(ox)));
+    Io<T>::st(y + off4(ys, n, static_cast<int>(c), static_cast<int>(oy), static_cast<int>(ox)), act_fwd<ACT>(v));
+  }
+}
+
+// Same, one thread per output PIXEL looping over the (few, e.g. 19) channels: the two
+// source-coordinate maps are computed once per pixel instead of once per element (the
+// per-element form is instruction-bound: ~80 VALU ops for 4 loads and 1 store).
+template <typename T, int ACT, bool SKIP>
+__global__ void __launch_bounds__(256) interp_fwd_cl_pix(
+    const T* __restrict__ x, Shape4 xs, const T* __restrict__ skip, Shape4 ks,
+    T* __restrict__ y, Shape4 ys, LinMap mh, LinMap mw, FastDiv fw, FastDiv fh, uint32_t npix) {
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < npix; i += gridDim.x * 256u) {
+    uint32_t ox, oy;
+    const uint32_t r1 = fw.divmod(i, ox);
+    const int n = static_cast<int>(fh.divmod(r1, oy));
+    int y0, y1, x0, x1; float ly, lx;
+    mh.map(static_cast<int>(oy), y0, y1, ly);
+    mw.map(static_cast<int>(ox), x0, x1, lx);
+    const float w00 = (1.f - ly) * (1.f - lx), w01 = (1.f - ly) * lx, w10 = ly * (1.f - lx), w11 = ly * lx;
+    const T* b = x + n * xs.sn;
+    const T* p00 = b + y0 * xs.sh + x0 * xs.sw;
+    const T* p01 = b + y0 * xs.sh + x1 * xs.sw;
+    const T* p10 = b + y1 * xs.sh + x0 * xs.sw;
+    const T* p11 = b + y1 * xs.sh + x1 * xs.sw;
+    T* q = y + off4(ys, n, 0, static_cast<int>(oy), static_cast<int>(ox));
+    const T* k = SKIP ? skip + off4(ks, n, 0, static_cast<int>(oy), static_cast<int>(ox)) : nullptr;
+    for (int c = 0; c < ys.c; ++c) {
+      float v = w00 * Io<T>::ld(p00 + c) + w01 * Io<T>::ld(p01 + c) + w10 * Io<T>::ld(p10 + c) +
+                w11 * Io<T>::ld(p11 + c);
+      if constexpr (SKIP) v += Io<T>::ld(k + c * ks.sc);
+      Io<T>::st(q + c, act_fwd<ACT>(v));
+    }
   }
 }
 
@@ -281,9 +310,17 @@ static void fwd_dispatch(const Tensor4& x, const Tensor4* skip, const Tensor4& y
     }
   }
   int64_t work = static_cast<int64_t>(y.n) * y.c * y.h * y.w;
-  if (y.sc == 1 && y.c > 1) {
+  const int64_t npix = static_cast<int64_t>(y.n) * y.h * y.w;
+  if (y.sc == 1 && x.sc == 1 && y.c > 1 && y.c <= 64 && npix < (int64_t{1} << 31)) {
+    interp_fwd_cl_pix<T, ACT, SKIP><<<stream_grid(npix, 256), 256, 0, st>>>(
+        static_cast<const T*>(x.data), xs, kp, ks, static_cast<T*>(y.data), ys, mh, mw, FastDiv::make(y.w),
+        FastDiv::make(y.h), static_cast<uint32_t>(npix));
+    return;
+  }
+  if (y.sc == 1 && y.c > 1 && work < (int64_t{1} << 31)) {
     interp_fwd_cl_scalar<T, ACT, SKIP><<<stream_grid(work, 256), 256, 0, st>>>(
-        static_cast<const T*>(x.data), xs, kp, ks, static_cast<T*>(y.data), ys, mh, mw);
+        static_cast<const T*>(x.data), xs, kp, ks, static_cast<T*>(y.data), ys, mh, mw, FastDiv::make(y.c),
+        FastDiv::make(y.w), FastDiv::make(y.h), static_cast<uint32_t>(work));
     return;
   }
   interp_fwd_scalar<T, ACT, SKIP><<<stream_grid(work, 256), 256, 0, st>>>(

@@ -84,7 +84,7 @@ class _FusedTail:
             y = self._mfma_tail(x, conv, bn, own, residual, act)
             if y is not None:
                 return y
-        y = conv(x)
+        y = ops.conv_forward(x, conv)
         if residual is None:
             return ops.bn_act(y, bn, own, act_module=own)
         own_code = ops.bn_act_code(own)

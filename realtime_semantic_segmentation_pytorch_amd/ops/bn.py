@@ -77,7 +77,7 @@ class _BNActFn(torch.autograd.Function):
                                            float(bn.eps))
         else:
             sums = None
-            mi, ss = ops().bn_eval_coeffs(weight, bias, bn.running_mean, bn.running_var, float(bn.eps))
+            mi, ss = eval_coeffs(bn)
         y = ops().bn_apply(x, ss, residual, act)
         if act == ACT_NONE:
             mask = MASK_NONE
@@ -106,6 +106,21 @@ class _BNActFn(torch.autograd.Function):
                                              ctx.mask, want_dres, ctx.batch_stats, want_dw)
         return (dx, dw if want_dw else None, db if want_dw else None,
                 dres if want_dres else None, None, None, None, None, None)
+
+
+def eval_coeffs(bn):
+    """(mean_invstd, scale_shift) of an eval-mode BN from its running statistics, cached on
+    the module until any of weight / bias / running stats changes (an inference forward --
+    and its HIP graph -- then has no per-layer coefficient kernel)."""
+    ts = (bn.weight, bn.bias, bn.running_mean, bn.running_var)
+    key = tuple((t.data_ptr(), t._version) if t is not None else None for t in ts) + (float(bn.eps),)
+    hit = getattr(bn, "_rtseg_eval_coeffs", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    out = ops().bn_eval_coeffs(bn.weight, bn.bias, bn.running_mean, bn.running_var, float(bn.eps))
+    if not torch.is_grad_enabled():
+        bn._rtseg_eval_coeffs = (key, out)
+    return out
 
 
 def vec_width(dtype: torch.dtype, c: int) -> int:

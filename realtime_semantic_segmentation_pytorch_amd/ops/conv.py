@@ -160,7 +160,9 @@ def conv_bn_act_eval(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, act_code: 
     res = residual.to(torch.bfloat16) if residual is not None else None
     stride, padding, dilation = _geom(conv)
     wk = weight_krsc(conv)
-    _, ss = ops().bn_eval_coeffs(bn.weight, bn.bias, bn.running_mean, bn.running_var, float(bn.eps))
+    from .bn import eval_coeffs
+
+    _, ss = eval_coeffs(bn)
     key = ("eval", tuple(x.shape), conv.out_channels, conv.kernel_size, tuple(stride), tuple(padding),
            tuple(dilation), res is not None)
 
@@ -175,6 +177,22 @@ def conv_bn_act_eval(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, act_code: 
         return None
     y, _ = ops().conv_mfma(x, wk, stride, padding, dilation, False, ss, res, act_code)
     return y
+
+
+def conv_forward(x: torch.Tensor, conv: nn.Module) -> torch.Tensor:
+    """``conv(x)``; in bf16-autocast inference the bf16 weight copy is cached on the module
+    (autocast would re-cast the fp32 weight -- one extra kernel per conv -- every forward)."""
+    if (type(conv) is nn.Conv2d and not conv.training and not torch.is_grad_enabled() and x.is_cuda
+            and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+        w = conv.weight
+        key = (w.data_ptr(), w._version, None if conv.bias is None else (conv.bias.data_ptr(), conv.bias._version))
+        hit = getattr(conv, "_rtseg_w16", None)
+        if hit is None or hit[0] != key:
+            b16 = conv.bias.detach().to(torch.bfloat16) if conv.bias is not None else None
+            hit = conv._rtseg_w16 = (key, w.detach().to(torch.bfloat16), b16)
+        with torch.autocast("cuda", enabled=False):
+            return conv._conv_forward(x.to(torch.bfloat16), hit[1], hit[2])
+    return conv(x)
 
 
 def conv_bn_act(x: torch.Tensor, conv: nn.Module, bn: nn.Module, act="none", residual=None, act_module=None):
@@ -195,7 +213,7 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Module, bn: nn.Module, act="none", res
                 r = conv_bn_stats(x, conv)
                 if r is not None:
                     return bn_act(r[0], bn, code, residual=residual, act_module=act_module, part=r[1])
-    return bn_act(conv(x), bn, act, residual=residual, act_module=act_module)
+    return bn_act(conv_forward(x, conv), bn, act, residual=residual, act_module=act_module)
 
 
 def decisions() -> dict:
