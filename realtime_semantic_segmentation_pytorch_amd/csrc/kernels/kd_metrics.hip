@@ -105,6 +105,101 @@ __global__ void __launch_bounds__(kKdBlock) kd_bwd_kernel(Tensor4 s, Tensor4 t, 
   }
 }
 
+// ---- channels-last, LDS-staged variants ----------------------------------------
+// With NHWC logits a pixel's C (e.g. 19) channels are 38 contiguous bytes, so a
+// per-pixel thread's scalar loads make every wave-instruction touch ~38 cache lines
+// (the texture path, not HBM, was the limit: 6x off roofline).  Here a block stages
+// its 256 pixels x C channels of both tensors with coalesced 16-byte loads into LDS,
+// computes per pixel from LDS, and (backward) stages the gradient the same way out.
+constexpr int kKdPix = 256;
+
+template <typename T>
+__device__ __forceinline__ void stage_in(const T* __restrict__ g, int64_t first, int64_t nelem, T* lds) {
+  // g + first is 16-byte aligned (host check); nelem elements, tail handled per element
+  const int64_t nvec = nelem * static_cast<int64_t>(sizeof(T)) / 16;
+  const uint4* src = reinterpret_cast<const uint4*>(g + first);
+  uint4* dst = reinterpret_cast<uint4*>(lds);
+  for (int64_t v = threadIdx.x; v < nvec; v += kKdPix) dst[v] = src[v];
+  for (int64_t e = nvec * 16 / static_cast<int64_t>(sizeof(T)) + threadIdx.x; e < nelem; e += kKdPix)
+    lds[e] = g[first + e];
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kKdPix) kd_fwd_cl_kernel(const T* __restrict__ s, const T* __restrict__ t, int C,
+                                                           int64_t npix, float inv_t, float* lse, double* part) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char kd_lds[];
+  T* ls = reinterpret_cast<T*>(kd_lds);
+  T* lt = ls + kKdPix * C;
+  double acc = 0.0;
+  for (int64_t p0 = static_cast<int64_t>(blockIdx.x) * kKdPix; p0 < npix; p0 += static_cast<int64_t>(gridDim.x) * kKdPix) {
+    const int np = static_cast<int>(npix - p0 < kKdPix ? npix - p0 : kKdPix);
+    __syncthreads();
+    stage_in(s, p0 * C, static_cast<int64_t>(np) * C, ls);
+    stage_in(t, p0 * C, static_cast<int64_t>(np) * C, lt);
+    __syncthreads();
+    if (static_cast<int>(threadIdx.x) < np) {
+      const T* a_ = ls + threadIdx.x * C;
+      const T* b_ = lt + threadIdx.x * C;
+      float ma = -INFINITY, mb = -INFINITY;
+      for (int c = 0; c < C; ++c) {
+        ma = fmaxf(ma, Io<T>::ld(a_ + c) * inv_t);
+        mb = fmaxf(mb, Io<T>::ld(b_ + c) * inv_t);
+      }
+      float za = 0.f, zb = 0.f, cross = 0.f;
+      for (int c = 0; c < C; ++c) {
+        const float a = Io<T>::ld(a_ + c) * inv_t, b = Io<T>::ld(b_ + c) * inv_t;
+        za += __expf(a - ma);
+        const float eb = __expf(b - mb);
+        zb += eb;
+        cross += eb * (b - a);
+      }
+      const float la = ma + __logf(za), lb = mb + __logf(zb);
+      const int64_t p = p0 + threadIdx.x;
+      lse[p] = la;
+      lse[npix + p] = lb;
+      acc += static_cast<double>(cross / zb - lb + la);
+    }
+  }
+  __shared__ double red[kKdPix / kWave];
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = acc;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kKdPix) kd_bwd_cl_kernel(const T* __restrict__ s, const T* __restrict__ t,
+                                                           T* __restrict__ gs, int C, int64_t npix, float inv_t,
+                                                           const float* lse, const float* gout, float coef) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char kd_lds[];
+  T* ls = reinterpret_cast<T*>(kd_lds);
+  T* lt = ls + kKdPix * C;
+  const float k = *gout * coef;
+  for (int64_t p0 = static_cast<int64_t>(blockIdx.x) * kKdPix; p0 < npix; p0 += static_cast<int64_t>(gridDim.x) * kKdPix) {
+    const int np = static_cast<int>(npix - p0 < kKdPix ? npix - p0 : kKdPix);
+    __syncthreads();
+    stage_in(s, p0 * C, static_cast<int64_t>(np) * C, ls);
+    stage_in(t, p0 * C, static_cast<int64_t>(np) * C, lt);
+    __syncthreads();
+    if (static_cast<int>(threadIdx.x) < np) {
+      const int64_t p = p0 + threadIdx.x;
+      const float la = lse[p], lb = lse[npix + p];
+      T* a_ = ls + threadIdx.x * C;
+      const T* b_ = lt + threadIdx.x * C;
+      for (int c = 0; c < C; ++c) {  // gradient overwrites the staged student logits in place
+        const float a = Io<T>::ld(a_ + c) * inv_t, b = Io<T>::ld(b_ + c) * inv_t;
+        Io<T>::st(a_ + c, k * (__expf(a - la) - __expf(b - lb)));
+      }
+    }
+    __syncthreads();
+    const int64_t nelem = static_cast<int64_t>(np) * C;
+    const int64_t nvec = nelem * static_cast<int64_t>(sizeof(T)) / 16;
+    uint4* dst = reinterpret_cast<uint4*>(gs + p0 * C);
+    const uint4* src = reinterpret_cast<const uint4*>(ls);
+    for (int64_t v = threadIdx.x; v < nvec; v += kKdPix) dst[v] = src[v];
+    for (int64_t e = nvec * 16 / static_cast<int64_t>(sizeof(T)) + threadIdx.x; e < nelem; e += kKdPix)
+      gs[p0 * C + e] = ls[e];
+  }
+}
+
 // ---- confusion matrix ---------------------------------------------------------
 constexpr int kCmBlock = 256;
 
@@ -157,14 +252,29 @@ void by_dtype(int dtype, F&& f) {
 
 int kd_partial_blocks(int64_t npix) { return stream_grid(npix, kKdBlock); }
 
+// dense channels-last (NHWC-contiguous), 16-byte aligned, LDS-sized channel count
+static bool kd_cl_ok(const Tensor4& a) {
+  const int64_t esz = a.dtype == kF32 ? 4 : 2;
+  return a.sc == 1 && a.sw == a.c && a.sh == static_cast<int64_t>(a.w) * a.c &&
+         a.sn == static_cast<int64_t>(a.h) * a.w * a.c && (reinterpret_cast<uintptr_t>(a.data) % 16) == 0 &&
+         2 * kKdPix * a.c * esz <= 64 * 1024;
+}
+
+static size_t kd_lds_bytes(const Tensor4& a) { return 2 * kKdPix * static_cast<size_t>(a.c) * (a.dtype == kF32 ? 4 : 2); }
+
 void launch_kd_fwd(const Tensor4& s, const Tensor4& t, float temperature, float* lse, double* part,
                    float* out, hipStream_t st) {
   const int64_t npix = static_cast<int64_t>(s.n) * s.h * s.w;
   const int g = kd_partial_blocks(npix);
   const float inv_t = 1.f / temperature;
+  const bool cl = kd_cl_ok(s) && kd_cl_ok(t);
   by_dtype(s.dtype, [&](auto tag) {
     using T = decltype(tag);
-    kd_fwd_kernel<T><<<g, kKdBlock, 0, st>>>(s, t, inv_t, lse, part);
+    if (cl)
+      kd_fwd_cl_kernel<T><<<g, kKdPix, kd_lds_bytes(s), st>>>(static_cast<const T*>(s.data),
+                                                              static_cast<const T*>(t.data), s.c, npix, inv_t, lse, part);
+    else
+      kd_fwd_kernel<T><<<g, kKdBlock, 0, st>>>(s, t, inv_t, lse, part);
   });
   const double numel = static_cast<double>(npix) * s.c;
   const double scale = static_cast<double>(temperature) * temperature / numel;
@@ -177,9 +287,15 @@ void launch_kd_bwd(const Tensor4& s, const Tensor4& t, const Tensor4& gs, float 
   const int g = kd_partial_blocks(npix);
   const double numel = static_cast<double>(npix) * s.c;
   const float coef = static_cast<float>(static_cast<double>(temperature) / numel);
+  const bool cl = kd_cl_ok(s) && kd_cl_ok(t) && kd_cl_ok(gs);
   by_dtype(s.dtype, [&](auto tag) {
     using T = decltype(tag);
-    kd_bwd_kernel<T><<<g, kKdBlock, 0, st>>>(s, t, gs, 1.f / temperature, lse, gout, coef);
+    if (cl)
+      kd_bwd_cl_kernel<T><<<g, kKdPix, kd_lds_bytes(s), st>>>(static_cast<const T*>(s.data), static_cast<const T*>(t.data),
+                                                              static_cast<T*>(gs.data), s.c, npix, 1.f / temperature, lse,
+                                                              gout, coef);
+    else
+      kd_bwd_kernel<T><<<g, kKdBlock, 0, st>>>(s, t, gs, 1.f / temperature, lse, gout, coef);
   });
 }
 
