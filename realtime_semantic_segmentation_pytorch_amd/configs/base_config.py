@@ -122,6 +122,8 @@ class BaseConfig:
         self.channels_last = True        # NHWC activations (MIOpen/HIP kernels prefer it)
         self.fused_loss = True           # fold the final upsample into the HIP loss kernel
         self.fused_optimizer = True      # HIP multi-tensor optimizer step that also writes the EMA
+        self.hip_depthwise = True        # depth-wise convs on the HIP kernels (else MIOpen)
+        self.hip_pooling = True          # avg / max / adaptive pooling on the HIP kernels
         self.ddp_bucket_mb = 32          # RCCL all-reduce bucket: ~3 buckets for DDRNet-23 (84 MB), overlapped with backward
         self.ddp_static_graph = True
         self.synthetic_data = False      # device-generated synthetic batches (benchmarks)

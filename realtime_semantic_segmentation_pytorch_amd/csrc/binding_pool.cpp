@@ -1,0 +1,114 @@
+// torch.library registration of the pooling operators (kernels: pool.hip).
+#include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <torch/library.h>
+
+#include "rtseg_launch.h"
+#include "rtseg_ops.h"
+
+namespace rtseg {
+
+static PoolParams pool_params(at::IntArrayRef k, at::IntArrayRef s, at::IntArrayRef p, int64_t mode,
+                              bool count_include_pad, bool adaptive) {
+  TORCH_CHECK(k.size() == 2 && s.size() == 2 && p.size() == 2, "rtseg.pool: kernel/stride/padding must have 2 entries");
+  PoolParams pp{static_cast<int>(k[0]), static_cast<int>(k[1]), static_cast<int>(s[0]), static_cast<int>(s[1]),
+                static_cast<int>(p[0]), static_cast<int>(p[1]), count_include_pad ? 1 : 0, static_cast<int>(mode),
+                adaptive ? 1 : 0};
+  if (!adaptive) {
+    TORCH_CHECK(pp.kh > 0 && pp.kw > 0 && pp.sh > 0 && pp.sw > 0, "rtseg.pool: kernel and stride must be positive");
+    TORCH_CHECK(pp.ph >= 0 && pp.pw >= 0 && 2 * pp.ph <= pp.kh && 2 * pp.pw <= pp.kw,
+                "rtseg.pool: padding must be at most half the kernel");
+  }
+  TORCH_CHECK(mode == kPoolAvg || (mode == kPoolMax && !adaptive && pp.kh * pp.kw <= 256),
+              "rtseg.pool: max pooling needs a fixed window of at most 256 taps");
+  return pp;
+}
+
+static void check_x(const at::Tensor& x) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4, "rtseg.pool: expected a 4-D GPU tensor");
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf,
+              "rtseg.pool: dtype must be fp32, bf16 or fp16");
+  TORCH_CHECK(x.numel() < (int64_t{1} << 31), "rtseg.pool: tensor too large for 32-bit indexing");
+}
+
+// -> (y, idx); idx is a uint8 [N, OH, OW, C] argmax map for max pooling, empty otherwise
+static std::tuple<at::Tensor, at::Tensor> pool2d_fwd(const at::Tensor& x, at::IntArrayRef kernel,
+                                                     at::IntArrayRef stride, at::IntArrayRef padding, int64_t mode,
+                                                     bool count_include_pad) {
+  check_x(x);
+  const PoolParams p = pool_params(kernel, stride, padding, mode, count_include_pad, false);
+  const int64_t oh = (x.size(2) + 2 * p.ph - p.kh) / p.sh + 1;
+  const int64_t ow = (x.size(3) + 2 * p.pw - p.kw) / p.sw + 1;
+  TORCH_CHECK(oh > 0 && ow > 0, "rtseg.pool: output would be empty");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  at::Tensor y = at::empty({x.size(0), x.size(1), oh, ow}, x.options().memory_format(x.suggest_memory_format()));
+  at::Tensor idx;
+  if (mode == kPoolMax) idx = at::empty({x.size(0), oh, ow, x.size(1)}, x.options().dtype(at::kByte));
+  else idx = at::empty({0}, x.options().dtype(at::kByte));
+  launch_pool_fwd(view4(x), view4(y), p, mode == kPoolMax ? idx.data_ptr<uint8_t>() : nullptr, cur_stream());
+  return {y, idx};
+}
+
+static at::Tensor pool2d_bwd(const at::Tensor& gy, const at::Tensor& idx, int64_t in_h, int64_t in_w,
+                             at::IntArrayRef kernel, at::IntArrayRef stride, at::IntArrayRef padding, int64_t mode,
+                             bool count_include_pad) {
+  check_x(gy);
+  const PoolParams p = pool_params(kernel, stride, padding, mode, count_include_pad, false);
+  TORCH_CHECK((in_h + 2 * p.ph - p.kh) / p.sh + 1 == gy.size(2) && (in_w + 2 * p.pw - p.kw) / p.sw + 1 == gy.size(3),
+              "rtseg.pool_bwd: grad_output shape does not match the pooling geometry");
+  if (mode == kPoolMax)
+    TORCH_CHECK(idx.scalar_type() == at::kByte && idx.is_contiguous() && idx.dim() == 4 &&
+                    idx.size(0) == gy.size(0) && idx.size(1) == gy.size(2) && idx.size(2) == gy.size(3) &&
+                    idx.size(3) == gy.size(1),
+                "rtseg.pool_bwd: bad argmax map");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(gy.device());
+  at::Tensor gx =
+      at::empty({gy.size(0), gy.size(1), in_h, in_w}, gy.options().memory_format(gy.suggest_memory_format()));
+  launch_pool_bwd(view4(gy), view4(gx), p, mode == kPoolMax ? idx.data_ptr<uint8_t>() : nullptr, cur_stream());
+  return gx;
+}
+
+static at::Tensor adaptive_avg_pool_fwd(const at::Tensor& x, int64_t out_h, int64_t out_w) {
+  check_x(x);
+  TORCH_CHECK(out_h > 0 && out_w > 0, "rtseg.adaptive_avg_pool: output size must be positive");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  at::Tensor y = at::empty({x.size(0), x.size(1), out_h, out_w}, x.options().memory_format(x.suggest_memory_format()));
+  if (out_h == 1 && out_w == 1) {
+    const Tensor4 xv = view4(x);
+    const GapPlan pl = gap_plan(xv);
+    at::Tensor part = at::empty({static_cast<int64_t>(pl.slices) * x.size(0) * x.size(1)}, x.options().dtype(at::kFloat));
+    launch_gap_fwd(xv, view4(y), pl, part.data_ptr<float>(), cur_stream());
+    return y;
+  }
+  const PoolParams p{1, 1, 1, 1, 0, 0, 1, kPoolAvg, 1};
+  launch_pool_fwd(view4(x), view4(y), p, nullptr, cur_stream());
+  return y;
+}
+
+static at::Tensor adaptive_avg_pool_bwd(const at::Tensor& gy, int64_t in_h, int64_t in_w, bool channels_last) {
+  check_x(gy);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(gy.device());
+  const auto fmt = channels_last ? at::MemoryFormat::ChannelsLast : at::MemoryFormat::Contiguous;
+  at::Tensor gx = at::empty({gy.size(0), gy.size(1), in_h, in_w}, gy.options().memory_format(fmt));
+  const PoolParams p{1, 1, 1, 1, 0, 0, 1, kPoolAvg, 1};
+  launch_pool_bwd(view4(gy), view4(gx), p, nullptr, cur_stream());
+  return gx;
+}
+
+}  // namespace rtseg
+
+TORCH_LIBRARY_FRAGMENT(rtseg, m) {
+  m.def("pool2d_fwd(Tensor x, int[] kernel, int[] stride, int[] padding, int mode, bool count_include_pad) "
+        "-> (Tensor, Tensor)");
+  m.def("pool2d_bwd(Tensor gy, Tensor idx, int in_h, int in_w, int[] kernel, int[] stride, int[] padding, int mode, "
+        "bool count_include_pad) -> Tensor");
+  m.def("adaptive_avg_pool_fwd(Tensor x, int out_h, int out_w) -> Tensor");
+  m.def("adaptive_avg_pool_bwd(Tensor gy, int in_h, int in_w, bool channels_last) -> Tensor");
+}
+
+TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
+  m.impl("pool2d_fwd", &rtseg::pool2d_fwd);
+  m.impl("pool2d_bwd", &rtseg::pool2d_bwd);
+  m.impl("adaptive_avg_pool_fwd", &rtseg::adaptive_avg_pool_fwd);
+  m.impl("adaptive_avg_pool_bwd", &rtseg::adaptive_avg_pool_bwd);
+}

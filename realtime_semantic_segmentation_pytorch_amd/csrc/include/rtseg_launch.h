@@ -150,4 +150,22 @@ struct ConvGeom {
 int conv_mfma_slabs(const ConvGeom& g);
 void launch_conv_mfma(const ConvGeom& g, hipStream_t st);
 
+// ---- pool.hip -----------------------------------------------------------------
+enum PoolMode : int { kPoolAvg = 0, kPoolMax = 1 };
+struct PoolParams {
+  int kh, kw, sh, sw, ph, pw;
+  int count_include_pad;  // avg: divisor over the padded window (ATen default)
+  int mode;               // PoolMode
+  int adaptive;           // avg only: ATen adaptive windows from the input/output sizes
+};
+// max pooling writes idx: dense NHWC uint8 [N, OH, OW, C] window offsets (kh*kw <= 256)
+void launch_pool_fwd(const Tensor4& x, const Tensor4& y, const PoolParams& p, uint8_t* idx, hipStream_t st);
+void launch_pool_bwd(const Tensor4& gy, const Tensor4& gx, const PoolParams& p, const uint8_t* idx, hipStream_t st);
+struct GapPlan {
+  int vec, cpb, cblocks, per_slice, slices;
+};
+GapPlan gap_plan(const Tensor4& x);
+// global average pool; part: fp32 workspace of plan.slices * N * C
+void launch_gap_fwd(const Tensor4& x, const Tensor4& y, const GapPlan& plan, float* part, hipStream_t st);
+
 }  // namespace rtseg

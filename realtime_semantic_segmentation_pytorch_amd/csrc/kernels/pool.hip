@@ -1,0 +1,366 @@
+// 2-D pooling family for CDNA4 (gfx950): average / max pooling with fixed windows,
+// adaptive average pooling (incl. the global 1x1 case) and their backward passes.
+//
+// Reference sites: DDRNet DAPPM AvgPool2d(5/9/17, s 2/4/8) + global pool
+// (models/ddrnet.py:248-264), STDC AvgPool2d(3,2,1) on every stride-2 module
+// (models/stdc.py:116), BiSeNetV2 stem MaxPool2d(3,2,1) / GE AvgPool / CE global pool
+// (models/bisenetv2.py:117,131,144), PPM AdaptiveAvgPool(1,2,4,6) (models/modules.py:147),
+// and every AdaptiveAvgPool2d(1) of the zoo and SMP decoders.
+//
+// Layout: NHWC (channels-last) activations; a work item is VEC contiguous channels
+// of one output (forward) or input (backward) pixel, so every access is a 16-byte
+// load/store for bf16 with C % 8 == 0.  Other layouts take the VEC = 1 strided path.
+//
+// * Forward: one item per output vector, loop over its window (semantics of ATen:
+//   count_include_pad divisor clipped to the padded extent; max keeps the first
+//   maximum in scan order and propagates the first NaN).  Max pooling also writes the
+//   window-relative argmax as one uint8 per output element.
+// * Backward: gather form (one item per INPUT vector, loop over the few windows that
+//   cover it), so there are no atomics and the result is deterministic.  Max backward
+//   compares the stored uint8 offsets -- no re-scan of the window.
+// * Global average pooling (output 1x1) is a reduction: a block owns a channel slab
+//   of one image and a slice of its pixels, rows of threads stride the pixels and
+//   reduce through LDS; slices write fp32 partials that a second kernel sums, scales
+//   and casts, so small batches still fill 256 CUs.
+#include "rtseg_common.h"
+#include "rtseg_launch.h"
+#include "rtseg_vec.h"
+
+#include <algorithm>
+#include <type_traits>
+
+namespace rtseg {
+
+namespace {
+
+constexpr int kPoolBlock = 256;
+
+struct PoolDivs {
+  FastDiv c, w, h;  // channel vectors, width, height of the indexed space
+};
+
+__device__ __forceinline__ void adaptive_range(int o, int in, int out, int& s, int& e) {
+  s = (o * in) / out;
+  e = ((o + 1) * in + out - 1) / out;
+}
+
+template <typename T, int VEC, int MODE, bool ADAPT>
+__global__ void __launch_bounds__(kPoolBlock) pool_fwd_kernel(Tensor4 x, Tensor4 y, PoolParams p, PoolDivs d,
+                                                              uint8_t* __restrict__ idx, uint32_t total) {
+  const T* xp = static_cast<const T*>(x.data);
+  T* yp = static_cast<T*>(y.data);
+  for (uint32_t i = blockIdx.x * kPoolBlock + threadIdx.x; i < total; i += gridDim.x * kPoolBlock) {
+    uint32_t cv, ow, oh;
+    const uint32_t r0 = d.c.divmod(i, cv);
+    const uint32_t r1 = d.w.divmod(r0, ow);
+    const uint32_t n = d.h.divmod(r1, oh);
+    int hs, he, ws, we, hs0, ws0;
+    float div = 1.f;
+    if constexpr (ADAPT) {
+      adaptive_range(static_cast<int>(oh), x.h, y.h, hs, he);
+      adaptive_range(static_cast<int>(ow), x.w, y.w, ws, we);
+      hs0 = hs;
+      ws0 = ws;
+      div = static_cast<float>((he - hs) * (we - ws));
+    } else {
+      hs0 = static_cast<int>(oh) * p.sh - p.ph;
+      ws0 = static_cast<int>(ow) * p.sw - p.pw;
+      he = min(hs0 + p.kh, x.h + p.ph);
+      we = min(ws0 + p.kw, x.w + p.pw);
+      const int padded = (he - hs0) * (we - ws0);
+      hs = max(hs0, 0);
+      ws = max(ws0, 0);
+      he = min(he, x.h);
+      we = min(we, x.w);
+      div = static_cast<float>(p.count_include_pad ? padded : (he - hs) * (we - ws));
+    }
+    const int c0 = static_cast<int>(cv) * VEC;
+    const T* xb = xp + static_cast<int64_t>(n) * x.sn + static_cast<int64_t>(c0) * x.sc;
+    float acc[VEC];
+    int arg[VEC];
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) {
+      acc[v] = MODE == kPoolMax ? -INFINITY : 0.f;
+      arg[v] = 0;
+    }
+    for (int ih = hs; ih < he; ++ih) {
+      for (int iw = ws; iw < we; ++iw) {
+        float v_[VEC];
+        Vec<T, VEC>::load(xb + static_cast<int64_t>(ih) * x.sh + static_cast<int64_t>(iw) * x.sw, v_);
+        if constexpr (MODE == kPoolMax) {
+          const int o = (ih - hs0) * p.kw + (iw - ws0);
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) {
+            const bool take = v_[v] > acc[v] || (v_[v] != v_[v] && acc[v] == acc[v]);
+            acc[v] = take ? v_[v] : acc[v];
+            arg[v] = take ? o : arg[v];
+          }
+        } else {
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) acc[v] += v_[v];
+        }
+      }
+    }
+    if constexpr (MODE == kPoolAvg) {
+      const float inv = 1.f / div;
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) acc[v] *= inv;
+    }
+    const int64_t yo = static_cast<int64_t>(n) * y.sn + static_cast<int64_t>(c0) * y.sc +
+                       static_cast<int64_t>(oh) * y.sh + static_cast<int64_t>(ow) * y.sw;
+    Vec<T, VEC>::store(yp + yo, acc);
+    if constexpr (MODE == kPoolMax) {
+      // idx is dense NHWC [n, oh, ow, c] whatever y's layout
+      uint8_t* ib = idx + ((static_cast<int64_t>(n) * y.h + oh) * y.w + ow) * y.c + c0;
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) ib[v] = static_cast<uint8_t>(arg[v]);
+    }
+  }
+}
+
+template <typename T, int VEC, int MODE, bool ADAPT>
+__global__ void __launch_bounds__(kPoolBlock) pool_bwd_kernel(Tensor4 gy, Tensor4 gx, PoolParams p, PoolDivs d,
+                                                              const uint8_t* __restrict__ idx, uint32_t total) {
+  const T* gp = static_cast<const T*>(gy.data);
+  T* xp = static_cast<T*>(gx.data);
+  for (uint32_t i = blockIdx.x * kPoolBlock + threadIdx.x; i < total; i += gridDim.x * kPoolBlock) {
+    uint32_t cv, iw_, ih_;
+    const uint32_t r0 = d.c.divmod(i, cv);
+    const uint32_t r1 = d.w.divmod(r0, iw_);
+    const uint32_t n = d.h.divmod(r1, ih_);
+    const int ih = static_cast<int>(ih_), iw = static_cast<int>(iw_);
+    int oh_lo, oh_hi, ow_lo, ow_hi;
+    if constexpr (ADAPT) {
+      oh_lo = max((ih * gy.h) / gx.h - 1, 0);
+      oh_hi = min(((ih + 1) * gy.h) / gx.h + 1, gy.h - 1);
+      ow_lo = max((iw * gy.w) / gx.w - 1, 0);
+      ow_hi = min(((iw + 1) * gy.w) / gx.w + 1, gy.w - 1);
+    } else {
+      const int ah = ih + p.ph - p.kh + 1, aw = iw + p.pw - p.kw + 1;
+      oh_lo = ah > 0 ? (ah + p.sh - 1) / p.sh : 0;
+      ow_lo = aw > 0 ? (aw + p.sw - 1) / p.sw : 0;
+      oh_hi = min((ih + p.ph) / p.sh, gy.h - 1);
+      ow_hi = min((iw + p.pw) / p.sw, gy.w - 1);
+    }
+    const int c0 = static_cast<int>(cv) * VEC;
+    const T* gb = gp + static_cast<int64_t>(n) * gy.sn + static_cast<int64_t>(c0) * gy.sc;
+    float acc[VEC];
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) acc[v] = 0.f;
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        float w = 1.f;
+        int rel = 0;
+        if constexpr (ADAPT) {
+          int hs, he, ws, we;
+          adaptive_range(oh, gx.h, gy.h, hs, he);
+          adaptive_range(ow, gx.w, gy.w, ws, we);
+          if (ih < hs || ih >= he || iw < ws || iw >= we) continue;
+          w = 1.f / static_cast<float>((he - hs) * (we - ws));
+        } else {
+          const int hs0 = oh * p.sh - p.ph, ws0 = ow * p.sw - p.pw;
+          if constexpr (MODE == kPoolAvg) {
+            int he = min(hs0 + p.kh, gx.h + p.ph), we = min(ws0 + p.kw, gx.w + p.pw);
+            int cnt = (he - hs0) * (we - ws0);
+            if (!p.count_include_pad)
+              cnt = (min(he, gx.h) - max(hs0, 0)) * (min(we, gx.w) - max(ws0, 0));
+            w = 1.f / static_cast<float>(cnt);
+          } else {
+            rel = (ih - hs0) * p.kw + (iw - ws0);
+          }
+        }
+        float g_[VEC];
+        Vec<T, VEC>::load(gb + static_cast<int64_t>(oh) * gy.sh + static_cast<int64_t>(ow) * gy.sw, g_);
+        if constexpr (MODE == kPoolMax) {
+          const uint8_t* ib = idx + ((static_cast<int64_t>(n) * gy.h + oh) * gy.w + ow) * gy.c + c0;
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) acc[v] += (static_cast<int>(ib[v]) == rel) ? g_[v] : 0.f;
+        } else {
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) acc[v] = fmaf(w, g_[v], acc[v]);
+        }
+      }
+    }
+    const int64_t xo = static_cast<int64_t>(n) * gx.sn + static_cast<int64_t>(c0) * gx.sc +
+                       static_cast<int64_t>(ih) * gx.sh + static_cast<int64_t>(iw) * gx.sw;
+    Vec<T, VEC>::store(xp + xo, acc);
+  }
+}
+
+// Global average pool, stage 1: block (cb, n, slice) sums pixels [slice*per, ...) of
+// image n for channel vectors cb*cpb .. +cpb.  rows = 256 / cpb thread rows stride
+// the pixels; LDS reduce over rows; fp32 partial [slice, n, C].
+template <typename T, int VEC>
+__global__ void __launch_bounds__(kPoolBlock) gap_partial_kernel(Tensor4 x, int cpb, int per_slice,
+                                                                 float* __restrict__ part) {
+  __shared__ float red[kPoolBlock * VEC];
+  const T* xp = static_cast<const T*>(x.data);
+  const int rows = kPoolBlock / cpb;
+  const int r = threadIdx.x / cpb, cl = threadIdx.x - r * cpb;
+  const int n = blockIdx.y;
+  const int cv = blockIdx.x * cpb + cl;
+  const int c0 = cv * VEC;
+  const int hw = x.h * x.w;
+  const int p_beg = blockIdx.z * per_slice;
+  const int p_end = min(p_beg + per_slice, hw);
+  float acc[VEC];
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) acc[v] = 0.f;
+  if (r < rows && c0 < x.c) {
+    const T* xb = xp + static_cast<int64_t>(n) * x.sn + static_cast<int64_t>(c0) * x.sc;
+    int ph = (p_beg + r) / x.w, pw = (p_beg + r) - ph * x.w;  // row/col of the first pixel
+    const int dh = rows / x.w, dw = rows - dh * x.w;
+    for (int q = p_beg + r; q < p_end; q += rows) {
+      float v_[VEC];
+      Vec<T, VEC>::load(xb + static_cast<int64_t>(ph) * x.sh + static_cast<int64_t>(pw) * x.sw, v_);
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) acc[v] += v_[v];
+      ph += dh;
+      pw += dw;
+      if (pw >= x.w) {
+        pw -= x.w;
+        ++ph;
+      }
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) red[(r * cpb + cl) * VEC + v] = acc[v];
+  __syncthreads();
+  if (r == 0 && c0 < x.c) {
+    for (int rr = 1; rr < rows; ++rr) {
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) acc[v] += red[(rr * cpb + cl) * VEC + v];
+    }
+    float* pb = part + (static_cast<int64_t>(blockIdx.z) * gridDim.y + n) * x.c + c0;
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) pb[v] = acc[v];
+  }
+}
+
+// stage 2: y[n, c] = sum_slices part / (H*W), cast to T (y is [N, C, 1, 1], any strides)
+template <typename T>
+__global__ void __launch_bounds__(kPoolBlock) gap_final_kernel(const float* __restrict__ part, int slices, int N,
+                                                               int C, float inv, Tensor4 y) {
+  T* yp = static_cast<T*>(y.data);
+  for (int i = blockIdx.x * kPoolBlock + threadIdx.x; i < N * C; i += gridDim.x * kPoolBlock) {
+    const int n = i / C, c = i - n * C;
+    float s = 0.f;
+    for (int k = 0; k < slices; ++k) s += part[(static_cast<int64_t>(k) * N + n) * C + c];
+    Io<T>::st(yp + static_cast<int64_t>(n) * y.sn + static_cast<int64_t>(c) * y.sc, s * inv);
+  }
+}
+
+template <typename F>
+void by_dtype(int dt, F&& f) {
+  switch (dt) {
+    case kF32: f(float{}); break;
+    case kBF16: f(uint16_t{}); break;
+    default: f(_Float16{}); break;
+  }
+}
+
+// VEC usable for a tensor: channel stride 1, C and the pixel strides multiples of VEC,
+// base aligned to VEC elements.
+int vec_of(const Tensor4& t, int want) {
+  const int esz = t.dtype == kF32 ? 4 : 2;
+  for (int v = want; v > 1; v >>= 1) {
+    if (t.sc == 1 && t.c % v == 0 && t.sw % v == 0 && t.sh % v == 0 && t.sn % v == 0 &&
+        reinterpret_cast<uintptr_t>(t.data) % (static_cast<uintptr_t>(v) * esz) == 0)
+      return v;
+  }
+  return 1;
+}
+
+template <typename T, int VEC, typename F>
+void with_vec(int vec, F&& f) {
+  if constexpr (VEC == 1) {
+    f(std::integral_constant<int, 1>{});
+  } else {
+    if (vec >= VEC) f(std::integral_constant<int, VEC>{});
+    else with_vec<T, VEC / 2>(vec, f);
+  }
+}
+
+int want_vec(int dt) { return dt == kF32 ? 4 : 8; }
+
+}  // namespace
+
+void launch_pool_fwd(const Tensor4& x, const Tensor4& y, const PoolParams& p, uint8_t* idx, hipStream_t st) {
+  const int vec = std::min(vec_of(x, want_vec(x.dtype)), vec_of(y, want_vec(y.dtype)));
+  by_dtype(x.dtype, [&](auto tag) {
+    using T = decltype(tag);
+    with_vec<T, 8>(vec, [&](auto vc) {
+      constexpr int V = decltype(vc)::value;
+      if constexpr (!(std::is_same_v<T, float> && V == 8)) {
+        const uint32_t cvs = static_cast<uint32_t>(y.c / V);
+        const uint32_t total = static_cast<uint32_t>(static_cast<int64_t>(y.n) * y.h * y.w * cvs);
+        PoolDivs d{FastDiv::make(cvs), FastDiv::make(y.w), FastDiv::make(y.h)};
+        const int g = stream_grid(total, kPoolBlock);
+        if (p.mode == kPoolMax)
+          pool_fwd_kernel<T, V, kPoolMax, false><<<g, kPoolBlock, 0, st>>>(x, y, p, d, idx, total);
+        else if (p.adaptive)
+          pool_fwd_kernel<T, V, kPoolAvg, true><<<g, kPoolBlock, 0, st>>>(x, y, p, d, nullptr, total);
+        else
+          pool_fwd_kernel<T, V, kPoolAvg, false><<<g, kPoolBlock, 0, st>>>(x, y, p, d, nullptr, total);
+      }
+    });
+  });
+}
+
+void launch_pool_bwd(const Tensor4& gy, const Tensor4& gx, const PoolParams& p, const uint8_t* idx, hipStream_t st) {
+  const int vec = std::min(vec_of(gy, want_vec(gy.dtype)), vec_of(gx, want_vec(gx.dtype)));
+  by_dtype(gy.dtype, [&](auto tag) {
+    using T = decltype(tag);
+    with_vec<T, 8>(vec, [&](auto vc) {
+      constexpr int V = decltype(vc)::value;
+      if constexpr (!(std::is_same_v<T, float> && V == 8)) {
+        const uint32_t cvs = static_cast<uint32_t>(gx.c / V);
+        const uint32_t total = static_cast<uint32_t>(static_cast<int64_t>(gx.n) * gx.h * gx.w * cvs);
+        PoolDivs d{FastDiv::make(cvs), FastDiv::make(gx.w), FastDiv::make(gx.h)};
+        const int g = stream_grid(total, kPoolBlock);
+        if (p.mode == kPoolMax)
+          pool_bwd_kernel<T, V, kPoolMax, false><<<g, kPoolBlock, 0, st>>>(gy, gx, p, d, idx, total);
+        else if (p.adaptive)
+          pool_bwd_kernel<T, V, kPoolAvg, true><<<g, kPoolBlock, 0, st>>>(gy, gx, p, d, nullptr, total);
+        else
+          pool_bwd_kernel<T, V, kPoolAvg, false><<<g, kPoolBlock, 0, st>>>(gy, gx, p, d, nullptr, total);
+      }
+    });
+  });
+}
+
+GapPlan gap_plan(const Tensor4& x) {
+  GapPlan pl;
+  pl.vec = vec_of(x, want_vec(x.dtype));
+  const int cvs = x.c / pl.vec;
+  pl.cpb = cvs < kPoolBlock ? cvs : kPoolBlock;
+  pl.cblocks = (cvs + pl.cpb - 1) / pl.cpb;
+  const int hw = x.h * x.w;
+  const int rows = kPoolBlock / pl.cpb;
+  int slices = (512 + x.n * pl.cblocks - 1) / (x.n * pl.cblocks);
+  const int max_slices = (hw + 4 * rows - 1) / (4 * rows);  // >= 4 pixels per thread row
+  if (slices > max_slices) slices = max_slices;
+  if (slices < 1) slices = 1;
+  if (slices > 65535) slices = 65535;
+  pl.per_slice = (hw + slices - 1) / slices;
+  pl.slices = (hw + pl.per_slice - 1) / pl.per_slice;
+  return pl;
+}
+
+void launch_gap_fwd(const Tensor4& x, const Tensor4& y, const GapPlan& pl, float* part, hipStream_t st) {
+  by_dtype(x.dtype, [&](auto tag) {
+    using T = decltype(tag);
+    with_vec<T, 8>(pl.vec, [&](auto vc) {
+      constexpr int V = decltype(vc)::value;
+      if constexpr (!(std::is_same_v<T, float> && V == 8)) {
+        dim3 grid(pl.cblocks, x.n, pl.slices);
+        gap_partial_kernel<T, V><<<grid, kPoolBlock, 0, st>>>(x, pl.cpb, pl.per_slice, part);
+      }
+    });
+    const int nc = x.n * x.c;
+    gap_final_kernel<T><<<stream_grid(nc, kPoolBlock), kPoolBlock, 0, st>>>(
+        part, pl.slices, x.n, x.c, 1.f / static_cast<float>(x.h * x.w), y);
+  });
+}
+
+}  // namespace rtseg

@@ -64,14 +64,17 @@ def _variant_kwargs(config, key):
 
 
 def get_model(config):
-    """Build the configured model; every BatchNorm2d and depth-wise conv is routed
-    through the HIP kernels (``ops.convert_batchnorm`` / ``ops.convert_depthwise``;
-    module classes only -- parameters and checkpoint keys are unchanged)."""
+    """Build the configured model; every BatchNorm2d, depth-wise conv and pooling
+    module is routed through the HIP kernels (``ops.convert_batchnorm`` /
+    ``ops.convert_depthwise`` / ``ops.convert_pooling``; module classes only --
+    parameters and checkpoint keys are unchanged)."""
     from .. import ops
 
     model = ops.convert_batchnorm(_build_model(config))
     if getattr(config, "hip_depthwise", True):
         ops.convert_depthwise(model)
+    if getattr(config, "hip_pooling", True):
+        ops.convert_pooling(model)
     return model
 
 
@@ -106,8 +109,8 @@ def get_teacher_model(config, device):
         raise ValueError(f"Unsupported teacher decoder type: {config.teacher_decoder}")
     from .. import ops
 
-    model = ops.convert_depthwise(ops.convert_batchnorm(
-        build_smp_model(config.teacher_decoder, config.teacher_encoder, None, config.num_class)))
+    model = ops.convert_pooling(ops.convert_depthwise(ops.convert_batchnorm(
+        build_smp_model(config.teacher_decoder, config.teacher_encoder, None, config.num_class))))
     ckpt_path = config.teacher_ckpt
     if ckpt_path:
         if not os.path.isfile(ckpt_path):

@@ -13,6 +13,8 @@ from .bn import (bn_act, act_code as bn_act_code, fused_ok as bn_fused_ok, conve
                  FusedBatchNorm2d, FusedSyncBatchNorm)
 from .confmat import confusion_matrix, confusion_matrix_reference
 from .dwconv import DepthwiseConv2d, convert_depthwise, depthwise_ok, dw_conv2d
+from .pool import (avg_pool2d, max_pool2d, adaptive_avg_pool2d, convert_pooling, AvgPool2d, MaxPool2d,
+                   AdaptiveAvgPool2d)
 from .optim import FusedAdam, FusedAdamW, FusedSGD
 from .conv import conv_ok, conv_bn_stats, conv_bn_act_eval, conv_bn_act, conv_forward
 
@@ -22,6 +24,8 @@ __all__ = [
     "seg_cross_entropy", "seg_cross_entropy_reference", "MODE_OHEM", "MODE_MEAN", "MODE_SUM",
     "kd_kl_div", "kd_kl_div_reference", "confusion_matrix", "confusion_matrix_reference",
     "DepthwiseConv2d", "convert_depthwise", "depthwise_ok", "dw_conv2d",
+    "avg_pool2d", "max_pool2d", "adaptive_avg_pool2d", "convert_pooling", "AvgPool2d", "MaxPool2d",
+    "AdaptiveAvgPool2d",
     "FusedSGD", "FusedAdam", "FusedAdamW", "conv_ok", "conv_bn_stats", "conv_bn_act_eval", "conv_bn_act", "conv_forward",
     "bn_act", "bn_act_code", "bn_fused_ok", "convert_batchnorm", "FusedBatchNorm2d", "FusedSyncBatchNorm",
 ]

@@ -101,3 +101,14 @@ def test_ema_params_done_updates_only_buffers():
     for a, b in zip(before, ema.ema.parameters()):
         torch.testing.assert_close(a, b)  # parameters left to the fused optimizer
     torch.testing.assert_close(ema.ema[1].running_mean, torch.full((8,), 0.5))  # decay 0.5 lerp
+
+
+def test_pooling_modules_cpu_match_torch():
+    m = nn.Sequential(nn.MaxPool2d(3, 2, 1), nn.AvgPool2d(5, 2, 2), nn.AdaptiveAvgPool2d((2, 3)))
+    ref = copy.deepcopy(m)
+    ops.convert_pooling(m)
+    assert isinstance(m[0], ops.MaxPool2d) and isinstance(m[1], ops.AvgPool2d)
+    assert isinstance(m[2], ops.AdaptiveAvgPool2d)
+    x = torch.randn(2, 4, 21, 30)
+    torch.testing.assert_close(m(x), ref(x))
+    assert m.state_dict().keys() == ref.state_dict().keys()
