@@ -19,7 +19,6 @@ import os
 
 import numpy as np
 import torch
-import torch.nn.functional as F
 from PIL import Image
 
 from .. import ops
@@ -83,13 +82,12 @@ class SegTrainer(BaseTrainer):
                 for coef, aux in zip(coefs, preds_aux):
                     loss = loss + float(coef) * self.loss_fn.aux(aux, labels)
             elif cfg.use_detail_head:
-                detail_gt = self.laplacian_conv(masks.unsqueeze(1).float())
-                detail_gt = de_parallel(self.model).detail_conv(detail_gt)
-                detail_gt = (detail_gt > cfg.detail_thrs).to(detail_gt.dtype)
+                # Laplacian detail target + x8 bilinear resize + Dice + BCE: one fused HIP op
+                # (ops/detail.py; the reference formulation on CPU)
                 preds, preds_detail = self.model(images, is_training=True)
-                preds_detail = F.interpolate(preds_detail, detail_gt.shape[2:], mode="bilinear",
-                                             align_corners=True)
-                loss_detail = self.detail_loss_fn(preds_detail.float(), detail_gt.float())
+                loss_detail = ops.detail_loss(preds_detail, labels, de_parallel(self.model).detail_conv,
+                                              cfg.detail_thrs, cfg.dice_loss_coef, cfg.bce_loss_coef,
+                                              laplacian=self.laplacian_conv)
                 loss = self.loss_fn(preds, labels) + cfg.detail_loss_coef * loss_detail
                 extras["loss_detail"] = loss_detail
             else:

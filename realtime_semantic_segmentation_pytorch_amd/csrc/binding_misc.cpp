@@ -104,11 +104,70 @@ static void ema_lerp(const at::Tensor& meta, int64_t ntensor, int64_t nblocks, d
                   static_cast<float>(w), cur_stream());
 }
 
+// ---- STDC detail loss (detail_loss.hip) ------------------------------------------
+static void check_detail(const at::Tensor& d) {
+  TORCH_CHECK(d.is_cuda() && d.dim() == 4 && d.size(1) == 1, "rtseg.detail_loss: logits must be [N, 1, h, w] on GPU");
+  TORCH_CHECK(d.scalar_type() == at::kFloat || d.scalar_type() == at::kBFloat16 || d.scalar_type() == at::kHalf,
+              "rtseg.detail_loss: logits dtype must be fp32, bf16 or fp16");
+}
+
+// -> (loss fp32 scalar, binary target uint8 [N, H, W], per-sample sums fp64 [N, 4])
+static std::tuple<at::Tensor, at::Tensor, at::Tensor> detail_loss_fwd(const at::Tensor& d, const at::Tensor& labels,
+                                                                      const at::Tensor& wb, double thrs,
+                                                                      double dice_coef, double bce_coef) {
+  check_detail(d);
+  TORCH_CHECK(labels.dim() == 3 && labels.is_contiguous() && labels.size(0) == d.size(0) &&
+                  (labels.scalar_type() == at::kByte || labels.scalar_type() == at::kLong) &&
+                  labels.device() == d.device(),
+              "rtseg.detail_loss: labels must be contiguous uint8/int64 [N, H, W] on the logits' device");
+  TORCH_CHECK(wb.scalar_type() == at::kFloat && wb.is_contiguous() && wb.numel() == 4 && wb.device() == d.device(),
+              "rtseg.detail_loss: wb must be fp32 (w0, w1, w2, bias) on the logits' device");
+  const int n = static_cast<int>(labels.size(0)), h = static_cast<int>(labels.size(1)),
+            w = static_cast<int>(labels.size(2));
+  TORCH_CHECK(static_cast<int64_t>(h) * w < (int64_t{1} << 31), "rtseg.detail_loss: image too large");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(d.device());
+  auto opt = d.options();
+  at::Tensor loss = at::empty({}, opt.dtype(at::kFloat));
+  at::Tensor y = at::empty({n, h, w}, opt.dtype(at::kByte));
+  at::Tensor sums = at::empty({n, 4}, opt.dtype(at::kDouble));
+  at::Tensor part = at::empty({static_cast<int64_t>(n) * detail_loss_blocks(n, h, w) * 4}, opt.dtype(at::kDouble));
+  launch_detail_fwd(view4(d), labels.data_ptr(), labels.scalar_type() == at::kByte, n, h, w, wb.data_ptr<float>(),
+                    static_cast<float>(thrs), static_cast<float>(dice_coef), static_cast<float>(bce_coef),
+                    y.data_ptr<uint8_t>(), part.data_ptr<double>(), sums.data_ptr<double>(), loss.data_ptr<float>(),
+                    cur_stream());
+  return {loss, y, sums};
+}
+
+static at::Tensor detail_loss_bwd(const at::Tensor& grad, const at::Tensor& d, const at::Tensor& y,
+                                  const at::Tensor& sums, double dice_coef, double bce_coef) {
+  check_detail(d);
+  TORCH_CHECK(y.scalar_type() == at::kByte && y.is_contiguous() && y.dim() == 3 && y.size(0) == d.size(0),
+              "rtseg.detail_loss_bwd: bad target");
+  TORCH_CHECK(sums.scalar_type() == at::kDouble && sums.is_contiguous() && sums.numel() == 4 * d.size(0),
+              "rtseg.detail_loss_bwd: bad sums");
+  const int n = static_cast<int>(y.size(0)), h = static_cast<int>(y.size(1)), w = static_cast<int>(y.size(2));
+  c10::hip::HIPGuardMasqueradingAsCUDA g(d.device());
+  at::Tensor g32 = grad.to(at::kFloat).contiguous();
+  auto f32 = d.options().dtype(at::kFloat);
+  at::Tensor gp = at::empty({n, 1, h, w}, f32);
+  launch_detail_bwd(view4(d), n, h, w, y.data_ptr<uint8_t>(), sums.data_ptr<double>(), g32.data_ptr<float>(),
+                    static_cast<float>(dice_coef), static_cast<float>(bce_coef), gp.data_ptr<float>(), cur_stream());
+  at::Tensor gd = at::empty({d.size(0), 1, d.size(2), d.size(3)}, f32);
+  const int64_t wsn = interp_bwd_ws_elems(view4(gp), view4(gd));
+  at::Tensor ws;
+  if (wsn > 0) ws = at::empty({wsn}, f32);
+  launch_interp_bwd(view4(gp), view4(gd), true, wsn > 0 ? ws.data_ptr<float>() : nullptr, cur_stream());
+  return gd.to(d.scalar_type());
+}
+
 }  // namespace rtseg
 
 TORCH_LIBRARY_FRAGMENT(rtseg, m) {
   m.def("kd_kl_fwd(Tensor s, Tensor t, float temperature) -> (Tensor, Tensor)");
   m.def("kd_kl_bwd(Tensor grad, Tensor s, Tensor t, Tensor lse, float temperature) -> Tensor");
+  m.def("detail_loss_fwd(Tensor d, Tensor labels, Tensor wb, float thrs, float dice_coef, float bce_coef) "
+        "-> (Tensor, Tensor, Tensor)");
+  m.def("detail_loss_bwd(Tensor grad, Tensor d, Tensor y, Tensor sums, float dice_coef, float bce_coef) -> Tensor");
   m.def("confmat(Tensor x, Tensor target, int num_class, int ignore_index) -> Tensor");
   m.def("fused_opt_step(Tensor meta, int ntensor, int nblocks, int mode, float lr, float momentum, "
         "float dampening, float weight_decay, bool nesterov, float beta1, float beta2, float eps, "
@@ -119,6 +178,8 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
 TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
   m.impl("kd_kl_fwd", &rtseg::kd_kl_fwd);
   m.impl("kd_kl_bwd", &rtseg::kd_kl_bwd);
+  m.impl("detail_loss_fwd", &rtseg::detail_loss_fwd);
+  m.impl("detail_loss_bwd", &rtseg::detail_loss_bwd);
   m.impl("confmat", &rtseg::confmat);
   m.impl("fused_opt_step", &rtseg::fused_opt_step);
   m.impl("ema_lerp", &rtseg::ema_lerp);

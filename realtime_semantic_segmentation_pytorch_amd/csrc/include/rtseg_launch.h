@@ -168,4 +168,16 @@ GapPlan gap_plan(const Tensor4& x);
 // global average pool; part: fp32 workspace of plan.slices * N * C
 void launch_gap_fwd(const Tensor4& x, const Tensor4& y, const GapPlan& plan, float* part, hipStream_t st);
 
+// ---- detail_loss.hip ----------------------------------------------------------
+// STDC detail loss: d = low-resolution detail logits [N,1,h,w]; labels [N,H,W] uint8 or int64;
+// wb = detail_conv (w0, w1, w2, bias) fp32 on device.  part: fp64 [N * detail_loss_blocks * 4],
+// sums: fp64 [N, 4], yout: uint8 [N, H, W] binary target, out: fp32 scalar loss.
+int detail_loss_blocks(int n, int h, int w);
+void launch_detail_fwd(const Tensor4& d, const void* labels, bool labels_u8, int n, int h, int w, const float* wb,
+                       float thrs, float dice_coef, float bce_coef, uint8_t* yout, double* part, double* sums,
+                       float* out, hipStream_t st);
+// gp: fp32 [N, H, W] = dL/d(upsampled logits)
+void launch_detail_bwd(const Tensor4& d, int n, int h, int w, const uint8_t* yin, const double* sums,
+                       const float* gout, float dice_coef, float bce_coef, float* gp, hipStream_t st);
+
 }  // namespace rtseg

@@ -8,9 +8,11 @@
 // channel).  A[m, k] = x[n, ho*s - p + i*d, wo*s - p + j*d, c] (zero outside the
 // image), B[k, co] = w[co, i, j, c] (weights pre-laid-out [Cout][KH][KW][Cin]).
 //
-//  * block tile 128 (pixels) x BN (Cout: 128, or 64 for narrow layers) x BK (K: 64 when
-//    Cin % 64 == 0, else 32); 256 threads = 4 waves in 2x2, each wave a 64 x BN/2
-//    sub-tile of v_mfma_f32_16x16x32_bf16 (BK/32 MFMA K-steps per stage);
+//  * block tile BM (pixels: 128; 256 selectable, see conv_bm) x BN (Cout: 128, or 64
+//    for narrow layers) x BK (K: 64 when Cin % 64 == 0, else 32); BM/64 x 2 waves (4 or 8),
+//    each wave a 64 x BN/2 sub-tile of v_mfma_f32_16x16x32_bf16 (BK/32 MFMA K-steps per
+//    stage).  The 256-row tile halves the B-operand DMA per MFMA and runs 8 waves (two per
+//    SIMD) in one block, so a CU's waves share one 144 KiB 3-stage ring;
 //  * a K-step is one tap and BK consecutive input channels, so every A row is one
 //    contiguous 64/128-byte read;
 //  * operands go global -> LDS by DMA (global_load_lds_dwordx4, no staging registers)
@@ -31,6 +33,7 @@
 #include "rtseg_common.h"
 #include "rtseg_launch.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace rtseg {
@@ -40,8 +43,6 @@ namespace {
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
-constexpr int kCBM = 128;  // pixels per block tile (N tile: 64 or 128, K step: 32 or 64)
-constexpr int kCThreads = 256;
 constexpr int kMaxSlabs = 512;                  // G of the BN statistics slab
 
 struct ConvK {
@@ -109,17 +110,21 @@ __device__ __forceinline__ float epi_act(float v, int act) {
   return v;
 }
 
-template <int EPI, bool STATS, int BN, int BK>
-__global__ void __launch_bounds__(kCThreads, 2) conv_mfma_kernel(ConvK a) {
+template <int EPI, bool STATS, int BM, int BN, int BK>
+__global__ void __launch_bounds__(BM * 2, 256 / BM) conv_mfma_kernel(ConvK a) {
+  constexpr int kCBM = BM;
+  constexpr int WAVES = BM / 32;               // (BM / 64) x 2 waves
   constexpr int QR = BK / 8;                   // 16-byte chunks per tile row
   constexpr int A_SUB = kCBM * 4;               // chunks of one 32-wide K sub-tile of A
   constexpr int B_SUB = BN * 4;
   constexpr int STAGE = (kCBM + BN) * QR;       // chunks per pipeline stage
-  constexpr int WNT = BN / 32;                  // 16-wide N tiles per wave (2x2 waves)
-  // pipeline stages: 3 keeps two K-steps of DMA in flight across each barrier; the widest tile
-  // (128 x 128 x 64: 32 KiB per stage) uses 2 so that two blocks still fit a CU's LDS
-  constexpr int NST = (BN == 128 && BK == 64) ? 2 : 3;
-  __shared__ uint4 lds[NST * STAGE > 2048 ? NST * STAGE : 2048];  // >= 32 KiB for the epilogue
+  constexpr int WNT = BN / 32;                  // 16-wide N tiles per wave (waves are 2 wide in N)
+  // pipeline stages: 3 keeps two K-steps of DMA in flight across each barrier; the 128 x 128 x 64
+  // tile (32 KiB per stage) uses 2 so that two blocks still fit a CU's LDS (the 256-row tile
+  // runs one block per CU: 3 x 48 KiB)
+  constexpr int NST = (BM == 128 && BN == 128 && BK == 64) ? 2 : 3;
+  constexpr int EPI_CHUNKS = WAVES * 64 * (BN / 2) / 8;  // bf16 epilogue staging, 16-byte chunks
+  __shared__ uint4 lds[NST * STAGE > EPI_CHUNKS ? NST * STAGE : EPI_CHUNKS];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int n0 = blockIdx.y * BN;
@@ -130,8 +135,9 @@ __global__ void __launch_bounds__(kCThreads, 2) conv_mfma_kernel(ConvK a) {
   // applied on the SOURCE side: lane L fills physical chunk L & 3 of row L >> 2, i.e. it loads
   // logical K chunk (L & 3) ^ h[(L >> 4) & 3] of that row (h = {0, 2, 3, 1}, see swz()).
   constexpr int A_INST = (BK / 32) * (kCBM / 16), B_INST = (BK / 32) * (BN / 16);
-  constexpr int A_IW = A_INST / 4, B_IW = B_INST / 4;  // DMA instructions per wave per stage
-  static_assert(A_IW >= 1 && B_IW >= 1, "tile too small for 4 waves");
+  constexpr int A_IW = A_INST / WAVES, B_IW = B_INST / WAVES;  // DMA instructions per wave per stage
+  static_assert(A_IW >= 1 && B_IW >= 1 && A_IW * WAVES == A_INST && B_IW * WAVES == B_INST,
+                "tile/wave mismatch");
   const int lrow = lane >> 2;
   const int lkc = (lane & 3) ^ ((0x1320 >> (((lane >> 4) & 3) * 4)) & 0xF);
   const int64_t wstride = static_cast<int64_t>(a.kh) * a.kw * a.cin;
@@ -158,7 +164,7 @@ __global__ void __launch_bounds__(kCThreads, 2) conv_mfma_kernel(ConvK a) {
 #pragma unroll
     for (int e = 0; e < A_IW; ++e) {
       const int I = wid * A_IW + e;
-      const int h = I / 8, rg = I % 8;
+      const int h = I / (kCBM / 16), rg = I % (kCBM / 16);
       const int m = m0 + 16 * rg + lrow;
       rok[e] = m < a.m;
       uint32_t wo_, ho_;
@@ -188,7 +194,7 @@ __global__ void __launch_bounds__(kCThreads, 2) conv_mfma_kernel(ConvK a) {
         const bool ok = rok[e] && hi >= 0 && hi < a.ih && wi >= 0 && wi < a.iw;
         const uint16_t* src = xbase[e] + (static_cast<int64_t>(hi) * a.iw + wi) * a.cin + c0;
         glds16(ok ? static_cast<const void*>(src) : static_cast<const void*>(g_zero16),
-               A + (I / 8) * A_SUB + (I % 8) * 64);
+               A + (I / (kCBM / 16)) * A_SUB + (I % (kCBM / 16)) * 64);
       }
 #pragma unroll
       for (int e = 0; e < B_IW; ++e) {
@@ -287,13 +293,13 @@ __global__ void __launch_bounds__(kCThreads, 2) conv_mfma_kernel(ConvK a) {
       csq[ni] += __shfl_xor(csq[ni], 16, kWave);
       csq[ni] += __shfl_xor(csq[ni], 32, kWave);
     }
-    float* red = reinterpret_cast<float*>(lds);
-    if (wm == 1 && lane < 16) {
+    float* red = reinterpret_cast<float*>(lds);  // [BM/64 M-waves][BN][2]
+    if (lane < 16) {
 #pragma unroll
       for (int ni = 0; ni < WNT; ++ni) {
         const int col = wn * (BN / 2) + ni * 16 + lane;
-        red[2 * col] = csum[ni];
-        red[2 * col + 1] = csq[ni];
+        red[(wm * BN + col) * 2] = csum[ni];
+        red[(wm * BN + col) * 2 + 1] = csq[ni];
       }
     }
     __syncthreads();
@@ -303,9 +309,15 @@ __global__ void __launch_bounds__(kCThreads, 2) conv_mfma_kernel(ConvK a) {
       for (int ni = 0; ni < WNT; ++ni) {
         const int col = wn * (BN / 2) + ni * 16 + lane;
         const int co = n0 + col;
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int w = 0; w < kCBM / 64; ++w) {
+          s1 += red[(w * BN + col) * 2];
+          s2 += red[(w * BN + col) * 2 + 1];
+        }
         if (co < a.cout) {
-          prow[co] = csum[ni] + red[2 * col];
-          prow[a.cout + co] = csq[ni] + red[2 * col + 1];
+          prow[co] = s1;
+          prow[a.cout + co] = s2;
         }
       }
     }
@@ -314,9 +326,21 @@ __global__ void __launch_bounds__(kCThreads, 2) conv_mfma_kernel(ConvK a) {
 
 }  // namespace
 
+// Pixel-tile height.  128 (two blocks per CU) by default: measured on the DDRNet-23 shapes at
+// batch 32 the 256-row / 8-wave tile is 0-5 % slower on 3x3 layers and up to 25 % slower on
+// 1x1 ones -- both waves of a SIMD then belong to one block and stall on the same per-K-step
+// barrier, which two independent blocks hide (profiles/r1_conv_mfma).  RTSEG_CONV_BM=256
+// selects it for wide (Cout > 64, Cin % 64 == 0) layers, for A/B work on the schedule.
+static int conv_bm(const ConvGeom& g) {
+  const char* e = std::getenv("RTSEG_CONV_BM");
+  const bool can = g.cout > 64 && g.cin % 64 == 0;
+  return (can && e != nullptr && std::atoi(e) == 256) ? 256 : 128;
+}
+
 int conv_mfma_slabs(const ConvGeom& g) {
   const int64_t m = static_cast<int64_t>(g.n) * g.ho * g.wo;
-  const int64_t mtiles = (m + kCBM - 1) / kCBM;
+  const int bm = conv_bm(g);
+  const int64_t mtiles = (m + bm - 1) / bm;
   return static_cast<int>(mtiles < kMaxSlabs ? mtiles : kMaxSlabs);
 }
 
@@ -332,7 +356,8 @@ void launch_conv_mfma(const ConvGeom& g, hipStream_t st) {
   k.ih = g.h; k.iw = g.w_in; k.cin = g.cin; k.ho = g.ho; k.wo = g.wo; k.cout = g.cout;
   k.kh = g.kh; k.kw = g.kw; k.sh = g.sh; k.sw = g.sw; k.ph = g.ph; k.pw = g.pw; k.dh = g.dh; k.dw = g.dw;
   k.m = g.n * g.ho * g.wo;
-  k.mtiles = (k.m + kCBM - 1) / kCBM;
+  const int bm = conv_bm(g);
+  k.mtiles = (k.m + bm - 1) / bm;
   k.fwo = FastDiv::make(g.wo);
   k.fho = FastDiv::make(g.ho);
   const bool stats = g.part != nullptr;
@@ -340,21 +365,24 @@ void launch_conv_mfma(const ConvGeom& g, hipStream_t st) {
   const bool bk64 = g.cin % 64 == 0;
   const int bn = bn64 ? 64 : 128;
   dim3 grid(conv_mfma_slabs(g), (g.cout + bn - 1) / bn);
-  auto go = [&](auto bnc, auto bkc) {
-    constexpr int BN = decltype(bnc)::value, BK = decltype(bkc)::value;
-    if (g.scale_shift != nullptr) conv_mfma_kernel<1, false, BN, BK><<<grid, kCThreads, 0, st>>>(k);
-    else if (stats) conv_mfma_kernel<0, true, BN, BK><<<grid, kCThreads, 0, st>>>(k);
-    else conv_mfma_kernel<0, false, BN, BK><<<grid, kCThreads, 0, st>>>(k);
+  auto go = [&](auto bmc, auto bnc, auto bkc) {
+    constexpr int BM = decltype(bmc)::value, BN = decltype(bnc)::value, BK = decltype(bkc)::value;
+    if (g.scale_shift != nullptr) conv_mfma_kernel<1, false, BM, BN, BK><<<grid, BM * 2, 0, st>>>(k);
+    else if (stats) conv_mfma_kernel<0, true, BM, BN, BK><<<grid, BM * 2, 0, st>>>(k);
+    else conv_mfma_kernel<0, false, BM, BN, BK><<<grid, BM * 2, 0, st>>>(k);
   };
   using I64 = std::integral_constant<int, 64>;
   using I128 = std::integral_constant<int, 128>;
+  using I256 = std::integral_constant<int, 256>;
   using I32 = std::integral_constant<int, 32>;
-  if (bn64) {
-    if (bk64) go(I64{}, I64{});
-    else go(I64{}, I32{});
+  if (bm == 256) {
+    go(I256{}, I128{}, I64{});
+  } else if (bn64) {
+    if (bk64) go(I128{}, I64{}, I64{});
+    else go(I128{}, I64{}, I32{});
   } else {
-    if (bk64) go(I128{}, I64{});
-    else go(I128{}, I32{});
+    if (bk64) go(I128{}, I128{}, I64{});
+    else go(I128{}, I128{}, I32{});
   }
 }
 

@@ -112,3 +112,14 @@ def test_pooling_modules_cpu_match_torch():
     x = torch.randn(2, 4, 21, 30)
     torch.testing.assert_close(m(x), ref(x))
     assert m.state_dict().keys() == ref.state_dict().keys()
+
+
+def test_detail_loss_cpu_is_reference():
+    conv = nn.Conv2d(3, 1, 1, bias=False)
+    labels = torch.randint(0, 19, (2, 32, 48))
+    d = torch.randn(2, 1, 4, 6, requires_grad=True)
+    got = ops.detail_loss(d, labels, conv, 0.1)
+    want = ops.detail_loss_reference(d, labels, conv, 0.1)
+    torch.testing.assert_close(got, want)
+    got.backward()
+    assert d.grad is not None and torch.isfinite(d.grad).all()
