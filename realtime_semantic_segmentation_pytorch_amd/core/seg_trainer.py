@@ -180,16 +180,26 @@ class SegTrainer(BaseTrainer):
                 images_aug = images_aug.contiguous(memory_format=torch.channels_last)
             with self._autocast():
                 preds = self.model(images_aug)
-            colored = self.colormap[ops.materialize(preds).argmax(1)].cpu().numpy()
+            logits = ops.materialize(preds)
+            raws = [np.asarray(im).astype(np.uint8) for im in images] if config.blend_prediction else None
+            # argmax + colormap (+ blend when the raw images match the logits' size) in one kernel
+            same = raws is not None and all(r.shape == (*logits.shape[2:], 3) for r in raws)
+            raw_dev = torch.from_numpy(np.stack(raws)).to(self.device) if same else None
+            _, colored, blended = ops.colorize(logits, self.colormap, raw_dev, config.blend_alpha)
+            colored = colored.cpu().numpy()
+            blended = blended.cpu().numpy() if blended is not None else None
             for i, name in enumerate(names):
                 path = os.path.join(out_dir, name)
                 suffix = name.rsplit(".", 1)[-1] if "." in name else "png"
-                mask_img = Image.fromarray(colored[i].astype(np.uint8))
+                mask_img = Image.fromarray(colored[i])
                 if config.save_mask:
                     mask_img.save(path)
                 if config.blend_prediction:
-                    raw = Image.fromarray(np.asarray(images[i]).astype(np.uint8))
-                    if raw.size != mask_img.size:
-                        raw = raw.resize(mask_img.size, Image.BILINEAR)
-                    Image.blend(raw, mask_img, config.blend_alpha).save(
-                        path[: -len(suffix) - 1] + f"_blend.{suffix}" if "." in name else path + "_blend.png")
+                    if blended is not None:
+                        out = Image.fromarray(blended[i])
+                    else:
+                        raw = Image.fromarray(raws[i])
+                        if raw.size != mask_img.size:
+                            raw = raw.resize(mask_img.size, Image.BILINEAR)
+                        out = Image.blend(raw, mask_img, config.blend_alpha)
+                    out.save(path[: -len(suffix) - 1] + f"_blend.{suffix}" if "." in name else path + "_blend.png")

@@ -160,6 +160,38 @@ static at::Tensor detail_loss_bwd(const at::Tensor& grad, const at::Tensor& d, c
   return gd.to(d.scalar_type());
 }
 
+// ---- prediction colouring (colorize.hip) ------------------------------------------
+// -> (class map uint8 [N,H,W], colour uint8 [N,H,W,3], blend uint8 [N,H,W,3] or empty)
+static std::tuple<at::Tensor, at::Tensor, at::Tensor> colorize(const at::Tensor& x, const at::Tensor& lut,
+                                                               const std::optional<at::Tensor>& image, double alpha) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.size(1) >= 1 && x.size(1) <= 256,
+              "rtseg.colorize: logits must be [N, C <= 256, H, W] on GPU");
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf,
+              "rtseg.colorize: logits dtype must be fp32, bf16 or fp16");
+  TORCH_CHECK(lut.scalar_type() == at::kByte && lut.is_contiguous() && lut.dim() == 2 && lut.size(1) == 3 &&
+                  lut.size(0) >= x.size(1) && lut.device() == x.device(),
+              "rtseg.colorize: colormap must be contiguous uint8 [>= C, 3] on the logits' device");
+  const int64_t n = x.size(0), h = x.size(2), w = x.size(3);
+  TORCH_CHECK(n * h * w < (int64_t{1} << 31), "rtseg.colorize: too many pixels");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto u8 = x.options().dtype(at::kByte);
+  at::Tensor cls = at::empty({n, h, w}, u8);
+  at::Tensor rgb = at::empty({n, h, w, 3}, u8);
+  at::Tensor blend = at::empty({0}, u8);
+  const uint8_t* img = nullptr;
+  if (image.has_value()) {
+    TORCH_CHECK(image->scalar_type() == at::kByte && image->is_contiguous() && image->dim() == 4 &&
+                    image->size(0) == n && image->size(1) == h && image->size(2) == w && image->size(3) == 3 &&
+                    image->device() == x.device(),
+                "rtseg.colorize: image must be contiguous uint8 [N, H, W, 3] matching the logits");
+    blend = at::empty({n, h, w, 3}, u8);
+    img = image->data_ptr<uint8_t>();
+  }
+  launch_colorize(view4(x), lut.data_ptr<uint8_t>(), img, static_cast<float>(alpha), cls.data_ptr<uint8_t>(),
+                  rgb.data_ptr<uint8_t>(), img != nullptr ? blend.data_ptr<uint8_t>() : nullptr, cur_stream());
+  return {cls, rgb, blend};
+}
+
 }  // namespace rtseg
 
 TORCH_LIBRARY_FRAGMENT(rtseg, m) {
@@ -168,6 +200,7 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
   m.def("detail_loss_fwd(Tensor d, Tensor labels, Tensor wb, float thrs, float dice_coef, float bce_coef) "
         "-> (Tensor, Tensor, Tensor)");
   m.def("detail_loss_bwd(Tensor grad, Tensor d, Tensor y, Tensor sums, float dice_coef, float bce_coef) -> Tensor");
+  m.def("colorize(Tensor x, Tensor lut, Tensor? image, float alpha) -> (Tensor, Tensor, Tensor)");
   m.def("confmat(Tensor x, Tensor target, int num_class, int ignore_index) -> Tensor");
   m.def("fused_opt_step(Tensor meta, int ntensor, int nblocks, int mode, float lr, float momentum, "
         "float dampening, float weight_decay, bool nesterov, float beta1, float beta2, float eps, "
@@ -180,6 +213,7 @@ TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
   m.impl("kd_kl_bwd", &rtseg::kd_kl_bwd);
   m.impl("detail_loss_fwd", &rtseg::detail_loss_fwd);
   m.impl("detail_loss_bwd", &rtseg::detail_loss_bwd);
+  m.impl("colorize", &rtseg::colorize);
   m.impl("confmat", &rtseg::confmat);
   m.impl("fused_opt_step", &rtseg::fused_opt_step);
   m.impl("ema_lerp", &rtseg::ema_lerp);

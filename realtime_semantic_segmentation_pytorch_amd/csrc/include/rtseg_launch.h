@@ -180,4 +180,10 @@ void launch_detail_fwd(const Tensor4& d, const void* labels, bool labels_u8, int
 void launch_detail_bwd(const Tensor4& d, int n, int h, int w, const uint8_t* yin, const double* sums,
                        const float* gout, float dice_coef, float bce_coef, float* gp, hipStream_t st);
 
+// ---- colorize.hip -------------------------------------------------------------
+// argmax over C of x [N,C,H,W] -> cls uint8 [N,H,W] (C <= 256), rgb = lut[cls] uint8 [N,H,W,3],
+// blend = trunc(img + alpha * (rgb - img)) in fp32 (bit-identical to PIL Image.blend) with img uint8 [N,H,W,3]; null outputs are skipped.
+void launch_colorize(const Tensor4& x, const uint8_t* lut, const uint8_t* img, float alpha, uint8_t* cls,
+                     uint8_t* rgb, uint8_t* blend, hipStream_t st);
+
 }  // namespace rtseg

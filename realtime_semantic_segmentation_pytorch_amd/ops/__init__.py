@@ -12,6 +12,7 @@ from .kd import kd_kl_div, kd_kl_div_reference
 from .bn import (bn_act, act_code as bn_act_code, fused_ok as bn_fused_ok, convert_batchnorm,
                  FusedBatchNorm2d, FusedSyncBatchNorm)
 from .detail import detail_loss, detail_loss_reference, detail_target_reference
+from .postprocess import colorize, colorize_reference
 from .confmat import confusion_matrix, confusion_matrix_reference
 from .dwconv import DepthwiseConv2d, convert_depthwise, depthwise_ok, dw_conv2d
 from .pool import (avg_pool2d, max_pool2d, adaptive_avg_pool2d, convert_pooling, AvgPool2d, MaxPool2d,
@@ -23,7 +24,7 @@ __all__ = [
     "load", "use_hip", "hip_disabled", "library_path",
     "interpolate", "final_upsample", "defer_final_upsample", "DeferredLogits", "materialize",
     "seg_cross_entropy", "seg_cross_entropy_reference", "MODE_OHEM", "MODE_MEAN", "MODE_SUM",
-    "kd_kl_div", "kd_kl_div_reference", "detail_loss", "detail_loss_reference", "detail_target_reference", "confusion_matrix", "confusion_matrix_reference",
+    "colorize", "colorize_reference", "kd_kl_div", "kd_kl_div_reference", "detail_loss", "detail_loss_reference", "detail_target_reference", "confusion_matrix", "confusion_matrix_reference",
     "DepthwiseConv2d", "convert_depthwise", "depthwise_ok", "dw_conv2d",
     "avg_pool2d", "max_pool2d", "adaptive_avg_pool2d", "convert_pooling", "AvgPool2d", "MaxPool2d",
     "AdaptiveAvgPool2d",

@@ -128,3 +128,20 @@ def test_ema_lerp_buffers():
     ema_lerp_(list(zip(src, ema)), 0.3)
     for a, b in zip(ema, ref):
         torch.testing.assert_close(a, b)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cl", [False, True])
+def test_colorize_matches_reference(dtype, cl):
+    torch.manual_seed(7)
+    x = torch.randn(2, 19, 33, 50, device=DEV).to(dtype)
+    x[:, 3] = x[:, 5]  # ties -> first maximum
+    if cl:
+        x = x.contiguous(memory_format=torch.channels_last)
+    cmap = torch.randint(0, 256, (19, 3), dtype=torch.uint8, device=DEV)
+    img = torch.randint(0, 256, (2, 33, 50, 3), dtype=torch.uint8, device=DEV)
+    cls, rgb, blend = ops.colorize(x, cmap, img, 0.3)
+    rc, rr, rb = ops.colorize_reference(x.float().cpu(), cmap.cpu(), img.cpu(), 0.3)
+    assert torch.equal(cls.cpu(), rc) and torch.equal(rgb.cpu(), rr) and torch.equal(blend.cpu(), rb)
+    cls2, _, none = ops.colorize(x, cmap)
+    assert none is None and torch.equal(cls2, cls)

@@ -123,3 +123,18 @@ def test_detail_loss_cpu_is_reference():
     torch.testing.assert_close(got, want)
     got.backward()
     assert d.grad is not None and torch.isfinite(d.grad).all()
+
+
+def test_colorize_reference_matches_pil_blend():
+    import numpy as np
+    from PIL import Image
+
+    torch.manual_seed(5)
+    logits = torch.randn(2, 19, 8, 12)
+    cmap = torch.randint(0, 256, (19, 3), dtype=torch.uint8)
+    img = torch.randint(0, 256, (2, 8, 12, 3), dtype=torch.uint8)
+    cls, rgb, blend = ops.colorize(logits, cmap, img, 0.3)
+    assert torch.equal(cls.long(), logits.argmax(1)) and torch.equal(rgb, cmap[logits.argmax(1)])
+    for i in range(2):
+        want = np.asarray(Image.blend(Image.fromarray(img[i].numpy()), Image.fromarray(rgb[i].numpy()), 0.3))
+        assert np.array_equal(blend[i].numpy(), want)
