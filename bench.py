@@ -156,7 +156,7 @@ def main():
     from realtime_semantic_segmentation_pytorch_amd import ops
     from realtime_semantic_segmentation_pytorch_amd.core import SegTrainer
     from realtime_semantic_segmentation_pytorch_amd.datasets import DeviceBatches
-    from realtime_semantic_segmentation_pytorch_amd.parallel import de_parallel
+    from realtime_semantic_segmentation_pytorch_amd.parallel import barrier, de_parallel
 
     torch.backends.cudnn.benchmark = not a.no_cudnn_benchmark
     cfg = make_config(a, world)
@@ -184,7 +184,7 @@ def main():
     def sync_all():
         torch.cuda.synchronize()
         if dist.is_initialized():
-            dist.barrier(device_ids=[dev.index])
+            barrier()
         torch.cuda.synchronize()
 
     sync_all()
@@ -234,7 +234,7 @@ def main():
             extra["ddrnet23slim_fps_fp32_bs1_512x1024"] = round(fps, 2)
             extra["ddrnet23slim_fps_vs_readme_rtx2080"] = round(fps / README_FPS_DDRNET23_SLIM, 3)
     if dist.is_initialized():
-        dist.barrier(device_ids=[dev.index])
+        barrier()
     if rank == 0:
         out = {
             "metric": "train_images_per_sec",

@@ -67,9 +67,12 @@ def set_device(config, local_rank=None):
     use_cuda = torch.cuda.is_available() and want != "cpu"
     if config.DDP:
         if use_cuda:
+            # one process per GPU; ranks beyond the visible devices share them round-robin (only
+            # for rehearsing N ranks on fewer GPUs with RTSEG_DIST_BACKEND=gloo -- RCCL refuses it)
+            local_rank = local_rank % torch.cuda.device_count()
             torch.cuda.set_device(local_rank)
             device = torch.device("cuda", local_rank)
-            backend = "nccl"
+            backend = os.getenv("RTSEG_DIST_BACKEND", "nccl")
         else:
             device = torch.device("cpu")
             backend = "gloo"
