@@ -108,6 +108,54 @@ __global__ void __launch_bounds__(256) interp_fwd_cl_pix(
   }
 }
 
+// Same, for a dense channels-last output whose pixel is not a whole number of 16-byte
+// vectors (e.g. 19-class logits: 38 bytes): a block computes 256 consecutive output pixels
+// into LDS and writes them back as one contiguous run of 16-byte stores -- the per-pixel
+// scalar stores above touch ~19 partial lines per wave instruction (TA-bound, ~5x off HBM).
+template <typename T, int ACT, bool SKIP>
+__global__ void __launch_bounds__(256) interp_fwd_cl_pix_lds(
+    const T* __restrict__ x, Shape4 xs, const T* __restrict__ skip, Shape4 ks,
+    T* __restrict__ y, Shape4 ys, LinMap mh, LinMap mw, FastDiv fw, FastDiv fh, uint32_t npix) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char ip_lds[];
+  T* st = reinterpret_cast<T*>(ip_lds);
+  const int C = ys.c;
+  for (uint32_t p0 = blockIdx.x * 256u; p0 < npix; p0 += gridDim.x * 256u) {
+    const uint32_t i = p0 + threadIdx.x;
+    if (i < npix) {
+      uint32_t ox, oy;
+      const uint32_t r1 = fw.divmod(i, ox);
+      const int n = static_cast<int>(fh.divmod(r1, oy));
+      int y0, y1, x0, x1; float ly, lx;
+      mh.map(static_cast<int>(oy), y0, y1, ly);
+      mw.map(static_cast<int>(ox), x0, x1, lx);
+      const float w00 = (1.f - ly) * (1.f - lx), w01 = (1.f - ly) * lx, w10 = ly * (1.f - lx), w11 = ly * lx;
+      const T* b = x + n * xs.sn;
+      const T* p00 = b + y0 * xs.sh + x0 * xs.sw;
+      const T* p01 = b + y0 * xs.sh + x1 * xs.sw;
+      const T* p10 = b + y1 * xs.sh + x0 * xs.sw;
+      const T* p11 = b + y1 * xs.sh + x1 * xs.sw;
+      const T* k = SKIP ? skip + off4(ks, n, 0, static_cast<int>(oy), static_cast<int>(ox)) : nullptr;
+      T* q = st + threadIdx.x * C;
+      for (int c = 0; c < C; ++c) {
+        float v = w00 * Io<T>::ld(p00 + c) + w01 * Io<T>::ld(p01 + c) + w10 * Io<T>::ld(p10 + c) +
+                  w11 * Io<T>::ld(p11 + c);
+        if constexpr (SKIP) v += Io<T>::ld(k + c * ks.sc);
+        Io<T>::st(q + c, act_fwd<ACT>(v));
+      }
+    }
+    __syncthreads();
+    const uint32_t np = npix - p0 < 256u ? npix - p0 : 256u;
+    const int64_t nelem = static_cast<int64_t>(np) * C;
+    const int64_t nvec = nelem * static_cast<int64_t>(sizeof(T)) / 16;
+    uint4* dst = reinterpret_cast<uint4*>(y + static_cast<int64_t>(p0) * C);
+    const uint4* src = reinterpret_cast<const uint4*>(st);
+    for (int64_t v = threadIdx.x; v < nvec; v += 256) dst[v] = src[v];
+    for (int64_t e = nvec * 16 / static_cast<int64_t>(sizeof(T)) + threadIdx.x; e < nelem; e += 256)
+      y[static_cast<int64_t>(p0) * C + e] = st[e];
+    __syncthreads();
+  }
+}
+
 typedef short short8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ void unpack8(const short8& v, float* f) {
@@ -311,6 +359,16 @@ static void fwd_dispatch(const Tensor4& x, const Tensor4* skip, const Tensor4& y
   }
   int64_t work = static_cast<int64_t>(y.n) * y.c * y.h * y.w;
   const int64_t npix = static_cast<int64_t>(y.n) * y.h * y.w;
+  const bool dense_cl = y.sc == 1 && y.sw == y.c && y.sh == static_cast<int64_t>(y.w) * y.c &&
+                        y.sn == static_cast<int64_t>(y.h) * y.w * y.c &&
+                        reinterpret_cast<uintptr_t>(y.data) % 16 == 0;
+  const size_t lds = static_cast<size_t>(256) * y.c * sizeof(T);
+  if (dense_cl && x.sc == 1 && y.c > 1 && lds <= 32768 && npix < (int64_t{1} << 31)) {
+    interp_fwd_cl_pix_lds<T, ACT, SKIP><<<stream_grid(npix, 256), 256, lds, st>>>(
+        static_cast<const T*>(x.data), xs, kp, ks, static_cast<T*>(y.data), ys, mh, mw, FastDiv::make(y.w),
+        FastDiv::make(y.h), static_cast<uint32_t>(npix));
+    return;
+  }
   if (y.sc == 1 && x.sc == 1 && y.c > 1 && y.c <= 64 && npix < (int64_t{1} << 31)) {
     interp_fwd_cl_pix<T, ACT, SKIP><<<stream_grid(npix, 256), 256, 0, st>>>(
         static_cast<const T*>(x.data), xs, kp, ks, static_cast<T*>(y.data), ys, mh, mw, FastDiv::make(y.w),

@@ -118,6 +118,67 @@ __global__ void __launch_bounds__(kPoolBlock) pool_fwd_kernel(Tensor4 x, Tensor4
   }
 }
 
+// Average pooling with large windows over few outputs (DDRNet's DAPPM: 5/9/17-tap windows
+// on a 1/64-resolution map -> a few thousand output vectors, each a serial loop of up to 289
+// loads): 16 lanes share one output vector, stride its window taps and reduce by shuffles.
+template <typename T, int VEC, bool ADAPT>
+__global__ void __launch_bounds__(kPoolBlock) pool_avg_split_kernel(Tensor4 x, Tensor4 y, PoolParams p, PoolDivs d,
+                                                                    uint32_t total) {
+  constexpr uint32_t G = 16;
+  const T* xp = static_cast<const T*>(x.data);
+  T* yp = static_cast<T*>(y.data);
+  const int lane = threadIdx.x & (G - 1);
+  for (uint32_t i = (blockIdx.x * kPoolBlock + threadIdx.x) / G; i < total; i += gridDim.x * (kPoolBlock / G)) {
+    uint32_t cv, ow, oh;
+    const uint32_t r0 = d.c.divmod(i, cv);
+    const uint32_t r1 = d.w.divmod(r0, ow);
+    const uint32_t n = d.h.divmod(r1, oh);
+    int hs, he, ws, we;
+    float div;
+    if constexpr (ADAPT) {
+      adaptive_range(static_cast<int>(oh), x.h, y.h, hs, he);
+      adaptive_range(static_cast<int>(ow), x.w, y.w, ws, we);
+      div = static_cast<float>((he - hs) * (we - ws));
+    } else {
+      const int hs0 = static_cast<int>(oh) * p.sh - p.ph, ws0 = static_cast<int>(ow) * p.sw - p.pw;
+      he = min(hs0 + p.kh, x.h + p.ph);
+      we = min(ws0 + p.kw, x.w + p.pw);
+      const int padded = (he - hs0) * (we - ws0);
+      hs = max(hs0, 0);
+      ws = max(ws0, 0);
+      he = min(he, x.h);
+      we = min(we, x.w);
+      div = static_cast<float>(p.count_include_pad ? padded : (he - hs) * (we - ws));
+    }
+    const int c0 = static_cast<int>(cv) * VEC;
+    const T* xb = xp + static_cast<int64_t>(n) * x.sn + static_cast<int64_t>(c0) * x.sc;
+    const int ww = we - ws, cnt = (he - hs) * ww;
+    float acc[VEC];
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) acc[v] = 0.f;
+    for (int t = lane; t < cnt; t += G) {
+      const int dh = t / ww;
+      const int ih = hs + dh, iw = ws + (t - dh * ww);
+      float v_[VEC];
+      Vec<T, VEC>::load(xb + static_cast<int64_t>(ih) * x.sh + static_cast<int64_t>(iw) * x.sw, v_);
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) acc[v] += v_[v];
+    }
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1)
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) acc[v] += __shfl_xor(acc[v], o, kWave);
+    if (lane == 0) {
+      const float inv = 1.f / div;
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) acc[v] *= inv;
+      const int64_t yo = static_cast<int64_t>(n) * y.sn + static_cast<int64_t>(c0) * y.sc +
+                         static_cast<int64_t>(oh) * y.sh + static_cast<int64_t>(ow) * y.sw;
+      Vec<T, VEC>::store(yp + yo, acc);
+    }
+  }
+}
+
 template <typename T, int VEC, int MODE, bool ADAPT>
 __global__ void __launch_bounds__(kPoolBlock) pool_bwd_kernel(Tensor4 gy, Tensor4 gx, PoolParams p, PoolDivs d,
                                                               const uint8_t* __restrict__ idx, uint32_t total) {
@@ -296,7 +357,14 @@ void launch_pool_fwd(const Tensor4& x, const Tensor4& y, const PoolParams& p, ui
         const uint32_t total = static_cast<uint32_t>(static_cast<int64_t>(y.n) * y.h * y.w * cvs);
         PoolDivs d{FastDiv::make(cvs), FastDiv::make(y.w), FastDiv::make(y.h)};
         const int g = stream_grid(total, kPoolBlock);
-        if (p.mode == kPoolMax)
+        // mean window size: taps per output (adaptive: input / output area)
+        const int64_t taps = p.adaptive ? (static_cast<int64_t>(x.h) * x.w) / (static_cast<int64_t>(y.h) * y.w)
+                                        : static_cast<int64_t>(p.kh) * p.kw;
+        if (p.mode == kPoolAvg && taps >= 16 && total < 256u * 256u) {
+          const int gs = stream_grid(static_cast<int64_t>(total) * 16, kPoolBlock);
+          if (p.adaptive) pool_avg_split_kernel<T, V, true><<<gs, kPoolBlock, 0, st>>>(x, y, p, d, total);
+          else pool_avg_split_kernel<T, V, false><<<gs, kPoolBlock, 0, st>>>(x, y, p, d, total);
+        } else if (p.mode == kPoolMax)
           pool_fwd_kernel<T, V, kPoolMax, false><<<g, kPoolBlock, 0, st>>>(x, y, p, d, idx, total);
         else if (p.adaptive)
           pool_fwd_kernel<T, V, kPoolAvg, true><<<g, kPoolBlock, 0, st>>>(x, y, p, d, nullptr, total);
@@ -338,7 +406,7 @@ GapPlan gap_plan(const Tensor4& x) {
   const int hw = x.h * x.w;
   const int rows = kPoolBlock / pl.cpb;
   int slices = (512 + x.n * pl.cblocks - 1) / (x.n * pl.cblocks);
-  const int max_slices = (hw + 4 * rows - 1) / (4 * rows);  // >= 4 pixels per thread row
+  const int max_slices = (hw + 16 * rows - 1) / (16 * rows);  // >= 16 pixels per thread row
   if (slices > max_slices) slices = max_slices;
   if (slices < 1) slices = 1;
   if (slices > 65535) slices = 65535;

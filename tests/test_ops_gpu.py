@@ -19,7 +19,10 @@ def _lib_loaded():
 @pytest.mark.parametrize("cl", [False, True])
 @pytest.mark.parametrize("align", [True, False])
 @pytest.mark.parametrize("shape,size", [((2, 16, 7, 9), (28, 36)), ((1, 24, 16, 32), (128, 256)),
-                                        ((2, 8, 32, 64), (16, 32)), ((1, 16, 1, 1), (16, 32))])
+                                        ((2, 8, 32, 64), (16, 32)), ((1, 16, 1, 1), (16, 32)),
+                                        # odd channel counts: dense channels-last output staged
+                                        # through LDS (19-class logits, RGB)
+                                        ((2, 19, 16, 24), (64, 96)), ((1, 3, 9, 11), (40, 50))])
 def test_interp_fwd_bwd(dtype, cl, align, shape, size):
     _lib_loaded()
     torch.manual_seed(0)
