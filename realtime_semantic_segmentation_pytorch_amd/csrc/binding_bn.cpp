@@ -134,10 +134,38 @@ at::Tensor bn_apply(const at::Tensor& x, const at::Tensor& scale_shift,
   return y;
 }
 
+// Residual + activation forward that also returns the activation-derivative bit mask
+// (one byte per channel vector; mask mode 3 of bn_bwd_sums / bn_backward).
+std::tuple<at::Tensor, at::Tensor> bn_apply_bits(const at::Tensor& x, const at::Tensor& scale_shift,
+                                                 const at::Tensor& res, int64_t act) {
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  check_cl(x, "x");
+  check_cl(res, "residual");
+  TORCH_CHECK(res.sizes() == x.sizes() && res.scalar_type() == x.scalar_type(),
+              "rtseg.bn_apply_bits: residual mismatch");
+  TORCH_CHECK(act == 1 || act == 2, "rtseg.bn_apply_bits: relu / relu6 only");
+  const int C = static_cast<int>(x.size(1));
+  const int V = bn_vec_width(dtype_code(x), C);
+  TORCH_CHECK(V > 0, "rtseg.bn_apply_bits: unsupported channel count");
+  at::Tensor y = at::empty_like(x);
+  at::Tensor bits = at::empty({rows_of(x) * (C / V)}, x.options().dtype(at::kByte));
+  launch_bn_apply_bits(x.data_ptr(), res.data_ptr(), scale_shift.data_ptr<float>(), y.data_ptr(),
+                       bits.data_ptr<uint8_t>(), dtype_code(x), rows_of(x), C, static_cast<int>(act),
+                       cur_stream());
+  return {y, bits};
+}
+
 const void* opt_y(const std::optional<at::Tensor>& y, int64_t mask) {
   const void* yp = nullptr;
-  if (y.has_value() && y->defined()) { check_cl(*y, "y"); yp = y->data_ptr(); }
-  TORCH_CHECK(mask != 1 || yp, "rtseg.bn_bwd: mask-from-y needs y");
+  if (y.has_value() && y->defined()) {
+    if (mask == 3) {
+      TORCH_CHECK(y->scalar_type() == at::kByte && y->is_contiguous(), "rtseg.bn_bwd: bad bit mask");
+    } else {
+      check_cl(*y, "y");
+    }
+    yp = y->data_ptr();
+  }
+  TORCH_CHECK((mask != 1 && mask != 3) || yp, "rtseg.bn_bwd: mask-from-y / bit mask needs y");
   return yp;
 }
 
@@ -217,6 +245,7 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
   m.def("bn_eval_coeffs(Tensor? weight, Tensor? bias, Tensor running_mean, Tensor running_var, "
         "float eps) -> (Tensor, Tensor)");
   m.def("bn_apply(Tensor x, Tensor scale_shift, Tensor? residual, int act) -> Tensor");
+  m.def("bn_apply_bits(Tensor x, Tensor scale_shift, Tensor residual, int act) -> (Tensor, Tensor)");
   m.def("bn_bwd_sums(Tensor grad, Tensor x, Tensor? y, Tensor mean_invstd, Tensor scale_shift, "
         "int act, int mask) -> Tensor");
   m.def("bn_backward(Tensor grad, Tensor x, Tensor? y, Tensor? bsums, Tensor? fwd_sums, "
@@ -230,6 +259,7 @@ TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
   m.impl("bn_finalize", &rtseg::bn_finalize);
   m.impl("bn_eval_coeffs", &rtseg::bn_eval_coeffs);
   m.impl("bn_apply", &rtseg::bn_apply);
+  m.impl("bn_apply_bits", &rtseg::bn_apply_bits);
   m.impl("bn_bwd_sums", &rtseg::bn_bwd_sums);
   m.impl("bn_backward", &rtseg::bn_backward);
 }

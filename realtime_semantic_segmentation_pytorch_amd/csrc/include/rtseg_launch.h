@@ -74,6 +74,8 @@ void launch_bn_finalize(const double* sums, int C, const float* w, const float* 
 void launch_bn_eval_coeffs(int C, const float* w, const float* b, const float* rmean,
                            const float* rvar, float eps, float* mean_invstd, float* scale_shift,
                            hipStream_t st);
+void launch_bn_apply_bits(const void* x, const void* res, const float* scale_shift, void* y,
+                          uint8_t* bits, int dtype, int64_t M, int C, int act, hipStream_t st);
 void launch_bn_apply(const void* x, const void* res, const float* scale_shift, void* y, int dtype,
                      int64_t M, int C, int act, hipStream_t st);
 void launch_bn_bwd_reduce(const void* dy, const void* x, const void* y, const float* mean_invstd,

@@ -18,13 +18,16 @@
 //
 // Backward "mask modes": the activation derivative is recomputed instead of
 // stored -- from the pre-activation x*scale+shift when there is no residual
-// (so the forward output need not be kept), or from the saved output y.
+// (so the forward output need not be kept), or from the saved output y, or -- with a
+// residual -- from a bit mask the forward wrote next to y (kMaskBits: one byte per
+// V-channel vector, bit j = activation derivative of channel c0+j is 1), which replaces
+// the 2-byte-per-element re-read of y in both backward passes by 1/8 byte.
 #include "rtseg_common.h"
 #include "rtseg_launch.h"
 
 namespace rtseg {
 
-enum MaskMode : int { kMaskNone = 0, kMaskFromY = 1, kMaskFromX = 2 };
+enum MaskMode : int { kMaskNone = 0, kMaskFromY = 1, kMaskFromX = 2, kMaskBits = 3 };
 
 // V-element channel vector of T: 16-byte vectors on the fast path (8 bf16/fp16 or
 // 4 fp32); narrower widths (down to one element) serve channel counts that are
@@ -275,29 +278,33 @@ __global__ void bn_eval_coeffs_kernel(int C, const float* __restrict__ w, const 
 }
 
 // --------------------------------------------------------------- apply ------
-template <typename T, int V, int ACT, bool RES>
+template <typename T, int V, int ACT, bool RES, bool BITS = false>
 __device__ __forceinline__ void apply_one(const T* __restrict__ x, const T* __restrict__ res,
                                           const float* coef, T* __restrict__ y, int64_t i, int cv,
-                                          int C) {
+                                          int C, uint8_t* __restrict__ bits = nullptr) {
   const int c0 = static_cast<int>(i % cv) * V;
   const int64_t off = (i / cv) * C + c0;
   float f[V], r[V];
   VecIO<T, V>::load(x + off, f);
   if constexpr (RES) VecIO<T, V>::load(res + off, r);
+  uint32_t b = 0;
 #pragma unroll
   for (int j = 0; j < V; ++j) {
     float z = f[j] * coef[c0 + j] + coef[C + c0 + j];
     if constexpr (RES) z += r[j];
     f[j] = act_fwd<ACT>(z);
+    if constexpr (BITS) b |= (act_grad_pre<ACT>(1.f, z) != 0.f ? 1u : 0u) << j;
   }
   VecIO<T, V>::store(y + off, f);
+  if constexpr (BITS) bits[i] = static_cast<uint8_t>(b);  // vector i = byte i (off / V)
 }
 
-template <typename T, int V, int ACT, bool RES>
+template <typename T, int V, int ACT, bool RES, bool BITS = false>
 __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x,
                                                        const T* __restrict__ res,
                                                        const float* __restrict__ scale_shift,
-                                                       T* __restrict__ y, int64_t M, int C) {
+                                                       T* __restrict__ y, int64_t M, int C,
+                                                       uint8_t* __restrict__ bits = nullptr) {
   extern __shared__ __attribute__((aligned(16))) float coef[];  // [2][C]
   for (int c = threadIdx.x; c < 2 * C; c += blockDim.x) coef[c] = scale_shift[c];
   __syncthreads();
@@ -306,10 +313,10 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x,
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
   for (; i + stride < total; i += 2 * stride) {  // two vectors in flight per thread
-    apply_one<T, V, ACT, RES>(x, res, coef, y, i, cv, C);
-    apply_one<T, V, ACT, RES>(x, res, coef, y, i + stride, cv, C);
+    apply_one<T, V, ACT, RES, BITS>(x, res, coef, y, i, cv, C, bits);
+    apply_one<T, V, ACT, RES, BITS>(x, res, coef, y, i + stride, cv, C, bits);
   }
-  if (i < total) apply_one<T, V, ACT, RES>(x, res, coef, y, i, cv, C);
+  if (i < total) apply_one<T, V, ACT, RES, BITS>(x, res, coef, y, i, cv, C, bits);
 }
 
 // ----------------------------------------------------------- backward -------
@@ -326,6 +333,11 @@ __device__ __forceinline__ void load_g(const T* dy, const T* x, const T* y, cons
   } else if constexpr (MASK == kMaskFromX) {
 #pragma unroll
     for (int j = 0; j < V; ++j) g[j] = act_grad_pre<ACT>(g[j], xv[j] * coef[c0 + j] + coef[C + c0 + j]);
+  } else if constexpr (MASK == kMaskBits) {
+    // off = row * C + c0 with V | C and V | c0: the vector index is off / V
+    const uint32_t b = reinterpret_cast<const uint8_t*>(y)[off / V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) g[j] = ((b >> j) & 1u) ? g[j] : 0.f;
   }
 }
 
@@ -545,6 +557,24 @@ static void apply_t(const void* x, const void* res, const float* ss, void* y, in
         static_cast<const T*>(x), nullptr, ss, static_cast<T*>(y), M, C);
 }
 
+template <typename T, int V, int ACT>
+static void apply_bits_t(const void* x, const void* res, const float* ss, void* y, uint8_t* bits,
+                         int64_t M, int C, hipStream_t st) {
+  const int64_t work = M * (C / V);
+  bn_apply_kernel<T, V, ACT, true, true><<<apply_grid(work), 256, sizeof(float) * 2 * C, st>>>(
+      static_cast<const T*>(x), static_cast<const T*>(res), ss, static_cast<T*>(y), M, C, bits);
+}
+
+// Residual + activation forward that also writes the derivative bit mask (kMaskBits):
+// bits holds M * C / V bytes, V = bn_vec_width(dtype, C).
+void launch_bn_apply_bits(const void* x, const void* res, const float* scale_shift, void* y,
+                          uint8_t* bits, int dtype, int64_t M, int C, int act, hipStream_t st) {
+  with_tv(dtype, C, [&]<typename T, int V>() {
+    if (act == kActReLU6) apply_bits_t<T, V, kActReLU6>(x, res, scale_shift, y, bits, M, C, st);
+    else apply_bits_t<T, V, kActReLU>(x, res, scale_shift, y, bits, M, C, st);
+  });
+}
+
 void launch_bn_apply(const void* x, const void* res, const float* scale_shift, void* y, int dtype,
                      int64_t M, int C, int act, hipStream_t st) {
   with_tv(dtype, C, [&]<typename T, int V>() {
@@ -580,9 +610,11 @@ static void bwd_apply_t(const void* dy, const void* x, const void* y, const floa
     if (act == kActNone) FN<T, V, kActNone, kMaskNone>(__VA_ARGS__);                    \
     else if (act == kActReLU) {                                                         \
       if (mask == kMaskFromY) FN<T, V, kActReLU, kMaskFromY>(__VA_ARGS__);              \
+      else if (mask == kMaskBits) FN<T, V, kActReLU, kMaskBits>(__VA_ARGS__);           \
       else FN<T, V, kActReLU, kMaskFromX>(__VA_ARGS__);                                 \
     } else {                                                                            \
       if (mask == kMaskFromY) FN<T, V, kActReLU6, kMaskFromY>(__VA_ARGS__);             \
+      else if (mask == kMaskBits) FN<T, V, kActReLU6, kMaskBits>(__VA_ARGS__);          \
       else FN<T, V, kActReLU6, kMaskFromX>(__VA_ARGS__);                                \
     }                                                                                   \
   } while (0)

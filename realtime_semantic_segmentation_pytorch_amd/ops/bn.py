@@ -15,6 +15,7 @@ reference's SyncBatchNorm all-gathers mean/invstd/count instead.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -24,7 +25,10 @@ import torch.nn as nn
 from ._ext import use_hip, ops
 
 ACT_NONE, ACT_RELU, ACT_RELU6 = 0, 1, 2
-MASK_NONE, MASK_FROM_Y, MASK_FROM_X = 0, 1, 2
+MASK_NONE, MASK_FROM_Y, MASK_FROM_X, MASK_BITS = 0, 1, 2, 3
+# residual + activation: the forward writes a 1-bit-per-element activation-derivative mask
+# (MASK_BITS) instead of the backward re-reading the bf16 output y twice (RTSEG_BN_BITS=0: off)
+_USE_BITS = os.environ.get("RTSEG_BN_BITS", "1") != "0"
 
 
 def act_code(act) -> Optional[int]:
@@ -78,18 +82,21 @@ class _BNActFn(torch.autograd.Function):
         else:
             sums = None
             mi, ss = eval_coeffs(bn)
-        y = ops().bn_apply(x, ss, residual, act)
         if act == ACT_NONE:
             mask = MASK_NONE
         elif residual is None:
             mask = MASK_FROM_X
         else:
-            mask = MASK_FROM_Y
+            mask = MASK_BITS if _USE_BITS else MASK_FROM_Y
+        if mask == MASK_BITS:
+            y, bits = ops().bn_apply_bits(x, ss, residual, act)
+        else:
+            y, bits = ops().bn_apply(x, ss, residual, act), None
         ctx.act, ctx.mask, ctx.pg = act, mask, pg
         ctx.batch_stats = use_batch_stats
         ctx.has_res = residual is not None
         ctx.has_w = weight is not None
-        ctx.save_for_backward(x, y if mask == MASK_FROM_Y else None, mi, ss, sums, weight)
+        ctx.save_for_backward(x, y if mask == MASK_FROM_Y else bits, mi, ss, sums, weight)
         return y
 
     @staticmethod

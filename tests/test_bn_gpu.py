@@ -137,3 +137,30 @@ def test_fused_batchnorm_module_matches_torch(dtype, shape):
         yb.backward(g)
         torch.testing.assert_close(xa.grad.float(), xb.grad, atol=10 * tol, rtol=10 * tol)
     torch.testing.assert_close(mod.running_mean, ref.running_mean, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("act", ["relu", "relu6"])
+@pytest.mark.parametrize("shape", [(2, 64, 17, 33), (2, 19, 16, 16), (3, 131, 4, 4)])
+def test_bn_residual_bitmask_matches_mask_from_y(monkeypatch, act, shape):
+    """Residual + activation backward: the 1-bit derivative mask written by the forward
+    (MASK_BITS) gives the same gradients as re-reading the saved output (MASK_FROM_Y)."""
+    from realtime_semantic_segmentation_pytorch_amd.ops import bn as bn_mod
+
+    assert ops.load()
+    grads = []
+    for use_bits in (True, False):
+        monkeypatch.setattr(bn_mod, "_USE_BITS", use_bits)
+        torch.manual_seed(3)
+        bn = nn.BatchNorm2d(shape[1]).to(DEV)
+        x = (torch.randn(shape, device=DEV) * 3).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        res = torch.randn(shape, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        x.requires_grad_(True)
+        res.requires_grad_(True)
+        y = ops.bn_act(x, bn, act, residual=res)
+        y.backward(torch.randn(shape, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+        grads.append((y.detach(), x.grad, res.grad, bn.weight.grad, bn.bias.grad))
+    for a, b in zip(*grads):
+        if act == "relu":
+            torch.testing.assert_close(a, b, atol=0, rtol=0)
+        else:  # relu6: the mask is taken from the fp32 pre-activation vs the bf16-rounded output
+            assert ((a.float() - b.float()).abs() > 1e-2 * (1 + b.float().abs())).float().mean() < 1e-3

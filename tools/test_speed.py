@@ -37,7 +37,10 @@ def test_model_speed(config, ratio=0.5, imgw=2048, imgh=1024, iterations=None, d
         if ratio <= 0:
             raise AssertionError("Ratio should be larger than 0.\n")
         imgw, imgh = int(imgw * ratio), int(imgh * ratio)
-    os.environ.setdefault("MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_FWD", "0")
+    if config.model in ("ddrnet", "bisenetv2", "stdc", "pp_liteseg", "ppliteseg"):
+        # shapes where the naive solvers only slow the find down; elsewhere they are the
+        # fallback for degenerate dilated geometries (see the package docstring)
+        os.environ.setdefault("MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_FWD", "0")
     torch.backends.cudnn.benchmark = True
     model = get_model(config)
     print("\n=========Speed Testing=========")
