@@ -69,7 +69,7 @@ __device__ uint4 g_zero16[1];
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= 0 && N <= 8, "vmcnt immediate");
+  static_assert(N >= 0 && N <= 16, "vmcnt immediate");
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
   else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
@@ -78,7 +78,10 @@ __device__ __forceinline__ void wait_vmcnt() {
   else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // other counts: drain (correct, slower)
 }
 
 // LDS-DMA issued from inline asm: hipcc's waitcnt pass cannot tell which LDS bytes a

@@ -134,7 +134,10 @@ def test_zoo_hip_matches_torch_path_gpu(key, monkeypatch):
     assert g_h.keys() == g_t.keys() == g_r.keys()
     cat = lambda g: torch.cat([g[n].flatten().double().cpu() for n in g_r])  # noqa: E731
     err = lambda a, b: ((a.double().cpu() - b.double().cpu()).norm() / (b.double().cpu().norm() + 1e-30)).item()  # noqa: E731
-    assert err(y_h, y_r) <= 4 * err(y_t, y_r) + 1e-5
+    # train-mode fp32 forward vs fp64: MIOpen's solver choice moves either path's error
+    # within ~1e-5 .. 1.2e-4 run to run (BiSeNetV2, tools/probe_zoo_err.py: HIP 2.0e-5 /
+    # 5.0e-5 vs torch 6.8e-5 / 7.5e-5 on two runs; 8.4e-5 vs 1.8e-5 on a third)
+    assert err(y_h, y_r) <= max(4 * err(y_t, y_r), 2e-4)
     gt = err(cat(g_t), cat(g_r))
     assert torch.isfinite(cat(g_h)).all()
     if gt > 0.1:  # DFANet: fp32 gradients of ~1e8 that differ from fp64 by O(1) on any path

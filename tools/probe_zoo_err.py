@@ -35,10 +35,12 @@ def main():
         cat = lambda g: torch.cat([g[n].flatten().double().cpu() for n in g_r])  # noqa: E731
         err = lambda a, b: ((a.double().cpu() - b.double().cpu()).norm() / (b.double().cpu().norm() + 1e-30)).item()  # noqa: E731
         rows = []
-        for name, dis, dw, sep in (("hip", False, "1", "1"), ("hip-no-dw", False, "0", "1"),
-                                   ("hip-no-sep", False, "1", "0"), ("torch", True, "1", "1")):
+        for name, dis, dw, sep, pool in (("hip", False, "1", "1", "1"), ("hip-no-dw", False, "0", "1", "1"),
+                                         ("hip-no-sep", False, "1", "0", "1"), ("hip-no-pool", False, "1", "1", "0"),
+                                         ("torch", True, "1", "1", "1")):
             os.environ["RTSEG_DWCONV"] = dw
             os.environ["RTSEG_INTERP_SEP"] = sep
+            os.environ["RTSEG_POOL"] = pool
             y, l, g = _run_gpu(copy.deepcopy(base), xg, labels.cuda(), dis, mp)
             rows.append(f"{name}: y {err(y, y_r):.2e} loss {abs(l.item() - l_r.item()):.2e} grad {err(cat(g), cat(g_r)):.2e}")
         os.environ["RTSEG_DWCONV"] = "1"
