@@ -75,6 +75,8 @@ def get_model(config):
         ops.convert_depthwise(model)
     if getattr(config, "hip_pooling", True):
         ops.convert_pooling(model)
+    if getattr(config, "tap_convs", True):
+        ops.convert_tap_convs(model)
     return model
 
 

@@ -1,0 +1,76 @@
+"""Narrow dilated 1-D convolutions as a sum of per-tap GEMMs.
+
+Reference: CFPNet's ``FeaturePyramidChannel`` (reference models/cfpnet.py:108-138) stacks
+dense ``(3, 1)`` / ``(1, 3)`` ConvBNActs with dilation up to 16 on 4..16 channels.  On
+MI355X, MIOpen's solver search for these shapes in channels-last at 1024x512 faulted the
+GPU (illegal memory access inside ``EvaluateInvokers``; tools/zoo_fps.py run of this round),
+so such layers do not go through MIOpen at all.  A K-tap 1-D conv with C_in, C_out <= 16
+is a bandwidth-bound op, and in NHWC it is exactly
+
+    y[n, h, w, :] = sum_t  x[n, h + (t - (K-1)/2) * d, w, :] @ W_t        (zero outside)
+
+i.e. K small GEMMs over shifted views of one zero-padded copy of ``x`` (rocBLAS /
+hipBLASLt), summed -- no solver search, autograd for free, identical numerics to a
+direct conv up to summation order.  :func:`convert_tap_convs` swaps the class of every
+eligible ``nn.Conv2d`` (parameters and checkpoint keys unchanged); CPU tensors and any
+other shape keep ``F.conv2d``.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+MAX_CHANNELS = 16
+
+
+def tapconv_ok(conv: nn.Module) -> bool:
+    if not isinstance(conv, nn.Conv2d) or conv.groups != 1 or conv.padding_mode != "zeros":
+        return False
+    if isinstance(conv.padding, str) or tuple(conv.stride) != (1, 1):
+        return False
+    kh, kw = conv.kernel_size
+    if min(kh, kw) != 1 or max(kh, kw) < 2 or max(kh, kw) % 2 == 0:
+        return False
+    axis = 0 if kh > 1 else 1
+    d, p = conv.dilation[axis], conv.padding[axis]
+    if d < 2 or p != d * (max(kh, kw) - 1) // 2 or conv.padding[1 - axis] != 0:
+        return False
+    return conv.in_channels <= MAX_CHANNELS and conv.out_channels <= MAX_CHANNELS
+
+
+def tap_conv2d(x: torch.Tensor, weight: torch.Tensor, bias, dilation: int, axis: int) -> torch.Tensor:
+    """Same-padded stride-1 1-D conv along H (axis 0) or W (axis 1) of ``x`` [N, C, H, W]."""
+    k = weight.shape[2 + axis]
+    p = dilation * (k - 1) // 2
+    xn = x.permute(0, 2, 3, 1)                                  # NHWC view (free for channels-last)
+    pad = (0, 0, 0, 0, p, p) if axis == 0 else (0, 0, p, p)
+    xp = F.pad(xn, pad)
+    n = x.shape[2 + axis]
+    w = weight.squeeze(3 - axis)                                # [Cout, Cin, K]
+    y = None
+    for t in range(k):
+        sl = xp.narrow(1 + axis, t * dilation, n)
+        term = torch.matmul(sl, w[:, :, t].t())
+        y = term if y is None else y + term
+    if bias is not None:
+        y = y + bias
+    return y.permute(0, 3, 1, 2)                                # NCHW logical, channels-last memory
+
+
+class TapConv2d(nn.Conv2d):
+    """``nn.Conv2d`` whose CUDA forward is :func:`tap_conv2d` (see module docstring)."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if not x.is_cuda:
+            return super().forward(x)
+        axis = 0 if self.kernel_size[0] > 1 else 1
+        return tap_conv2d(x, self.weight, self.bias, self.dilation[axis], axis)
+
+
+def convert_tap_convs(model: nn.Module) -> nn.Module:
+    """Swap the class of every eligible narrow dilated 1-D ``nn.Conv2d`` to :class:`TapConv2d`."""
+    for m in model.modules():
+        if type(m) is nn.Conv2d and tapconv_ok(m):
+            m.__class__ = TapConv2d
+    return model

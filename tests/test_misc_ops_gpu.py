@@ -145,3 +145,31 @@ def test_colorize_matches_reference(dtype, cl):
     assert torch.equal(cls.cpu(), rc) and torch.equal(rgb.cpu(), rr) and torch.equal(blend.cpu(), rb)
     cls2, _, none = ops.colorize(x, cmap)
     assert none is None and torch.equal(cls2, cls)
+
+
+@pytest.mark.parametrize("axis,d,dt", [(0, 2, torch.float32), (1, 16, torch.float32), (0, 8, torch.bfloat16)])
+def test_tap_conv_gpu_vs_cpu_fp64(axis, d, dt):
+    """TapConv2d (CFPNet's narrow dilated 1-D convs, ops/tapconv.py) on the GPU vs a CPU fp64
+    F.conv2d -- the GPU reference would be the MIOpen path this module avoids."""
+    import torch.nn.functional as F
+
+    torch.manual_seed(0)
+    ks, pad, dil = ((3, 1), (d, 0), (d, 1)) if axis == 0 else ((1, 3), (0, d), (1, d))
+    conv = nn.Conv2d(8, 8, ks, padding=pad, dilation=dil, bias=False)
+    assert ops.tapconv_ok(conv)
+    x = torch.randn(2, 8, 64, 128).contiguous(memory_format=torch.channels_last)
+    g = torch.randn(2, 8, 64, 128)
+    xr = x.double().requires_grad_(True)
+    wr = conv.weight.detach().double().requires_grad_(True)
+    ref = F.conv2d(xr, wr, None, 1, pad, dil)
+    gxr, gwr = torch.autograd.grad(ref, (xr, wr), g.double())
+    m = copy.deepcopy(conv).cuda()
+    m.__class__ = ops.TapConv2d
+    xc = x.cuda().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dt == torch.bfloat16):
+        out = m(xc)
+    gx, gw = torch.autograd.grad(out, (xc, m.weight), g.cuda().to(out.dtype))
+    tol = dict(atol=5e-2, rtol=5e-2) if dt == torch.bfloat16 else dict(atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(out.float().cpu(), ref.float(), **tol)
+    torch.testing.assert_close(gx.float().cpu(), gxr.float(), **tol)
+    torch.testing.assert_close(gw.float().cpu(), gwr.float(), **dict(tol, atol=tol["atol"] * 20))

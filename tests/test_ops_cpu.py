@@ -138,3 +138,40 @@ def test_colorize_reference_matches_pil_blend():
     for i in range(2):
         want = np.asarray(Image.blend(Image.fromarray(img[i].numpy()), Image.fromarray(rgb[i].numpy()), 0.3))
         assert np.array_equal(blend[i].numpy(), want)
+
+
+@pytest.mark.parametrize("k,axis,d,cin,cout", [(3, 0, 2, 4, 4), (3, 1, 16, 8, 8), (5, 0, 3, 16, 8), (3, 1, 4, 4, 16)])
+def test_tap_conv_matches_conv2d_cpu(k, axis, d, cin, cout):
+    """ops/tapconv.py: per-tap GEMM formulation == F.conv2d (values and gradients)."""
+    import torch.nn.functional as F
+    from realtime_semantic_segmentation_pytorch_amd.ops import tap_conv2d, tapconv_ok
+
+    torch.manual_seed(0)
+    ks = (k, 1) if axis == 0 else (1, k)
+    pad = (d * (k - 1) // 2, 0) if axis == 0 else (0, d * (k - 1) // 2)
+    conv = torch.nn.Conv2d(cin, cout, ks, padding=pad, dilation=(d, 1) if axis == 0 else (1, d), bias=True).double()
+    assert tapconv_ok(conv)
+    x = torch.randn(2, cin, 37, 41, dtype=torch.float64).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    ref = F.conv2d(x, conv.weight, conv.bias, 1, pad, conv.dilation)
+    got = tap_conv2d(x, conv.weight, conv.bias, d, axis)
+    torch.testing.assert_close(got, ref)
+    g = torch.randn_like(ref)
+    gx_ref, gw_ref = torch.autograd.grad(ref, (x, conv.weight), g)
+    gx, gw = torch.autograd.grad(got, (x, conv.weight), g)
+    torch.testing.assert_close(gx, gx_ref)
+    torch.testing.assert_close(gw, gw_ref)
+
+
+def test_tap_conv_converted_only_in_cfpnet_like_layers_cpu():
+    from realtime_semantic_segmentation_pytorch_amd.configs import BaseConfig
+    from realtime_semantic_segmentation_pytorch_amd.models import get_model
+    from realtime_semantic_segmentation_pytorch_amd.ops import TapConv2d
+
+    c = BaseConfig()
+    c.model, c.num_class = "cfpnet", 19
+    m = get_model(c)
+    n = sum(type(x) is TapConv2d for x in m.modules())
+    assert n > 0
+    keys = set(m.state_dict())
+    assert any(k.endswith("block1.0.0.weight") for k in keys)

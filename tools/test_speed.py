@@ -41,7 +41,9 @@ def test_model_speed(config, ratio=0.5, imgw=2048, imgh=1024, iterations=None, d
         # shapes where the naive solvers only slow the find down; elsewhere they are the
         # fallback for degenerate dilated geometries (see the package docstring)
         os.environ.setdefault("MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_FWD", "0")
-    torch.backends.cudnn.benchmark = True
+        # MIOpen find mode only on the shapes it has been verified on: its exhaustive search
+        # faulted the GPU on CFPNet's 1024x512 fp32 convolutions (tools/zoo_fps.py)
+        torch.backends.cudnn.benchmark = True
     model = get_model(config)
     print("\n=========Speed Testing=========")
     print(f"Model: {config.model}\nEncoder: {config.encoder}\nDecoder: {config.decoder}")

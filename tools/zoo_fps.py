@@ -67,18 +67,25 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="gpurun_out/zoo_fps.jsonl")
     ap.add_argument("--only", default="")
+    ap.add_argument("--skip", default="")
     ap.add_argument("--seconds", type=float, default=0.5)
     ap.add_argument("--width", type=int, default=1024)
     ap.add_argument("--height", type=int, default=512)
+    ap.add_argument("--benchmark", action="store_true",
+                    help="MIOpen find mode (cudnn.benchmark); off by default: its exhaustive search "
+                         "faulted the GPU on CFPNet's 1024x512 fp32 shapes")
     args = ap.parse_args()
     only = set(filter(None, args.only.split(",")))
+    skip = set(filter(None, args.skip.split(",")))
     os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
-    torch.backends.cudnn.benchmark = True
+    torch.backends.cudnn.benchmark = args.benchmark
     x = torch.randn(1, 3, args.height, args.width, device="cuda")
     rows = []
-    with open(args.out, "w") as f:
+    with open(args.out, "a") as f:
         for label, key, over, ref in ROWS:
             if only and key not in only and label not in only:
+                continue
+            if key in skip or label in skip:
                 continue
             c = BaseConfig()
             c.model, c.num_class, c.use_aux, c.use_detail_head = key, 19, False, False
@@ -87,6 +94,7 @@ def main():
                 setattr(c, k, v)
             torch.manual_seed(0)
             rec = {"model": label, "key": key, "ref_fps_rtx2080": ref}
+            print(f"[zoo_fps] {label} ...", flush=True)
             try:
                 for name, dt in (("fp32", torch.float32), ("bf16", torch.bfloat16)):
                     eng = InferenceEngine(get_model(c), (1, 3, args.height, args.width), dtype=dt,
