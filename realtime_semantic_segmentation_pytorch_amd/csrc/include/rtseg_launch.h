@@ -188,4 +188,16 @@ void launch_detail_bwd(const Tensor4& d, int n, int h, int w, const uint8_t* yin
 void launch_colorize(const Tensor4& x, const uint8_t* lut, const uint8_t* img, float alpha, uint8_t* cls,
                      uint8_t* rgb, uint8_t* blend, hipStream_t st);
 
+// ---- tapconv.hip --------------------------------------------------------------
+// Same-padded stride-1 1-D conv with K <= kTapConvMaxTaps taps, dilation dil, along H (axis 0)
+// or W (axis 1) of channels-last x [N, H, W, ci] -> y [N, H, W, co]; ci, co in {4, 8, 16};
+// w fp32 [K, ci, co]; bias fp32 [co] or nullptr.  tap_stride: pixels between taps / dil.
+constexpr int kTapConvMaxTaps = 7;
+struct TapConvGeo {
+  int n, h, w, k, dil, axis;
+  int64_t tap_stride;
+};
+void launch_tapconv(const void* x, const float* w, const float* bias, void* y, const TapConvGeo& g, int ci, int co,
+                    int dtype, hipStream_t st);
+
 }  // namespace rtseg

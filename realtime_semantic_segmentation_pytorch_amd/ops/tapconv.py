@@ -9,11 +9,13 @@ is a bandwidth-bound op, and in NHWC it is exactly
 
     y[n, h, w, :] = sum_t  x[n, h + (t - (K-1)/2) * d, w, :] @ W_t        (zero outside)
 
-i.e. K small GEMMs over shifted views of one zero-padded copy of ``x`` (rocBLAS /
-hipBLASLt), summed -- no solver search, autograd for free, identical numerics to a
-direct conv up to summation order.  :func:`convert_tap_convs` swaps the class of every
-eligible ``nn.Conv2d`` (parameters and checkpoint keys unchanged); CPU tensors and any
-other shape keep ``F.conv2d``.
+On the GPU the forward and the data gradient run on ``csrc/kernels/tapconv.hip`` (one
+thread per pixel, weights in LDS, one read of x / one write of y; the data gradient is the
+same kernel with flipped taps and transposed W_t); the weight gradient is K small GEMMs
+over shifted views of one zero-padded copy of ``x`` -- the formulation :func:`tap_conv2d`
+also uses for CPU tensors (autograd, identical numerics up to summation order).
+:func:`convert_tap_convs` swaps the class of every eligible ``nn.Conv2d`` (parameters and
+checkpoint keys unchanged).
 """
 from __future__ import annotations
 
@@ -21,7 +23,10 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ._ext import ops, use_hip
+
 MAX_CHANNELS = 16
+HIP_CHANNELS = (4, 8, 16)
 
 
 def tapconv_ok(conv: nn.Module) -> bool:
@@ -58,13 +63,63 @@ def tap_conv2d(x: torch.Tensor, weight: torch.Tensor, bias, dilation: int, axis:
     return y.permute(0, 3, 1, 2)                                # NCHW logical, channels-last memory
 
 
+def _shift_wgrad(x, gy, k, dilation, axis):
+    """dW [Cout, Cin, K] = sum_p gy_p^T shift_t(x)_p, as K GEMMs over one padded copy of x."""
+    p = dilation * (k - 1) // 2
+    xn = x.permute(0, 2, 3, 1)
+    xp = F.pad(xn, (0, 0, 0, 0, p, p) if axis == 0 else (0, 0, p, p))
+    n = x.shape[2 + axis]
+    g2 = gy.permute(0, 2, 3, 1).reshape(-1, gy.shape[1]).float()
+    cols = [g2.t() @ xp.narrow(1 + axis, t * dilation, n).reshape(-1, x.shape[1]).float() for t in range(k)]
+    return torch.stack(cols, dim=2)
+
+
+class _TapConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, dilation, axis):
+        k = weight.shape[2 + axis]
+        w = weight.detach().float().squeeze(3 - axis)                 # [Cout, Cin, K]
+        wf = w.permute(2, 1, 0).contiguous()                          # [K, Cin, Cout]
+        b = bias.detach().float().contiguous() if bias is not None else x.new_empty(0, dtype=torch.float32)
+        y = ops().tapconv_fwd(x, wf, b, dilation, axis)
+        ctx.save_for_backward(x, weight)
+        ctx.geo = (k, dilation, axis, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        k, dilation, axis, has_b = ctx.geo
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            w = weight.detach().float().squeeze(3 - axis)             # [Cout, Cin, K]
+            wb = w.flip(2).permute(2, 0, 1).contiguous()              # [K, Cout, Cin], taps flipped
+            gx = ops().tapconv_fwd(gy, wb, gy.new_empty(0, dtype=torch.float32), dilation, axis)
+        if ctx.needs_input_grad[1]:
+            gw = _shift_wgrad(x, gy, k, dilation, axis).unsqueeze(3 - axis).to(weight.dtype)
+        if has_b and ctx.needs_input_grad[2]:
+            gb = gy.float().sum(dim=(0, 2, 3)).to(weight.dtype)
+        return gx, gw, gb, None, None
+
+
+def hip_tapconv_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
+    return (use_hip(x) and conv.in_channels in HIP_CHANNELS and conv.out_channels in HIP_CHANNELS
+            and max(conv.kernel_size) <= 7 and x.dtype in (torch.float32, torch.bfloat16))
+
+
 class TapConv2d(nn.Conv2d):
-    """``nn.Conv2d`` whose CUDA forward is :func:`tap_conv2d` (see module docstring)."""
+    """``nn.Conv2d`` routed to the tap-conv HIP kernel on the GPU (see module docstring)."""
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if not x.is_cuda:
             return super().forward(x)
         axis = 0 if self.kernel_size[0] > 1 else 1
+        if torch.is_autocast_enabled("cuda"):
+            x = x.to(torch.get_autocast_dtype("cuda"))
+        if hip_tapconv_ok(x, self):
+            x = x.contiguous(memory_format=torch.channels_last)
+            return _TapConvFn.apply(x, self.weight, self.bias, self.dilation[axis], axis)
         return tap_conv2d(x, self.weight, self.bias, self.dilation[axis], axis)
 
 

@@ -147,18 +147,19 @@ def test_colorize_matches_reference(dtype, cl):
     assert none is None and torch.equal(cls2, cls)
 
 
-@pytest.mark.parametrize("axis,d,dt", [(0, 2, torch.float32), (1, 16, torch.float32), (0, 8, torch.bfloat16)])
-def test_tap_conv_gpu_vs_cpu_fp64(axis, d, dt):
+@pytest.mark.parametrize("axis,d,dt,cin,cout", [(0, 2, torch.float32, 8, 8), (1, 16, torch.float32, 4, 16),
+                                                (0, 8, torch.bfloat16, 16, 4), (1, 4, torch.bfloat16, 8, 8)])
+def test_tap_conv_gpu_vs_cpu_fp64(axis, d, dt, cin, cout):
     """TapConv2d (CFPNet's narrow dilated 1-D convs, ops/tapconv.py) on the GPU vs a CPU fp64
     F.conv2d -- the GPU reference would be the MIOpen path this module avoids."""
     import torch.nn.functional as F
 
     torch.manual_seed(0)
     ks, pad, dil = ((3, 1), (d, 0), (d, 1)) if axis == 0 else ((1, 3), (0, d), (1, d))
-    conv = nn.Conv2d(8, 8, ks, padding=pad, dilation=dil, bias=False)
+    conv = nn.Conv2d(cin, cout, ks, padding=pad, dilation=dil, bias=False)
     assert ops.tapconv_ok(conv)
-    x = torch.randn(2, 8, 64, 128).contiguous(memory_format=torch.channels_last)
-    g = torch.randn(2, 8, 64, 128)
+    x = torch.randn(2, cin, 64, 128).contiguous(memory_format=torch.channels_last)
+    g = torch.randn(2, cout, 64, 128)
     xr = x.double().requires_grad_(True)
     wr = conv.weight.detach().double().requires_grad_(True)
     ref = F.conv2d(xr, wr, None, 1, pad, dil)
