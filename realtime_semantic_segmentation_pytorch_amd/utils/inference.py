@@ -30,12 +30,12 @@ class InferenceEngine:
         self.channels_last = channels_last
         self.autocast = dtype in (torch.bfloat16, torch.float16)
         if self.autocast and cast_weights:
-            # autocast re-casts every fp32 conv / linear weight on every forward (one extra
+            # autocast re-casts every fp32 conv / linear (and PReLU) weight on every forward (one extra
             # kernel per layer inside the graph: 18 % of CGNet's bf16 replay time); cast them
             # once, on a private copy so the caller's fp32 model is untouched
             model = copy.deepcopy(model)
             for m in model.modules():
-                if type(m) in (nn.Conv2d, nn.ConvTranspose2d, nn.Linear):
+                if type(m) in (nn.Conv2d, nn.ConvTranspose2d, nn.Linear, nn.PReLU):
                     m.to(dtype)
         self.model = model.eval().to(self.device)
         if channels_last:

@@ -174,3 +174,26 @@ def test_tap_conv_gpu_vs_cpu_fp64(axis, d, dt, cin, cout):
     torch.testing.assert_close(out.float().cpu(), ref.float(), **tol)
     torch.testing.assert_close(gx.float().cpu(), gxr.float(), **tol)
     torch.testing.assert_close(gw.float().cpu(), gwr.float(), **dict(tol, atol=tol["atol"] * 20))
+
+
+@pytest.mark.parametrize("key", ["cgnet", "dabnet", "ddrnet"])
+def test_inference_engine_bf16_matches_eager_autocast(key):
+    """utils/inference.py: the graph engine (weights pre-cast to bf16 on a private copy) gives
+    the eager bf16-autocast output of the same model, and leaves the caller's model fp32."""
+    from realtime_semantic_segmentation_pytorch_amd.configs import BaseConfig
+    from realtime_semantic_segmentation_pytorch_amd.models import get_model
+    from realtime_semantic_segmentation_pytorch_amd.utils.inference import InferenceEngine
+
+    c = BaseConfig()
+    c.model, c.num_class = key, 19
+    torch.manual_seed(0)
+    m = get_model(c).cuda().eval().to(memory_format=torch.channels_last)
+    x = torch.randn(1, 3, 128, 256, device="cuda")
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        ref = ops.materialize(m(x.contiguous(memory_format=torch.channels_last))).float()
+    eng = InferenceEngine(m, (1, 3, 128, 256), dtype=torch.bfloat16)
+    out = eng(x).float()
+    assert all(p.dtype == torch.float32 for p in m.parameters())
+    assert torch.isfinite(out).all()
+    err = (out - ref).abs().max().item()
+    assert err <= 0.05 * ref.abs().max().item() + 1e-2, err
