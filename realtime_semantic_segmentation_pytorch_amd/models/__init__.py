@@ -77,6 +77,8 @@ def get_model(config):
         ops.convert_pooling(model)
     if getattr(config, "tap_convs", True):
         ops.convert_tap_convs(model)
+    if getattr(config, "dilated_group_convs", True):
+        ops.convert_dilated_group_convs(model)
     return model
 
 

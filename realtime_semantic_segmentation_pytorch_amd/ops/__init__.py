@@ -18,6 +18,7 @@ from .dwconv import DepthwiseConv2d, convert_depthwise, depthwise_ok, dw_conv2d
 from .pool import (avg_pool2d, max_pool2d, adaptive_avg_pool2d, convert_pooling, AvgPool2d, MaxPool2d,
                    AdaptiveAvgPool2d)
 from .tapconv import TapConv2d, convert_tap_convs, tap_conv2d, tapconv_ok
+from .dilated import DilatedGroupConv2d, convert_dilated_group_convs, dilated_group_conv2d, dilated_group_ok
 from .optim import FusedAdam, FusedAdamW, FusedSGD
 from .conv import conv_ok, conv_bn_stats, conv_bn_act_eval, conv_bn_act, conv_forward
 
@@ -29,6 +30,7 @@ __all__ = [
     "DepthwiseConv2d", "convert_depthwise", "depthwise_ok", "dw_conv2d",
     "avg_pool2d", "max_pool2d", "adaptive_avg_pool2d", "convert_pooling", "AvgPool2d", "MaxPool2d",
     "AdaptiveAvgPool2d", "TapConv2d", "convert_tap_convs", "tap_conv2d", "tapconv_ok",
+    "DilatedGroupConv2d", "convert_dilated_group_convs", "dilated_group_conv2d", "dilated_group_ok",
     "FusedSGD", "FusedAdam", "FusedAdamW", "conv_ok", "conv_bn_stats", "conv_bn_act_eval", "conv_bn_act", "conv_forward",
     "bn_act", "bn_act_code", "bn_fused_ok", "convert_batchnorm", "FusedBatchNorm2d", "FusedSyncBatchNorm",
 ]

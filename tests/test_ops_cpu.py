@@ -175,3 +175,33 @@ def test_tap_conv_converted_only_in_cfpnet_like_layers_cpu():
     assert n > 0
     keys = set(m.state_dict())
     assert any(k.endswith("block1.0.0.weight") for k in keys)
+
+
+@pytest.mark.parametrize("hw,d,groups", [((20, 24), (2, 2), 4), ((19, 23), (3, 5), 2), ((17, 16), (14, 14), 8)])
+def test_dilated_group_conv_space_to_batch_cpu(hw, d, groups):
+    """ops/dilated.py: space-to-batch grouped conv == dilated grouped F.conv2d (values, grads)."""
+    import torch.nn.functional as F
+    from realtime_semantic_segmentation_pytorch_amd.ops import dilated_group_conv2d, dilated_group_ok
+
+    torch.manual_seed(0)
+    conv = torch.nn.Conv2d(32, 32, 3, padding=d, dilation=d, groups=groups, bias=True).double()
+    assert dilated_group_ok(conv)
+    x = torch.randn(2, 32, *hw, dtype=torch.float64).requires_grad_(True)
+    ref = F.conv2d(x, conv.weight, conv.bias, 1, d, d, groups)
+    got = dilated_group_conv2d(x, conv.weight, conv.bias, d, groups)
+    torch.testing.assert_close(got, ref)
+    g = torch.randn_like(ref)
+    r = torch.autograd.grad(ref, (x, conv.weight, conv.bias), g)
+    q = torch.autograd.grad(got, (x, conv.weight, conv.bias), g)
+    for a, b in zip(q, r):
+        torch.testing.assert_close(a, b)
+
+
+def test_dilated_group_conv_converted_in_regseg_cpu():
+    from realtime_semantic_segmentation_pytorch_amd.configs import BaseConfig
+    from realtime_semantic_segmentation_pytorch_amd.models import get_model
+    from realtime_semantic_segmentation_pytorch_amd.ops import DilatedGroupConv2d
+
+    c = BaseConfig()
+    c.model, c.num_class = "regseg", 19
+    assert any(type(x) is DilatedGroupConv2d for x in get_model(c).modules())
