@@ -103,8 +103,12 @@ def get_parser() -> argparse.ArgumentParser:
 
 
 def load_parser(config, argv=None):
-    """Overlay every explicitly-given CLI flag onto ``config``."""
-    args, _unknown = get_parser().parse_known_args(argv)
+    """Overlay every explicitly-given CLI flag onto ``config``.  An unknown or misspelled flag
+    is an error (argparse exits with usage), never silently ignored."""
+    parser = get_parser()
+    args, unknown = parser.parse_known_args(argv)
+    if unknown:
+        parser.error(f"unrecognized arguments: {' '.join(unknown)}")
     for k, v in vars(args).items():
         if v is None:
             continue

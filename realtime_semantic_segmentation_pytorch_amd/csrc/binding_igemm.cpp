@@ -1,0 +1,134 @@
+// torch.library registration of the 32x32x16-MFMA implicit-GEMM conv family (conv_igemm.hip):
+// forward (+ BN statistics / inference BN epilogue), data gradient and weight gradient.
+#include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <torch/library.h>
+
+#include "rtseg_launch.h"
+#include "rtseg_ops.h"
+
+namespace rtseg {
+namespace {
+
+void check_act(const at::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.dim() == 4 && t.scalar_type() == at::kBFloat16 &&
+                  t.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+              "rtseg.conv_igemm: ", what, " must be a 16-byte aligned channels-last bf16 GPU tensor");
+}
+
+ConvGeom geom(int64_t N, int64_t Cin, int64_t H, int64_t W, int64_t Cout, int64_t KH, int64_t KW,
+              at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation) {
+  TORCH_CHECK(stride.size() == 2 && padding.size() == 2 && dilation.size() == 2, "rtseg.conv_igemm: 2-D geometry");
+  ConvGeom g{};
+  g.n = static_cast<int>(N); g.cin = static_cast<int>(Cin); g.h = static_cast<int>(H); g.w_in = static_cast<int>(W);
+  g.cout = static_cast<int>(Cout); g.kh = static_cast<int>(KH); g.kw = static_cast<int>(KW);
+  g.sh = static_cast<int>(stride[0]); g.sw = static_cast<int>(stride[1]);
+  g.ph = static_cast<int>(padding[0]); g.pw = static_cast<int>(padding[1]);
+  g.dh = static_cast<int>(dilation[0]); g.dw = static_cast<int>(dilation[1]);
+  TORCH_CHECK(g.sh >= 1 && g.sw >= 1 && g.dh >= 1 && g.dw >= 1 && g.ph >= 0 && g.pw >= 0,
+              "rtseg.conv_igemm: bad geometry");
+  g.ho = static_cast<int>((H + 2 * padding[0] - dilation[0] * (KH - 1) - 1) / stride[0] + 1);
+  g.wo = static_cast<int>((W + 2 * padding[1] - dilation[1] * (KW - 1) - 1) / stride[1] + 1);
+  TORCH_CHECK(g.ho > 0 && g.wo > 0, "rtseg.conv_igemm: empty output");
+  TORCH_CHECK(N * H * W < (int64_t{1} << 31) && N * g.ho * g.wo < (int64_t{1} << 31) &&
+                  H * W * std::max(Cin, Cout) < (int64_t{1} << 31),
+              "rtseg.conv_igemm: problem too large for 32-bit pixel indexing");
+  return g;
+}
+
+// x [N,Cin,H,W] CL bf16, wk [Cout,KH,KW,Cin] bf16 -> (y CL bf16, BN statistics slab or empty)
+std::tuple<at::Tensor, at::Tensor> conv_igemm(const at::Tensor& x, const at::Tensor& wk, at::IntArrayRef stride,
+                                              at::IntArrayRef padding, at::IntArrayRef dilation, bool stats,
+                                              const std::optional<at::Tensor>& scale_shift,
+                                              const std::optional<at::Tensor>& residual, int64_t act) {
+  check_act(x, "input");
+  TORCH_CHECK(wk.is_cuda() && wk.dim() == 4 && wk.scalar_type() == at::kBFloat16 && wk.is_contiguous() &&
+                  wk.size(3) == x.size(1),
+              "rtseg.conv_igemm: weights must be contiguous bf16 [Cout, KH, KW, Cin]");
+  TORCH_CHECK(act >= 0 && act <= 2, "rtseg.conv_igemm: bad activation");
+  ConvGeom g = geom(x.size(0), x.size(1), x.size(2), x.size(3), wk.size(0), wk.size(1), wk.size(2), stride, padding,
+                    dilation);
+  TORCH_CHECK(conv_igemm_supported(g, 0), "rtseg.conv_igemm: needs Cin % 64 == 0, Cout % 8 == 0, <= 49 taps");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  at::Tensor y = at::empty({g.n, g.cout, g.ho, g.wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  g.x = x.data_ptr(); g.w = wk.data_ptr(); g.y = y.data_ptr();
+  g.part = nullptr; g.scale_shift = nullptr; g.res = nullptr; g.act = static_cast<int>(act);
+  at::Tensor part;
+  if (stats) {
+    part = at::empty({conv_igemm_slabs(g), 2 * g.cout}, x.options().dtype(at::kFloat));
+    g.part = part.data_ptr<float>();
+  }
+  if (scale_shift.has_value() && scale_shift->defined()) {
+    TORCH_CHECK(!stats, "rtseg.conv_igemm: statistics and the inference BN epilogue are exclusive");
+    TORCH_CHECK(scale_shift->scalar_type() == at::kFloat && scale_shift->is_contiguous() &&
+                    scale_shift->numel() == 2 * g.cout && scale_shift->is_cuda(),
+                "rtseg.conv_igemm: scale_shift must be fp32 [2*Cout]");
+    g.scale_shift = scale_shift->data_ptr<float>();
+    if (residual.has_value() && residual->defined()) {
+      check_act(*residual, "residual");
+      TORCH_CHECK(residual->sizes() == y.sizes(), "rtseg.conv_igemm: residual must match the output");
+      g.res = residual->data_ptr();
+    }
+  } else {
+    TORCH_CHECK(!(residual.has_value() && residual->defined()) && act == 0,
+                "rtseg.conv_igemm: residual / activation need the BN epilogue (scale_shift)");
+  }
+  launch_conv_igemm_fwd(g, cur_stream());
+  return {y, part};
+}
+
+// dy [N,Cout,Ho,Wo] CL bf16, wt [Cin,KH,KW,Cout] bf16 -> dx [N,Cin,H,W] CL bf16
+at::Tensor conv_igemm_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
+                            at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation) {
+  check_act(dy, "grad_output");
+  TORCH_CHECK(x_size.size() == 4, "rtseg.conv_igemm_dgrad: x_size must be [N, Cin, H, W]");
+  TORCH_CHECK(wt.is_cuda() && wt.dim() == 4 && wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() &&
+                  wt.size(0) == x_size[1] && wt.size(3) == dy.size(1),
+              "rtseg.conv_igemm_dgrad: weights must be contiguous bf16 [Cin, KH, KW, Cout]");
+  ConvGeom g = geom(x_size[0], x_size[1], x_size[2], x_size[3], dy.size(1), wt.size(1), wt.size(2), stride, padding,
+                    dilation);
+  TORCH_CHECK(g.ho == dy.size(2) && g.wo == dy.size(3) && g.n == dy.size(0),
+              "rtseg.conv_igemm_dgrad: grad_output does not match the geometry");
+  TORCH_CHECK(conv_igemm_supported(g, 1), "rtseg.conv_igemm_dgrad: needs Cout % 64 == 0, Cin % 8 == 0");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  at::Tensor dx = at::empty({g.n, g.cin, g.h, g.w_in}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  g.x = dy.data_ptr(); g.w = wt.data_ptr(); g.y = dx.data_ptr();
+  launch_conv_igemm_dgrad(g, cur_stream());
+  return dx;
+}
+
+// x [N,Cin,H,W], dy [N,Cout,Ho,Wo] (CL bf16) -> dw fp32 [Cout,Cin,KH,KW]
+at::Tensor conv_igemm_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t kh, int64_t kw,
+                            at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation) {
+  check_act(x, "input");
+  check_act(dy, "grad_output");
+  ConvGeom g = geom(x.size(0), x.size(1), x.size(2), x.size(3), dy.size(1), kh, kw, stride, padding, dilation);
+  TORCH_CHECK(g.ho == dy.size(2) && g.wo == dy.size(3) && g.n == dy.size(0),
+              "rtseg.conv_igemm_wgrad: grad_output does not match the geometry");
+  TORCH_CHECK(conv_igemm_supported(g, 2), "rtseg.conv_igemm_wgrad: needs Cin % 64 == 0 and Cout % 64 == 0");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  g.x = x.data_ptr(); g.y = dy.data_ptr();
+  at::Tensor ws = at::empty({conv_igemm_wgrad_ws_elems(g)}, x.options().dtype(at::kFloat));
+  at::Tensor dw = at::empty({g.cout, g.cin, g.kh, g.kw}, x.options().dtype(at::kFloat));
+  launch_conv_igemm_wgrad(g, ws.data_ptr<float>(), dw.data_ptr<float>(), cur_stream());
+  return dw;
+}
+
+}  // namespace
+}  // namespace rtseg
+
+TORCH_LIBRARY_FRAGMENT(rtseg, m) {
+  m.def("conv_igemm(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats, "
+        "Tensor? scale_shift, Tensor? residual, int act) -> (Tensor, Tensor)");
+  m.def("conv_igemm_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation) "
+        "-> Tensor");
+  m.def("conv_igemm_wgrad(Tensor x, Tensor dy, int kh, int kw, int[] stride, int[] padding, int[] dilation) "
+        "-> Tensor");
+}
+
+TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
+  m.impl("conv_igemm", &rtseg::conv_igemm);
+  m.impl("conv_igemm_dgrad", &rtseg::conv_igemm_dgrad);
+  m.impl("conv_igemm_wgrad", &rtseg::conv_igemm_wgrad);
+}

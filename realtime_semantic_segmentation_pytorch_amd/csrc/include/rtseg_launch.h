@@ -152,6 +152,21 @@ struct ConvGeom {
 int conv_mfma_slabs(const ConvGeom& g);
 void launch_conv_mfma(const ConvGeom& g, hipStream_t st);
 
+// ---- conv_igemm.hip -----------------------------------------------------------
+// 32x32x16-MFMA implicit-GEMM conv family (ConvGeom always describes the FORWARD conv).
+// mode 0 = forward, 1 = data gradient, 2 = weight gradient.
+constexpr int kIgemmMaxTaps = 49;
+bool conv_igemm_supported(const ConvGeom& g, int mode);
+// rows of the BN statistics slab [rows, 2*Cout] written by the forward when g.part != nullptr
+int conv_igemm_slabs(const ConvGeom& g);
+void launch_conv_igemm_fwd(const ConvGeom& g, hipStream_t st);
+// g.x = dy [N,Ho,Wo,Cout], g.w = [Cin][KH][KW][Cout] bf16, g.y = dx [N,H,W,Cin]
+void launch_conv_igemm_dgrad(const ConvGeom& g, hipStream_t st);
+// g.x = x [N,H,W,Cin], g.y = dy [N,Ho,Wo,Cout]; ws fp32 of conv_igemm_wgrad_ws_elems(g);
+// dw fp32 [Cout][Cin][KH][KW]
+int64_t conv_igemm_wgrad_ws_elems(const ConvGeom& g);
+void launch_conv_igemm_wgrad(const ConvGeom& g, float* ws, float* dw, hipStream_t st);
+
 // ---- pool.hip -----------------------------------------------------------------
 enum PoolMode : int { kPoolAvg = 0, kPoolMax = 1 };
 struct PoolParams {

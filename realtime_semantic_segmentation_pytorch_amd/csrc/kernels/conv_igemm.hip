@@ -1,0 +1,786 @@
+// Implicit-GEMM convolution family on bf16 MFMA (v_mfma_f32_32x32x16_bf16) for channels-last
+// activations on gfx950: forward, data gradient and weight gradient of every dense conv.
+//
+// Reference sites: every dense conv of the zoo -- ConvBNAct (models/modules.py:73-85), DDRNet's
+// RB / RBB residual blocks (ddrnet.py:168-219), SegHead (modules.py:161-166), DeConvBNAct's
+// ConvTranspose2d (modules.py:89-108) -- which the reference leaves to cuDNN (fwd / bwd-data /
+// bwd-filter) followed by separate BatchNorm passes.
+//
+// ---- igemm_gather_kernel: forward conv, dgrad and transposed conv ---------------------------
+// D[co, m] = sum_{t, c} W[co, wtap[t], c] * X[pix(m, t), c]
+//   m    : a pixel of a "virtual" output grid (N x Hv x Wv); it is written to
+//          y[n, hv*osh + oph, wv*osw + opw, co] (osh = 1, oph = 0 for a plain conv; the
+//          dgrad of a strided conv runs one launch per output phase, sub-pixel style),
+//   t    : an entry of a tap table (dh[t], dw[t], wtap[t]); X's pixel is
+//          (hv*sh + dh[t], wv*sw + dw[t]) -- zero outside the image.
+// A forward conv is tap table {(-p + i*d, wtap = i*KW+j)}; the data gradient of a stride-s
+// conv is, per phase (a, b), the taps with (a + p - i*d) % s == 0 at dh = (a + p - i*d) / s
+// over dy, with weights re-laid-out [Cin][KH][KW][Cout] -- the same kernel, no col2im.
+//
+//  * block tile: BN output channels (MFMA A operand = weights) x BM pixels (B operand = gathered
+//    activations) x BK = 64 (one tap, 64 channels) per K-step; 8 waves (WN x WM), each a
+//    (BN/WN) x (BM/WM) sub-tile of 32 x 32 MFMA tiles (the 32-row shape halves the LDS fragment
+//    reads per FLOP against 16x16x32);
+//  * operands go global -> LDS by LDS-DMA (global_load_lds_dwordx4, per-lane source address =
+//    the gather), 128-byte LDS rows with chunk c of row r at c ^ ((r >> 1) & 7) (source-side
+//    swizzle), which makes every ds_read_b128 fragment read conflict-free;
+//  * a persistent, XCD-contiguous tile walk with ONE flat DMA stream across tiles: the NST-stage
+//    ring keeps NST-1 K-steps in flight across tile boundaries, published by a counted vmcnt +
+//    raw s_barrier (never vmcnt(0) inside the stream);
+//  * epilogue straight from the accumulators (D rows = channels: each lane owns 4 consecutive
+//    channels of one pixel per register quad -> 8-byte stores), packed at the end of a tile and
+//    stored after the next K-step's barrier so the stores never sit in front of a DMA wait;
+//    optional per-channel (sum, sum of squares) of the bf16 outputs for training BatchNorm
+//    (one [2*Cout] slab row per block), or the inference BN scale/shift + residual + ReLU(6).
+//
+// ---- igemm_wgrad_kernel: weight gradient ----------------------------------------------------
+// D[co, (t, ci)] = sum_m dy[m, co] * x[pix(m, t), ci]: K = pixels.  Both operands are staged as
+// [64 pixels][64 channels] sub-tiles (one DMA stream, the x side gathered per tap) and read
+// with ds_read_b64_tr_b16 (the hardware transpose delivers 4 consecutive pixels per lane),
+// chunk swizzle c ^ (((r >> 1) & 1) << 2) makes those reads conflict-free.  The pixel range is
+// split over blocks (split-K); fp32 partial tiles go to a slab that igemm_wgrad_reduce sums
+// (deterministic, no atomics) into the [Cout][Cin][KH][KW] fp32 weight gradient.
+#include "rtseg_common.h"
+#include "rtseg_launch.h"
+
+#include <algorithm>
+#include <cstdlib>
+
+namespace rtseg {
+
+namespace {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+typedef short i16x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+
+constexpr int kMaxTaps = kIgemmMaxTaps;
+
+// 64 zero bytes: the DMA source of padding taps / rows past the edge
+__device__ uint4 g_igemm_zero[4];
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt immediate");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const void*)p));
+}
+
+// LDS-DMA from inline asm (opaque to hipcc's waitcnt pass, which would otherwise drain vmcnt(0)
+// before every later ds_read): 64 lanes x 16 B land at M0 + 16 * lane.
+// M0 is compiler-reserved, so the statement saves and restores it around the DMA.
+__device__ __forceinline__ void dma16(const void* src, uint32_t lds_dst) {
+  const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_dst);
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(dst)
+      : "memory");
+}
+
+// Tap table entry: dh (10-bit signed) | dw (10-bit signed) << 10 | weight tap (12-bit) << 20.
+// int32 (not short[]) because SMEM loads are dword-only on gfx950: a 16-bit table entry read
+// with a uniform index becomes a VMEM load whose s_waitcnt would also drain the DMA ring.
+__host__ __device__ inline int pack_tap(int dh, int dw, int wt) {
+  return (dh & 0x3ff) | ((dw & 0x3ff) << 10) | (wt << 20);
+}
+__device__ __forceinline__ int tap_dh(int v) { return (v << 22) >> 22; }
+__device__ __forceinline__ int tap_dw(int v) { return (v << 12) >> 22; }
+__device__ __forceinline__ int tap_wt(int v) { return static_cast<int>(static_cast<unsigned>(v) >> 20); }
+
+__device__ __forceinline__ bf16x8_t as_frag(uint4 v) { return __builtin_bit_cast(bf16x8_t, v); }
+
+__device__ __forceinline__ float epi_act(float v, int act) {
+  if (act == kActReLU) return fmaxf(v, 0.f);
+  if (act == kActReLU6) return fminf(fmaxf(v, 0.f), 6.f);
+  return v;
+}
+
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  return static_cast<uint32_t>(f32_to_bf16(lo)) | (static_cast<uint32_t>(f32_to_bf16(hi)) << 16);
+}
+
+// Bijective block -> logical id map that gives each XCD (blockIdx % 8 under round-robin
+// dispatch) a contiguous range of logical ids: neighbouring tiles share L2.  Speed only.
+__device__ __forceinline__ int xcd_logical(int b, int G) {
+  const int q = G / 8, r = G % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+struct IgArgs {
+  const uint16_t* x;
+  const uint16_t* w;
+  uint16_t* y;
+  float* part;
+  const float* ss;
+  const uint16_t* res;
+  int act;
+  int H, W, C;            // gathered operand [N][H][W][C]
+  int Hv, Wv;             // virtual output grid
+  int Ho, Wo, cout;       // output tensor [N][Ho][Wo][cout]
+  int osh, osw, oph, opw; // output pixel = (hv*osh + oph, wv*osw + opw)
+  int sh, sw;             // input pixel = (hv*sh + dh[t], wv*sw + dw[t])
+  int wrow;               // weight row stride (elements) = KT * C
+  int ntap, cch, nk;      // taps, 64-channel chunks per tap, K-steps per tile
+  int M, mtiles, ntiles;
+  FastDiv fwv, fhv;
+  int taps[kMaxTaps];     // packed tap: see pack_tap (32-bit so the scalar unit can load it)
+};
+
+template <int BM, int BN, int WM, int WN, int NST, int EPI, bool STATS>
+__global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs a) {
+  constexpr int NW = WM * WN;
+  constexpr int TI = BN / WN / 32;  // 32-channel MFMA tiles per wave
+  constexpr int TJ = BM / WM / 32;  // 32-pixel MFMA tiles per wave
+  constexpr int STAGE = (BN + BM) * 8;  // 16-byte chunks per ring stage
+  constexpr int WI = BN / 8 / NW, PI = BM / 8 / NW;  // DMA instructions per wave per stage
+  static_assert(TI >= 1 && TJ >= 1 && TI * WN * 32 == BN && TJ * WM * 32 == BM, "wave tiling");
+  static_assert(WI >= 1 && PI >= 1 && WI * NW * 8 == BN && PI * NW * 8 == BM, "DMA tiling");
+  static_assert(NST >= 2 && NST <= 4, "ring depth");
+  constexpr int PER = WI + PI;
+  __shared__ uint4 lds[NST * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wid % WN, wm = wid / WN;
+  const int G = gridDim.x;
+  const int lb = xcd_logical(blockIdx.x, G);
+  const int ntile = lb % a.ntiles;
+  const int co0 = ntile * BN;
+  const int mstep = G / a.ntiles;
+  const int mfirst = lb / a.ntiles;
+  const int my_tiles = mfirst < a.mtiles ? (a.mtiles - mfirst + mstep - 1) / mstep : 0;
+  const int nk = a.nk;
+
+  // ---- DMA geometry: instruction I fills 8 rows (I*8 + lane/8) x 8 chunks of one operand
+  const int lr8 = lane >> 3, lch = lane & 7;
+  const uint16_t* wsrc[WI];
+  bool wok[WI];
+#pragma unroll
+  for (int e = 0; e < WI; ++e) {
+    const int row = (wid * WI + e) * 8 + lr8;
+    const int lc = lch ^ ((row >> 1) & 7);
+    const int co = co0 + row;
+    wok[e] = co < a.cout;
+    wsrc[e] = a.w + static_cast<int64_t>(min(co, a.cout - 1)) * a.wrow + lc * 8;
+  }
+  int plc[PI];
+#pragma unroll
+  for (int e = 0; e < PI; ++e) {
+    const int row = (wid * PI + e) * 8 + lr8;
+    plc[e] = lch ^ ((row >> 1) & 7);
+  }
+  const uint16_t* pbase[PI];
+  int phb[PI], pwb[PI];
+  auto set_rows = [&](int mt) {
+#pragma unroll
+    for (int e = 0; e < PI; ++e) {
+      const int m = mt * BM + (wid * PI + e) * 8 + lr8;
+      const bool ok = m < a.M;
+      uint32_t wv, hv;
+      const uint32_t t = a.fwv.divmod(static_cast<uint32_t>(ok ? m : 0), wv);
+      const uint32_t n = a.fhv.divmod(t, hv);
+      phb[e] = ok ? static_cast<int>(hv) * a.sh : -(1 << 28);
+      pwb[e] = static_cast<int>(wv) * a.sw;
+      pbase[e] = a.x + static_cast<int64_t>(n) * a.H * a.W * a.C + plc[e] * 8;
+    }
+  };
+
+  // staging cursor (wave-uniform): tile ordinal, tap, channel chunk
+  int st_ord = 0, st_t = 0, st_c = 0, st_buf = 0;
+  auto stage = [&]() {
+    // uniform indices -> scalar (SMEM) tap-table loads: a VGPR-indexed kernarg load is a VMEM
+    // load whose s_waitcnt vmcnt(0) would drain the whole DMA ring every K-step
+    const int tv = a.taps[__builtin_amdgcn_readfirstlane(st_t)];
+    const int dh = tap_dh(tv), dw = tap_dw(tv);
+    const int c0 = __builtin_amdgcn_readfirstlane(st_c) * 64;
+    const int woff = tap_wt(tv) * a.C + c0;
+    const uint32_t base = lds_addr(lds + st_buf * STAGE);
+#pragma unroll
+    for (int e = 0; e < WI; ++e) {
+      const void* src = wok[e] ? static_cast<const void*>(wsrc[e] + woff) : static_cast<const void*>(g_igemm_zero);
+      dma16(src, base + (wid * WI + e) * 1024);
+    }
+#pragma unroll
+    for (int e = 0; e < PI; ++e) {
+      const int hi = phb[e] + dh, wi = pwb[e] + dw;
+      const bool ok = static_cast<unsigned>(hi) < static_cast<unsigned>(a.H) &&
+                      static_cast<unsigned>(wi) < static_cast<unsigned>(a.W);
+      const uint16_t* s = pbase[e] + static_cast<int64_t>(hi * a.W + wi) * a.C + c0;
+      dma16(ok ? static_cast<const void*>(s) : static_cast<const void*>(g_igemm_zero),
+            base + BN * 128 + (wid * PI + e) * 1024);
+    }
+    if (++st_buf == NST) st_buf = 0;
+    if (++st_c == a.cch) {
+      st_c = 0;
+      if (++st_t == a.ntap) {
+        st_t = 0;
+        if (++st_ord < my_tiles) set_rows(mfirst + st_ord * mstep);
+      }
+    }
+  };
+
+  // ---- fragment read geometry (ds_read_b128, conflict-free by the chunk swizzle)
+  const int frow = lane & 31, fhi = lane >> 5, fx = (lane >> 1) & 7;
+
+  f32x16_t acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  float csum[STATS ? TI : 1][16], csq[STATS ? TI : 1][16];
+  if constexpr (STATS) {
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { csum[i][r] = 0.f; csq[i][r] = 0.f; }
+  }
+
+  // pending (packed bf16) output of the previous tile, stored after the next barrier
+  uint2 pend[TI][TJ][4];
+  int64_t pend_off[TJ];
+  bool pend_ok[TJ];
+  bool have_pend = false;
+  const int co_lane = co0 + wn * (BN / WN) + 4 * fhi;  // + ti*32 + 8g
+
+  auto pack_tile = [&](int mt) {
+#pragma unroll
+    for (int tj = 0; tj < TJ; ++tj) {
+      const int m = mt * BM + wm * (BM / WM) + tj * 32 + frow;
+      const bool ok = m < a.M;
+      uint32_t wv, hv;
+      const uint32_t t = a.fwv.divmod(static_cast<uint32_t>(ok ? m : 0), wv);
+      const uint32_t n = a.fhv.divmod(t, hv);
+      const int ho = static_cast<int>(hv) * a.osh + a.oph, wo = static_cast<int>(wv) * a.osw + a.opw;
+      pend_ok[tj] = ok;
+      pend_off[tj] = ((static_cast<int64_t>(n) * a.Ho + ho) * a.Wo + wo) * a.cout;
+#pragma unroll
+      for (int ti = 0; ti < TI; ++ti) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int co = co_lane + ti * 32 + 8 * g;
+          float v[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = acc[ti][tj][4 * g + q];
+          if constexpr (EPI == 1) {
+            const int cc = min(co, a.cout - 4);
+            const float4 sc = *reinterpret_cast<const float4*>(a.ss + cc);
+            const float4 sf = *reinterpret_cast<const float4*>(a.ss + a.cout + cc);
+            v[0] = fmaf(v[0], sc.x, sf.x); v[1] = fmaf(v[1], sc.y, sf.y);
+            v[2] = fmaf(v[2], sc.z, sf.z); v[3] = fmaf(v[3], sc.w, sf.w);
+            if (a.res != nullptr && ok && co < a.cout) {
+              const uint2 r = *reinterpret_cast<const uint2*>(a.res + pend_off[tj] + co);
+              v[0] += bf16_to_f32(static_cast<uint16_t>(r.x & 0xffff));
+              v[1] += bf16_to_f32(static_cast<uint16_t>(r.x >> 16));
+              v[2] += bf16_to_f32(static_cast<uint16_t>(r.y & 0xffff));
+              v[3] += bf16_to_f32(static_cast<uint16_t>(r.y >> 16));
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = epi_act(v[q], a.act);
+          }
+          uint2 pk;
+          pk.x = pack2(v[0], v[1]);
+          pk.y = pack2(v[2], v[3]);
+          pend[ti][tj][g] = pk;
+          if constexpr (STATS) {
+            const bool sok = ok && co < a.cout;
+            const float q0 = sok ? bf16_to_f32(static_cast<uint16_t>(pk.x & 0xffff)) : 0.f;
+            const float q1 = sok ? bf16_to_f32(static_cast<uint16_t>(pk.x >> 16)) : 0.f;
+            const float q2 = sok ? bf16_to_f32(static_cast<uint16_t>(pk.y & 0xffff)) : 0.f;
+            const float q3 = sok ? bf16_to_f32(static_cast<uint16_t>(pk.y >> 16)) : 0.f;
+            csum[ti][4 * g + 0] += q0; csq[ti][4 * g + 0] += q0 * q0;
+            csum[ti][4 * g + 1] += q1; csq[ti][4 * g + 1] += q1 * q1;
+            csum[ti][4 * g + 2] += q2; csq[ti][4 * g + 2] += q2 * q2;
+            csum[ti][4 * g + 3] += q3; csq[ti][4 * g + 3] += q3 * q3;
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[ti][tj][r] = 0.f;
+      }
+    }
+  };
+  auto store_pending = [&]() {
+#pragma unroll
+    for (int tj = 0; tj < TJ; ++tj) {
+      if (!pend_ok[tj]) continue;
+#pragma unroll
+      for (int ti = 0; ti < TI; ++ti)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int co = co_lane + ti * 32 + 8 * g;
+          if (co < a.cout) *reinterpret_cast<uint2*>(a.y + pend_off[tj] + co) = pend[ti][tj][g];
+        }
+    }
+  };
+
+  const int total = my_tiles * nk;
+  if (nk == 0) {  // empty tap set (a dgrad phase no tap reaches): the outputs are zero
+    for (int i = 0; i < my_tiles; ++i) {
+      pack_tile(mfirst + i * mstep);
+      store_pending();
+    }
+  } else {
+    if (my_tiles > 0) set_rows(mfirst);
+#pragma unroll
+    for (int p = 0; p < NST - 1; ++p)
+      if (p < total) stage();
+
+    int kk = 0, ord = 0, buf = 0;
+    for (int gs = 0; gs < total; ++gs) {
+      if (NST >= 3 && gs + 1 < total) {
+        vm_wait<(NST - 2) * PER>();
+      } else {
+        vm_wait<0>();
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // step gs landed for every wave; step gs-1's buffer is free
+      if (have_pend) {
+        store_pending();
+        have_pend = false;
+      }
+      if (gs + NST - 1 < total) stage();
+
+      const uint4* Wt = lds + buf * STAGE + (wn * (BN / WN) + frow) * 8;
+      const uint4* Pt = lds + buf * STAGE + BN * 8 + (wm * (BM / WM) + frow) * 8;
+      // fragments of sub-step s+1 are read while the MFMAs of sub-step s run
+      bf16x8_t af[2][TI], bfg[2][TJ];
+      auto load_frags = [&](int s, int slot) {
+        const int ch = ((2 * s + fhi) ^ fx);
+#pragma unroll
+        for (int ti = 0; ti < TI; ++ti) af[slot][ti] = as_frag(Wt[ti * 256 + ch]);
+#pragma unroll
+        for (int tj = 0; tj < TJ; ++tj) bfg[slot][tj] = as_frag(Pt[tj * 256 + ch]);
+      };
+      load_frags(0, 0);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        if (s < 3) load_frags(s + 1, (s + 1) & 1);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int ti = 0; ti < TI; ++ti)
+#pragma unroll
+          for (int tj = 0; tj < TJ; ++tj)
+            acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s & 1][ti], bfg[s & 1][tj], acc[ti][tj], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+      if (++buf == NST) buf = 0;
+      if (++kk == nk) {
+        kk = 0;
+        pack_tile(mfirst + ord * mstep);
+        ++ord;
+        have_pend = true;
+      }
+    }
+    if (have_pend) store_pending();
+  }
+
+  if constexpr (STATS) {
+    // per-channel sums: lanes l and l^k (k < 32) hold the same channels for different pixels
+#pragma unroll
+    for (int ti = 0; ti < TI; ++ti)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+          csum[ti][r] += __shfl_xor(csum[ti][r], o, kWave);
+          csq[ti][r] += __shfl_xor(csq[ti][r], o, kWave);
+        }
+      }
+    vm_wait<0>();
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(lds);  // [WM][BN][2]
+    if (frow == 0) {
+#pragma unroll
+      for (int ti = 0; ti < TI; ++ti)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int col = wn * (BN / WN) + ti * 32 + (r & 3) + 8 * (r >> 2) + 4 * fhi;
+          red[(wm * BN + col) * 2] = csum[ti][r];
+          red[(wm * BN + col) * 2 + 1] = csq[ti][r];
+        }
+    }
+    __syncthreads();
+    for (int col = tid; col < BN; col += NW * 64) {
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        s1 += red[(w * BN + col) * 2];
+        s2 += red[(w * BN + col) * 2 + 1];
+      }
+      const int co = co0 + col;
+      if (co < a.cout) {
+        float* prow = a.part + static_cast<int64_t>(mfirst) * 2 * a.cout;
+        prow[co] = s1;
+        prow[a.cout + co] = s2;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------- wgrad
+struct WgArgs {
+  const uint16_t* x;
+  const uint16_t* dy;
+  float* ws;
+  int H, W, C, Ho, Wo, cout, sh, sw;
+  int kp;          // KT * C (GEMM N)
+  int M, ksteps, steps_per_split;
+  int ntiles, tiles;
+  FastDiv fwo, fho;
+  int taps[kMaxTaps];  // pack_tap(dh, dw, tap)
+};
+
+// transposed 4 x bf16 read: lane (within its 16-lane group) 4q+p supplies row q, columns 4p..4p+3
+__device__ __forceinline__ i16x4_t tr_read(const uint4* base, int byte_off) {
+  auto p = (__attribute__((address_space(3))) i16x4_t*)(
+      (__attribute__((address_space(3))) char*)((__attribute__((address_space(3))) void*)base) + byte_off);
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(p);
+}
+
+template <int MS, int NS, int WM, int WN, int NST>
+__global__ void __launch_bounds__(WM* WN * 64) igemm_wgrad_kernel(const WgArgs a) {
+  constexpr int NW = WM * WN;
+  static_assert(NW == 8, "one DMA row group per wave");
+  constexpr int SUB = 512;  // 16-byte chunks per [64][64] bf16 sub-tile
+  constexpr int STAGE = (MS + NS) * SUB;
+  constexpr int BMc = MS * 64, BNk = NS * 64;
+  constexpr int TI = BMc / WM / 32, TJ = BNk / WN / 32;
+  static_assert(TI >= 1 && TJ >= 1 && TI * WM * 32 == BMc && TJ * WN * 32 == BNk, "wave tiling");
+  constexpr int PER = MS + NS;  // DMA instructions per wave per stage
+  __shared__ uint4 lds[NST * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int lb = xcd_logical(blockIdx.x, gridDim.x);
+  const int split = lb / a.tiles, tile = lb % a.tiles;
+  const int co0 = (tile / a.ntiles) * BMc, kp0 = (tile % a.ntiles) * BNk;
+  const int s0 = split * a.steps_per_split;
+  const int s1 = min(s0 + a.steps_per_split, a.ksteps);
+  const int nsteps = max(s1 - s0, 0);
+
+  // DMA: wave w fills row group w (rows 8w .. 8w+7) of every sub-tile; lane -> row, chunk
+  const int row = wid * 8 + (lane >> 3);
+  const int lc = (lane & 7) ^ (((row >> 1) & 1) << 2);
+  int aoff[MS];
+#pragma unroll
+  for (int s = 0; s < MS; ++s) aoff[s] = co0 + s * 64 + lc * 8;
+  int bdh[NS], bdw[NS], boff[NS];
+  bool bok[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int kb = kp0 + s * 64;
+    bok[s] = kb < a.kp;
+    const int t = __builtin_amdgcn_readfirstlane(bok[s] ? kb / a.C : 0);  // scalar table loads
+    const int tv = a.taps[t];
+    bdh[s] = tap_dh(tv);
+    bdw[s] = tap_dw(tv);
+    boff[s] = (bok[s] ? kb - t * a.C : 0) + lc * 8;
+  }
+  auto stage = [&](int step, int buf) {
+    const int m = step * 64 + row;
+    const bool mok = m < a.M;
+    uint32_t wo, ho;
+    const uint32_t t = a.fwo.divmod(static_cast<uint32_t>(mok ? m : 0), wo);
+    const uint32_t n = a.fho.divmod(t, ho);
+    const uint16_t* ximg = a.x + static_cast<int64_t>(n) * a.H * a.W * a.C;
+    const uint32_t base = lds_addr(lds + buf * STAGE) + wid * 1024;
+#pragma unroll
+    for (int s = 0; s < MS; ++s) {
+      const void* src = mok ? static_cast<const void*>(a.dy + static_cast<int64_t>(m) * a.cout + aoff[s])
+                            : static_cast<const void*>(g_igemm_zero);
+      dma16(src, base + s * SUB * 16);
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int hi = static_cast<int>(ho) * a.sh + bdh[s], wi = static_cast<int>(wo) * a.sw + bdw[s];
+      const bool ok = mok && bok[s] && static_cast<unsigned>(hi) < static_cast<unsigned>(a.H) &&
+                      static_cast<unsigned>(wi) < static_cast<unsigned>(a.W);
+      const uint16_t* src = ximg + static_cast<int64_t>(hi * a.W + wi) * a.C + boff[s];
+      dma16(ok ? static_cast<const void*>(src) : static_cast<const void*>(g_igemm_zero),
+            base + (MS + s) * SUB * 16);
+    }
+  };
+
+  // transposed fragment reads: lane -> (row q within the 4-row block, column 4p), group g16
+  const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4, g16 = (lane >> 4) & 1, hh = lane >> 5;
+  const int swz = ((q >> 1) & 1) << 2;
+  auto frag = [&](const uint4* sub, int col0, int k0) -> bf16x8_t {
+    // col0: first of the 32 columns of this MFMA operand tile within the [64][64] sub-tile
+    const int col = col0 + g16 * 16 + p4;
+    const int ch = ((col >> 3) ^ swz);
+    const int half = (col >> 2) & 1;
+    const int r0 = k0 + hh * 8 + q;
+    const i16x4_t lo = tr_read(sub, r0 * 128 + ch * 16 + half * 8);
+    const i16x4_t hi = tr_read(sub, (r0 + 4) * 128 + ch * 16 + half * 8);
+    return __builtin_shufflevector(__builtin_bit_cast(bf16x4_t, lo), __builtin_bit_cast(bf16x4_t, hi), 0, 1, 2,
+                                   3, 4, 5, 6, 7);
+  };
+
+  f32x16_t acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+#pragma unroll
+  for (int pp = 0; pp < NST - 1; ++pp)
+    if (pp < nsteps) stage(s0 + pp, pp);
+  int buf = 0;
+  for (int k = 0; k < nsteps; ++k) {
+    if (NST >= 3 && k + 1 < nsteps) {
+      vm_wait<(NST - 2) * PER>();
+    } else {
+      vm_wait<0>();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (k + NST - 1 < nsteps) {
+      int nb = buf + NST - 1;
+      if (nb >= NST) nb -= NST;
+      stage(s0 + k + NST - 1, nb);
+    }
+    const uint4* A = lds + buf * STAGE;
+    const uint4* B = A + MS * SUB;
+    bf16x8_t af[2][TI], bfg[2][TJ];
+    auto load_frags = [&](int s, int slot) {
+#pragma unroll
+      for (int ti = 0; ti < TI; ++ti) {
+        const int c = wm * (BMc / WM) + ti * 32;
+        af[slot][ti] = frag(A + (c >> 6) * SUB, c & 63, s * 16);
+      }
+#pragma unroll
+      for (int tj = 0; tj < TJ; ++tj) {
+        const int c = wn * (BNk / WN) + tj * 32;
+        bfg[slot][tj] = frag(B + (c >> 6) * SUB, c & 63, s * 16);
+      }
+    };
+    load_frags(0, 0);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      if (s < 3) load_frags(s + 1, (s + 1) & 1);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ti = 0; ti < TI; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < TJ; ++tj)
+          acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s & 1][ti], bfg[s & 1][tj], acc[ti][tj], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    if (++buf == NST) buf = 0;
+  }
+
+  // fp32 partial tile -> slab [split][cout][kp]
+  float* slab = a.ws + static_cast<int64_t>(split) * a.cout * a.kp;
+#pragma unroll
+  for (int ti = 0; ti < TI; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < TJ; ++tj) {
+      const int kcol = kp0 + wn * (BNk / WN) + tj * 32 + (lane & 31);
+      if (kcol >= a.kp) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = co0 + wm * (BMc / WM) + ti * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (co < a.cout) slab[static_cast<int64_t>(co) * a.kp + kcol] = acc[ti][tj][r];
+      }
+    }
+}
+
+// dw[co][ci][tap] = sum_s slab[s][co][tap*C + ci]
+__global__ void igemm_wgrad_reduce(const float* __restrict__ ws, float* __restrict__ dw, int splits, int cout,
+                                   int C, int kt) {
+  const int64_t kp = static_cast<int64_t>(kt) * C;
+  const int64_t total = static_cast<int64_t>(cout) * kp;
+  const int64_t plane = total;
+  for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+       e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    float s = 0.f;
+    for (int sp = 0; sp < splits; ++sp) s += ws[sp * plane + e];
+    const int64_t co = e / kp;
+    const int64_t r = e - co * kp;
+    const int64_t t = r / C, ci = r - t * C;
+    dw[(co * C + ci) * kt + t] = s;
+  }
+}
+
+// ------------------------------------------------------------------------------- host side
+struct Cfg {
+  int bm, bn;
+};
+
+Cfg fwd_cfg(int cout) { return cout <= 64 ? Cfg{256, 64} : Cfg{256, 128}; }
+
+int persistent_grid(int mtiles, int ntiles) {
+  const int64_t tiles = static_cast<int64_t>(mtiles) * ntiles;
+  const int cap = std::max(ntiles, (256 / ntiles) * ntiles);
+  return static_cast<int>(tiles < cap ? tiles : cap);
+}
+
+void fill_common(IgArgs& k, const Cfg& c, int n) {
+  k.M = n * k.Hv * k.Wv;
+  k.mtiles = (k.M + c.bm - 1) / c.bm;
+  k.ntiles = (k.cout + c.bn - 1) / c.bn;
+  k.nk = k.ntap * k.cch;
+  k.fwv = FastDiv::make(static_cast<uint32_t>(k.Wv));
+  k.fhv = FastDiv::make(static_cast<uint32_t>(k.Hv));
+}
+
+template <int EPI, bool STATS>
+void launch_cfg(const IgArgs& k, const Cfg& c, int grid, hipStream_t st) {
+  if (c.bn == 64) igemm_gather_kernel<256, 64, 8, 1, 3, EPI, STATS><<<grid, 512, 0, st>>>(k);
+  else igemm_gather_kernel<256, 128, 4, 2, 3, EPI, STATS><<<grid, 512, 0, st>>>(k);
+}
+
+void launch_gather(const IgArgs& k, const Cfg& c, hipStream_t st) {
+  const int grid = persistent_grid(k.mtiles, k.ntiles);
+  if (grid <= 0) return;
+  if (k.ss != nullptr) launch_cfg<1, false>(k, c, grid, st);
+  else if (k.part != nullptr) launch_cfg<0, true>(k, c, grid, st);
+  else launch_cfg<0, false>(k, c, grid, st);
+}
+
+}  // namespace
+
+bool conv_igemm_supported(const ConvGeom& g, int mode) {
+  const int red = mode == 1 ? g.cout : g.cin;  // reduction channels (dgrad: forward Cout)
+  const int outc = mode == 1 ? g.cin : g.cout;
+  if (red % 64 != 0 || outc % 8 != 0) return false;
+  if (g.kh * g.kw > kMaxTaps) return false;
+  if (mode == 2 && (g.cout % 64 != 0)) return false;
+  return true;
+}
+
+int conv_igemm_slabs(const ConvGeom& g) {
+  const Cfg c = fwd_cfg(g.cout);
+  const int64_t M = static_cast<int64_t>(g.n) * g.ho * g.wo;
+  const int mtiles = static_cast<int>((M + c.bm - 1) / c.bm);
+  const int ntiles = (g.cout + c.bn - 1) / c.bn;
+  return persistent_grid(mtiles, ntiles) / ntiles;
+}
+
+void launch_conv_igemm_fwd(const ConvGeom& g, hipStream_t st) {
+  IgArgs k{};
+  k.x = static_cast<const uint16_t*>(g.x);
+  k.w = static_cast<const uint16_t*>(g.w);
+  k.y = static_cast<uint16_t*>(g.y);
+  k.part = g.part;
+  k.ss = g.scale_shift;
+  k.res = static_cast<const uint16_t*>(g.res);
+  k.act = g.act;
+  k.H = g.h; k.W = g.w_in; k.C = g.cin;
+  k.Hv = g.ho; k.Wv = g.wo; k.Ho = g.ho; k.Wo = g.wo; k.cout = g.cout;
+  k.osh = 1; k.osw = 1; k.oph = 0; k.opw = 0; k.sh = g.sh; k.sw = g.sw;
+  k.wrow = g.kh * g.kw * g.cin;
+  k.cch = g.cin / 64;
+  k.ntap = 0;
+  for (int i = 0; i < g.kh; ++i)
+    for (int j = 0; j < g.kw; ++j) {
+      k.taps[k.ntap++] = pack_tap(i * g.dh - g.ph, j * g.dw - g.pw, i * g.kw + j);
+    }
+  const Cfg c = fwd_cfg(g.cout);
+  fill_common(k, c, g.n);
+  launch_gather(k, c, st);
+}
+
+// g: forward geometry; g.x = dy [N,Ho,Wo,Cout], g.w = wt [Cin][KH][KW][Cout], g.y = dx [N,H,W,Cin]
+void launch_conv_igemm_dgrad(const ConvGeom& g, hipStream_t st) {
+  const Cfg c = fwd_cfg(g.cin);
+  for (int a = 0; a < g.sh; ++a)
+    for (int b = 0; b < g.sw; ++b) {
+      IgArgs k{};
+      k.x = static_cast<const uint16_t*>(g.x);
+      k.w = static_cast<const uint16_t*>(g.w);
+      k.y = static_cast<uint16_t*>(g.y);
+      k.H = g.ho; k.W = g.wo; k.C = g.cout;
+      k.Hv = (g.h - a + g.sh - 1) / g.sh;
+      k.Wv = (g.w_in - b + g.sw - 1) / g.sw;
+      if (k.Hv <= 0 || k.Wv <= 0) continue;
+      k.Ho = g.h; k.Wo = g.w_in; k.cout = g.cin;
+      k.osh = g.sh; k.osw = g.sw; k.oph = a; k.opw = b; k.sh = 1; k.sw = 1;
+      k.wrow = g.kh * g.kw * g.cout;
+      k.cch = g.cout / 64;
+      k.ntap = 0;
+      for (int i = 0; i < g.kh; ++i) {
+        const int vh = a + g.ph - i * g.dh;
+        if (((vh % g.sh) + g.sh) % g.sh != 0) continue;
+        for (int j = 0; j < g.kw; ++j) {
+          const int vw = b + g.pw - j * g.dw;
+          if (((vw % g.sw) + g.sw) % g.sw != 0) continue;
+          k.taps[k.ntap++] = pack_tap(vh / g.sh, vw / g.sw, i * g.kw + j);
+        }
+      }
+      fill_common(k, c, g.n);
+      launch_gather(k, c, st);
+    }
+}
+
+namespace {
+struct WgPlan {
+  int ms, ns, ntiles, mtiles, tiles, ksteps, splits, steps_per_split;
+};
+WgPlan wgrad_plan(const ConvGeom& g) {
+  WgPlan p{};
+  p.ms = g.cout % 128 == 0 ? 2 : 1;
+  p.ns = 4;
+  const int kp = g.kh * g.kw * g.cin;
+  p.mtiles = g.cout / (64 * p.ms);
+  p.ntiles = (kp + 64 * p.ns - 1) / (64 * p.ns);
+  p.tiles = p.mtiles * p.ntiles;
+  const int64_t M = static_cast<int64_t>(g.n) * g.ho * g.wo;
+  p.ksteps = static_cast<int>((M + 63) / 64);
+  int splits = std::max(1, 256 / p.tiles);
+  splits = std::min(splits, std::max(1, p.ksteps / 8));  // >= 8 K-steps per split
+  p.steps_per_split = (p.ksteps + splits - 1) / splits;
+  p.splits = (p.ksteps + p.steps_per_split - 1) / p.steps_per_split;
+  return p;
+}
+}  // namespace
+
+int64_t conv_igemm_wgrad_ws_elems(const ConvGeom& g) {
+  const WgPlan p = wgrad_plan(g);
+  return static_cast<int64_t>(p.splits) * g.cout * g.kh * g.kw * g.cin;
+}
+
+// g.x = x [N,H,W,Cin], g.y = dy [N,Ho,Wo,Cout] (bf16); dw fp32 [Cout][Cin][KH][KW]
+void launch_conv_igemm_wgrad(const ConvGeom& g, float* ws, float* dw, hipStream_t st) {
+  const WgPlan p = wgrad_plan(g);
+  WgArgs k{};
+  k.x = static_cast<const uint16_t*>(g.x);
+  k.dy = static_cast<const uint16_t*>(g.y);
+  k.ws = ws;
+  k.H = g.h; k.W = g.w_in; k.C = g.cin; k.Ho = g.ho; k.Wo = g.wo; k.cout = g.cout;
+  k.sh = g.sh; k.sw = g.sw;
+  k.kp = g.kh * g.kw * g.cin;
+  k.M = g.n * g.ho * g.wo;
+  k.ksteps = p.ksteps;
+  k.steps_per_split = p.steps_per_split;
+  k.ntiles = p.ntiles;
+  k.tiles = p.tiles;
+  k.fwo = FastDiv::make(static_cast<uint32_t>(g.wo));
+  k.fho = FastDiv::make(static_cast<uint32_t>(g.ho));
+  int t = 0;
+  for (int i = 0; i < g.kh; ++i)
+    for (int j = 0; j < g.kw; ++j, ++t) k.taps[t] = pack_tap(i * g.dh - g.ph, j * g.dw - g.pw, t);
+  const int grid = p.tiles * p.splits;
+  if (p.ms == 2) igemm_wgrad_kernel<2, 4, 2, 4, 3><<<grid, 512, 0, st>>>(k);
+  else igemm_wgrad_kernel<1, 4, 1, 8, 3><<<grid, 512, 0, st>>>(k);
+  const int64_t total = static_cast<int64_t>(g.cout) * k.kp;
+  const int rg = static_cast<int>(std::min<int64_t>((total + 255) / 256, 2048));
+  igemm_wgrad_reduce<<<rg, 256, 0, st>>>(ws, dw, p.splits, g.cout, g.cin, g.kh * g.kw);
+}
+
+}  // namespace rtseg

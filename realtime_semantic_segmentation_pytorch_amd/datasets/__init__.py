@@ -7,7 +7,7 @@ GLOBAL rank (multi-node correct) and ``num_workers`` is per rank.
 from __future__ import annotations
 
 import torch
-from torch.utils.data import DataLoader
+from torch.utils.data import DataLoader, RandomSampler, Sampler
 
 from .cityscapes import Cityscapes
 from .custom import Custom
@@ -29,6 +29,29 @@ def get_dataset(config):
     return cls(config=config, mode="train"), cls(config=config, mode="val")
 
 
+class EpochSampler(Sampler):
+    """Wraps a sampler so it yields ``(index, epoch)``: the datasets seed their augmentation
+    from (random_seed, epoch, index), so every epoch draws new augmentations, reproducibly and
+    independently of worker processes (persistent workers never see a ``set_epoch``; the keys
+    they receive carry it)."""
+
+    def __init__(self, base: Sampler):
+        self.base = base
+        self.epoch = 0
+
+    def set_epoch(self, epoch: int):
+        self.epoch = int(epoch)
+        if hasattr(self.base, "set_epoch"):
+            self.base.set_epoch(epoch)
+
+    def __iter__(self):
+        e = self.epoch
+        return ((int(i), e) for i in self.base)
+
+    def __len__(self):
+        return len(self.base)
+
+
 def get_loader(config, rank=None, pin_memory=True):
     train_ds, val_ds = get_dataset(config)
     config.train_num = int(len(train_ds) // config.train_bs * config.train_bs)
@@ -43,13 +66,15 @@ def get_loader(config, rank=None, pin_memory=True):
         tr_s = DistributedSampler(train_ds, num_replicas=config.gpu_num, rank=grank, shuffle=True,
                                   seed=config.random_seed, drop_last=True)
         va_s = DistributedSampler(val_ds, num_replicas=config.gpu_num, rank=grank, shuffle=False)
-        train_loader = DataLoader(train_ds, batch_size=config.train_bs, sampler=tr_s,
+        train_loader = DataLoader(train_ds, batch_size=config.train_bs, sampler=EpochSampler(tr_s),
                                   num_workers=workers, pin_memory=pin, drop_last=True,
                                   persistent_workers=persistent)
         val_loader = DataLoader(val_ds, batch_size=config.val_bs, sampler=va_s, num_workers=workers,
                                 pin_memory=pin, persistent_workers=persistent)
     else:
-        train_loader = DataLoader(train_ds, batch_size=config.train_bs, shuffle=True,
+        gen = torch.Generator().manual_seed(int(config.random_seed))
+        train_loader = DataLoader(train_ds, batch_size=config.train_bs,
+                                  sampler=EpochSampler(RandomSampler(train_ds, generator=gen)),
                                   num_workers=workers, pin_memory=pin, drop_last=True,
                                   persistent_workers=persistent)
         val_loader = DataLoader(val_ds, batch_size=config.val_bs, shuffle=False,
@@ -72,5 +97,5 @@ def get_test_loader(config):
                       num_workers=int(getattr(config, "num_workers", 0)), collate_fn=_collate_test)
 
 
-__all__ = ["Cityscapes", "Custom", "TestDataset", "SyntheticSegDataset", "DeviceBatches",
+__all__ = ["EpochSampler", "Cityscapes", "Custom", "TestDataset", "SyntheticSegDataset", "DeviceBatches",
            "get_dataset", "get_loader", "get_test_loader", "dataset_hub"]

@@ -25,8 +25,23 @@ CLASS_NAMES = ["road", "sidewalk", "building", "wall", "fence", "pole", "traffic
                "bus", "train", "motorcycle", "bicycle"]
 
 
-def _sample_rng(index: int) -> np.random.Generator:
-    return np.random.default_rng([torch.initial_seed() % (2 ** 63), int(index)])
+def split_key(key):
+    """Dataset key -> (index, epoch): ``EpochSampler`` yields (index, epoch) pairs, plain
+    samplers (and direct ``ds[i]``) yield the index alone (epoch 0)."""
+    if isinstance(key, (tuple, list)):
+        return int(key[0]), int(key[1])
+    return int(key), 0
+
+
+def sample_rng(seed: int, epoch: int, index: int) -> np.random.Generator:
+    """Augmentation stream of one (epoch, sample) draw.
+
+    The reference's albumentations pipeline draws fresh randomness on every call
+    (reference datasets/cityscapes.py:115-124).  Seeding from (seed, epoch, index) keeps that
+    -- a sample gets a new scale / crop / jitter / flip every epoch -- while staying
+    reproducible and independent of the worker count or persistent workers (the epoch comes
+    from the sampler, in the main process)."""
+    return np.random.default_rng([int(seed) % (2 ** 63), int(epoch), int(index)])
 
 
 class Cityscapes(Dataset):
@@ -44,6 +59,7 @@ class Cityscapes(Dataset):
         if not os.path.isdir(msk_dir):
             raise RuntimeError(f"Mask directory: {msk_dir} does not exist.")
         self.mode = mode
+        self.seed = int(getattr(config, "random_seed", 1))
         self.transform = T.train_transform(config) if mode == "train" else T.val_transform(config)
         self.images, self.masks = [], []
         for city in sorted(os.listdir(img_dir)):
@@ -55,10 +71,11 @@ class Cityscapes(Dataset):
     def __len__(self):
         return len(self.images)
 
-    def __getitem__(self, index):
+    def __getitem__(self, key):
+        index, epoch = split_key(key)
         image = np.asarray(Image.open(self.images[index]).convert("RGB"))
         mask = np.asarray(Image.open(self.masks[index]).convert("L"))
-        image, mask = self.transform(image, mask, _sample_rng(index))
+        image, mask = self.transform(image, mask, sample_rng(self.seed, epoch, index))
         return T.to_tensor(image), torch.from_numpy(self.encode_target(mask).astype(np.int64))
 
     @classmethod

@@ -15,7 +15,7 @@ from PIL import Image
 from torch.utils.data import Dataset
 
 from . import transforms as T
-from .cityscapes import _sample_rng
+from .cityscapes import sample_rng, split_key
 
 
 class Custom(Dataset):
@@ -36,6 +36,7 @@ class Custom(Dataset):
             raise RuntimeError(f"Image directory: {img_dir} does not exist.")
         if not os.path.isdir(msk_dir):
             raise RuntimeError(f"Mask directory: {msk_dir} does not exist.")
+        self.seed = int(getattr(config, "random_seed", 1))
         norm = ((0.0, 0.0, 0.0), (1.0, 1.0, 1.0))
         if mode == "train":
             self.transform = T.train_transform(config, norm, square_size=config.train_size)
@@ -49,8 +50,9 @@ class Custom(Dataset):
     def __len__(self):
         return len(self.images)
 
-    def __getitem__(self, index):
+    def __getitem__(self, key):
+        index, epoch = split_key(key)
         image = np.asarray(Image.open(self.images[index]).convert("RGB"))
         mask = np.asarray(Image.open(self.masks[index]).convert("L"))
-        image, mask = self.transform(image, mask, _sample_rng(index))
+        image, mask = self.transform(image, mask, sample_rng(self.seed, epoch, index))
         return T.to_tensor(image), torch.from_numpy(np.asarray(mask, np.int64))

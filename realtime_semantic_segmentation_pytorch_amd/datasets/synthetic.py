@@ -33,7 +33,8 @@ class SyntheticSegDataset(Dataset):
     def __len__(self):
         return self.length
 
-    def __getitem__(self, index):
+    def __getitem__(self, key):
+        index = int(key[0]) if isinstance(key, (tuple, list)) else int(key)
         g = torch.Generator().manual_seed(self.seed * 100003 + index)
         h, w = self.size
         img = torch.randn((3, h, w), generator=g)

@@ -38,7 +38,15 @@ def load_pretrained(module: nn.Module, name: str, strict: bool = False) -> bool:
     if path and os.path.isfile(path):
         sd = torch.load(path, map_location="cpu", weights_only=True)
         sd = sd.get("state_dict", sd) if isinstance(sd, dict) else sd
+        own = module.state_dict()
+        bad = [f"{k}: checkpoint {tuple(v.shape)} vs model {tuple(own[k].shape)}"
+               for k, v in sd.items() if k in own and tuple(own[k].shape) != tuple(v.shape)]
+        if bad:
+            raise RuntimeError(f"pretrained weights {path} do not fit {name}: " + "; ".join(bad[:8]))
         missing, unexpected = module.load_state_dict(sd, strict=strict)
+        if missing or unexpected:  # e.g. a classifier head the backbone wrapper drops
+            warnings.warn(f"pretrained {name} ({path}): {len(missing)} missing key(s) {list(missing)[:6]}, "
+                          f"{len(unexpected)} unexpected key(s) {list(unexpected)[:6]}")
         return True
     warnings.warn(f"pretrained weights for {name} not found (set RTSEG_PRETRAINED_DIR); "
                   "using random initialisation")

@@ -33,25 +33,35 @@ def dilated_group_ok(conv: nn.Module) -> bool:
 
 
 def dilated_group_conv2d(x, weight, bias, dilation, groups):
+    """Space-to-batch dilated grouped conv.  Both rearrangements are done on the channels-last
+    (NHWC) view, so each side is ONE copy (plus one for the crop when H or W is not a
+    multiple of the dilation)."""
     n, c, h, w = x.shape
     dh, dw = dilation
     hp, wp = -(-h // dh) * dh, -(-w // dw) * dw
+    xn = x.permute(0, 2, 3, 1)  # NHWC view (free for a channels-last x)
     if (hp, wp) != (h, w):
-        x = F.pad(x, (0, wp - w, 0, hp - h))
-    xs = x.reshape(n, c, hp // dh, dh, wp // dw, dw).permute(0, 3, 5, 1, 2, 4)
-    xs = xs.reshape(n * dh * dw, c, hp // dh, wp // dw).contiguous(memory_format=torch.channels_last)
+        xn = F.pad(xn, (0, 0, 0, wp - w, 0, hp - h))
+    hs, ws = hp // dh, wp // dw
+    xs = xn.reshape(n, hs, dh, ws, dw, c).permute(0, 2, 4, 1, 3, 5).reshape(n * dh * dw, hs, ws, c)
+    xs = xs.permute(0, 3, 1, 2)  # NCHW logical, channels-last physical
     kh, kw = weight.shape[2:]
     ys = F.conv2d(xs, weight, bias, 1, ((kh - 1) // 2, (kw - 1) // 2), 1, groups)
     co = ys.shape[1]
-    y = ys.reshape(n, dh, dw, co, hp // dh, wp // dw).permute(0, 3, 4, 1, 5, 2).reshape(n, co, hp, wp)
-    return y[:, :, :h, :w].contiguous(memory_format=torch.channels_last)
+    yn = ys.permute(0, 2, 3, 1).reshape(n, dh, dw, hs, ws, co).permute(0, 3, 1, 4, 2, 5).reshape(n, hp, wp, co)
+    y = yn.permute(0, 3, 1, 2)
+    if (hp, wp) != (h, w):
+        y = y[:, :, :h, :w].contiguous(memory_format=torch.channels_last)
+    return y
 
 
 class DilatedGroupConv2d(nn.Conv2d):
     """``nn.Conv2d`` (grouped + dilated) run as space-to-batch on the GPU (module docstring)."""
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        if not x.is_cuda:
+        from ._ext import use_hip
+
+        if not x.is_cuda or not use_hip(x):  # RTSEG_DISABLE_HIP=1: the stock conv, for A/B runs
             return super().forward(x)
         return dilated_group_conv2d(x, self.weight, self.bias, tuple(self.dilation), self.groups)
 

@@ -88,7 +88,13 @@ class _FusedMixin:
         return bool(ps) and all(_dense_ok(p) for p in ps) and use_hip(ps[0])
 
     def _launch(self, slot, rows, hp):
-        key = tuple((r[0].data_ptr(), r[1].data_ptr(), r[5], r[4] is not None) for r in rows)
+        """One fused launch over ``rows``.  The device pointer table is cached per ``slot`` (a
+        stable id: the param-group index and bucket ordinal, never a per-step value) and rebuilt
+        only when a pointer or flag in it changes -- so the cache holds at most one table per
+        slot and a replaced state buffer can never leave a stale pointer behind."""
+        key = tuple((r[0].data_ptr(), r[1].data_ptr(), r[2].data_ptr() if r[2] is not None else 0,
+                     r[3].data_ptr() if r[3] is not None else 0, r[4].data_ptr() if r[4] is not None else 0,
+                     r[5]) for r in rows)
         cache = self._tables
         if cache.get(slot, (None,))[0] != key:
             cache[slot] = (key, build_table(rows, rows[0][0].device))
@@ -171,12 +177,12 @@ class _FusedAdamBase(_FusedMixin):
                      self._ema_of.get(p) if ema_w is not None else None, False))
             lr = float(group["lr"])
             # normally one bucket; several only after loading a hand-assembled state
-            for steps, rows in by_step.items():
+            for bi, (steps, rows) in enumerate(sorted(by_step.items())):
                 bc1 = 1.0 - beta1 ** steps
                 bc2 = 1.0 - beta2 ** steps
                 hp = (lr, 0.0, 0.0, float(group["weight_decay"]), False, beta1, beta2, float(group["eps"]),
                       lr / bc1, 1.0 / math.sqrt(bc2), 1.0, float(ema_w) if ema_w is not None else 0.0)
-                self._launch((gi, steps), rows, hp)
+                self._launch((gi, bi), rows, hp)
         self.last_step_fused = ema_w is not None and bool(self._ema_of)
         return loss
 

@@ -118,8 +118,10 @@ def destroy_ddp_process(config):
 
 
 def sampler_set_epoch(config, loader, cur_epochs):
+    """Epoch of the shuffling (DistributedSampler) and of the augmentation stream (EpochSampler,
+    which also forwards to the sampler it wraps) -- DDP or not."""
     sampler = getattr(loader, "sampler", None)
-    if config.DDP and hasattr(sampler, "set_epoch"):
+    if hasattr(sampler, "set_epoch"):
         sampler.set_epoch(cur_epochs)
 
 

@@ -35,7 +35,9 @@ class InferenceEngine:
             # once, on a private copy so the caller's fp32 model is untouched
             model = copy.deepcopy(model)
             for m in model.modules():
-                if type(m) in (nn.Conv2d, nn.ConvTranspose2d, nn.Linear, nn.PReLU):
+                # isinstance: the rtseg conv subclasses (DilatedGroupConv2d, DepthwiseConv2d, ...)
+                # carry fp32 weights too
+                if isinstance(m, (nn.Conv2d, nn.ConvTranspose2d, nn.Linear, nn.PReLU)):
                     m.to(dtype)
         self.model = model.eval().to(self.device)
         if channels_last:

@@ -1,0 +1,126 @@
+"""32x32x16-MFMA implicit-GEMM conv family (csrc/kernels/conv_igemm.hip) vs fp32 PyTorch:
+forward (+ BN-statistics slab, + inference BN/residual/act epilogue), data gradient (tap-table /
+sub-pixel phases for strided convs) and weight gradient (split-K over pixels)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from realtime_semantic_segmentation_pytorch_amd import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+# (n, cin, h, w, cout, k, stride, dilation) -- odd sizes, partial tiles, strides, dilation
+GEOMS = [
+    (2, 64, 17, 23, 64, 3, 1, 1),
+    (2, 64, 32, 40, 128, 3, 2, 1),
+    (1, 128, 9, 14, 200, 3, 1, 2),
+    (3, 128, 16, 16, 64, 1, 1, 1),
+    (1, 64, 7, 5, 24, 5, 1, 1),
+    (2, 256, 12, 20, 256, 3, 1, 1),
+    (2, 128, 15, 21, 128, 1, 2, 1),
+    (1, 192, 11, 13, 320, 3, 2, 1),
+]
+
+
+@pytest.fixture(autouse=True)
+def _lib():
+    assert ops.load(), "HIP extension must load on the GPU box"
+
+
+def _case(n, cin, h, w, cout, k, s, d, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = torch.randn(n, cin, h, w, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    wt = (torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5).to(DEV, torch.bfloat16)
+    return x, wt
+
+
+def _close(got, ref, tol):
+    torch.testing.assert_close(got.float(), ref, atol=tol * ref.abs().max().item() + 1e-6, rtol=tol)
+
+
+@pytest.mark.parametrize("geom", GEOMS)
+def test_igemm_forward_and_stats(geom):
+    n, cin, h, w, cout, k, s, d = geom
+    x, wt = _case(*geom)
+    p = (k - 1) // 2 * d
+    y, part = torch.ops.rtseg.conv_igemm(x, wt.permute(0, 2, 3, 1).contiguous(), [s, s], [p, p], [d, d], True,
+                                         None, None, 0)
+    ref = F.conv2d(x.float(), wt.float(), None, s, p, d)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    _close(y, ref, 2e-2)
+    yf = y.double()
+    torch.testing.assert_close(part[:, :cout].double().sum(0), yf.sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(part[:, cout:].double().sum(0), yf.square().sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("act", [0, 1, 2])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_igemm_bn_epilogue(act, with_res):
+    n, cin, h, w, cout, k = 2, 64, 20, 24, 128, 3
+    x, wt = _case(n, cin, h, w, cout, k, 1, 1, seed=3)
+    ss = torch.cat([torch.rand(cout, device=DEV) + 0.5, torch.randn(cout, device=DEV)]).contiguous()
+    res = None
+    if with_res:
+        res = torch.randn(n, cout, h, w, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y, _ = torch.ops.rtseg.conv_igemm(x, wt.permute(0, 2, 3, 1).contiguous(), [1, 1], [1, 1], [1, 1], False,
+                                      ss, res, act)
+    ref = F.conv2d(x.float(), wt.float(), None, 1, 1) * ss[:cout].view(1, -1, 1, 1) + ss[cout:].view(1, -1, 1, 1)
+    if with_res:
+        ref = ref + res.float()
+    if act == 1:
+        ref = ref.relu()
+    elif act == 2:
+        ref = ref.clamp(0, 6)
+    _close(y, ref, 3e-2)
+
+
+DGRAD = [
+    (2, 64, 17, 23, 64, 3, 1, 1),
+    (2, 64, 32, 40, 128, 3, 2, 1),
+    (2, 48, 33, 41, 128, 3, 2, 1),   # odd input: the last phase rows are partial
+    (1, 128, 9, 14, 192, 3, 1, 2),
+    (3, 128, 16, 16, 64, 1, 1, 1),
+    (2, 64, 15, 21, 128, 1, 2, 1),   # 1x1 stride 2: three of four phases have no tap (zeros)
+    (1, 24, 7, 9, 64, 5, 1, 1),
+]
+
+
+@pytest.mark.parametrize("geom", DGRAD)
+def test_igemm_dgrad(geom):
+    n, cin, h, w, cout, k, s, d = geom
+    x, wt = _case(*geom, seed=7)
+    p = (k - 1) // 2 * d
+    ho = (h + 2 * p - d * (k - 1) - 1) // s + 1
+    wo = (w + 2 * p - d * (k - 1) - 1) // s + 1
+    dy = torch.randn(n, cout, ho, wo, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dx = torch.ops.rtseg.conv_igemm_dgrad(dy, wt.permute(1, 2, 3, 0).contiguous(), list(x.shape), [s, s], [p, p],
+                                          [d, d])
+    ref = torch.nn.grad.conv2d_input(x.shape, wt.float(), dy.float(), s, p, d)
+    assert dx.shape == x.shape and dx.is_contiguous(memory_format=torch.channels_last)
+    _close(dx, ref, 2e-2)
+
+
+WGRAD = [
+    (2, 64, 17, 23, 64, 3, 1, 1),
+    (2, 64, 32, 40, 128, 3, 2, 1),
+    (1, 128, 9, 14, 192, 3, 1, 2),
+    (3, 128, 16, 16, 64, 1, 1, 1),
+    (2, 128, 15, 21, 256, 1, 2, 1),
+    (1, 64, 7, 9, 128, 5, 1, 1),
+    (4, 256, 32, 48, 256, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("geom", WGRAD)
+def test_igemm_wgrad(geom):
+    n, cin, h, w, cout, k, s, d = geom
+    x, wt = _case(*geom, seed=11)
+    p = (k - 1) // 2 * d
+    ho = (h + 2 * p - d * (k - 1) - 1) // s + 1
+    wo = (w + 2 * p - d * (k - 1) - 1) // s + 1
+    dy = torch.randn(n, cout, ho, wo, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dw = torch.ops.rtseg.conv_igemm_wgrad(x, dy, k, k, [s, s], [p, p], [d, d])
+    ref = torch.nn.grad.conv2d_weight(x.float(), wt.shape, dy.float(), s, p, d)
+    assert dw.shape == wt.shape and dw.dtype == torch.float32 and dw.is_contiguous()
+    _close(dw, ref, 1e-2)

@@ -1,9 +1,11 @@
-"""MFMA implicit-GEMM conv (``torch.ops.rtseg.conv_mfma``) vs MIOpen on the DDRNet-23 layer shapes.
+"""Hand-written MFMA conv kernels vs MIOpen on the DDRNet-23 layer shapes: forward, data gradient
+and weight gradient.
 
-Run on the GPU box:  python tools/bench_conv.py [--batch 16] [--iters 20]
-Prints one line per shape: max-abs error vs F.conv2d (fp32 accumulate), times (us) and TFLOP/s of
-MIOpen conv, conv_mfma, conv_mfma + BN-statistics epilogue, and MIOpen conv + the separate BN
-statistics pass it replaces.
+Run on the GPU box:  python tools/bench_conv.py [--batch 32] [--iters 20] [--only fwd,dgrad,wgrad]
+One line per shape and pass: relative max error vs MIOpen, time (us) of MIOpen and of ours,
+TFLOP/s of both.  Ours: ``conv_igemm`` (+ its BN-statistics epilogue, ``fwd+st``),
+``conv_igemm_dgrad``, ``conv_igemm_wgrad``; MIOpen: ``F.conv2d`` / ``aten.convolution_backward``
+(MIOpen find mode, i.e. its best solver per shape).
 """
 import argparse
 import os
@@ -45,15 +47,22 @@ def timeit(fn, iters):
     return e0.elapsed_time(e1) / iters * 1e3
 
 
+def relerr(a, b):
+    return (a.float() - b.float()).abs().max().item() / max(1e-6, b.float().abs().max().item())
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", default="fwd,dgrad,wgrad")
     a = ap.parse_args()
+    passes = set(a.only.split(","))
     assert ops.load()
     torch.backends.cudnn.benchmark = True
     dev = "cuda"
-    print(f"{'shape':42s} {'err':>9s} {'miopen':>8s} {'mfma':>8s} {'mfma+st':>8s} {'mio+st':>8s}  TF(mio/mfma)")
+    print(f"{'shape':34s} {'pass':7s} {'err':>9s} {'miopen':>8s} {'ours':>8s}  TF(mio/ours)  speedup", flush=True)
+    conv_bw = torch.ops.aten.convolution_backward
     for cin, h, w, cout, k, s in SHAPES:
         n = a.batch
         torch.manual_seed(0)
@@ -61,19 +70,43 @@ def main():
         wt = (torch.randn(cout, cin, k, k, device=dev) * (1.0 / (cin * k * k) ** 0.5)).to(torch.bfloat16)
         wcl = wt.contiguous(memory_format=torch.channels_last)
         wk = wt.permute(0, 2, 3, 1).contiguous()
+        wtr = wt.permute(1, 2, 3, 0).contiguous()
         p = k // 2
         y_ref = F.conv2d(x, wcl, None, s, p)
-        y, _ = torch.ops.rtseg.conv_mfma(x, wk, [s, s], [p, p], [1, 1], False, None, None, 0)
-        err = (y.float() - y_ref.float()).abs().max().item() / max(1e-6, y_ref.float().abs().max().item())
-        t_mio = timeit(lambda: F.conv2d(x, wcl, None, s, p), a.iters)
-        t_mf = timeit(lambda: torch.ops.rtseg.conv_mfma(x, wk, [s, s], [p, p], [1, 1], False, None, None, 0), a.iters)
-        t_mfs = timeit(lambda: torch.ops.rtseg.conv_mfma(x, wk, [s, s], [p, p], [1, 1], True, None, None, 0), a.iters)
-        t_mios = timeit(lambda: torch.ops.rtseg.bn_stats_sums(F.conv2d(x, wcl, None, s, p)), a.iters)
-        ho, wo = y.shape[2], y.shape[3]
+        ho, wo = y_ref.shape[2], y_ref.shape[3]
         flop = 2.0 * n * ho * wo * cout * cin * k * k
-        tag = f"{n}x{cin}x{h}x{w} -> {cout} k{k} s{s}"
-        print(f"{tag:42s} {err:9.2e} {t_mio:8.1f} {t_mf:8.1f} {t_mfs:8.1f} {t_mios:8.1f}  "
-              f"{flop / t_mio / 1e6:6.0f}/{flop / t_mf / 1e6:6.0f}", flush=True)
+        dy = torch.randn_like(y_ref).contiguous(memory_format=torch.channels_last)
+        tag = f"{n}x{cin}x{h}x{w}->{cout} k{k}s{s}"
+        rows = []
+        if "fwd" in passes:
+            y, _ = torch.ops.rtseg.conv_igemm(x, wk, [s, s], [p, p], [1, 1], False, None, None, 0)
+            t_m = timeit(lambda: F.conv2d(x, wcl, None, s, p), a.iters)
+            t_o = timeit(lambda: torch.ops.rtseg.conv_igemm(x, wk, [s, s], [p, p], [1, 1], False, None, None, 0),
+                         a.iters)
+            t_os = timeit(lambda: torch.ops.rtseg.conv_igemm(x, wk, [s, s], [p, p], [1, 1], True, None, None, 0),
+                          a.iters)
+            rows.append(("fwd", relerr(y, y_ref), t_m, t_o))
+            rows.append(("fwd+st", 0.0, t_m, t_os))
+        if "dgrad" in passes:
+            dx_ref = conv_bw(dy, x, wcl, None, [s, s], [p, p], [1, 1], False, [0, 0], 1, [True, False, False])[0]
+            dx = torch.ops.rtseg.conv_igemm_dgrad(dy, wtr, list(x.shape), [s, s], [p, p], [1, 1])
+            t_m = timeit(lambda: conv_bw(dy, x, wcl, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
+                                         [True, False, False]), a.iters)
+            t_o = timeit(lambda: torch.ops.rtseg.conv_igemm_dgrad(dy, wtr, list(x.shape), [s, s], [p, p], [1, 1]),
+                         a.iters)
+            rows.append(("dgrad", relerr(dx, dx_ref), t_m, t_o))
+        if "wgrad" in passes:
+            dw_ref = conv_bw(dy, x, wcl, None, [s, s], [p, p], [1, 1], False, [0, 0], 1, [False, True, False])[1]
+            dw = torch.ops.rtseg.conv_igemm_wgrad(x, dy, k, k, [s, s], [p, p], [1, 1])
+            t_m = timeit(lambda: conv_bw(dy, x, wcl, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
+                                         [False, True, False]), a.iters)
+            t_o = timeit(lambda: torch.ops.rtseg.conv_igemm_wgrad(x, dy, k, k, [s, s], [p, p], [1, 1]), a.iters)
+            rows.append(("wgrad", relerr(dw, dw_ref), t_m, t_o))
+        for name, err, t_m, t_o in rows:
+            print(f"{tag:34s} {name:7s} {err:9.2e} {t_m:8.1f} {t_o:8.1f}  {flop / t_m / 1e6:5.0f}/{flop / t_o / 1e6:5.0f}"
+                  f"   {t_m / t_o:5.2f}x", flush=True)
+        del x, dy, y_ref
+        torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":
