@@ -24,22 +24,14 @@ import os
 import sys
 import time
 
-# MIOpen's exhaustive find (cudnn.benchmark) also times the reference "naive"
-# convolution solvers, which take tens of seconds per shape at 1024x2048; they
-# are never the winner, so keep them out of the search.
-for _k in ("MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_FWD", "MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_BWD",
-           "MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_WRW"):
-    os.environ.setdefault(_k, "0")
-
 _ROOT = os.path.dirname(os.path.abspath(__file__))
-# MIOpen find results (solver choice per conv shape on gfx950) persist in-tree, so a fresh
-# box reuses them instead of re-benchmarking every solver during warm-up.
-os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(_ROOT, "miopen_db"))
+sys.path.insert(0, _ROOT)
+# MIOpen find mode without the naive solvers + the in-tree find database: the SAME settings
+# SegTrainer applies (utils/runtime.py), so the bench measures what `main.py --train` runs.
+from realtime_semantic_segmentation_pytorch_amd.utils.runtime import configure_backend  # noqa: E402
 
 import torch
 import torch.distributed as dist
-
-sys.path.insert(0, _ROOT)
 
 from realtime_semantic_segmentation_pytorch_amd.configs import BaseConfig  # noqa: E402
 
@@ -158,8 +150,9 @@ def main():
     from realtime_semantic_segmentation_pytorch_amd.datasets import DeviceBatches
     from realtime_semantic_segmentation_pytorch_amd.parallel import barrier, de_parallel
 
-    torch.backends.cudnn.benchmark = not a.no_cudnn_benchmark
     cfg = make_config(a, world)
+    cfg.cudnn_benchmark = not a.no_cudnn_benchmark
+    configure_backend(cfg.cudnn_benchmark)
     ops.load()
     trainer = SegTrainer(cfg)
     trainer.parallel_model(cfg)
@@ -216,6 +209,13 @@ def main():
              "peak_mem_gb": torch.cuda.max_memory_allocated(dev) / 2 ** 30,
              "hip_ext_loaded": bool(ops.load()), "channels_last": cfg.channels_last,
              "fused_loss": cfg.fused_loss}
+    from realtime_semantic_segmentation_pytorch_amd.ops.conv import decisions
+
+    picks = {}
+    for k, (_, name, _t) in decisions().items():
+        tag = f"{k[0]}:{name}"
+        picks[tag] = picks.get(tag, 0) + 1
+    extra["conv_kernel_choices"] = dict(sorted(picks.items()))  # per layer shape, per pass
     if rank == 0 and not a.no_infer:
         m = de_parallel(trainer.model)
         tag = f"{a.height}x{a.width}"

@@ -23,6 +23,7 @@ from ..parallel import barrier, dist_env
 from ..utils import (de_parallel, destroy_ddp_process, get_ema_model, get_logger, get_optimizer,
                      get_scheduler, get_writer, log_config, mkdir, parallel_model, save_config,
                      set_device, set_seed)
+from ..utils.runtime import configure_backend
 from .loss import get_loss_fn
 
 
@@ -34,6 +35,7 @@ class BaseTrainer:
         if hasattr(config, "init_dependent_config"):
             config.init_dependent_config()  # idempotent; main.py calls it too
         self.logger = get_logger(config, self.main_rank)
+        configure_backend(getattr(config, "cudnn_benchmark", True))  # same MIOpen setup as bench.py
         self.device = set_device(config, self.local_rank)
         self.amp_dtype = torch.float16 if getattr(config, "amp_dtype", "bf16") == "fp16" else torch.bfloat16
         use_scaler = bool(config.amp_training) and self.amp_dtype == torch.float16 and self.device.type == "cuda"

@@ -75,6 +75,13 @@ std::tuple<at::Tensor, at::Tensor> conv_igemm(const at::Tensor& x, const at::Ten
                 "rtseg.conv_igemm: residual / activation need the BN epilogue (scale_shift)");
   }
   launch_conv_igemm_fwd(g, cur_stream());
+  if (stats && part.size(0) > 256) {  // fold the per-tile rows so the BN finalize stays cheap
+    const int rows = static_cast<int>(part.size(0));
+    const int chunk = (rows + 255) / 256;
+    at::Tensor small = at::empty({(rows + chunk - 1) / chunk, 2 * g.cout}, part.options());
+    launch_slab_compact(part.data_ptr<float>(), rows, 2 * g.cout, chunk, small.data_ptr<float>(), cur_stream());
+    part = small;
+  }
   return {y, part};
 }
 

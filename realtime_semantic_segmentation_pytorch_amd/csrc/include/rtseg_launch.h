@@ -158,7 +158,9 @@ void launch_conv_mfma(const ConvGeom& g, hipStream_t st);
 constexpr int kIgemmMaxTaps = 49;
 bool conv_igemm_supported(const ConvGeom& g, int mode);
 // rows of the BN statistics slab [rows, 2*Cout] written by the forward when g.part != nullptr
+// (one per M tile and pixel wave); launch_slab_compact sums groups of `chunk` rows
 int conv_igemm_slabs(const ConvGeom& g);
+void launch_slab_compact(const float* in, int rows, int width, int chunk, float* out, hipStream_t st);
 void launch_conv_igemm_fwd(const ConvGeom& g, hipStream_t st);
 // g.x = dy [N,Ho,Wo,Cout], g.w = [Cin][KH][KW][Cout] bf16, g.y = dx [N,H,W,Cin]
 void launch_conv_igemm_dgrad(const ConvGeom& g, hipStream_t st);

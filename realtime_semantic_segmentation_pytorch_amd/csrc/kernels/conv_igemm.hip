@@ -109,6 +109,21 @@ __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
   return static_cast<uint32_t>(f32_to_bf16(lo)) | (static_cast<uint32_t>(f32_to_bf16(hi)) << 16);
 }
 
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROWS, 0xF, false));
+}
+// Sum over each 32-lane half of the wave; valid in lanes 16..31 and 48..63 (DPP only, no LDS):
+// quad swaps, half-row and row mirrors, then row 0 -> 1 / row 2 -> 3 broadcast of lane 15.
+__device__ __forceinline__ float half_wave_sum(float v) {
+  v += dpp_f<0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x141, 0xF>(v);  // row_half_mirror
+  v += dpp_f<0x140, 0xF>(v);  // row_mirror
+  v += dpp_f<0x142, 0xA>(v);  // row_bcast15 into rows 1 and 3
+  return v;
+}
+
 // Bijective block -> logical id map that gives each XCD (blockIdx % 8 under round-robin
 // dispatch) a contiguous range of logical ids: neighbouring tiles share L2.  Speed only.
 __device__ __forceinline__ int xcd_logical(int b, int G) {
@@ -240,22 +255,25 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  float csum[STATS ? TI : 1][16], csq[STATS ? TI : 1][16];
-  if constexpr (STATS) {
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { csum[i][r] = 0.f; csq[i][r] = 0.f; }
-  }
 
-  // pending (packed bf16) output of the previous tile, stored after the next barrier
-  uint2 pend[TI][TJ][4];
+  // pending (packed bf16) output of the previous tile, stored after the next barrier (small
+  // wave tiles; big ones store at once -- the deferred copy would cost TI*TJ*8 registers)
+  constexpr bool DEFER = TI * TJ <= 4;
+  uint2 pend[DEFER ? TI : 1][DEFER ? TJ : 1][4];
   int64_t pend_off[TJ];
   bool pend_ok[TJ];
   bool have_pend = false;
   const int co_lane = co0 + wn * (BN / WN) + 4 * fhi;  // + ti*32 + 8g
 
   auto pack_tile = [&](int mt) {
+    // BN statistics of this tile: per-lane partial sums over the lane's TJ pixels
+    float ts[STATS ? TI : 1][16], tq[STATS ? TI : 1][16];
+    if constexpr (STATS) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { ts[i][r] = 0.f; tq[i][r] = 0.f; }
+    }
 #pragma unroll
     for (int tj = 0; tj < TJ; ++tj) {
       const int m = mt * BM + wm * (BM / WM) + tj * 32 + frow;
@@ -293,25 +311,57 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
           uint2 pk;
           pk.x = pack2(v[0], v[1]);
           pk.y = pack2(v[2], v[3]);
-          pend[ti][tj][g] = pk;
+          if constexpr (DEFER) {
+            pend[ti][tj][g] = pk;
+          } else if (ok && co < a.cout) {
+            *reinterpret_cast<uint2*>(a.y + pend_off[tj] + co) = pk;
+          }
           if constexpr (STATS) {
             const bool sok = ok && co < a.cout;
             const float q0 = sok ? bf16_to_f32(static_cast<uint16_t>(pk.x & 0xffff)) : 0.f;
             const float q1 = sok ? bf16_to_f32(static_cast<uint16_t>(pk.x >> 16)) : 0.f;
             const float q2 = sok ? bf16_to_f32(static_cast<uint16_t>(pk.y & 0xffff)) : 0.f;
             const float q3 = sok ? bf16_to_f32(static_cast<uint16_t>(pk.y >> 16)) : 0.f;
-            csum[ti][4 * g + 0] += q0; csq[ti][4 * g + 0] += q0 * q0;
-            csum[ti][4 * g + 1] += q1; csq[ti][4 * g + 1] += q1 * q1;
-            csum[ti][4 * g + 2] += q2; csq[ti][4 * g + 2] += q2 * q2;
-            csum[ti][4 * g + 3] += q3; csq[ti][4 * g + 3] += q3 * q3;
+            ts[ti][4 * g + 0] += q0; tq[ti][4 * g + 0] += q0 * q0;
+            ts[ti][4 * g + 1] += q1; tq[ti][4 * g + 1] += q1 * q1;
+            ts[ti][4 * g + 2] += q2; tq[ti][4 * g + 2] += q2 * q2;
+            ts[ti][4 * g + 3] += q3; tq[ti][4 * g + 3] += q3 * q3;
           }
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[ti][tj][r] = 0.f;
       }
     }
+    if constexpr (STATS) {
+      // reduce over the 32 pixel lanes of each half-wave (DPP, full rate): lanes 31 / 63 end
+      // up with the tile's sums for channels (r & 3) + 8 (r >> 2) + 4 * half; one slab row per
+      // (M tile, pixel wave) -> every entry written once, deterministic, no atomics
+#pragma unroll
+      for (int ti = 0; ti < TI; ++ti)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          ts[ti][r] = half_wave_sum(ts[ti][r]);
+          tq[ti][r] = half_wave_sum(tq[ti][r]);
+        }
+      if (frow == 31) {
+        float* prow = a.part + (static_cast<int64_t>(mt) * WM + wm) * 2 * a.cout;
+#pragma unroll
+        for (int ti = 0; ti < TI; ++ti)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int co = co_lane + ti * 32 + 8 * g;
+            if (co < a.cout) {
+              *reinterpret_cast<float4*>(prow + co) =
+                  make_float4(ts[ti][4 * g], ts[ti][4 * g + 1], ts[ti][4 * g + 2], ts[ti][4 * g + 3]);
+              *reinterpret_cast<float4*>(prow + a.cout + co) =
+                  make_float4(tq[ti][4 * g], tq[ti][4 * g + 1], tq[ti][4 * g + 2], tq[ti][4 * g + 3]);
+            }
+          }
+      }
+    }
   };
   auto store_pending = [&]() {
+    if constexpr (!DEFER) return;
 #pragma unroll
     for (int tj = 0; tj < TJ; ++tj) {
       if (!pend_ok[tj]) continue;
@@ -320,7 +370,7 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int co = co_lane + ti * 32 + 8 * g;
-          if (co < a.cout) *reinterpret_cast<uint2*>(a.y + pend_off[tj] + co) = pend[ti][tj][g];
+          if (co < a.cout) *reinterpret_cast<uint2*>(a.y + pend_off[tj] + co) = pend[DEFER ? ti : 0][DEFER ? tj : 0][g];
         }
     }
   };
@@ -380,53 +430,12 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
         kk = 0;
         pack_tile(mfirst + ord * mstep);
         ++ord;
-        have_pend = true;
+        have_pend = DEFER;
       }
     }
     if (have_pend) store_pending();
   }
 
-  if constexpr (STATS) {
-    // per-channel sums: lanes l and l^k (k < 32) hold the same channels for different pixels
-#pragma unroll
-    for (int ti = 0; ti < TI; ++ti)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-#pragma unroll
-        for (int o = 1; o < 32; o <<= 1) {
-          csum[ti][r] += __shfl_xor(csum[ti][r], o, kWave);
-          csq[ti][r] += __shfl_xor(csq[ti][r], o, kWave);
-        }
-      }
-    vm_wait<0>();
-    __syncthreads();
-    float* red = reinterpret_cast<float*>(lds);  // [WM][BN][2]
-    if (frow == 0) {
-#pragma unroll
-      for (int ti = 0; ti < TI; ++ti)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int col = wn * (BN / WN) + ti * 32 + (r & 3) + 8 * (r >> 2) + 4 * fhi;
-          red[(wm * BN + col) * 2] = csum[ti][r];
-          red[(wm * BN + col) * 2 + 1] = csq[ti][r];
-        }
-    }
-    __syncthreads();
-    for (int col = tid; col < BN; col += NW * 64) {
-      float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int w = 0; w < WM; ++w) {
-        s1 += red[(w * BN + col) * 2];
-        s2 += red[(w * BN + col) * 2 + 1];
-      }
-      const int co = co0 + col;
-      if (co < a.cout) {
-        float* prow = a.part + static_cast<int64_t>(mfirst) * 2 * a.cout;
-        prow[co] = s1;
-        prow[a.cout + co] = s2;
-      }
-    }
-  }
 }
 
 // ------------------------------------------------------------------------------- wgrad
@@ -475,8 +484,12 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_wgrad_kernel(const WgArgs a
   const int row = wid * 8 + (lane >> 3);
   const int lc = (lane & 7) ^ (((row >> 1) & 1) << 2);
   int aoff[MS];
+  bool aok[MS];  // sub-tiles past Cout (a tile wider than the layer) read the zero page
 #pragma unroll
-  for (int s = 0; s < MS; ++s) aoff[s] = co0 + s * 64 + lc * 8;
+  for (int s = 0; s < MS; ++s) {
+    aok[s] = co0 + s * 64 < a.cout;
+    aoff[s] = co0 + s * 64 + lc * 8;
+  }
   int bdh[NS], bdw[NS], boff[NS];
   bool bok[NS];
 #pragma unroll
@@ -499,8 +512,8 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_wgrad_kernel(const WgArgs a
     const uint32_t base = lds_addr(lds + buf * STAGE) + wid * 1024;
 #pragma unroll
     for (int s = 0; s < MS; ++s) {
-      const void* src = mok ? static_cast<const void*>(a.dy + static_cast<int64_t>(m) * a.cout + aoff[s])
-                            : static_cast<const void*>(g_igemm_zero);
+      const void* src = (mok && aok[s]) ? static_cast<const void*>(a.dy + static_cast<int64_t>(m) * a.cout + aoff[s])
+                                        : static_cast<const void*>(g_igemm_zero);
       dma16(src, base + s * SUB * 16);
     }
 #pragma unroll
@@ -600,16 +613,32 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_wgrad_kernel(const WgArgs a
     }
 }
 
-// dw[co][ci][tap] = sum_s slab[s][co][tap*C + ci]
-__global__ void igemm_wgrad_reduce(const float* __restrict__ ws, float* __restrict__ dw, int splits, int cout,
+// Split-K reduction, deterministic.  Stage 1 (only when there are > 16 splits): groups of 16
+// slab rows -> one partial row each, float4 per thread, 16 loads in flight.  Stage 2: sum the
+// (<= 16) remaining rows and write dw[co][ci][tap] from slab column co * KT*C + tap*C + ci.
+__global__ void igemm_wgrad_reduce16(const float4* __restrict__ ws, float4* __restrict__ out, int splits,
+                                     int64_t plane4) {
+  const int64_t c = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (c >= plane4) return;
+  const int s0 = blockIdx.y * 16, s1 = min(s0 + 16, splits);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 16
+  for (int sp = s0; sp < s1; ++sp) {
+    const float4 v = ws[sp * plane4 + c];
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  out[blockIdx.y * plane4 + c] = acc;
+}
+
+__global__ void igemm_wgrad_reduce(const float* __restrict__ ws, float* __restrict__ dw, int rows, int cout,
                                    int C, int kt) {
   const int64_t kp = static_cast<int64_t>(kt) * C;
-  const int64_t total = static_cast<int64_t>(cout) * kp;
-  const int64_t plane = total;
-  for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+  const int64_t plane = static_cast<int64_t>(cout) * kp;
+  for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < plane;
        e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     float s = 0.f;
-    for (int sp = 0; sp < splits; ++sp) s += ws[sp * plane + e];
+#pragma unroll 16
+    for (int sp = 0; sp < rows; ++sp) s += ws[sp * plane + e];
     const int64_t co = e / kp;
     const int64_t r = e - co * kp;
     const int64_t t = r / C, ci = r - t * C;
@@ -618,15 +647,37 @@ __global__ void igemm_wgrad_reduce(const float* __restrict__ ws, float* __restri
 }
 
 // ------------------------------------------------------------------------------- host side
+// Block-tile configurations (BM pixels x BN channels, WM x WN waves, NST ring stages):
+//   0: 256 x  64, 8 x 1 waves (64 x 32 wave tiles), 3 stages, 120 KiB
+//   1: 256 x 128, 4 x 2 waves (64 x 64),            3 stages, 144 KiB
+//   2: 512 x  64, 8 x 1 waves (64 x 64),            2 stages, 144 KiB  -- Cout <= 64
+//   3: 256 x 256, 2 x 4 waves (64 x 128),           2 stages, 128 KiB  -- Cout >= 256
+//   4: 512 x 128, 4 x 2 waves (64 x 128),           2 stages, 160 KiB  -- Cout 65..128 (..255)
+// The big wave tiles halve the LDS fragment reads per MFMA (profiles/r2_conv_igemm: 64 x 128
+// tiles beat MIOpen's forward and its backward-data by 1.1-1.5x at batch 32); problems with
+// fewer than one tile per CU fall back to the smaller tiles.
+// RTSEG_IGEMM_CFG=<n> forces one (A/B sweeps, tools/bench_conv.py --cfgs).
 struct Cfg {
-  int bm, bn;
+  int id, bm, bn, wm;
 };
+constexpr Cfg kCfgs[] = {{0, 256, 64, 8}, {1, 256, 128, 4}, {2, 512, 64, 8}, {3, 256, 256, 2}, {4, 512, 128, 4}};
 
-Cfg fwd_cfg(int cout) { return cout <= 64 ? Cfg{256, 64} : Cfg{256, 128}; }
+int64_t cfg_tiles(const Cfg& c, int64_t M, int cout) { return ((M + c.bm - 1) / c.bm) * ((cout + c.bn - 1) / c.bn); }
+
+Cfg pick_cfg(int cout, int64_t M) {
+  const char* e = std::getenv("RTSEG_IGEMM_CFG");
+  if (e != nullptr && *e != '\0') {
+    const int i = std::atoi(e);
+    if (i >= 0 && i < static_cast<int>(sizeof(kCfgs) / sizeof(kCfgs[0]))) return kCfgs[i];
+  }
+  const Cfg big = cout <= 64 ? kCfgs[2] : cout <= 128 ? kCfgs[4] : kCfgs[3];
+  const Cfg small = cout <= 64 ? kCfgs[0] : kCfgs[1];
+  return cfg_tiles(big, M, cout) >= 256 ? big : small;
+}
 
 int persistent_grid(int mtiles, int ntiles) {
   const int64_t tiles = static_cast<int64_t>(mtiles) * ntiles;
-  const int cap = std::max(ntiles, (256 / ntiles) * ntiles);
+  const int cap = std::max(ntiles, (256 / ntiles) * ntiles);  // one block per CU (LDS-bound)
   return static_cast<int>(tiles < cap ? tiles : cap);
 }
 
@@ -641,8 +692,28 @@ void fill_common(IgArgs& k, const Cfg& c, int n) {
 
 template <int EPI, bool STATS>
 void launch_cfg(const IgArgs& k, const Cfg& c, int grid, hipStream_t st) {
-  if (c.bn == 64) igemm_gather_kernel<256, 64, 8, 1, 3, EPI, STATS><<<grid, 512, 0, st>>>(k);
-  else igemm_gather_kernel<256, 128, 4, 2, 3, EPI, STATS><<<grid, 512, 0, st>>>(k);
+  switch (c.id) {
+    case 0: igemm_gather_kernel<256, 64, 8, 1, 3, EPI, STATS><<<grid, 512, 0, st>>>(k); break;
+    case 2: igemm_gather_kernel<512, 64, 8, 1, 2, EPI, STATS><<<grid, 512, 0, st>>>(k); break;
+    case 3:
+      if constexpr (EPI == 0) igemm_gather_kernel<256, 256, 2, 4, 2, 0, STATS><<<grid, 512, 0, st>>>(k);
+      break;
+    case 4:
+      if constexpr (EPI == 0) igemm_gather_kernel<512, 128, 4, 2, 2, 0, STATS><<<grid, 512, 0, st>>>(k);
+      break;
+    default: igemm_gather_kernel<256, 128, 4, 2, 3, EPI, STATS><<<grid, 512, 0, st>>>(k); break;
+  }
+}
+
+// out[r][c] = sum_{i < chunk} in[r * chunk + i][c] (rows past `rows` count as zero)
+__global__ void slab_compact_kernel(const float* __restrict__ in, int rows, int width, int chunk,
+                                    float* __restrict__ out) {
+  const int c = blockIdx.y * blockDim.x + threadIdx.x;
+  if (c >= width) return;
+  const int r0 = blockIdx.x * chunk, r1 = min(r0 + chunk, rows);
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += in[static_cast<int64_t>(r) * width + c];
+  out[static_cast<int64_t>(blockIdx.x) * width + c] = s;
 }
 
 void launch_gather(const IgArgs& k, const Cfg& c, hipStream_t st) {
@@ -665,11 +736,14 @@ bool conv_igemm_supported(const ConvGeom& g, int mode) {
 }
 
 int conv_igemm_slabs(const ConvGeom& g) {
-  const Cfg c = fwd_cfg(g.cout);
   const int64_t M = static_cast<int64_t>(g.n) * g.ho * g.wo;
-  const int mtiles = static_cast<int>((M + c.bm - 1) / c.bm);
-  const int ntiles = (g.cout + c.bn - 1) / c.bn;
-  return persistent_grid(mtiles, ntiles) / ntiles;
+  const Cfg c = pick_cfg(g.cout, M);
+  return static_cast<int>((M + c.bm - 1) / c.bm) * c.wm;
+}
+
+void launch_slab_compact(const float* in, int rows, int width, int chunk, float* out, hipStream_t st) {
+  const dim3 grid((rows + chunk - 1) / chunk, (width + 255) / 256);
+  slab_compact_kernel<<<grid, 256, 0, st>>>(in, rows, width, chunk, out);
 }
 
 void launch_conv_igemm_fwd(const ConvGeom& g, hipStream_t st) {
@@ -691,14 +765,16 @@ void launch_conv_igemm_fwd(const ConvGeom& g, hipStream_t st) {
     for (int j = 0; j < g.kw; ++j) {
       k.taps[k.ntap++] = pack_tap(i * g.dh - g.ph, j * g.dw - g.pw, i * g.kw + j);
     }
-  const Cfg c = fwd_cfg(g.cout);
+  Cfg c = pick_cfg(g.cout, static_cast<int64_t>(g.n) * g.ho * g.wo);
+  // the inference BN epilogue (scale/shift/residual loads) spills on the 64 x 128 wave tiles
+  if (g.scale_shift != nullptr && (c.id == 3 || c.id == 4)) c = kCfgs[1];
   fill_common(k, c, g.n);
   launch_gather(k, c, st);
 }
 
 // g: forward geometry; g.x = dy [N,Ho,Wo,Cout], g.w = wt [Cin][KH][KW][Cout], g.y = dx [N,H,W,Cin]
 void launch_conv_igemm_dgrad(const ConvGeom& g, hipStream_t st) {
-  const Cfg c = fwd_cfg(g.cin);
+  const Cfg c = pick_cfg(g.cin, static_cast<int64_t>(g.n) * g.h * g.w_in / (g.sh * g.sw));
   for (int a = 0; a < g.sh; ++a)
     for (int b = 0; b < g.sw; ++b) {
       IgArgs k{};
@@ -729,21 +805,45 @@ void launch_conv_igemm_dgrad(const ConvGeom& g, hipStream_t st) {
 }
 
 namespace {
+// Weight-gradient tile configurations (MS x 64 output channels, NS x 64 (tap, ci) columns,
+// WM x WN waves, NST stages):
+//   0: 128 x 256, 2 x 4 waves (64 x 64),  3 stages, 144 KiB
+//   1:  64 x 256, 1 x 8 waves (64 x 32),  3 stages, 120 KiB
+//   2: 128 x 512, 2 x 4 waves (64 x 128), 2 stages, 160 KiB
+//   3: 256 x 256, 2 x 4 waves (128 x 64), 2 stages, 128 KiB
+//   4:  64 x 512, 1 x 8 waves (64 x 64),  2 stages, 144 KiB
+//   5: 128 x 384, 2 x 4 waves (64 x 96),  2 stages, 128 KiB
+// RTSEG_WGRAD_CFG=<n> forces one.
+struct WgCfg {
+  int id, ms, ns;
+};
+constexpr WgCfg kWgCfgs[] = {{0, 2, 4}, {1, 1, 4}, {2, 2, 8}, {3, 4, 4}, {4, 1, 8}, {5, 2, 6}};
+
 struct WgPlan {
-  int ms, ns, ntiles, mtiles, tiles, ksteps, splits, steps_per_split;
+  WgCfg c;
+  int ntiles, mtiles, tiles, ksteps, splits, steps_per_split;
 };
 WgPlan wgrad_plan(const ConvGeom& g) {
   WgPlan p{};
-  p.ms = g.cout % 128 == 0 ? 2 : 1;
-  p.ns = 4;
+  const char* e = std::getenv("RTSEG_WGRAD_CFG");
   const int kp = g.kh * g.kw * g.cin;
-  p.mtiles = g.cout / (64 * p.ms);
-  p.ntiles = (kp + 64 * p.ns - 1) / (64 * p.ns);
+  // measured at batch 32 (profiles/r2_conv_igemm/sweep): 256 x 256 for Cout >= 256 (up to 1.9x
+  // MIOpen), 128 x 384 for 128-channel layers, 64 x 256 for 64-channel ones
+  int id = g.cout % 256 == 0 ? 3 : g.cout % 128 == 0 ? 5 : 1;
+  if (e != nullptr && *e != '\0') {
+    const int i = std::atoi(e);
+    if (i >= 0 && i < static_cast<int>(sizeof(kWgCfgs) / sizeof(kWgCfgs[0]))) id = i;
+  }
+  // never a channel tile wider than the layer (the kernel masks it, but it is wasted work)
+  if (kWgCfgs[id].ms * 64 > g.cout) id = g.cout % 128 == 0 ? 0 : 1;
+  p.c = kWgCfgs[id];
+  p.mtiles = (g.cout + 64 * p.c.ms - 1) / (64 * p.c.ms);
+  p.ntiles = (kp + 64 * p.c.ns - 1) / (64 * p.c.ns);
   p.tiles = p.mtiles * p.ntiles;
   const int64_t M = static_cast<int64_t>(g.n) * g.ho * g.wo;
   p.ksteps = static_cast<int>((M + 63) / 64);
-  int splits = std::max(1, 256 / p.tiles);
-  splits = std::min(splits, std::max(1, p.ksteps / 8));  // >= 8 K-steps per split
+  int splits = std::max(1, (256 + p.tiles / 2) / p.tiles);
+  splits = std::min(splits, std::max(1, p.ksteps / 16));  // >= 16 K-steps per split
   p.steps_per_split = (p.ksteps + splits - 1) / splits;
   p.splits = (p.ksteps + p.steps_per_split - 1) / p.steps_per_split;
   return p;
@@ -752,7 +852,8 @@ WgPlan wgrad_plan(const ConvGeom& g) {
 
 int64_t conv_igemm_wgrad_ws_elems(const ConvGeom& g) {
   const WgPlan p = wgrad_plan(g);
-  return static_cast<int64_t>(p.splits) * g.cout * g.kh * g.kw * g.cin;
+  const int64_t plane = static_cast<int64_t>(g.cout) * g.kh * g.kw * g.cin;
+  return plane * (p.splits + (p.splits > 16 ? (p.splits + 15) / 16 : 0));
 }
 
 // g.x = x [N,H,W,Cin], g.y = dy [N,Ho,Wo,Cout] (bf16); dw fp32 [Cout][Cin][KH][KW]
@@ -776,11 +877,28 @@ void launch_conv_igemm_wgrad(const ConvGeom& g, float* ws, float* dw, hipStream_
   for (int i = 0; i < g.kh; ++i)
     for (int j = 0; j < g.kw; ++j, ++t) k.taps[t] = pack_tap(i * g.dh - g.ph, j * g.dw - g.pw, t);
   const int grid = p.tiles * p.splits;
-  if (p.ms == 2) igemm_wgrad_kernel<2, 4, 2, 4, 3><<<grid, 512, 0, st>>>(k);
-  else igemm_wgrad_kernel<1, 4, 1, 8, 3><<<grid, 512, 0, st>>>(k);
-  const int64_t total = static_cast<int64_t>(g.cout) * k.kp;
-  const int rg = static_cast<int>(std::min<int64_t>((total + 255) / 256, 2048));
-  igemm_wgrad_reduce<<<rg, 256, 0, st>>>(ws, dw, p.splits, g.cout, g.cin, g.kh * g.kw);
+  switch (p.c.id) {
+    case 1: igemm_wgrad_kernel<1, 4, 1, 8, 3><<<grid, 512, 0, st>>>(k); break;
+    case 2: igemm_wgrad_kernel<2, 8, 2, 4, 2><<<grid, 512, 0, st>>>(k); break;
+    case 3: igemm_wgrad_kernel<4, 4, 2, 4, 2><<<grid, 512, 0, st>>>(k); break;
+    case 4: igemm_wgrad_kernel<1, 8, 1, 8, 2><<<grid, 512, 0, st>>>(k); break;
+    case 5: igemm_wgrad_kernel<2, 6, 2, 4, 2><<<grid, 512, 0, st>>>(k); break;
+    default: igemm_wgrad_kernel<2, 4, 2, 4, 3><<<grid, 512, 0, st>>>(k); break;
+  }
+  const int64_t plane = static_cast<int64_t>(g.cout) * k.kp;
+  const float* src = ws;
+  int rows = p.splits;
+  if (rows > 16) {  // plane % 4 == 0: Cout % 64 == 0
+    float* mid = ws + plane * p.splits;
+    const int64_t plane4 = plane / 4;
+    const dim3 g1(static_cast<unsigned>((plane4 + 255) / 256), static_cast<unsigned>((rows + 15) / 16));
+    igemm_wgrad_reduce16<<<g1, 256, 0, st>>>(reinterpret_cast<const float4*>(ws), reinterpret_cast<float4*>(mid),
+                                             rows, plane4);
+    src = mid;
+    rows = (rows + 15) / 16;
+  }
+  const int rg = static_cast<int>(std::min<int64_t>((plane + 255) / 256, 4096));
+  igemm_wgrad_reduce<<<rg, 256, 0, st>>>(src, dw, rows, g.cout, g.cin, g.kh * g.kw);
 }
 
 }  // namespace rtseg

@@ -1,19 +1,27 @@
-"""Dense convolution on the MFMA implicit-GEMM kernel (``csrc/kernels/conv_mfma.hip``).
+"""Dense convolution on the hand-written MFMA kernels (``csrc/kernels/conv_igemm.hip``, and the
+older 16x16x32 ``conv_mfma.hip`` for Cin % 64 != 0).
 
 Reference: the ``nn.Conv2d`` of every ConvBNAct / residual block (models/modules.py:73-85,
-ddrnet.py:168-219), executed by cuDNN in the reference and followed by a separate
-BatchNorm pass.  Here, for channels-last bf16 activations:
+ddrnet.py:168-219), executed by cuDNN in the reference (forward, backward-data and
+backward-filter) and followed by a separate BatchNorm pass.  Here, for channels-last bf16
+activations, every such conv is ONE autograd node (:class:`_ConvFn`) whose three passes are
+each routed to our kernel or to MIOpen:
 
-* training: ``conv_bn_stats`` runs the conv with the BN statistics in its epilogue
-  (per-channel sum / sum of squares -> a [G, 2C] slab that ``ops.bn_act`` finalizes),
-  so the BatchNorm forward no longer re-reads the conv output; the backward is
-  ``aten.convolution_backward`` (MIOpen dgrad / wgrad);
-* inference: ``conv_bn_act_eval`` folds BatchNorm (running statistics), the residual
-  add and ReLU / ReLU6 into the conv epilogue -- one kernel per ConvBNAct / RB tail.
+* forward (training): ``conv_igemm`` with the BN statistics in its epilogue (per-channel sum /
+  sum of squares -> a [G, 2C] slab that ``ops.bn_act`` finalizes), so the BatchNorm forward no
+  longer re-reads the conv output;
+* data gradient: ``conv_igemm_dgrad`` -- the same gather kernel over dy with a flipped tap
+  table (one launch per output phase for strided convs, no col2im, no zero-fill);
+* weight gradient: ``conv_igemm_wgrad`` -- split-K over pixels with transposed LDS reads, fp32
+  partial tiles reduced deterministically straight into the fp32 weight-gradient layout
+  (MIOpen's wrw needs a zero-filled output buffer every call);
+* inference: ``conv_igemm`` with BatchNorm (running statistics), residual add and ReLU / ReLU6
+  folded into the epilogue -- one kernel per ConvBNAct / RB tail.
 
-Whether a layer takes this path or MIOpen (+ the separate BN pass) is decided per
-shape by timing both the first time the shape is seen (``cudnn.benchmark``-style,
-outside graph capture); ``RTSEG_CONV_MFMA=0`` disables the path, ``=1`` forces it.
+Each pass of each layer shape is timed once against MIOpen the first time it runs
+(``cudnn.benchmark``-style; never during HIP-graph capture) and the faster one is kept --
+``decisions()`` lists the outcomes.  ``RTSEG_CONV_MFMA=0`` disables our kernels, ``=1`` forces
+them wherever they apply.
 """
 from __future__ import annotations
 
@@ -32,121 +40,191 @@ def _mode() -> str:
     return os.environ.get("RTSEG_CONV_MFMA", "auto")
 
 
+def _autocast_bf16(x: torch.Tensor) -> bool:
+    dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
+    return dt == torch.bfloat16
+
+
 def conv_ok(x: torch.Tensor, conv: nn.Module) -> bool:
-    """Shapes/layouts the kernel handles (anything else stays on MIOpen)."""
+    """Convs this module routes (anything else stays ``conv(x)`` on MIOpen): dense, bias-free,
+    channels-last bf16 activations.  Which kernel runs each pass is decided per shape."""
     if type(conv) is not nn.Conv2d or conv.groups != 1 or conv.bias is not None:
         return False
     if conv.padding_mode != "zeros" or isinstance(conv.padding, str):
         return False
-    if x.dim() != 4 or not x.is_cuda or conv.in_channels % 32 or conv.out_channels % 8:
+    if x.dim() != 4 or not x.is_cuda or _mode() == "0" or not use_hip(x):
         return False
-    if _mode() == "0" or not use_hip(x):
+    if conv.kernel_size[0] * conv.kernel_size[1] > 49:
         return False
-    dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
-    if dt != torch.bfloat16:
-        return False
-    return x.is_contiguous(memory_format=torch.channels_last)
+    return _autocast_bf16(x) and x.is_contiguous(memory_format=torch.channels_last)
 
 
 def _geom(conv):
     return list(conv.stride), list(conv.padding), list(conv.dilation)
 
 
-def weight_krsc(conv: nn.Conv2d) -> torch.Tensor:
-    """bf16 [Cout, KH, KW, Cin] copy of the weight, cached until the parameter changes."""
+def _cached(conv, attr, make):
+    """bf16 re-layouts of the fp32 weight.  Cached on the module only for inference (no grad /
+    eval): in training the fused optimizer rewrites parameters through raw pointers, which does
+    not bump their version counters, so a cached copy could go stale -- the training path
+    builds the copy once per forward and hands it to its backward instead."""
     w = conv.weight
-    key = (w.data_ptr(), w._version, w.dtype)
-    cached = getattr(conv, "_rtseg_wk", None)
-    if cached is not None and cached[0] == key:
-        return cached[1]
-    wk = w.detach().to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()
-    if not torch.is_grad_enabled() or not conv.training:
-        conv._rtseg_wk = (key, wk)  # eval / inference: weights are static between steps
-    return wk
+    if conv.training and torch.is_grad_enabled():
+        return make(w.detach())
+    key = (w.data_ptr(), w._version)
+    hit = getattr(conv, attr, None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    t = make(w.detach())
+    setattr(conv, attr, (key, t))
+    return t
 
 
-class _ConvStatsFn(torch.autograd.Function):
+def weight_krsc(conv: nn.Conv2d) -> torch.Tensor:
+    """[Cout, KH, KW, Cin] bf16 (forward B operand)."""
+    return _cached(conv, "_rtseg_wk", lambda w: w.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous())
+
+
+def _time(fn, reps=8):
+    """GPU time of ``fn`` (eager; the candidates are >= tens of microseconds at training sizes)."""
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e)
+
+
+def _choose(key, candidates):
+    """Index of the fastest candidate (timed once per key, never while a graph is captured).
+    ``candidates``: [(name, fn)] with ours first; ``RTSEG_CONV_MFMA=1`` forces index 0."""
+    if len(candidates) == 1 or _mode() == "1":
+        return 0
+    got = _DECISIONS.get(key)
+    if got is not None:
+        return got[0]
+    if torch.cuda.is_current_stream_capturing():
+        return len(candidates) - 1  # MIOpen is last
+    with torch.no_grad():
+        times = [_time(fn) for _, fn in candidates]
+    best = min(range(len(times)), key=times.__getitem__)
+    _DECISIONS[key] = (best, candidates[best][0], [round(t, 4) for t in times])
+    return best
+
+
+# ----------------------------------------------------------------------------- autograd node
+class _ConvFn(torch.autograd.Function):
+    """y (+ BN statistics slab) = conv(x, w); backward via our dgrad / wgrad or MIOpen."""
+
     @staticmethod
-    def forward(ctx, x, weight, wk, stride, padding, dilation):
-        y, part = ops().conv_mfma(x, wk, stride, padding, dilation, True, None, None, 0)
+    def forward(ctx, x, weight, conv, stats):
+        stride, padding, dilation = _geom(conv)
+        cout, cin, kh, kw = weight.shape
+        key = (tuple(x.shape), cout, kh, kw, tuple(stride), tuple(padding), tuple(dilation))
+        part = None
+        wk = weight_krsc(conv)
+        impl = _fwd_impl(x, wk, conv, key, stats)
+        if impl == "igemm":
+            y, part = ops().conv_igemm(x, wk, stride, padding, dilation, stats, None, None, 0)
+        elif impl == "mfma":
+            y, part = ops().conv_mfma(x, wk, stride, padding, dilation, stats, None, None, 0)
+        else:
+            y = F.conv2d(x, wk.permute(0, 3, 1, 2), None, stride, padding, dilation)
+            y = y.contiguous(memory_format=torch.channels_last)
+        if part is not None and part.numel() == 0:
+            part = None
         ctx.save_for_backward(x, wk)
-        ctx.geom = (stride, padding, dilation)
+        ctx.conv, ctx.key = conv, key
         ctx.wdtype = weight.dtype
-        ctx.mark_non_differentiable(part)
+        if part is not None:
+            ctx.mark_non_differentiable(part)
         return y, part
 
     @staticmethod
     def backward(ctx, dy, _dpart):
         x, wk = ctx.saved_tensors
-        stride, padding, dilation = ctx.geom
-        w4 = wk.permute(0, 3, 1, 2)  # [Cout, Cin, KH, KW] with channels-last strides
-        dy = dy.contiguous(memory_format=torch.channels_last)
-        mask = [ctx.needs_input_grad[0], ctx.needs_input_grad[1], False]
-        dx, dw, _ = torch.ops.aten.convolution_backward(dy, x, w4, None, stride, padding, dilation, False,
-                                                         [0, 0], 1, mask)
-        if dw is not None:
-            dw = dw.to(ctx.wdtype)
-        return dx, dw, None, None, None, None
+        conv, key = ctx.conv, ctx.key
+        stride, padding, dilation = _geom(conv)
+        dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        if dy.data_ptr() % 16:
+            dy = dy.clone(memory_format=torch.channels_last)
+        want_dx, want_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        dx = dw = None
+        if want_dx:
+            dx = _dgrad(x, dy, wk, conv, key, stride, padding, dilation)
+        if want_dw:
+            dw = _wgrad(x, dy, wk, conv, key, stride, padding, dilation).to(ctx.wdtype)
+        return dx, dw, None, None
 
 
-def _time(fn, reps=10):
-    """GPU time of ``fn``: captured into a HIP graph and replayed, so two candidates with
-    different launch counts are compared the way a captured / GPU-bound step runs them
-    (eager timing of ~20 us kernels measures the host launch path instead)."""
-    fn()  # warm-up: MIOpen find / kernel load happen outside the capture
-    torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    try:
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            fn()
-        g.replay()
-        s.record()
-        for _ in range(reps):
-            g.replay()
-        e.record()
-    except RuntimeError:  # capture not possible here: fall back to eager timing
-        s.record()
-        for _ in range(reps):
-            fn()
-        e.record()
-    e.synchronize()
-    return s.elapsed_time(e)
-
-
-def _decide(key, ours, theirs) -> bool:
-    """True -> MFMA path.  Timed once per key (never while a HIP graph is being captured)."""
-    mode = _mode()
-    if mode == "1":
-        return True
-    got = _DECISIONS.get(key)
-    if got is not None:
-        return got
-    if torch.cuda.is_current_stream_capturing():
-        return False
-    with torch.no_grad():
-        t_ours, t_theirs = _time(ours), _time(theirs)
-    _DECISIONS[key] = t_ours < t_theirs
-    return _DECISIONS[key]
-
-
-def conv_bn_stats(x: torch.Tensor, conv: nn.Conv2d):
-    """Training forward: (y, slab) with the BN statistics of y, or None -> caller uses MIOpen."""
-    x = x.to(torch.bfloat16)
+def _fwd_impl(x, wk, conv, key, stats) -> str:
+    cin, cout = conv.in_channels, conv.out_channels
     stride, padding, dilation = _geom(conv)
-    wk = weight_krsc(conv)
-    key = ("train", tuple(x.shape), conv.out_channels, conv.kernel_size, tuple(stride), tuple(padding),
-           tuple(dilation))
+    cands = []
+    if cin % 64 == 0 and cout % 8 == 0:
+        cands.append(("igemm", lambda: ops().conv_igemm(x, wk, stride, padding, dilation, stats, None, None, 0)))
+    elif cin % 32 == 0 and cout % 8 == 0:
+        cands.append(("mfma", lambda: ops().conv_mfma(x, wk, stride, padding, dilation, stats, None, None, 0)))
+    if not cands:
+        return "miopen"
+
+    def miopen():
+        y = F.conv2d(x, wk.permute(0, 3, 1, 2), None, stride, padding, dilation)
+        if stats:
+            ops().bn_stats_sums(y)  # the statistics pass our epilogue replaces
+
+    cands.append(("miopen", miopen))
+    return cands[_choose(("fwd", stats) + key, cands)][0]
+
+
+def _dgrad(x, dy, wk, conv, key, stride, padding, dilation):
+    cin, cout = conv.in_channels, conv.out_channels
+    wt = []
 
     def ours():
-        ops().conv_mfma(x, wk, stride, padding, dilation, True, None, None, 0)
+        if not wt:  # [Cin, KH, KW, Cout] bf16, the dgrad B operand
+            wt.append(wk.permute(3, 1, 2, 0).contiguous())
+        return ops().conv_igemm_dgrad(dy, wt[0], list(x.shape), stride, padding, dilation)
 
-    def theirs():
-        ops().bn_stats_sums(F.conv2d(x, wk.permute(0, 3, 1, 2), None, stride, padding, dilation))
+    def miopen():
+        return torch.ops.aten.convolution_backward(dy, x, wk.permute(0, 3, 1, 2), None, stride, padding, dilation, False,
+                                                   [0, 0], 1, [True, False, False])[0]
 
-    if not _decide(key, ours, theirs):
-        return None
-    return _ConvStatsFn.apply(x, conv.weight, wk, stride, padding, dilation)
+    cands = [("igemm", ours)] if cout % 64 == 0 and cin % 8 == 0 else []
+    cands.append(("miopen", miopen))
+    return cands[_choose(("dgrad",) + key, cands)][1]()
+
+
+def _wgrad(x, dy, wk, conv, key, stride, padding, dilation):
+    cin, cout = conv.in_channels, conv.out_channels
+    kh, kw = conv.kernel_size
+
+    def ours():
+        return ops().conv_igemm_wgrad(x, dy, kh, kw, stride, padding, dilation)
+
+    def miopen():
+        return torch.ops.aten.convolution_backward(dy, x, wk.permute(0, 3, 1, 2), None, stride, padding, dilation,
+                                                   False, [0, 0], 1, [False, True, False])[1]
+
+    cands = [("igemm", ours)] if cin % 64 == 0 and cout % 64 == 0 else []
+    cands.append(("miopen", miopen))
+    dw = cands[_choose(("wgrad",) + key, cands)][1]()
+    return dw.contiguous()
+
+
+# ----------------------------------------------------------------------------- public entry points
+def conv_bn_stats(x: torch.Tensor, conv: nn.Conv2d):
+    """Training forward of a conv followed by batch-statistics BN: (y, slab | None).  The slab
+    holds the BN statistics of y when our kernel produced y (else ``ops.bn_act`` computes
+    them).  None -> the caller's stock path."""
+    if x.dtype != torch.bfloat16:
+        x = x.to(torch.bfloat16)
+    if x.data_ptr() % 16:
+        x = x.clone(memory_format=torch.channels_last)
+    return _ConvFn.apply(x, conv.weight, conv, True)
 
 
 def conv_bn_act_eval(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, act_code: int, residual=None):
@@ -156,27 +234,32 @@ def conv_bn_act_eval(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, act_code: 
     if residual is not None and not (residual.is_contiguous(memory_format=torch.channels_last)
                                      and residual.dim() == 4):
         return None
+    cin, cout = conv.in_channels, conv.out_channels
+    if cout % 8 or cin % 32:
+        return None
     x = x.to(torch.bfloat16)
     res = residual.to(torch.bfloat16) if residual is not None else None
+    if (x.data_ptr() % 16) or (res is not None and res.data_ptr() % 16):
+        return None
     stride, padding, dilation = _geom(conv)
     wk = weight_krsc(conv)
     from .bn import eval_coeffs
 
     _, ss = eval_coeffs(bn)
-    key = ("eval", tuple(x.shape), conv.out_channels, conv.kernel_size, tuple(stride), tuple(padding),
-           tuple(dilation), res is not None)
+    key = ("eval", tuple(x.shape), cout, conv.kernel_size, tuple(stride), tuple(padding), tuple(dilation),
+           res is not None)
+    op = ops().conv_igemm if cin % 64 == 0 else ops().conv_mfma
 
     def ours():
-        ops().conv_mfma(x, wk, stride, padding, dilation, False, ss, res, act_code)
+        return op(x, wk, stride, padding, dilation, False, ss, res, act_code)[0]
 
     def theirs():
         y = F.conv2d(x, wk.permute(0, 3, 1, 2), None, stride, padding, dilation)
         ops().bn_apply(y, ss, res, act_code)
 
-    if not _decide(key, ours, theirs):
+    if _choose(key, [("igemm" if cin % 64 == 0 else "mfma", ours), ("miopen", theirs)]) != 0:
         return None
-    y, _ = ops().conv_mfma(x, wk, stride, padding, dilation, False, ss, res, act_code)
-    return y
+    return ours()
 
 
 def conv_forward(x: torch.Tensor, conv: nn.Module) -> torch.Tensor:
@@ -192,13 +275,16 @@ def conv_forward(x: torch.Tensor, conv: nn.Module) -> torch.Tensor:
             hit = conv._rtseg_w16 = (key, w.detach().to(torch.bfloat16), b16)
         with torch.autocast("cuda", enabled=False):
             return conv._conv_forward(x.to(torch.bfloat16), hit[1], hit[2])
+    if conv_ok(x, conv) and torch.is_grad_enabled() and conv.weight.requires_grad:
+        y, _ = _ConvFn.apply(x.to(torch.bfloat16), conv.weight, conv, False)
+        return y
     return conv(x)
 
 
 def conv_bn_act(x: torch.Tensor, conv: nn.Module, bn: nn.Module, act="none", residual=None, act_module=None):
-    """``act(bn(conv(x)) + residual)`` with the conv on the MFMA kernel when it wins: BN
-    statistics in its epilogue (training) or the whole BN + residual + activation tail
-    (inference).  Any other case is ``conv`` followed by ``ops.bn_act``."""
+    """``act(bn(conv(x)) + residual)`` with the conv on our kernels where they win: BN statistics
+    in its epilogue (training) or the whole BN + residual + activation tail (inference).  Any
+    other case is ``conv`` followed by ``ops.bn_act``."""
     from .bn import act_code, bn_act
 
     if conv_ok(x, conv) and isinstance(bn, (nn.BatchNorm2d, nn.SyncBatchNorm)):
@@ -210,12 +296,11 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Module, bn: nn.Module, act="none", res
                 if y is not None:
                     return y
             else:
-                r = conv_bn_stats(x, conv)
-                if r is not None:
-                    return bn_act(r[0], bn, code, residual=residual, act_module=act_module, part=r[1])
+                y, part = conv_bn_stats(x, conv)
+                return bn_act(y, bn, code, residual=residual, act_module=act_module, part=part)
     return bn_act(conv_forward(x, conv), bn, act, residual=residual, act_module=act_module)
 
 
 def decisions() -> dict:
-    """Per-shape autotune outcomes so far (for logs / profiles)."""
+    """Per-shape kernel choices so far: key -> (index, name, [ms per candidate])."""
     return dict(_DECISIONS)

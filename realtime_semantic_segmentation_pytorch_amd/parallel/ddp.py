@@ -94,12 +94,27 @@ def set_device(config, local_rank=None):
     return device
 
 
+_SYNCBN_PG = None
+
+
+def syncbn_group():
+    """Process group dedicated to SyncBatchNorm statistics (created once, on every rank)."""
+    global _SYNCBN_PG
+    if _SYNCBN_PG is None and is_dist():
+        _SYNCBN_PG = dist.new_group(ranks=list(range(dist.get_world_size())))
+    return _SYNCBN_PG
+
+
 def parallel_model(config, model, rank, device):
     if not config.DDP:
         return model.to(device)
     sync = bool(config.synBN) and device.type == "cuda"
     if sync:
-        model = nn.SyncBatchNorm.convert_sync_batchnorm(model)
+        # SyncBN gets its OWN process group: its per-layer statistics all-reduces are small and
+        # latency-bound, and on the default group (one RCCL communicator / stream) they would
+        # queue behind DDP's 32 MiB gradient buckets in backward.  All ranks create it in the
+        # same order here.
+        model = nn.SyncBatchNorm.convert_sync_batchnorm(model, process_group=syncbn_group())
         from ..ops import convert_batchnorm
         convert_batchnorm(model)  # SyncBN -> fused HIP SyncBN (one fp64 all-reduce per layer)
     model = model.to(device)
@@ -113,7 +128,9 @@ def parallel_model(config, model, rank, device):
 
 
 def destroy_ddp_process(config):
+    global _SYNCBN_PG
     if config.DDP and is_dist():
+        _SYNCBN_PG = None
         dist.destroy_process_group()
 
 

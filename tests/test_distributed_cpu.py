@@ -20,7 +20,23 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, save_dir, out_dir):
+# training-step variants that exercise the DDP wiring differently
+VARIANTS = {
+    "enet": dict(model="enet"),
+    # aux head: extra logits + OHEM terms in the loss
+    "ddrnet_aux": dict(model="ddrnet", arch_type="DDRNet-23-slim", use_aux=True),
+    # detail head: detail_conv must get a (zero) gradient -- run WITHOUT static_graph so DDP's
+    # unused-parameter check would fail if it did not
+    "stdc_detail": dict(model="stdc", encoder_type="stdc1", use_detail_head=True, use_aux=False,
+                        ddp_static_graph=False),
+    # knowledge distillation from a (random-init) SMP teacher on every rank
+    "ddrnet_kd": dict(model="ddrnet", arch_type="DDRNet-23-slim", use_aux=False, kd_training=True,
+                      teacher_model="smp", teacher_encoder="resnet18", teacher_decoder="deeplabv3p",
+                      teacher_random_init=True),
+}
+
+
+def _worker(rank, world, port, save_dir, out_dir, variant="enet"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       LOCAL_RANK=str(rank), WORLD_SIZE=str(world))
     torch.set_num_threads(2)
@@ -34,6 +50,8 @@ def _worker(rank, world, port, save_dir, out_dir):
     c.crop_size, c.train_bs, c.val_bs, c.total_epoch = 32, 2, 2, 2
     c.base_workers, c.device, c.use_ema, c.use_tb = 0, "cpu", True, False
     c.save_dir = save_dir
+    for k, v in VARIANTS[variant].items():
+        setattr(c, k, v)
     c.init_dependent_config()
     tr = SegTrainer(c)
     assert c.DDP and c.gpu_num == world and c.global_rank == rank
@@ -45,11 +63,12 @@ def _worker(rank, world, port, save_dir, out_dir):
                 "itrs": tr.train_itrs}, os.path.join(out_dir, f"rank{rank}.pt"))
 
 
-@pytest.mark.timeout(600)
-def test_ddp_gloo_two_ranks(tmp_path):
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("variant", list(VARIANTS))
+def test_ddp_gloo_two_ranks(tmp_path, variant):
     save_dir = str(tmp_path / "save")
     out_dir = str(tmp_path)
-    mp.spawn(_worker, args=(2, _free_port(), save_dir, out_dir), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), save_dir, out_dir, variant), nprocs=2, join=True)
     r0 = torch.load(os.path.join(out_dir, "rank0.pt"), weights_only=True)
     r1 = torch.load(os.path.join(out_dir, "rank1.pt"), weights_only=True)
     # disjoint shards from the global rank

@@ -1,0 +1,149 @@
+"""HIP SyncBatchNorm (ops/bn.py + bn_act.hip, RCCL/gloo all-reduce of fp64 sums) across 2 ranks
+vs single-process BatchNorm2d over the concatenated batch: forward output, input / weight /
+bias gradients, running statistics and num_batches_tracked -- for the plain BN, the fused
+BN + residual + ReLU tail, and the conv-epilogue statistics path (conv_igemm slab ->
+bn_slab_sums -> all-reduce).  Reference wiring: utils/parallel.py:34-43 (SyncBN + DDP).
+
+Two processes share the one GPU of the box and talk over gloo (RCCL needs one GPU per rank)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+N, C, H, W = 4, 64, 12, 20
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _data():
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(N, C, H, W, generator=g) * 2 + 0.5
+    res = torch.randn(N, C, H, W, generator=g)
+    gy = torch.randn(N, C, H, W, generator=g)
+    conv_w = torch.randn(C, C, 3, 3, generator=g) / (9 * C) ** 0.5
+    bn_w = torch.rand(C, generator=g) + 0.5
+    bn_b = torch.randn(C, generator=g) * 0.1
+    return x, res, gy, conv_w, bn_w, bn_b
+
+
+def _make_bn(bn_w, bn_b, sync, pg=None):
+    import torch.nn as nn
+
+    from realtime_semantic_segmentation_pytorch_amd.ops import convert_batchnorm
+
+    bn = nn.BatchNorm2d(C)
+    with torch.no_grad():
+        bn.weight.copy_(bn_w)
+        bn.bias.copy_(bn_b)
+    if sync:
+        bn = nn.SyncBatchNorm.convert_sync_batchnorm(bn, process_group=pg)
+    convert_batchnorm(bn)
+    return bn.cuda()
+
+
+def _case(kind, x, res, gy, conv_w, bn, conv=None):
+    """-> (y, dx, dres)"""
+    from realtime_semantic_segmentation_pytorch_amd import ops
+
+    x = x.cuda().contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    r = res.cuda().contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    g = gy.cuda().contiguous(memory_format=torch.channels_last)
+    if kind == "plain":
+        y = bn(x)
+    elif kind == "tail":
+        y = ops.bn_act(x, bn, "relu", residual=r)
+    else:  # conv with the BN statistics in its epilogue, bf16
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = ops.conv_bn_act(x.to(torch.bfloat16), conv, bn, "relu")
+    y.float().backward(g)
+    return y.detach().float(), x.grad.float(), (r.grad.float() if r.grad is not None else None)
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      RTSEG_CONV_MFMA="1")
+    import torch.distributed as dist
+    import torch.nn as nn
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pg = dist.new_group(ranks=list(range(world)))
+    x, res, gy, conv_w, bn_w, bn_b = _data()
+    sl = slice(rank * N // world, (rank + 1) * N // world)
+    res_out = {}
+    for kind in ("plain", "tail", "conv"):
+        bn = _make_bn(bn_w, bn_b, True, pg)
+        conv = None
+        if kind == "conv":
+            conv = nn.Conv2d(C, C, 3, 1, 1, bias=False).cuda()
+            with torch.no_grad():
+                conv.weight.copy_(conv_w)
+            conv = conv.to(memory_format=torch.channels_last)
+        y, dx, dres = _case(kind, x[sl], res[sl], gy[sl], conv_w, bn, conv)
+        dw, db = bn.weight.grad.clone(), bn.bias.grad.clone()
+        dist.all_reduce(dw)  # DDP would sum (then average) the per-rank contributions
+        dist.all_reduce(db)
+        res_out[kind] = dict(y=y.cpu(), dx=dx.cpu(), dres=None if dres is None else dres.cpu(), dw=dw.cpu(),
+                             db=db.cpu(), rm=bn.running_mean.cpu(), rv=bn.running_var.cpu(),
+                             nbt=bn.num_batches_tracked.cpu(),
+                             cw=None if conv is None else conv.weight.grad.clone().cpu())
+        if conv is not None:
+            cw = res_out[kind]["cw"].cuda()
+            dist.all_reduce(cw)
+            res_out[kind]["cw"] = cw.cpu()
+    torch.save(res_out, os.path.join(out, f"rank{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_hip_syncbn_two_ranks_matches_full_batch_bn(tmp_path):
+    import torch.nn as nn
+
+    from realtime_semantic_segmentation_pytorch_amd import ops
+
+    assert ops.load(), "HIP extension must load on the GPU box"
+    mp.spawn(_worker, args=(2, _port(), str(tmp_path)), nprocs=2, join=True)
+    got = [torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=True) for r in (0, 1)]
+    x, res, gy, conv_w, bn_w, bn_b = _data()
+    os.environ["RTSEG_CONV_MFMA"] = "1"
+    try:
+        for kind in ("plain", "tail", "conv"):
+            bn = _make_bn(bn_w, bn_b, False)
+            conv = None
+            if kind == "conv":
+                conv = nn.Conv2d(C, C, 3, 1, 1, bias=False).cuda()
+                with torch.no_grad():
+                    conv.weight.copy_(conv_w)
+                conv = conv.to(memory_format=torch.channels_last)
+            y, dx, dres = _case(kind, x, res, gy, conv_w, bn, conv)
+            tol = dict(rtol=2e-2, atol=3e-2) if kind == "conv" else dict(rtol=1e-4, atol=2e-4)
+            y2 = torch.cat([got[0][kind]["y"], got[1][kind]["y"]])
+            dx2 = torch.cat([got[0][kind]["dx"], got[1][kind]["dx"]])
+            torch.testing.assert_close(y2, y.cpu(), **tol, msg=f"{kind}: forward")
+            torch.testing.assert_close(dx2, dx.cpu(), **tol, msg=f"{kind}: grad input")
+            if dres is not None:
+                torch.testing.assert_close(torch.cat([got[0][kind]["dres"], got[1][kind]["dres"]]), dres.cpu(),
+                                           **tol, msg=f"{kind}: grad residual")
+            for r in (0, 1):
+                g = got[r][kind]
+                torch.testing.assert_close(g["dw"], bn.weight.grad.cpu(), rtol=1e-3, atol=5e-2 if kind == "conv" else 1e-3,
+                                           msg=f"{kind}: grad weight")
+                torch.testing.assert_close(g["db"], bn.bias.grad.cpu(), rtol=1e-3, atol=5e-2 if kind == "conv" else 1e-3,
+                                           msg=f"{kind}: grad bias")
+                torch.testing.assert_close(g["rm"], bn.running_mean.cpu(), rtol=1e-3, atol=1e-3, msg=f"{kind}: mean")
+                torch.testing.assert_close(g["rv"], bn.running_var.cpu(), rtol=2e-3, atol=1e-3, msg=f"{kind}: var")
+                assert int(g["nbt"]) == int(bn.num_batches_tracked) == 1
+                if conv is not None:
+                    torch.testing.assert_close(g["cw"], conv.weight.grad.cpu(), rtol=3e-2, atol=3e-2,
+                                               msg="conv weight grad")
+    finally:
+        os.environ.pop("RTSEG_CONV_MFMA", None)

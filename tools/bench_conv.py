@@ -56,6 +56,9 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="fwd,dgrad,wgrad")
+    ap.add_argument("--cfgs", default="", help="comma list of RTSEG_IGEMM_CFG tile configs to sweep (fwd/dgrad)")
+    ap.add_argument("--shapes", default="", help="comma list of shape indices")
+    ap.add_argument("--wcfgs", default="", help="comma list of RTSEG_WGRAD_CFG configs to sweep (wgrad)")
     a = ap.parse_args()
     passes = set(a.only.split(","))
     assert ops.load()
@@ -63,7 +66,9 @@ def main():
     dev = "cuda"
     print(f"{'shape':34s} {'pass':7s} {'err':>9s} {'miopen':>8s} {'ours':>8s}  TF(mio/ours)  speedup", flush=True)
     conv_bw = torch.ops.aten.convolution_backward
-    for cin, h, w, cout, k, s in SHAPES:
+    cfgs = [c for c in a.cfgs.split(",") if c != ""] or [None]
+    shapes = [SHAPES[int(i)] for i in a.shapes.split(",")] if a.shapes else SHAPES
+    for cin, h, w, cout, k, s in shapes:
         n = a.batch
         torch.manual_seed(0)
         x = torch.randn(n, cin, h, w, device=dev, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
@@ -78,32 +83,42 @@ def main():
         dy = torch.randn_like(y_ref).contiguous(memory_format=torch.channels_last)
         tag = f"{n}x{cin}x{h}x{w}->{cout} k{k}s{s}"
         rows = []
-        if "fwd" in passes:
-            y, _ = torch.ops.rtseg.conv_igemm(x, wk, [s, s], [p, p], [1, 1], False, None, None, 0)
-            t_m = timeit(lambda: F.conv2d(x, wcl, None, s, p), a.iters)
-            t_o = timeit(lambda: torch.ops.rtseg.conv_igemm(x, wk, [s, s], [p, p], [1, 1], False, None, None, 0),
-                         a.iters)
-            t_os = timeit(lambda: torch.ops.rtseg.conv_igemm(x, wk, [s, s], [p, p], [1, 1], True, None, None, 0),
-                          a.iters)
-            rows.append(("fwd", relerr(y, y_ref), t_m, t_o))
-            rows.append(("fwd+st", 0.0, t_m, t_os))
-        if "dgrad" in passes:
-            dx_ref = conv_bw(dy, x, wcl, None, [s, s], [p, p], [1, 1], False, [0, 0], 1, [True, False, False])[0]
-            dx = torch.ops.rtseg.conv_igemm_dgrad(dy, wtr, list(x.shape), [s, s], [p, p], [1, 1])
-            t_m = timeit(lambda: conv_bw(dy, x, wcl, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
-                                         [True, False, False]), a.iters)
-            t_o = timeit(lambda: torch.ops.rtseg.conv_igemm_dgrad(dy, wtr, list(x.shape), [s, s], [p, p], [1, 1]),
-                         a.iters)
-            rows.append(("dgrad", relerr(dx, dx_ref), t_m, t_o))
+        for cfg in cfgs:
+            sfx = "" if cfg is None else f"@{cfg}"
+            if cfg is not None:
+                os.environ["RTSEG_IGEMM_CFG"] = cfg
+            if "fwd" in passes:
+                y, _ = torch.ops.rtseg.conv_igemm(x, wk, [s, s], [p, p], [1, 1], False, None, None, 0)
+                t_m = timeit(lambda: F.conv2d(x, wcl, None, s, p), a.iters)
+                t_o = timeit(lambda: torch.ops.rtseg.conv_igemm(x, wk, [s, s], [p, p], [1, 1], False, None, None, 0),
+                             a.iters)
+                rows.append(("fwd" + sfx, relerr(y, y_ref), t_m, t_o))
+                if cfg is None:
+                    t_os = timeit(lambda: torch.ops.rtseg.conv_igemm(x, wk, [s, s], [p, p], [1, 1], True, None, None,
+                                                                     0), a.iters)
+                    rows.append(("fwd+st", 0.0, t_m, t_os))
+            if "dgrad" in passes:
+                dx_ref = conv_bw(dy, x, wcl, None, [s, s], [p, p], [1, 1], False, [0, 0], 1, [True, False, False])[0]
+                dx = torch.ops.rtseg.conv_igemm_dgrad(dy, wtr, list(x.shape), [s, s], [p, p], [1, 1])
+                t_m = timeit(lambda: conv_bw(dy, x, wcl, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
+                                             [True, False, False]), a.iters)
+                t_o = timeit(lambda: torch.ops.rtseg.conv_igemm_dgrad(dy, wtr, list(x.shape), [s, s], [p, p], [1, 1]),
+                             a.iters)
+                rows.append(("dgrad" + sfx, relerr(dx, dx_ref), t_m, t_o))
+        os.environ.pop("RTSEG_IGEMM_CFG", None)
         if "wgrad" in passes:
             dw_ref = conv_bw(dy, x, wcl, None, [s, s], [p, p], [1, 1], False, [0, 0], 1, [False, True, False])[1]
-            dw = torch.ops.rtseg.conv_igemm_wgrad(x, dy, k, k, [s, s], [p, p], [1, 1])
             t_m = timeit(lambda: conv_bw(dy, x, wcl, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
                                          [False, True, False]), a.iters)
-            t_o = timeit(lambda: torch.ops.rtseg.conv_igemm_wgrad(x, dy, k, k, [s, s], [p, p], [1, 1]), a.iters)
-            rows.append(("wgrad", relerr(dw, dw_ref), t_m, t_o))
+            for wc in [c for c in a.wcfgs.split(",") if c != ""] or [None]:
+                if wc is not None:
+                    os.environ["RTSEG_WGRAD_CFG"] = wc
+                dw = torch.ops.rtseg.conv_igemm_wgrad(x, dy, k, k, [s, s], [p, p], [1, 1])
+                t_o = timeit(lambda: torch.ops.rtseg.conv_igemm_wgrad(x, dy, k, k, [s, s], [p, p], [1, 1]), a.iters)
+                rows.append(("wgrad" + ("" if wc is None else f"@{wc}"), relerr(dw, dw_ref), t_m, t_o))
+            os.environ.pop("RTSEG_WGRAD_CFG", None)
         for name, err, t_m, t_o in rows:
-            print(f"{tag:34s} {name:7s} {err:9.2e} {t_m:8.1f} {t_o:8.1f}  {flop / t_m / 1e6:5.0f}/{flop / t_o / 1e6:5.0f}"
+            print(f"{tag:34s} {name:9s} {err:9.2e} {t_m:8.1f} {t_o:8.1f}  {flop / t_m / 1e6:5.0f}/{flop / t_o / 1e6:5.0f}"
                   f"   {t_m / t_o:5.2f}x", flush=True)
         del x, dy, y_ref
         torch.cuda.empty_cache()
