@@ -216,6 +216,11 @@ def main():
         tag = f"{k[0]}:{name}"
         picks[tag] = picks.get(tag, 0) + 1
     extra["conv_kernel_choices"] = dict(sorted(picks.items()))  # per layer shape, per pass
+    dec_out = os.environ.get("RTSEG_DECISIONS_OUT")
+    if dec_out and rank == 0:  # full per-shape table: key -> (choice, [ms per candidate])
+        with open(dec_out, "w") as f:
+            for k, (_, name, ts) in sorted(decisions().items(), key=lambda kv: str(kv[0])):
+                f.write(f"{k}\t{name}\t{ts}\n")
     if rank == 0 and not a.no_infer:
         m = de_parallel(trainer.model)
         tag = f"{a.height}x{a.width}"

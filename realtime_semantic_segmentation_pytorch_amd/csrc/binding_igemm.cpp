@@ -87,7 +87,8 @@ std::tuple<at::Tensor, at::Tensor> conv_igemm(const at::Tensor& x, const at::Ten
 
 // dy [N,Cout,Ho,Wo] CL bf16, wt [Cin,KH,KW,Cout] bf16 -> dx [N,Cin,H,W] CL bf16
 at::Tensor conv_igemm_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
-                            at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation) {
+                            at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
+                            const std::optional<at::Tensor>& bias, const std::optional<at::Tensor>& addend) {
   check_act(dy, "grad_output");
   TORCH_CHECK(x_size.size() == 4, "rtseg.conv_igemm_dgrad: x_size must be [N, Cin, H, W]");
   TORCH_CHECK(wt.is_cuda() && wt.dim() == 4 && wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() &&
@@ -101,6 +102,19 @@ at::Tensor conv_igemm_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntA
   c10::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
   at::Tensor dx = at::empty({g.n, g.cin, g.h, g.w_in}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   g.x = dy.data_ptr(); g.w = wt.data_ptr(); g.y = dx.data_ptr();
+  g.scale_shift = nullptr;
+  if (bias.has_value() && bias->defined()) {  // transposed-conv forward: y = convT(x) + b
+    TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == at::kFloat && bias->is_contiguous() &&
+                    bias->numel() == g.cin,
+                "rtseg.conv_igemm_dgrad: bias must be fp32 [Cin]");
+    g.scale_shift = bias->data_ptr<float>();
+  }
+  g.res = nullptr;
+  if (addend.has_value() && addend->defined()) {  // dx = dgrad(dy) + addend, fused in the epilogue
+    check_act(*addend, "addend");
+    TORCH_CHECK(addend->sizes() == dx.sizes(), "rtseg.conv_igemm_dgrad: addend must match dx");
+    g.res = addend->data_ptr();
+  }
   launch_conv_igemm_dgrad(g, cur_stream());
   return dx;
 }
@@ -128,8 +142,8 @@ at::Tensor conv_igemm_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t k
 TORCH_LIBRARY_FRAGMENT(rtseg, m) {
   m.def("conv_igemm(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats, "
         "Tensor? scale_shift, Tensor? residual, int act) -> (Tensor, Tensor)");
-  m.def("conv_igemm_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation) "
-        "-> Tensor");
+  m.def("conv_igemm_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
+        "Tensor? bias=None, Tensor? addend=None) -> Tensor");
   m.def("conv_igemm_wgrad(Tensor x, Tensor dy, int kh, int kw, int[] stride, int[] padding, int[] dilation) "
         "-> Tensor");
 }

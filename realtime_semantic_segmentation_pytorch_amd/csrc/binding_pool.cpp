@@ -95,9 +95,67 @@ static at::Tensor adaptive_avg_pool_bwd(const at::Tensor& gy, int64_t in_h, int6
   return gx;
 }
 
+static Tensor4 idx_view(const at::Tensor& idx) {
+  TORCH_CHECK(idx.is_cuda() && idx.dim() == 4 && idx.scalar_type() == at::kLong, "rtseg.unpool: indices must be int64 4-D");
+  Tensor4 v{};
+  v.data = idx.data_ptr();
+  v.dtype = -1;
+  v.n = static_cast<int>(idx.size(0)); v.c = static_cast<int>(idx.size(1));
+  v.h = static_cast<int>(idx.size(2)); v.w = static_cast<int>(idx.size(3));
+  v.sn = idx.stride(0); v.sc = idx.stride(1); v.sh = idx.stride(2); v.sw = idx.stride(3);
+  return v;
+}
+
+// max pool with PyTorch-style int64 indices: (y, flat indices, uint8 window map for the backward)
+static std::tuple<at::Tensor, at::Tensor, at::Tensor> max_pool_indices(const at::Tensor& x, at::IntArrayRef kernel,
+                                                                       at::IntArrayRef stride, at::IntArrayRef padding) {
+  auto [y, win] = pool2d_fwd(x, kernel, stride, padding, kPoolMax, true);
+  const PoolParams p = pool_params(kernel, stride, padding, kPoolMax, true, false);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  at::Tensor idx = at::empty(y.sizes(), y.options().dtype(at::kLong).memory_format(y.suggest_memory_format()));
+  launch_maxpool_flat_index(win.data_ptr<uint8_t>(), idx_view(idx), static_cast<int>(x.size(3)), p, cur_stream());
+  return {y, idx, win};
+}
+
+// MaxUnpool2d with kernel == stride, no padding: y [N, C, out_h, out_w] gathered from x / idx
+static at::Tensor max_unpool_fwd(const at::Tensor& x, const at::Tensor& idx, int64_t kh, int64_t kw, int64_t out_h,
+                                 int64_t out_w) {
+  check_x(x);
+  TORCH_CHECK(idx.sizes() == x.sizes(), "rtseg.max_unpool: indices must match the input");
+  TORCH_CHECK(kh > 0 && kw > 0 && out_h >= x.size(2) * kh - kh + 1 && out_w >= x.size(3) * kw - kw + 1,
+              "rtseg.max_unpool: output too small for the windows");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  at::Tensor y = at::empty({x.size(0), x.size(1), out_h, out_w}, x.options().memory_format(x.suggest_memory_format()));
+  launch_unpool_gather(view4(x), idx_view(idx), view4(y), static_cast<int>(kh), static_cast<int>(kw), cur_stream());
+  return y;
+}
+
+// backward of max_unpool_fwd: gx[n, c, i, j] = gy at the plane position idx[n, c, i, j]
+static at::Tensor max_unpool_bwd(const at::Tensor& gy, const at::Tensor& idx) {
+  check_x(gy);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(gy.device());
+  at::Tensor gx = at::empty(idx.sizes(), gy.options().memory_format(gy.suggest_memory_format()));
+  launch_unpool_bwd(view4(gy), idx_view(idx), view4(gx), cur_stream());
+  return gx;
+}
+
+// AdaptiveMaxPool2d(1): (y [N, C, 1, 1], idx int64 [N, C, 1, 1])
+static std::tuple<at::Tensor, at::Tensor> global_max_pool(const at::Tensor& x) {
+  check_x(x);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  at::Tensor y = at::empty({x.size(0), x.size(1), 1, 1}, x.options());
+  at::Tensor idx = at::empty({x.size(0), x.size(1), 1, 1}, x.options().dtype(at::kLong));
+  launch_global_max(view4(x), y.data_ptr(), idx.data_ptr<int64_t>(), cur_stream());
+  return {y, idx};
+}
+
 }  // namespace rtseg
 
 TORCH_LIBRARY_FRAGMENT(rtseg, m) {
+  m.def("global_max_pool(Tensor x) -> (Tensor, Tensor)");
+  m.def("max_pool_indices(Tensor x, int[] kernel, int[] stride, int[] padding) -> (Tensor, Tensor, Tensor)");
+  m.def("max_unpool_fwd(Tensor x, Tensor idx, int kh, int kw, int out_h, int out_w) -> Tensor");
+  m.def("max_unpool_bwd(Tensor gy, Tensor idx) -> Tensor");
   m.def("pool2d_fwd(Tensor x, int[] kernel, int[] stride, int[] padding, int mode, bool count_include_pad) "
         "-> (Tensor, Tensor)");
   m.def("pool2d_bwd(Tensor gy, Tensor idx, int in_h, int in_w, int[] kernel, int[] stride, int[] padding, int mode, "
@@ -111,4 +169,8 @@ TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
   m.impl("pool2d_bwd", &rtseg::pool2d_bwd);
   m.impl("adaptive_avg_pool_fwd", &rtseg::adaptive_avg_pool_fwd);
   m.impl("adaptive_avg_pool_bwd", &rtseg::adaptive_avg_pool_bwd);
+  m.impl("max_pool_indices", &rtseg::max_pool_indices);
+  m.impl("max_unpool_fwd", &rtseg::max_unpool_fwd);
+  m.impl("max_unpool_bwd", &rtseg::max_unpool_bwd);
+  m.impl("global_max_pool", &rtseg::global_max_pool);
 }

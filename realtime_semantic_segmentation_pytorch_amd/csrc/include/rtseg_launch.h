@@ -162,7 +162,9 @@ bool conv_igemm_supported(const ConvGeom& g, int mode);
 int conv_igemm_slabs(const ConvGeom& g);
 void launch_slab_compact(const float* in, int rows, int width, int chunk, float* out, hipStream_t st);
 void launch_conv_igemm_fwd(const ConvGeom& g, hipStream_t st);
-// g.x = dy [N,Ho,Wo,Cout], g.w = [Cin][KH][KW][Cout] bf16, g.y = dx [N,H,W,Cin]
+// g.x = dy [N,Ho,Wo,Cout], g.w = [Cin][KH][KW][Cout] bf16, g.y = dx [N,H,W,Cin];
+// g.scale_shift, when set, is a [Cin] bias added to dx (the forward of a transposed conv);
+// g.res, when set, is a bf16 tensor of dx's layout added to dx (a residual branch's gradient)
 void launch_conv_igemm_dgrad(const ConvGeom& g, hipStream_t st);
 // g.x = x [N,H,W,Cin], g.y = dy [N,Ho,Wo,Cout]; ws fp32 of conv_igemm_wgrad_ws_elems(g);
 // dw fp32 [Cout][Cin][KH][KW]
@@ -184,6 +186,14 @@ struct GapPlan {
   int vec, cpb, cblocks, per_slice, slices;
 };
 GapPlan gap_plan(const Tensor4& x);
+// indexed max pool / max unpool (int64 flat plane indices, PyTorch's convention); idx is a
+// Tensor4 view of an int64 tensor (its dtype field is ignored)
+void launch_unpool_gather(const Tensor4& x, const Tensor4& idx, const Tensor4& y, int kh, int kw, hipStream_t st);
+void launch_unpool_bwd(const Tensor4& gy, const Tensor4& idx, const Tensor4& gx, hipStream_t st);
+void launch_maxpool_flat_index(const uint8_t* win, const Tensor4& out, int in_w, const PoolParams& p,
+                               hipStream_t st);
+// global max pool (AdaptiveMaxPool2d(1)) with first-max int64 argmax: y dense [N, C], idx [N, C]
+void launch_global_max(const Tensor4& x, void* y, int64_t* idx, hipStream_t st);
 // global average pool; part: fp32 workspace of plan.slices * N * C
 void launch_gap_fwd(const Tensor4& x, const Tensor4& y, const GapPlan& plan, float* part, hipStream_t st);
 

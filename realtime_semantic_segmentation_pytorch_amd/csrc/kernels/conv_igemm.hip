@@ -28,8 +28,9 @@
 //    ring keeps NST-1 K-steps in flight across tile boundaries, published by a counted vmcnt +
 //    raw s_barrier (never vmcnt(0) inside the stream);
 //  * epilogue straight from the accumulators (D rows = channels: each lane owns 4 consecutive
-//    channels of one pixel per register quad -> 8-byte stores), packed at the end of a tile and
-//    stored after the next K-step's barrier so the stores never sit in front of a DMA wait;
+//    channels of one pixel per register quad -> 8-byte stores), run after the NEXT K-step's
+//    barrier and before its DMA issue, so the stores retire under that step's MFMAs and never
+//    hold up a ring wait;
 //    optional per-channel (sum, sum of squares) of the bf16 outputs for training BatchNorm
 //    (one [2*Cout] slab row per block), or the inference BN scale/shift + residual + ReLU(6).
 //
@@ -138,6 +139,8 @@ struct IgArgs {
   float* part;
   const float* ss;
   const uint16_t* res;
+  const float* bias;      // [cout] added to the accumulators first (transposed conv), or null
+  const uint16_t* addend; // bf16 tensor of the output's layout added in the epilogue, or null
   int act;
   int H, W, C;            // gathered operand [N][H][W][C]
   int Hv, Wv;             // virtual output grid
@@ -256,13 +259,10 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
 
-  // pending (packed bf16) output of the previous tile, stored after the next barrier (small
-  // wave tiles; big ones store at once -- the deferred copy would cost TI*TJ*8 registers)
-  constexpr bool DEFER = TI * TJ <= 4;
-  uint2 pend[DEFER ? TI : 1][DEFER ? TJ : 1][4];
+  // A finished tile is packed and stored at the start of the NEXT K-step, after its barrier and
+  // before its DMA issue: the accumulators are the deferred buffer (no extra registers), and the
+  // stores get a whole compute step to retire before any counted vmcnt waits behind them.
   int64_t pend_off[TJ];
-  bool pend_ok[TJ];
-  bool have_pend = false;
   const int co_lane = co0 + wn * (BN / WN) + 4 * fhi;  // + ti*32 + 8g
 
   auto pack_tile = [&](int mt) {
@@ -282,7 +282,6 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
       const uint32_t t = a.fwv.divmod(static_cast<uint32_t>(ok ? m : 0), wv);
       const uint32_t n = a.fhv.divmod(t, hv);
       const int ho = static_cast<int>(hv) * a.osh + a.oph, wo = static_cast<int>(wv) * a.osw + a.opw;
-      pend_ok[tj] = ok;
       pend_off[tj] = ((static_cast<int64_t>(n) * a.Ho + ho) * a.Wo + wo) * a.cout;
 #pragma unroll
       for (int ti = 0; ti < TI; ++ti) {
@@ -292,6 +291,17 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
           float v[4];
 #pragma unroll
           for (int q = 0; q < 4; ++q) v[q] = acc[ti][tj][4 * g + q];
+          if (a.bias != nullptr) {
+            const float4 bb = *reinterpret_cast<const float4*>(a.bias + min(co, a.cout - 4));
+            v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+          }
+          if (a.addend != nullptr && ok && co < a.cout) {  // e.g. a residual branch's gradient
+            const uint2 r = *reinterpret_cast<const uint2*>(a.addend + pend_off[tj] + co);
+            v[0] += bf16_to_f32(static_cast<uint16_t>(r.x & 0xffff));
+            v[1] += bf16_to_f32(static_cast<uint16_t>(r.x >> 16));
+            v[2] += bf16_to_f32(static_cast<uint16_t>(r.y & 0xffff));
+            v[3] += bf16_to_f32(static_cast<uint16_t>(r.y >> 16));
+          }
           if constexpr (EPI == 1) {
             const int cc = min(co, a.cout - 4);
             const float4 sc = *reinterpret_cast<const float4*>(a.ss + cc);
@@ -311,11 +321,7 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
           uint2 pk;
           pk.x = pack2(v[0], v[1]);
           pk.y = pack2(v[2], v[3]);
-          if constexpr (DEFER) {
-            pend[ti][tj][g] = pk;
-          } else if (ok && co < a.cout) {
-            *reinterpret_cast<uint2*>(a.y + pend_off[tj] + co) = pk;
-          }
+          if (ok && co < a.cout) *reinterpret_cast<uint2*>(a.y + pend_off[tj] + co) = pk;
           if constexpr (STATS) {
             const bool sok = ok && co < a.cout;
             const float q0 = sok ? bf16_to_f32(static_cast<uint16_t>(pk.x & 0xffff)) : 0.f;
@@ -360,34 +366,16 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
       }
     }
   };
-  auto store_pending = [&]() {
-    if constexpr (!DEFER) return;
-#pragma unroll
-    for (int tj = 0; tj < TJ; ++tj) {
-      if (!pend_ok[tj]) continue;
-#pragma unroll
-      for (int ti = 0; ti < TI; ++ti)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int co = co_lane + ti * 32 + 8 * g;
-          if (co < a.cout) *reinterpret_cast<uint2*>(a.y + pend_off[tj] + co) = pend[DEFER ? ti : 0][DEFER ? tj : 0][g];
-        }
-    }
-  };
-
   const int total = my_tiles * nk;
   if (nk == 0) {  // empty tap set (a dgrad phase no tap reaches): the outputs are zero
-    for (int i = 0; i < my_tiles; ++i) {
-      pack_tile(mfirst + i * mstep);
-      store_pending();
-    }
+    for (int i = 0; i < my_tiles; ++i) pack_tile(mfirst + i * mstep);
   } else {
     if (my_tiles > 0) set_rows(mfirst);
 #pragma unroll
     for (int p = 0; p < NST - 1; ++p)
       if (p < total) stage();
 
-    int kk = 0, ord = 0, buf = 0;
+    int kk = 0, ord = 0, buf = 0, pend_mt = -1;
     for (int gs = 0; gs < total; ++gs) {
       if (NST >= 3 && gs + 1 < total) {
         vm_wait<(NST - 2) * PER>();
@@ -396,16 +384,19 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // step gs landed for every wave; step gs-1's buffer is free
-      if (have_pend) {
-        store_pending();
-        have_pend = false;
+      if (pend_mt >= 0) {  // previous tile: epilogue + stores, ahead of this step's DMA issue
+        pack_tile(pend_mt);
+        pend_mt = -1;
       }
       if (gs + NST - 1 < total) stage();
 
       const uint4* Wt = lds + buf * STAGE + (wn * (BN / WN) + frow) * 8;
       const uint4* Pt = lds + buf * STAGE + BN * 8 + (wm * (BM / WM) + frow) * 8;
-      // fragments of sub-step s+1 are read while the MFMAs of sub-step s run
-      bf16x8_t af[2][TI], bfg[2][TJ];
+      // fragments of sub-step s+1 are read while the MFMAs of sub-step s run (double-buffered
+      // registers for the 64 x 64 wave tiles; the 64 x 128 ones have no room and rely on the
+      // partner wave of the SIMD to cover the read latency)
+      constexpr int FB = TI + TJ <= 4 ? 2 : 1;
+      bf16x8_t af[FB][TI], bfg[FB][TJ];
       auto load_frags = [&](int s, int slot) {
         const int ch = ((2 * s + fhi) ^ fx);
 #pragma unroll
@@ -413,27 +404,31 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
 #pragma unroll
         for (int tj = 0; tj < TJ; ++tj) bfg[slot][tj] = as_frag(Pt[tj * 256 + ch]);
       };
-      load_frags(0, 0);
+      if constexpr (FB == 2) load_frags(0, 0);
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        if (s < 3) load_frags(s + 1, (s + 1) & 1);
+        if constexpr (FB == 2) {
+          if (s < 3) load_frags(s + 1, (s + 1) & 1);
+        } else {
+          load_frags(s, 0);
+        }
+        const int sl = FB == 2 ? (s & 1) : 0;
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int ti = 0; ti < TI; ++ti)
 #pragma unroll
           for (int tj = 0; tj < TJ; ++tj)
-            acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s & 1][ti], bfg[s & 1][tj], acc[ti][tj], 0, 0, 0);
+            acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[sl][ti], bfg[sl][tj], acc[ti][tj], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
       }
       if (++buf == NST) buf = 0;
       if (++kk == nk) {
         kk = 0;
-        pack_tile(mfirst + ord * mstep);
+        pend_mt = mfirst + ord * mstep;
         ++ord;
-        have_pend = DEFER;
       }
     }
-    if (have_pend) store_pending();
+    if (pend_mt >= 0) pack_tile(pend_mt);
   }
 
 }
@@ -781,6 +776,8 @@ void launch_conv_igemm_dgrad(const ConvGeom& g, hipStream_t st) {
       k.x = static_cast<const uint16_t*>(g.x);
       k.w = static_cast<const uint16_t*>(g.w);
       k.y = static_cast<uint16_t*>(g.y);
+      k.bias = g.scale_shift;  // dgrad launches reuse the field as an optional bias (transposed conv)
+      k.addend = static_cast<const uint16_t*>(g.res);  // ... and res as an optional addend
       k.H = g.ho; k.W = g.wo; k.C = g.cout;
       k.Hv = (g.h - a + g.sh - 1) / g.sh;
       k.Wv = (g.w_in - b + g.sw - 1) / g.sw;

@@ -432,3 +432,166 @@ void launch_gap_fwd(const Tensor4& x, const Tensor4& y, const GapPlan& pl, float
 }
 
 }  // namespace rtseg
+
+// ---------------------------------------------------------------------------------------------
+// MaxPool2d(return_indices=True) / MaxUnpool2d (reference enet.py:131,139, segnet.py:54,65).
+// Indices follow PyTorch: int64 flat offsets h * W + w into each input plane.  Unpooling with
+// kernel == stride and no padding (the paired pool's windows tile the plane) is a GATHER: output
+// pixel (h, w) belongs to exactly one window (h / kh, w / kw) and takes that window's value iff
+// the window's index names it -- every output is written once, no zero-fill, no scatter.  The
+// same kernel is the backward of the indexed max pool.
+namespace rtseg {
+namespace {
+
+template <typename T>
+__global__ void __launch_bounds__(256) unpool_gather_kernel(Tensor4 x, Tensor4 idx, Tensor4 y, int kh, int kw) {
+  const int64_t total = static_cast<int64_t>(y.n) * y.c * y.h * y.w;
+  const T* xs = static_cast<const T*>(x.data);
+  const int64_t* is = static_cast<const int64_t*>(idx.data);
+  T* ys = static_cast<T*>(y.data);
+  for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+       e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    // e enumerates y in (n, h, w, c) order: channel-fastest, coalesced for channels-last y
+    const int c = static_cast<int>(e % y.c);
+    int64_t r = e / y.c;
+    const int w = static_cast<int>(r % y.w);
+    r /= y.w;
+    const int h = static_cast<int>(r % y.h);
+    const int n = static_cast<int>(r / y.h);
+    const int i = h / kh, j = w / kw;
+    float v = 0.f;
+    if (i < x.h && j < x.w) {
+      const int64_t want = static_cast<int64_t>(h) * y.w + w;
+      if (is[n * idx.sn + c * idx.sc + i * idx.sh + j * idx.sw] == want)
+        v = Io<T>::ld(xs + n * x.sn + c * x.sc + i * x.sh + j * x.sw);
+    }
+    Io<T>::st(ys + n * y.sn + c * y.sc + h * y.sh + w * y.sw, v);
+  }
+}
+
+// gx[n, c, i, j] = gy[n, c, idx / W, idx % W]   (backward of the unpool)
+template <typename T>
+__global__ void __launch_bounds__(256) unpool_bwd_kernel(Tensor4 gy, Tensor4 idx, Tensor4 gx) {
+  const int64_t total = static_cast<int64_t>(gx.n) * gx.c * gx.h * gx.w;
+  const T* gs = static_cast<const T*>(gy.data);
+  const int64_t* is = static_cast<const int64_t*>(idx.data);
+  T* xs = static_cast<T*>(gx.data);
+  for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+       e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int c = static_cast<int>(e % gx.c);
+    int64_t r = e / gx.c;
+    const int j = static_cast<int>(r % gx.w);
+    r /= gx.w;
+    const int i = static_cast<int>(r % gx.h);
+    const int n = static_cast<int>(r / gx.h);
+    const int64_t f = is[n * idx.sn + c * idx.sc + i * idx.sh + j * idx.sw];
+    float v = 0.f;
+    if (f >= 0 && f < static_cast<int64_t>(gy.h) * gy.w) {
+      const int64_t hh = f / gy.w, ww = f - hh * gy.w;
+      v = Io<T>::ld(gs + n * gy.sn + c * gy.sc + hh * gy.sh + ww * gy.sw);
+    }
+    Io<T>::st(xs + n * gx.sn + c * gx.sc + i * gx.sh + j * gx.sw, v);
+  }
+}
+
+// uint8 window offsets [N, OH, OW, C] (pool2d_fwd's argmax map) -> int64 flat plane indices
+__global__ void __launch_bounds__(256) maxpool_flat_index_kernel(const uint8_t* __restrict__ win, Tensor4 out,
+                                                                 int in_w, PoolParams p) {
+  const int64_t total = static_cast<int64_t>(out.n) * out.c * out.h * out.w;
+  int64_t* os = static_cast<int64_t*>(out.data);
+  for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+       e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int c = static_cast<int>(e % out.c);
+    int64_t r = e / out.c;
+    const int ow = static_cast<int>(r % out.w);
+    r /= out.w;
+    const int oh = static_cast<int>(r % out.h);
+    const int n = static_cast<int>(r / out.h);
+    const int k = win[e];
+    const int hh = oh * p.sh - p.ph + k / p.kw, ww = ow * p.sw - p.pw + k % p.kw;
+    os[n * out.sn + c * out.sc + oh * out.sh + ow * out.sw] = static_cast<int64_t>(hh) * in_w + ww;
+  }
+}
+
+}  // namespace
+
+void launch_unpool_gather(const Tensor4& x, const Tensor4& idx, const Tensor4& y, int kh, int kw, hipStream_t st) {
+  const int64_t total = static_cast<int64_t>(y.n) * y.c * y.h * y.w;
+  by_dtype(y.dtype, [&](auto tag) {
+    using T = decltype(tag);
+    unpool_gather_kernel<T><<<stream_grid(total, 256), 256, 0, st>>>(x, idx, y, kh, kw);
+  });
+}
+
+void launch_unpool_bwd(const Tensor4& gy, const Tensor4& idx, const Tensor4& gx, hipStream_t st) {
+  const int64_t total = static_cast<int64_t>(gx.n) * gx.c * gx.h * gx.w;
+  by_dtype(gx.dtype, [&](auto tag) {
+    using T = decltype(tag);
+    unpool_bwd_kernel<T><<<stream_grid(total, 256), 256, 0, st>>>(gy, idx, gx);
+  });
+}
+
+void launch_maxpool_flat_index(const uint8_t* win, const Tensor4& out, int in_w, const PoolParams& p,
+                               hipStream_t st) {
+  const int64_t total = static_cast<int64_t>(out.n) * out.c * out.h * out.w;
+  maxpool_flat_index_kernel<<<stream_grid(total, 256), 256, 0, st>>>(win, out, in_w, p);
+}
+
+}  // namespace rtseg
+
+// ---------------------------------------------------------------------------------------------
+// Global max pool with argmax (AdaptiveMaxPool2d(1): canet.py:103, dfanet.py:149,
+// pp_liteseg.py:190).  Block = (image, 64-channel group); 4 rows of 64 lanes scan the plane
+// (channel-fastest lanes: coalesced for channels-last), LDS merge.  Ties keep the first pixel
+// and NaN wins, as ATen's adaptive max pool.  idx: int64 flat plane index [N, C].
+namespace rtseg {
+namespace {
+
+__device__ __forceinline__ bool gmax_better(float v, int i, float m, int mi) {
+  if (v != v) return !(m != m) || i < mi;  // NaN propagates (first NaN)
+  if (m != m) return false;
+  return v > m || (v == m && i < mi);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) global_max_kernel(Tensor4 x, T* __restrict__ y, int64_t* __restrict__ idx) {
+  __shared__ float sm[256];
+  __shared__ int si[256];
+  const int n = blockIdx.y, c = blockIdx.x * 64 + (threadIdx.x & 63), row = threadIdx.x >> 6;
+  const T* xp = static_cast<const T*>(x.data);
+  const int hw = x.h * x.w;
+  float m = -INFINITY;
+  int mi = 0x7fffffff;
+  if (c < x.c) {
+    const T* xb = xp + static_cast<int64_t>(n) * x.sn + static_cast<int64_t>(c) * x.sc;
+    for (int p = row; p < hw; p += 4) {
+      const int hh = p / x.w, ww = p - hh * x.w;
+      const float v = Io<T>::ld(xb + static_cast<int64_t>(hh) * x.sh + static_cast<int64_t>(ww) * x.sw);
+      if (gmax_better(v, p, m, mi)) { m = v; mi = p; }
+    }
+  }
+  sm[threadIdx.x] = m;
+  si[threadIdx.x] = mi;
+  __syncthreads();
+  if (row == 0 && c < x.c) {
+    for (int r = 1; r < 4; ++r) {
+      const float v = sm[threadIdx.x + 64 * r];
+      const int i = si[threadIdx.x + 64 * r];
+      if (gmax_better(v, i, m, mi)) { m = v; mi = i; }
+    }
+    Io<T>::st(y + static_cast<int64_t>(n) * x.c + c, m);
+    idx[static_cast<int64_t>(n) * x.c + c] = mi == 0x7fffffff ? 0 : mi;
+  }
+}
+
+}  // namespace
+
+// y: dense [N, C] of x's dtype, idx: int64 [N, C]
+void launch_global_max(const Tensor4& x, void* y, int64_t* idx, hipStream_t st) {
+  by_dtype(x.dtype, [&](auto tag) {
+    using T = decltype(tag);
+    global_max_kernel<T><<<dim3((x.c + 63) / 64, x.n), 256, 0, st>>>(x, static_cast<T*>(y), idx);
+  });
+}
+
+}  // namespace rtseg

@@ -79,6 +79,8 @@ def get_model(config):
         ops.convert_tap_convs(model)
     if getattr(config, "dilated_group_convs", True):
         ops.convert_dilated_group_convs(model)
+    if getattr(config, "hip_deconv", True):
+        ops.convert_transposed_convs(model)
     return model
 
 

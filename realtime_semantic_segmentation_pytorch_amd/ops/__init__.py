@@ -16,11 +16,13 @@ from .postprocess import colorize, colorize_reference
 from .confmat import confusion_matrix, confusion_matrix_reference
 from .dwconv import DepthwiseConv2d, convert_depthwise, depthwise_ok, dw_conv2d
 from .pool import (avg_pool2d, max_pool2d, adaptive_avg_pool2d, convert_pooling, AvgPool2d, MaxPool2d,
-                   AdaptiveAvgPool2d)
+                   AdaptiveAvgPool2d, MaxUnpool2d, max_pool2d_with_indices, max_unpool2d, AdaptiveMaxPool2d,
+                   adaptive_max_pool2d)
 from .tapconv import TapConv2d, convert_tap_convs, tap_conv2d, tapconv_ok
 from .dilated import DilatedGroupConv2d, convert_dilated_group_convs, dilated_group_conv2d, dilated_group_ok
 from .optim import FusedAdam, FusedAdamW, FusedSGD
 from .conv import conv_ok, conv_bn_stats, conv_bn_act_eval, conv_bn_act, conv_forward
+from .deconv import TransposedConv2d, conv_transpose2d, convert_transposed_convs, deconv_ok
 
 __all__ = [
     "load", "use_hip", "hip_disabled", "library_path",
@@ -29,8 +31,9 @@ __all__ = [
     "colorize", "colorize_reference", "kd_kl_div", "kd_kl_div_reference", "detail_loss", "detail_loss_reference", "detail_target_reference", "confusion_matrix", "confusion_matrix_reference",
     "DepthwiseConv2d", "convert_depthwise", "depthwise_ok", "dw_conv2d",
     "avg_pool2d", "max_pool2d", "adaptive_avg_pool2d", "convert_pooling", "AvgPool2d", "MaxPool2d",
-    "AdaptiveAvgPool2d", "TapConv2d", "convert_tap_convs", "tap_conv2d", "tapconv_ok",
+    "AdaptiveAvgPool2d", "AdaptiveMaxPool2d", "adaptive_max_pool2d", "MaxUnpool2d", "max_pool2d_with_indices", "max_unpool2d", "TapConv2d", "convert_tap_convs", "tap_conv2d", "tapconv_ok",
     "DilatedGroupConv2d", "convert_dilated_group_convs", "dilated_group_conv2d", "dilated_group_ok",
     "FusedSGD", "FusedAdam", "FusedAdamW", "conv_ok", "conv_bn_stats", "conv_bn_act_eval", "conv_bn_act", "conv_forward",
+    "TransposedConv2d", "conv_transpose2d", "convert_transposed_convs", "deconv_ok",
     "bn_act", "bn_act_code", "bn_fused_ok", "convert_batchnorm", "FusedBatchNorm2d", "FusedSyncBatchNorm",
 ]

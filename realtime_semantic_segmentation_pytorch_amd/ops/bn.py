@@ -29,6 +29,8 @@ MASK_NONE, MASK_FROM_Y, MASK_FROM_X, MASK_BITS = 0, 1, 2, 3
 # residual + activation: the forward writes a 1-bit-per-element activation-derivative mask
 # (MASK_BITS) instead of the backward re-reading the bf16 output y twice (RTSEG_BN_BITS=0: off)
 _USE_BITS = os.environ.get("RTSEG_BN_BITS", "1") != "0"
+# residual-gradient hand-off to the upstream conv's dgrad (RTSEG_RES_HANDOFF=0: off, for A/B)
+_HANDOFF = os.environ.get("RTSEG_RES_HANDOFF", "1") != "0"
 
 
 def act_code(act) -> Optional[int]:
@@ -95,6 +97,16 @@ class _BNActFn(torch.autograd.Function):
         ctx.act, ctx.mask, ctx.pg = act, mask, pg
         ctx.batch_stats = use_batch_stats
         ctx.has_res = residual is not None
+        # residual add whose residual is the input of an upstream routed conv (DDRNet's RB, ResNet
+        # BasicBlock): hand the residual gradient to that conv, whose dgrad epilogue adds it --
+        # autograd's separate gradient-accumulation add over the whole tensor disappears
+        ctx.handoff = None
+        if residual is not None and residual.requires_grad and _HANDOFF:
+            from .conv import find_conv_consumer
+
+            node = find_conv_consumer(x, residual)
+            if node is not None and node.addend_slot is None:
+                node.addend_slot = ctx.handoff = []
         ctx.has_w = weight is not None
         ctx.save_for_backward(x, y if mask == MASK_FROM_Y else bits, mi, ss, sums, weight)
         return y
@@ -103,14 +115,25 @@ class _BNActFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, y, mi, ss, sums, weight = ctx.saved_tensors
         dy = _aligned_cl(dy)
-        bsums = None
-        if ctx.pg is not None:
-            bsums = ops().bn_bwd_sums(dy, x, y, mi, ss, ctx.act, ctx.mask)
-            dist.all_reduce(bsums, group=ctx.pg)
+        bsums = local = None
         want_dres = ctx.has_res and ctx.needs_input_grad[3]
         want_dw = ctx.has_w and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
+        if ctx.pg is not None:
+            bsums = ops().bn_bwd_sums(dy, x, y, mi, ss, ctx.act, ctx.mask)
+            if want_dw:
+                local = bsums.clone()
+            dist.all_reduce(bsums, group=ctx.pg)
         dx, dres, dw, db = ops().bn_backward(dy, x, y, bsums, sums, mi, ss, weight, ctx.act,
                                              ctx.mask, want_dres, ctx.batch_stats, want_dw)
+        if local is not None:
+            # parameter gradients are this rank's contribution (DDP averages them), as in torch's
+            # SyncBatchNorm; only the input-gradient coefficients use the all-reduced sums
+            c = local.numel() // 2
+            dw = (local[c:] * mi[c:].double()).float()
+            db = local[:c].float()
+        if want_dres and ctx.handoff is not None:
+            ctx.handoff.append(dres)  # the conv node adds it in its dgrad epilogue
+            dres = None
         return (dx, dw if want_dw else None, db if want_dw else None,
                 dres if want_dres else None, None, None, None, None, None)
 

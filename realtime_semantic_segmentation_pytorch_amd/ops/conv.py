@@ -129,6 +129,8 @@ class _ConvFn(torch.autograd.Function):
         impl = _fwd_impl(x, wk, conv, key, stats)
         if impl == "igemm":
             y, part = ops().conv_igemm(x, wk, stride, padding, dilation, stats, None, None, 0)
+        elif impl == "igemm_nostats":  # short-K convs: the epilogue reduction costs more than a pass
+            y, part = ops().conv_igemm(x, wk, stride, padding, dilation, False, None, None, 0)
         elif impl == "mfma":
             y, part = ops().conv_mfma(x, wk, stride, padding, dilation, stats, None, None, 0)
         else:
@@ -138,6 +140,10 @@ class _ConvFn(torch.autograd.Function):
             part = None
         ctx.save_for_backward(x, wk)
         ctx.conv, ctx.key = conv, key
+        # identity of the input, so a residual-add node downstream can hand this node the
+        # residual branch's gradient to fuse into the dgrad epilogue (see ops.bn)
+        ctx.in_key = (x.data_ptr(), tuple(x.shape), x.dtype)
+        ctx.addend_slot = None
         ctx.wdtype = weight.dtype
         if part is not None:
             ctx.mark_non_differentiable(part)
@@ -153,8 +159,9 @@ class _ConvFn(torch.autograd.Function):
             dy = dy.clone(memory_format=torch.channels_last)
         want_dx, want_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         dx = dw = None
+        addend = ctx.addend_slot.pop() if ctx.addend_slot else None
         if want_dx:
-            dx = _dgrad(x, dy, wk, conv, key, stride, padding, dilation)
+            dx = _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend)
         if want_dw:
             dw = _wgrad(x, dy, wk, conv, key, stride, padding, dilation).to(ctx.wdtype)
         return dx, dw, None, None
@@ -166,6 +173,12 @@ def _fwd_impl(x, wk, conv, key, stats) -> str:
     cands = []
     if cin % 64 == 0 and cout % 8 == 0:
         cands.append(("igemm", lambda: ops().conv_igemm(x, wk, stride, padding, dilation, stats, None, None, 0)))
+        if stats:
+            def nostats():
+                y, _ = ops().conv_igemm(x, wk, stride, padding, dilation, False, None, None, 0)
+                ops().bn_stats_sums(y)
+
+            cands.append(("igemm_nostats", nostats))
     elif cin % 32 == 0 and cout % 8 == 0:
         cands.append(("mfma", lambda: ops().conv_mfma(x, wk, stride, padding, dilation, stats, None, None, 0)))
     if not cands:
@@ -180,14 +193,19 @@ def _fwd_impl(x, wk, conv, key, stats) -> str:
     return cands[_choose(("fwd", stats) + key, cands)][0]
 
 
-def _dgrad(x, dy, wk, conv, key, stride, padding, dilation):
+def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None):
+    """dx (+ addend: a residual branch's gradient, added in our kernel's epilogue)."""
     cin, cout = conv.in_channels, conv.out_channels
     wt = []
+    if addend is not None:
+        addend = addend.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        if addend.data_ptr() % 16:
+            addend = addend.clone(memory_format=torch.channels_last)
 
     def ours():
         if not wt:  # [Cin, KH, KW, Cout] bf16, the dgrad B operand
             wt.append(wk.permute(3, 1, 2, 0).contiguous())
-        return ops().conv_igemm_dgrad(dy, wt[0], list(x.shape), stride, padding, dilation)
+        return ops().conv_igemm_dgrad(dy, wt[0], list(x.shape), stride, padding, dilation, None, addend)
 
     def miopen():
         return torch.ops.aten.convolution_backward(dy, x, wk.permute(0, 3, 1, 2), None, stride, padding, dilation, False,
@@ -195,7 +213,28 @@ def _dgrad(x, dy, wk, conv, key, stride, padding, dilation):
 
     cands = [("igemm", ours)] if cout % 64 == 0 and cin % 8 == 0 else []
     cands.append(("miopen", miopen))
-    return cands[_choose(("dgrad",) + key, cands)][1]()
+    name, fn = cands[_choose(("dgrad",) + key, cands)]
+    dx = fn()
+    if addend is not None and name != "igemm":
+        dx = dx + addend
+    return dx
+
+
+def find_conv_consumer(t: torch.Tensor, r: torch.Tensor, max_nodes: int = 64):
+    """The routed-conv autograd node (:class:`_ConvFn`) whose input is exactly ``r`` among the
+    ancestors of ``t`` -- its backward is then guaranteed to run after the backward of any
+    node that consumes ``t`` -- or None."""
+    want = (r.data_ptr(), tuple(r.shape), r.dtype)
+    seen, stack = set(), [t.grad_fn]
+    while stack and len(seen) < max_nodes:
+        fn = stack.pop()
+        if fn is None or id(fn) in seen:
+            continue
+        seen.add(id(fn))
+        if getattr(fn, "in_key", None) == want:
+            return fn
+        stack.extend(f for f, _ in fn.next_functions)
+    return None
 
 
 def _wgrad(x, dy, wk, conv, key, stride, padding, dilation):

@@ -11,9 +11,12 @@ attention blocks and SMP decoders.
 subclass whose forward takes the HIP path for GPU inputs (modules have no state,
 so checkpoints are unaffected).  Semantics are ATen's: ``count_include_pad``
 divisors, first-maximum argmax, adaptive windows ``[floor(o*I/O), ceil((o+1)*I/O))``.
-Unsupported variants (``ceil_mode``, ``divisor_override``, dilation,
-``return_indices``) keep the PyTorch module.  ``RTSEG_POOL=0`` disables the path
-for A/B comparisons.
+``MaxPool2d(return_indices=True)`` returns PyTorch's int64 flat plane indices and
+``MaxUnpool2d`` (kernel == stride, no padding: ENet / SegNet, reference enet.py:131,139 and
+segnet.py:54,65) runs as a gather -- each output pixel reads its own window's index -- so
+neither direction scatters or zero-fills.  Unsupported variants (``ceil_mode``,
+``divisor_override``, dilation) keep the PyTorch module.  ``RTSEG_POOL=0`` disables the
+path for A/B comparisons.
 """
 from __future__ import annotations
 
@@ -68,6 +71,90 @@ class _AdaptiveAvgFn(torch.autograd.Function):
         return ops().adaptive_avg_pool_bwd(gy, h, w, cl), None, None
 
 
+class _MaxPoolIdxFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        y, idx, win = ops().max_pool_indices(x, k, s, p)
+        ctx.geom = (x.shape[2], x.shape[3], k, s, p)
+        ctx.save_for_backward(win)
+        ctx.mark_non_differentiable(idx)
+        return y, idx
+
+    @staticmethod
+    def backward(ctx, gy, _gidx):
+        h, w, k, s, p = ctx.geom
+        (win,) = ctx.saved_tensors
+        return ops().pool2d_bwd(gy, win, h, w, k, s, p, _MAX, True), None, None, None
+
+
+class _UnpoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, idx, kh, kw, oh, ow):
+        ctx.save_for_backward(idx)
+        return ops().max_unpool_fwd(x, idx, kh, kw, oh, ow)
+
+    @staticmethod
+    def backward(ctx, gy):
+        (idx,) = ctx.saved_tensors
+        return ops().max_unpool_bwd(gy, idx), None, None, None, None, None
+
+
+def max_pool2d_with_indices(x, kernel_size, stride=None, padding=0):
+    """``F.max_pool2d(..., return_indices=True)``: (y, int64 flat plane indices)."""
+    k = _pair(kernel_size)
+    s = _pair(stride) if stride is not None else k
+    p = _pair(padding)
+    if _hip_ok(x) and 2 * p[0] <= k[0] and 2 * p[1] <= k[1] and k[0] * k[1] <= 256:
+        return _MaxPoolIdxFn.apply(x, k, s, p)
+    return F.max_pool2d(x, k, s, p, return_indices=True)
+
+
+def max_unpool2d(x, indices, kernel_size, stride=None, padding=0, output_size=None):
+    """``F.max_unpool2d`` -- gather form when kernel == stride and padding == 0 (the indices
+    then come from a pool whose windows tile the plane)."""
+    k = _pair(kernel_size)
+    s = _pair(stride) if stride is not None else k
+    p = _pair(padding)
+    if output_size is not None:
+        oh, ow = tuple(output_size)[-2:]
+    else:
+        oh, ow = (x.shape[2] - 1) * s[0] - 2 * p[0] + k[0], (x.shape[3] - 1) * s[1] - 2 * p[1] + k[1]
+    if (_hip_ok(x) and k == s and p == (0, 0) and indices.dtype == torch.int64 and indices.shape == x.shape
+            and indices.is_cuda):
+        return _UnpoolFn.apply(x, indices, k[0], k[1], int(oh), int(ow))
+    return F.max_unpool2d(x, indices, k, s, p, (oh, ow))
+
+
+class _GlobalMaxFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        y, idx = ops().global_max_pool(x)
+        ctx.save_for_backward(idx)
+        ctx.shape = x.shape
+        ctx.fmt = torch.channels_last if (x.is_contiguous(memory_format=torch.channels_last)
+                                          and not x.is_contiguous()) else torch.contiguous_format
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (idx,) = ctx.saved_tensors
+        n, c, h, w = ctx.shape
+        gx = torch.zeros(ctx.shape, dtype=gy.dtype, device=gy.device).contiguous(memory_format=ctx.fmt)
+        i = idx.view(n, c)
+        nn_ = torch.arange(n, device=gy.device).view(n, 1).expand(n, c)
+        cc = torch.arange(c, device=gy.device).view(1, c).expand(n, c)
+        gx[nn_, cc, i // w, i % w] = gy.view(n, c)  # the max's gradient goes to its first argmax
+        return gx
+
+
+def adaptive_max_pool2d(x, output_size):
+    """``F.adaptive_max_pool2d``; the global case (output 1x1) on the HIP kernel."""
+    oh, ow = _pair(output_size)
+    if (oh, ow) == (1, 1) and _hip_ok(x):
+        return _GlobalMaxFn.apply(x)
+    return F.adaptive_max_pool2d(x, (oh, ow))
+
+
 def avg_pool2d(x, kernel_size, stride=None, padding=0, count_include_pad=True):
     """``F.avg_pool2d`` (ceil_mode False, no divisor override) on the HIP kernels."""
     k = _pair(kernel_size)
@@ -105,12 +192,26 @@ class AvgPool2d(nn.AvgPool2d):
 
 class MaxPool2d(nn.MaxPool2d):
     def forward(self, x):
+        if self.return_indices:
+            return max_pool2d_with_indices(x, self.kernel_size, self.stride, self.padding)
         return max_pool2d(x, self.kernel_size, self.stride, self.padding)
+
+
+class MaxUnpool2d(nn.MaxUnpool2d):
+    def forward(self, x, indices, output_size=None):
+        return max_unpool2d(x, indices, self.kernel_size, self.stride, self.padding, output_size)
 
 
 class AdaptiveAvgPool2d(nn.AdaptiveAvgPool2d):
     def forward(self, x):
         return adaptive_avg_pool2d(x, self.output_size)
+
+
+class AdaptiveMaxPool2d(nn.AdaptiveMaxPool2d):
+    def forward(self, x):
+        if self.return_indices:
+            return nn.AdaptiveMaxPool2d.forward(self, x)
+        return adaptive_max_pool2d(x, self.output_size)
 
 
 def convert_pooling(model: nn.Module) -> nn.Module:
@@ -120,9 +221,12 @@ def convert_pooling(model: nn.Module) -> nn.Module:
         t = type(m)
         if t is nn.AvgPool2d and not m.ceil_mode and m.divisor_override is None:
             m.__class__ = AvgPool2d
-        elif (t is nn.MaxPool2d and not m.ceil_mode and not m.return_indices
-              and _pair(m.dilation) == (1, 1)):
+        elif t is nn.MaxPool2d and not m.ceil_mode and _pair(m.dilation) == (1, 1):
             m.__class__ = MaxPool2d
+        elif t is nn.MaxUnpool2d:
+            m.__class__ = MaxUnpool2d
         elif t is nn.AdaptiveAvgPool2d:
             m.__class__ = AdaptiveAvgPool2d
+        elif t is nn.AdaptiveMaxPool2d:
+            m.__class__ = AdaptiveMaxPool2d
     return model

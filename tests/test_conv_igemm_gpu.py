@@ -124,3 +124,55 @@ def test_igemm_wgrad(geom):
     ref = torch.nn.grad.conv2d_weight(x.float(), wt.shape, dy.float(), s, p, d)
     assert dw.shape == wt.shape and dw.dtype == torch.float32 and dw.is_contiguous()
     _close(dw, ref, 1e-2)
+
+
+def _handoff_nodes(out):
+    seen, stack, hit = set(), [out.grad_fn], 0
+    while stack:
+        fn = stack.pop()
+        if fn is None or id(fn) in seen:
+            continue
+        seen.add(id(fn))
+        hit += isinstance(getattr(fn, "addend_slot", None), list)
+        stack.extend(f for f, _ in fn.next_functions)
+    return hit
+
+
+@pytest.mark.parametrize("with_addend", [False, True])
+def test_igemm_dgrad_addend(with_addend):
+    x, wt = _case(2, 64, 17, 23, 64, 3, 2, 1, seed=5)
+    dy = torch.randn(2, 64, 9, 12, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    add = torch.randn(x.shape, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dx = torch.ops.rtseg.conv_igemm_dgrad(dy, wt.permute(1, 2, 3, 0).contiguous(), list(x.shape), [2, 2], [1, 1],
+                                          [1, 1], None, add if with_addend else None)
+    ref = torch.nn.grad.conv2d_input(x.shape, wt.float(), dy.float(), 2, 1, 1)
+    _close(dx, ref + add.float() if with_addend else ref, 2e-2)
+
+
+def test_residual_grad_handoff_matches_plain_add(monkeypatch):
+    """A chain of DDRNet RBs: each RB tail hands its residual gradient to the next-upstream conv's
+    dgrad epilogue (ops/bn.py); the gradients must match the autograd accumulation."""
+    from realtime_semantic_segmentation_pytorch_amd.models.ddrnet import RB
+    from realtime_semantic_segmentation_pytorch_amd.ops import bn as bn_mod
+
+    monkeypatch.setenv("RTSEG_CONV_MFMA", "1")
+    torch.manual_seed(0)
+    net = ops.convert_batchnorm(torch.nn.Sequential(RB(64, 64), RB(64, 64), RB(64, 64))).to(DEV)
+    net = net.to(memory_format=torch.channels_last).train()
+    x0 = torch.randn(2, 64, 24, 40, device=DEV).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(2, 64, 24, 40, device=DEV)
+    res = {}
+    for on in (True, False):
+        monkeypatch.setattr(bn_mod, "_HANDOFF", on)
+        net.zero_grad(set_to_none=True)
+        x = x0.to(torch.bfloat16).requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = net(x)
+        nodes = _handoff_nodes(y)
+        (y.float() * gy).sum().backward()
+        res[on] = (nodes, x.grad.float().clone(),
+                   {n: p.grad.float().clone() for n, p in net.named_parameters() if p.grad is not None})
+    assert res[True][0] >= 2 and res[False][0] == 0
+    _close(res[True][1], res[False][1], 2e-2)
+    for n, g in res[False][2].items():
+        _close(res[True][2][n], g, 2e-2)

@@ -1,8 +1,9 @@
 """Model-level numerics of the bench configuration on the GPU.
 
 * one DDRNet-23 (+aux) training step in bf16 / channels-last with every HIP kernel on (MFMA
-  conv fwd/dgrad/wgrad, fused BN, fused OHEM, interp) vs the same step with
-  ``RTSEG_DISABLE_HIP=1`` (stock PyTorch / MIOpen): loss and gradient agreement;
+  conv fwd/dgrad/wgrad, fused BN, fused OHEM, interp) and the same step in stock bf16
+  (``RTSEG_DISABLE_HIP=1``), both against the stock fp32 step (tools/probe_train_numerics.py
+  prints the per-layer table);
 * 200 steps overfitting one synthetic batch with every HIP kernel on: the loss must fall;
 * an fp16 + GradScaler step (``amp_dtype='fp16'``, reference core/base_trainer.py:30).
 Reference training step: core/seg_trainer.py:38-119.
@@ -51,7 +52,8 @@ def _batch(tr, seed=0):
     return data.next()
 
 
-def _grads(tr, imgs, masks):
+def _grads(tr, imgs, masks, amp=True):
+    tr.config.amp_training = amp
     tr.model.zero_grad(set_to_none=True)
     loss, _, _ = tr.compute_loss(imgs, masks)
     loss.backward()
@@ -59,24 +61,39 @@ def _grads(tr, imgs, masks):
     return float(loss), g
 
 
-def test_ddrnet23_bf16_step_hip_vs_stock(tmp_path, monkeypatch):
+def _cos(g, ref):
+    return {n: float(torch.nn.functional.cosine_similarity(g[n].flatten(), ref[n].flatten(), dim=0))
+            for n in ref if ref[n].norm() > 1e-8}
+
+
+def test_ddrnet23_bf16_step_vs_fp32_reference(tmp_path, monkeypatch):
+    """One training step's gradients against a stock-PyTorch fp32 reference.  At random init the
+    BN-heavy backward amplifies rounding noise layer by layer (two stock bf16 runs with different
+    reduction orders already disagree on a few layers), so the bf16 yardstick is the stock bf16
+    path's own distance to fp32: the HIP bf16 path (MFMA convs, fused BN, residual-gradient
+    hand-off, OHEM, interp) must be at least as close.  The HIP fp32 path (our BN / loss / interp
+    kernels around MIOpen convs) must agree with the fp32 reference tightly."""
     tr = _trainer(tmp_path)
     imgs, masks = _batch(tr)
-    monkeypatch.setenv("RTSEG_CONV_MFMA", "1")  # our conv kernels on every eligible layer
-    loss_hip, g_hip = _grads(tr, imgs, masks)
     monkeypatch.setenv("RTSEG_DISABLE_HIP", "1")
-    loss_ref, g_ref = _grads(tr, imgs, masks)
-    assert set(g_hip) == set(g_ref)
-    assert abs(loss_hip - loss_ref) <= 2e-2 * abs(loss_ref), (loss_hip, loss_ref)
-    n_hip = torch.sqrt(sum((g * g).sum() for g in g_hip.values()))
-    n_ref = torch.sqrt(sum((g * g).sum() for g in g_ref.values()))
-    assert abs(float(n_hip) - float(n_ref)) <= 5e-2 * float(n_ref), (float(n_hip), float(n_ref))
-    # per-tensor direction: bf16 rounding and OHEM ties may move a few values, never a whole layer
-    cos = {n: float(torch.nn.functional.cosine_similarity(g_hip[n].flatten(), g_ref[n].flatten(), dim=0))
-           for n in g_ref if g_ref[n].norm() > 1e-6}
-    bad = {n: c for n, c in cos.items() if c < 0.95}
-    assert len(bad) <= len(cos) // 50, bad
-    assert sorted(cos.values())[len(cos) // 2] > 0.99  # median layer
+    loss_ref, g_ref = _grads(tr, imgs, masks, amp=False)
+    loss_sb, g_sb = _grads(tr, imgs, masks)
+    monkeypatch.delenv("RTSEG_DISABLE_HIP")
+    monkeypatch.setenv("RTSEG_CONV_MFMA", "1")  # our conv kernels on every eligible layer
+    loss_hb, g_hb = _grads(tr, imgs, masks)
+    monkeypatch.delenv("RTSEG_CONV_MFMA")
+    loss_hf, g_hf = _grads(tr, imgs, masks, amp=False)
+    assert set(g_hb) == set(g_ref) == set(g_hf)
+    for loss in (loss_sb, loss_hb):
+        assert abs(loss - loss_ref) <= 2e-2 * abs(loss_ref), (loss, loss_ref)
+    assert abs(loss_hf - loss_ref) <= 1e-4 * abs(loss_ref), (loss_hf, loss_ref)
+    c_sb, c_hb, c_hf = (sorted(_cos(g, g_ref).values()) for g in (g_sb, g_hb, g_hf))
+    med = len(c_sb) // 2
+    assert c_hb[med] >= c_sb[med] - 5e-3, (c_hb[med], c_sb[med])
+    assert sum(c < 0.9 for c in c_hb) <= sum(c < 0.9 for c in c_sb) + len(c_hb) // 50
+    # measured on MI355X: median 0.9986, 10th percentile 0.9978 (fp32 reduction-order noise through
+    # ~70 BN backward passes at random init)
+    assert c_hf[med] > 0.995 and c_hf[len(c_hf) // 10] > 0.99, (c_hf[med], c_hf[len(c_hf) // 10])
 
 
 def test_ddrnet23_overfits_one_batch_with_hip_kernels(tmp_path):

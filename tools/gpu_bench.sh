@@ -3,7 +3,7 @@
 # usage: tools/gpu_bench.sh TAG [bench args...]
 TAG=${1:-b32}; shift || true
 mkdir -p gpurun_out
-timeout -k 10 900 python -u bench.py "$@" > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
+RTSEG_DECISIONS_OUT=gpurun_out/decisions_$TAG.txt timeout -k 10 900 python -u bench.py "$@" > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
 rc=$?
 tail -3 gpurun_out/bench_$TAG.err; cat gpurun_out/bench_$TAG.json
 if [ $rc -ne 0 ]; then exit $rc; fi
