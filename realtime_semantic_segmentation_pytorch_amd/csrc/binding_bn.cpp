@@ -137,19 +137,23 @@ at::Tensor bn_apply(const at::Tensor& x, const at::Tensor& scale_shift,
 // Residual + activation forward that also returns the activation-derivative bit mask
 // (one byte per channel vector; mask mode 3 of bn_bwd_sums / bn_backward).
 std::tuple<at::Tensor, at::Tensor> bn_apply_bits(const at::Tensor& x, const at::Tensor& scale_shift,
-                                                 const at::Tensor& res, int64_t act) {
+                                                 const std::optional<at::Tensor>& res, int64_t act) {
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   check_cl(x, "x");
-  check_cl(res, "residual");
-  TORCH_CHECK(res.sizes() == x.sizes() && res.scalar_type() == x.scalar_type(),
-              "rtseg.bn_apply_bits: residual mismatch");
+  const void* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    check_cl(*res, "residual");
+    TORCH_CHECK(res->sizes() == x.sizes() && res->scalar_type() == x.scalar_type(),
+                "rtseg.bn_apply_bits: residual mismatch");
+    rp = res->data_ptr();
+  }
   TORCH_CHECK(act == 1 || act == 2, "rtseg.bn_apply_bits: relu / relu6 only");
   const int C = static_cast<int>(x.size(1));
   const int V = bn_vec_width(dtype_code(x), C);
   TORCH_CHECK(V > 0, "rtseg.bn_apply_bits: unsupported channel count");
   at::Tensor y = at::empty_like(x);
   at::Tensor bits = at::empty({rows_of(x) * (C / V)}, x.options().dtype(at::kByte));
-  launch_bn_apply_bits(x.data_ptr(), res.data_ptr(), scale_shift.data_ptr<float>(), y.data_ptr(),
+  launch_bn_apply_bits(x.data_ptr(), rp, scale_shift.data_ptr<float>(), y.data_ptr(),
                        bits.data_ptr<uint8_t>(), dtype_code(x), rows_of(x), C, static_cast<int>(act),
                        cur_stream());
   return {y, bits};
@@ -200,7 +204,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_backward(
     const at::Tensor& dy, const at::Tensor& x, const std::optional<at::Tensor>& y,
     const std::optional<at::Tensor>& bsums, const std::optional<at::Tensor>& fwd_sums,
     const at::Tensor& mi, const at::Tensor& ss, const std::optional<at::Tensor>& w, int64_t act,
-    int64_t mask, bool want_dres, bool batch_stats, bool want_dw) {
+    int64_t mask, bool want_dres, bool batch_stats, bool want_dw, const std::optional<at::Tensor>& slab) {
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   check_cl(x, "x");
   check_cl(dy, "grad");
@@ -210,8 +214,17 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_backward(
   at::Tensor part;
   int G = 0;
   const double* sums_p = nullptr;
-  if (bsums.has_value() && bsums->defined()) sums_p = bsums->data_ptr<double>();
-  else part = bwd_slab(dy, x, yp, mi, ss, act, mask, G);
+  if (bsums.has_value() && bsums->defined()) {
+    sums_p = bsums->data_ptr<double>();
+  } else if (slab.has_value() && slab->defined()) {  // reduction already done by the producer of dy
+    TORCH_CHECK(slab->is_cuda() && slab->scalar_type() == at::kFloat && slab->dim() == 2 &&
+                    slab->is_contiguous() && slab->size(1) == 2 * C,
+                "rtseg.bn_backward: slab must be contiguous fp32 [G, 2C]");
+    part = *slab;
+    G = static_cast<int>(part.size(0));
+  } else {
+    part = bwd_slab(dy, x, yp, mi, ss, act, mask, G);
+  }
   at::Tensor k = at::empty({3 * C}, f32);
   at::Tensor dw, db;
   if (want_dw) { dw = at::empty({C}, f32); db = at::empty({C}, f32); }
@@ -245,12 +258,12 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
   m.def("bn_eval_coeffs(Tensor? weight, Tensor? bias, Tensor running_mean, Tensor running_var, "
         "float eps) -> (Tensor, Tensor)");
   m.def("bn_apply(Tensor x, Tensor scale_shift, Tensor? residual, int act) -> Tensor");
-  m.def("bn_apply_bits(Tensor x, Tensor scale_shift, Tensor residual, int act) -> (Tensor, Tensor)");
+  m.def("bn_apply_bits(Tensor x, Tensor scale_shift, Tensor? residual, int act) -> (Tensor, Tensor)");
   m.def("bn_bwd_sums(Tensor grad, Tensor x, Tensor? y, Tensor mean_invstd, Tensor scale_shift, "
         "int act, int mask) -> Tensor");
   m.def("bn_backward(Tensor grad, Tensor x, Tensor? y, Tensor? bsums, Tensor? fwd_sums, "
         "Tensor mean_invstd, Tensor scale_shift, Tensor? weight, int act, int mask, bool want_dres, "
-        "bool batch_stats, bool want_dw) -> (Tensor, Tensor, Tensor, Tensor)");
+        "bool batch_stats, bool want_dw, Tensor? slab=None) -> (Tensor, Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {

@@ -561,11 +561,15 @@ template <typename T, int V, int ACT>
 static void apply_bits_t(const void* x, const void* res, const float* ss, void* y, uint8_t* bits,
                          int64_t M, int C, hipStream_t st) {
   const int64_t work = M * (C / V);
-  bn_apply_kernel<T, V, ACT, true, true><<<apply_grid(work), 256, sizeof(float) * 2 * C, st>>>(
-      static_cast<const T*>(x), static_cast<const T*>(res), ss, static_cast<T*>(y), M, C, bits);
+  if (res != nullptr)
+    bn_apply_kernel<T, V, ACT, true, true><<<apply_grid(work), 256, sizeof(float) * 2 * C, st>>>(
+        static_cast<const T*>(x), static_cast<const T*>(res), ss, static_cast<T*>(y), M, C, bits);
+  else
+    bn_apply_kernel<T, V, ACT, false, true><<<apply_grid(work), 256, sizeof(float) * 2 * C, st>>>(
+        static_cast<const T*>(x), nullptr, ss, static_cast<T*>(y), M, C, bits);
 }
 
-// Residual + activation forward that also writes the derivative bit mask (kMaskBits):
+// (Residual +) activation forward that also writes the derivative bit mask (kMaskBits):
 // bits holds M * C / V bytes, V = bn_vec_width(dtype, C).
 void launch_bn_apply_bits(const void* x, const void* res, const float* scale_shift, void* y,
                           uint8_t* bits, int dtype, int64_t M, int C, int act, hipStream_t st) {
@@ -607,7 +611,7 @@ static void bwd_apply_t(const void* dy, const void* x, const void* y, const floa
 
 #define RT_ACT_MASK_DISPATCH(FN, ...)                                                   \
   do {                                                                                  \
-    if (act == kActNone) FN<T, V, kActNone, kMaskNone>(__VA_ARGS__);                    \
+    if (act == kActNone || mask == kMaskNone) FN<T, V, kActNone, kMaskNone>(__VA_ARGS__); \
     else if (act == kActReLU) {                                                         \
       if (mask == kMaskFromY) FN<T, V, kActReLU, kMaskFromY>(__VA_ARGS__);              \
       else if (mask == kMaskBits) FN<T, V, kActReLU, kMaskBits>(__VA_ARGS__);           \
