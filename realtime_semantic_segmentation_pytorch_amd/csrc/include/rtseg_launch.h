@@ -185,6 +185,28 @@ void launch_conv_igemm_dgrad(const ConvGeom& g, hipStream_t st);
 int64_t conv_igemm_wgrad_ws_elems(const ConvGeom& g);
 void launch_conv_igemm_wgrad(const ConvGeom& g, float* ws, float* dw, hipStream_t st);
 
+// ---- gate.hip -----------------------------------------------------------------
+// out = x * s (mul), x * (1 + s) (residual), x * s + y * (1 - s) (blend); s = att or
+// sigmoid(att), broadcast per (n, c) (att fp32 [N, C]), per pixel (fp32 [N, H*W]) or full (x's
+// dtype and layout).  x / y / out channels-last [M = N*H*W][C].
+enum GateMode : int { kGateMul = 0, kGateResidual = 1, kGateBlend = 2 };
+enum GateBcast : int { kGateChannel = 0, kGateSpatial = 1, kGateFull = 2 };
+struct GateArgs {
+  const void* x;
+  const void* y;
+  const void* att;
+  void* out;
+  int dtype, mode, bc;
+  bool sigmoid;
+  int64_t M;
+  int HW, C;
+};
+int gate_vec_width(int dtype, int C);  // 0: unsupported channel count
+bool gate_bwd_supported(int dtype, int C, int bc);
+int gate_channel_blocks(int64_t HW, int N);  // part: fp32 [N, blocks, C] for the channel gate
+void launch_gate_fwd(const GateArgs& g, hipStream_t st);
+void launch_gate_bwd(const GateArgs& g, const void* go, void* gx, void* gy, void* gatt, float* part, hipStream_t st);
+
 // ---- pool.hip -----------------------------------------------------------------
 enum PoolMode : int { kPoolAvg = 0, kPoolMax = 1 };
 struct PoolParams {

@@ -98,7 +98,7 @@ class SpatialAttentionBlock(nn.Module):
         self.conv = conv1x1(channels, 1)
 
     def forward(self, x):
-        return x * torch.sigmoid(self.conv(x))
+        return ops.gate(x, self.conv(x), sigmoid=True)
 
 
 class ChannelAttentionBlock(nn.Module):
@@ -108,4 +108,4 @@ class ChannelAttentionBlock(nn.Module):
         self.conv = conv1x1(in_channels, out_channels)
 
     def forward(self, x):
-        return x * torch.sigmoid(self.conv(self.pool(x)))
+        return ops.gate(x, self.conv(self.pool(x)), sigmoid=True)

@@ -66,7 +66,7 @@ class AttentionRefinementModule(nn.Module):
 
     def forward(self, x):
         att = pooled_conv_bn_act(self.conv, self.pool(x), x.shape[2] * x.shape[3])
-        return x * att
+        return ops.gate(x, att)
 
 
 class FeatureFusionModule(nn.Module):
@@ -80,4 +80,4 @@ class FeatureFusionModule(nn.Module):
     def forward(self, x_low, x_high):
         x = self.conv1(torch.cat([x_low, x_high], dim=1))
         att = self.conv2(self.pool(x))  # per-channel gate; broadcast == reference expand_as
-        return x + x * att
+        return ops.gate(x, att, mode="residual")  # x + x * att in one pass

@@ -151,7 +151,8 @@ class BilateralGuidedAggregationLayer(nn.Module):
 
     def forward(self, x_d, x_s):
         s_high = self.semantic_high[0](x_s)
-        s_high = torch.sigmoid(ops.interpolate(s_high, (s_high.shape[2] * 4, s_high.shape[3] * 4), True))
-        x_high = self.detail_high(x_d) * s_high
-        x_low = self.detail_low(x_d) * self.semantic_low(x_s)
+        s_high = ops.interpolate(s_high, (s_high.shape[2] * 4, s_high.shape[3] * 4), True)
+        x_high = ops.gate(self.detail_high(x_d), s_high, sigmoid=True)  # * sigmoid(.), one pass
+        s_low = self.semantic_low[1](self.semantic_low[0](x_s))
+        x_low = ops.gate(self.detail_low(x_d), s_low, sigmoid=True)
         return self.conv_last(ops.interpolate(x_low, x_high.shape[2:], True, skip=x_high))

@@ -11,6 +11,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
+from .. import ops
 from .backbone import Mobilenetv2, ResNet
 from .modules import ConvBNAct, DeConvBNAct
 
@@ -64,7 +65,7 @@ class FeatureCrossAttentionModule(nn.Module):
     def forward(self, x_s, x_c):
         fused = self.conv_init(torch.cat([x_s, x_c], dim=1))
         gate = self.sa(x_s) * self.ca(x_c)  # [N,1,H,W] * [N,C,1,1]
-        return self.conv_last(fused * gate + fused)
+        return self.conv_last(ops.gate(fused, gate, mode="residual"))  # fused * gate + fused
 
 
 class SpatialAttentionBlock(nn.Sequential):

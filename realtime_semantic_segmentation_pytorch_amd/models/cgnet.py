@@ -77,8 +77,7 @@ class CGBlock(nn.Module):
                        act_module=self.joi[1])
         if self.use_skip and self.res_type == "LRL":
             y = y + x
-        g = torch.sigmoid(self.glo(y.mean(dim=(2, 3))))
-        y = y * g[:, :, None, None].to(y.dtype)
+        y = ops.gate(y, self.glo(y.mean(dim=(2, 3)))[:, :, None, None], sigmoid=True)
         if self.use_skip and self.res_type == "GRL":
             y = y + x
         return y

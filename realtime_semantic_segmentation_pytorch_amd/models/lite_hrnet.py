@@ -119,8 +119,8 @@ class CCWBlock(nn.Module):
         fl, fr = torch.split(feats, self.split_ch, dim=1)
         if cr_weight.shape[2:] != fr.shape[2:]:
             cr_weight = F.interpolate(cr_weight, fr.shape[2:], mode="nearest")
-        fr = self.right_branch(fr * cr_weight)
-        fr = fr * self.sw(fr)
+        fr = self.right_branch(ops.gate(fr, cr_weight))
+        fr = ops.gate(fr, self.sw(fr))
         return channel_shuffle(torch.cat([self.left_branch(fl), fr], dim=1))
 
 

@@ -115,7 +115,7 @@ class UAFM(nn.Module):
         x_low = self.conv(x_low)
         x_up = ops.interpolate(x_high, x_low.shape[2:], True)
         alpha = self.attention(x_up, x_low)
-        return x_low + alpha * (x_up - x_low)
+        return ops.gate(x_up, alpha, x_low, mode="blend")  # x_low + alpha * (x_up - x_low)
 
 
 class SpatialAttentionModule(nn.Module):

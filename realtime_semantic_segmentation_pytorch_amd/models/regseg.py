@@ -91,7 +91,7 @@ class SEBlock(nn.Module):
 
     def forward(self, x):
         w = self.se_block(x.mean(dim=(2, 3)))
-        return x * w[:, :, None, None].to(x.dtype)
+        return ops.gate(x, w[:, :, None, None])
 
 
 class Decoder(nn.Module):

@@ -23,6 +23,7 @@ from .dilated import DilatedGroupConv2d, convert_dilated_group_convs, dilated_gr
 from .optim import FusedAdam, FusedAdamW, FusedSGD
 from .conv import conv_ok, conv_bn_stats, conv_bn_act_eval, conv_bn_act, conv_forward
 from .deconv import TransposedConv2d, conv_transpose2d, convert_transposed_convs, deconv_ok
+from .gate import gate, gate_reference
 
 __all__ = [
     "load", "use_hip", "hip_disabled", "library_path",
@@ -34,6 +35,6 @@ __all__ = [
     "AdaptiveAvgPool2d", "AdaptiveMaxPool2d", "adaptive_max_pool2d", "MaxUnpool2d", "max_pool2d_with_indices", "max_unpool2d", "TapConv2d", "convert_tap_convs", "tap_conv2d", "tapconv_ok",
     "DilatedGroupConv2d", "convert_dilated_group_convs", "dilated_group_conv2d", "dilated_group_ok",
     "FusedSGD", "FusedAdam", "FusedAdamW", "conv_ok", "conv_bn_stats", "conv_bn_act_eval", "conv_bn_act", "conv_forward",
-    "TransposedConv2d", "conv_transpose2d", "convert_transposed_convs", "deconv_ok",
+    "TransposedConv2d", "conv_transpose2d", "convert_transposed_convs", "deconv_ok", "gate", "gate_reference",
     "bn_act", "bn_act_code", "bn_fused_ok", "convert_batchnorm", "FusedBatchNorm2d", "FusedSyncBatchNorm",
 ]
