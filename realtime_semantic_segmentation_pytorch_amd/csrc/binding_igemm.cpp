@@ -38,10 +38,10 @@ ConvGeom geom(int64_t N, int64_t Cin, int64_t H, int64_t W, int64_t Cout, int64_
 }
 
 // x [N,Cin,H,W] CL bf16, wk [Cout,KH,KW,Cin] bf16 -> (y CL bf16, BN statistics slab or empty)
-std::tuple<at::Tensor, at::Tensor> conv_igemm(const at::Tensor& x, const at::Tensor& wk, at::IntArrayRef stride,
-                                              at::IntArrayRef padding, at::IntArrayRef dilation, bool stats,
-                                              const std::optional<at::Tensor>& scale_shift,
-                                              const std::optional<at::Tensor>& residual, int64_t act) {
+std::tuple<at::Tensor, at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::Tensor& wk, at::IntArrayRef stride,
+                                                 at::IntArrayRef padding, at::IntArrayRef dilation, bool stats,
+                                                 const std::optional<at::Tensor>& scale_shift,
+                                                 const std::optional<at::Tensor>& residual, int64_t act, bool halo) {
   check_act(x, "input");
   TORCH_CHECK(wk.is_cuda() && wk.dim() == 4 && wk.scalar_type() == at::kBFloat16 && wk.is_contiguous() &&
                   wk.size(3) == x.size(1),
@@ -49,14 +49,19 @@ std::tuple<at::Tensor, at::Tensor> conv_igemm(const at::Tensor& x, const at::Ten
   TORCH_CHECK(act >= 0 && act <= 2, "rtseg.conv_igemm: bad activation");
   ConvGeom g = geom(x.size(0), x.size(1), x.size(2), x.size(3), wk.size(0), wk.size(1), wk.size(2), stride, padding,
                     dilation);
-  TORCH_CHECK(conv_igemm_supported(g, 0), "rtseg.conv_igemm: needs Cin % 64 == 0, Cout % 8 == 0, <= 49 taps");
+  if (halo) {
+    TORCH_CHECK(conv_halo_supported(g, 0),
+                "rtseg.conv_halo: needs stride 1, taps within 3 x 3, Cin % 64 == 0, Cout % 64 == 0");
+  } else {
+    TORCH_CHECK(conv_igemm_supported(g, 0), "rtseg.conv_igemm: needs Cin % 64 == 0, Cout % 8 == 0, <= 49 taps");
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   at::Tensor y = at::empty({g.n, g.cout, g.ho, g.wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   g.x = x.data_ptr(); g.w = wk.data_ptr(); g.y = y.data_ptr();
   g.part = nullptr; g.scale_shift = nullptr; g.res = nullptr; g.act = static_cast<int>(act);
   at::Tensor part;
   if (stats) {
-    part = at::empty({conv_igemm_slabs(g), 2 * g.cout}, x.options().dtype(at::kFloat));
+    part = at::empty({halo ? conv_halo_slabs(g) : conv_igemm_slabs(g), 2 * g.cout}, x.options().dtype(at::kFloat));
     g.part = part.data_ptr<float>();
   }
   if (scale_shift.has_value() && scale_shift->defined()) {
@@ -74,7 +79,8 @@ std::tuple<at::Tensor, at::Tensor> conv_igemm(const at::Tensor& x, const at::Ten
     TORCH_CHECK(!(residual.has_value() && residual->defined()) && act == 0,
                 "rtseg.conv_igemm: residual / activation need the BN epilogue (scale_shift)");
   }
-  launch_conv_igemm_fwd(g, cur_stream());
+  if (halo) launch_conv_halo_fwd(g, cur_stream());
+  else launch_conv_igemm_fwd(g, cur_stream());
   if (stats && part.size(0) > 256) {  // fold the per-tile rows so the BN finalize stays cheap
     const int rows = static_cast<int>(part.size(0));
     const int chunk = (rows + 255) / 256;
@@ -85,10 +91,25 @@ std::tuple<at::Tensor, at::Tensor> conv_igemm(const at::Tensor& x, const at::Ten
   return {y, part};
 }
 
+std::tuple<at::Tensor, at::Tensor> conv_igemm(const at::Tensor& x, const at::Tensor& wk, at::IntArrayRef stride,
+                                              at::IntArrayRef padding, at::IntArrayRef dilation, bool stats,
+                                              const std::optional<at::Tensor>& scale_shift,
+                                              const std::optional<at::Tensor>& residual, int64_t act) {
+  return conv_fwd_impl(x, wk, stride, padding, dilation, stats, scale_shift, residual, act, false);
+}
+
+// the halo-tiled kernel (conv_halo.hip): stride-1 convs whose taps fit a 3 x 3 footprint
+std::tuple<at::Tensor, at::Tensor> conv_halo(const at::Tensor& x, const at::Tensor& wk, at::IntArrayRef stride,
+                                             at::IntArrayRef padding, at::IntArrayRef dilation, bool stats,
+                                             const std::optional<at::Tensor>& scale_shift,
+                                             const std::optional<at::Tensor>& residual, int64_t act) {
+  return conv_fwd_impl(x, wk, stride, padding, dilation, stats, scale_shift, residual, act, true);
+}
+
 // dy [N,Cout,Ho,Wo] CL bf16, wt [Cin,KH,KW,Cout] bf16 -> dx [N,Cin,H,W] CL bf16
-at::Tensor conv_igemm_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
-                            at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
-                            const std::optional<at::Tensor>& bias, const std::optional<at::Tensor>& addend) {
+at::Tensor conv_dgrad_impl(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
+                           at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
+                           const std::optional<at::Tensor>& bias, const std::optional<at::Tensor>& addend, bool halo) {
   check_act(dy, "grad_output");
   TORCH_CHECK(x_size.size() == 4, "rtseg.conv_igemm_dgrad: x_size must be [N, Cin, H, W]");
   TORCH_CHECK(wt.is_cuda() && wt.dim() == 4 && wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() &&
@@ -98,7 +119,13 @@ at::Tensor conv_igemm_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntA
                     dilation);
   TORCH_CHECK(g.ho == dy.size(2) && g.wo == dy.size(3) && g.n == dy.size(0),
               "rtseg.conv_igemm_dgrad: grad_output does not match the geometry");
-  TORCH_CHECK(conv_igemm_supported(g, 1), "rtseg.conv_igemm_dgrad: needs Cout % 64 == 0, Cin % 8 == 0");
+  if (halo) {
+    TORCH_CHECK(conv_halo_supported(g, 1),
+                "rtseg.conv_halo_dgrad: needs stride 1, taps within 3 x 3, Cin % 64 == 0, Cout % 64 == 0");
+    TORCH_CHECK(!(bias.has_value() && bias->defined()), "rtseg.conv_halo_dgrad: no bias");
+  } else {
+    TORCH_CHECK(conv_igemm_supported(g, 1), "rtseg.conv_igemm_dgrad: needs Cout % 64 == 0, Cin % 8 == 0");
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
   at::Tensor dx = at::empty({g.n, g.cin, g.h, g.w_in}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   g.x = dy.data_ptr(); g.w = wt.data_ptr(); g.y = dx.data_ptr();
@@ -115,8 +142,21 @@ at::Tensor conv_igemm_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntA
     TORCH_CHECK(addend->sizes() == dx.sizes(), "rtseg.conv_igemm_dgrad: addend must match dx");
     g.res = addend->data_ptr();
   }
-  launch_conv_igemm_dgrad(g, cur_stream());
+  if (halo) launch_conv_halo_dgrad(g, cur_stream());
+  else launch_conv_igemm_dgrad(g, cur_stream());
   return dx;
+}
+
+at::Tensor conv_igemm_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
+                            at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
+                            const std::optional<at::Tensor>& bias, const std::optional<at::Tensor>& addend) {
+  return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, bias, addend, false);
+}
+
+at::Tensor conv_halo_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
+                           at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
+                           const std::optional<at::Tensor>& addend) {
+  return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, std::nullopt, addend, true);
 }
 
 // dgrad with the BN-backward epilogue: dx is the gradient of y = act(BN(z) [+ r]) where y is the
@@ -202,6 +242,10 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
         "Tensor? scale_shift, Tensor? residual, int act) -> (Tensor, Tensor)");
   m.def("conv_igemm_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
         "Tensor? bias=None, Tensor? addend=None) -> Tensor");
+  m.def("conv_halo(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats, "
+        "Tensor? scale_shift, Tensor? residual, int act) -> (Tensor, Tensor)");
+  m.def("conv_halo_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
+        "Tensor? addend=None) -> Tensor");
   m.def("conv_igemm_dgrad_bn(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
         "Tensor? addend, Tensor z, Tensor? mask, Tensor mean_invstd, int mode) "
         "-> (Tensor, Tensor)");
@@ -212,6 +256,8 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
 TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
   m.impl("conv_igemm", &rtseg::conv_igemm);
   m.impl("conv_igemm_dgrad", &rtseg::conv_igemm_dgrad);
+  m.impl("conv_halo", &rtseg::conv_halo);
+  m.impl("conv_halo_dgrad", &rtseg::conv_halo_dgrad);
   m.impl("conv_igemm_dgrad_bn", &rtseg::conv_igemm_dgrad_bn);
   m.impl("conv_igemm_wgrad", &rtseg::conv_igemm_wgrad);
 }

@@ -185,6 +185,15 @@ void launch_conv_igemm_dgrad(const ConvGeom& g, hipStream_t st);
 int64_t conv_igemm_wgrad_ws_elems(const ConvGeom& g);
 void launch_conv_igemm_wgrad(const ConvGeom& g, float* ws, float* dw, hipStream_t st);
 
+// ---- conv_halo.hip ------------------------------------------------------------
+// Halo-tiled stride-1 conv (taps within a 3 x 3 footprint, Cin % 64 == 0, Cout % 64 == 0):
+// forward (+ BN statistics slab of conv_halo_slabs(g) rows / inference BN epilogue) and data
+// gradient (g as for launch_conv_igemm_dgrad; g.res = optional addend).  mode 0 fwd, 1 dgrad.
+bool conv_halo_supported(const ConvGeom& g, int mode);
+int conv_halo_slabs(const ConvGeom& g);
+void launch_conv_halo_fwd(const ConvGeom& g, hipStream_t st);
+void launch_conv_halo_dgrad(const ConvGeom& g, hipStream_t st);
+
 // ---- gate.hip -----------------------------------------------------------------
 // out = x * s (mul), x * (1 + s) (residual), x * s + y * (1 - s) (blend); s = att or
 // sigmoid(att), broadcast per (n, c) (att fp32 [N, C]), per pixel (fp32 [N, H*W]) or full (x's

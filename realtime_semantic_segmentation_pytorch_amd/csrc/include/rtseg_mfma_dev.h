@@ -1,0 +1,100 @@
+// Device helpers shared by the MFMA conv kernels (conv_igemm.hip, conv_halo.hip): LDS-DMA issue,
+// counted vmcnt waits, packed tap tables, bf16 packing, DPP half-wave sums and the XCD-aware
+// block -> tile map.  gfx950 only.
+#pragma once
+
+#include "rtseg_common.h"
+
+namespace rtseg {
+namespace mdev {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+typedef short i16x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt immediate");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const void*)p));
+}
+
+// LDS-DMA from inline asm (opaque to hipcc's waitcnt pass, which would otherwise drain vmcnt(0)
+// before every later ds_read): 64 lanes x 16 B land at M0 + 16 * lane.
+// M0 is compiler-reserved, so the statement saves and restores it around the DMA.
+__device__ __forceinline__ void dma16(const void* src, uint32_t lds_dst) {
+  const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_dst);
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(dst)
+      : "memory");
+}
+
+// Tap table entry: dh (8-bit signed) | dw (8-bit signed) << 8 | weight tap (8-bit) << 16 |
+// tap-row index ri << 24 | tap-column index ci << 28.  The taps of every conv pass form a product
+// set (rows x columns, possibly filtered by a dgrad phase); ri / ci index its distinct rows /
+// columns so a gathered row's per-tap validity is two bits of a per-row mask.
+// int32 (not short[]) because SMEM loads are dword-only on gfx950: a 16-bit table entry read
+// with a uniform index becomes a VMEM load whose s_waitcnt would also drain the DMA ring.
+__host__ __device__ inline int pack_tap(int dh, int dw, int wt, int ri = 0, int ci = 0) {
+  return (dh & 0xff) | ((dw & 0xff) << 8) | ((wt & 0xff) << 16) | ((ri & 0xf) << 24) | (ci << 28);
+}
+__device__ __forceinline__ int tap_dh(int v) { return (v << 24) >> 24; }
+__device__ __forceinline__ int tap_dw(int v) { return (v << 16) >> 24; }
+__device__ __forceinline__ int tap_wt(int v) { return (v >> 16) & 0xff; }
+__device__ __forceinline__ int tap_ri(int v) { return (v >> 24) & 0xf; }
+__device__ __forceinline__ int tap_ci(int v) { return static_cast<int>(static_cast<unsigned>(v) >> 28); }
+
+__device__ __forceinline__ bf16x8_t as_frag(uint4 v) { return __builtin_bit_cast(bf16x8_t, v); }
+
+__device__ __forceinline__ float epi_act(float v, int act) {
+  if (act == kActReLU) return fmaxf(v, 0.f);
+  if (act == kActReLU6) return fminf(fmaxf(v, 0.f), 6.f);
+  return v;
+}
+
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  return static_cast<uint32_t>(f32_to_bf16(lo)) | (static_cast<uint32_t>(f32_to_bf16(hi)) << 16);
+}
+
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROWS, 0xF, false));
+}
+// Sum over each 32-lane half of the wave; valid in lanes 16..31 and 48..63 (DPP only, no LDS):
+// quad swaps, half-row and row mirrors, then row 0 -> 1 / row 2 -> 3 broadcast of lane 15.
+__device__ __forceinline__ float half_wave_sum(float v) {
+  v += dpp_f<0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x141, 0xF>(v);  // row_half_mirror
+  v += dpp_f<0x140, 0xF>(v);  // row_mirror
+  v += dpp_f<0x142, 0xA>(v);  // row_bcast15 into rows 1 and 3
+  return v;
+}
+
+// Bijective block -> logical id map that gives each XCD (blockIdx % 8 under round-robin
+// dispatch) a contiguous range of logical ids: neighbouring tiles share L2.  Speed only.
+__device__ __forceinline__ int xcd_logical(int b, int G) {
+  const int q = G / 8, r = G % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+__device__ __forceinline__ void bf16x4_unpack(uint2 r, float* f) {
+  f[0] = bf16_to_f32(static_cast<uint16_t>(r.x & 0xffff));
+  f[1] = bf16_to_f32(static_cast<uint16_t>(r.x >> 16));
+  f[2] = bf16_to_f32(static_cast<uint16_t>(r.y & 0xffff));
+  f[3] = bf16_to_f32(static_cast<uint16_t>(r.y >> 16));
+}
+
+}  // namespace mdev
+}  // namespace rtseg

@@ -43,6 +43,7 @@
 // (deterministic, no atomics) into the [Cout][Cin][KH][KW] fp32 weight gradient.
 #include "rtseg_common.h"
 #include "rtseg_launch.h"
+#include "rtseg_mfma_dev.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -51,86 +52,12 @@ namespace rtseg {
 
 namespace {
 
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-typedef short i16x4_t __attribute__((ext_vector_type(4)));
-typedef float f32x16_t __attribute__((ext_vector_type(16)));
+using namespace mdev;
 
 constexpr int kMaxTaps = kIgemmMaxTaps;
 
 // 64 zero bytes: the DMA source of padding taps / rows past the edge
 __device__ uint4 g_igemm_zero[4];
-
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-  static_assert(N >= 0 && N < 64, "vmcnt immediate");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
-}
-
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const void*)p));
-}
-
-// LDS-DMA from inline asm (opaque to hipcc's waitcnt pass, which would otherwise drain vmcnt(0)
-// before every later ds_read): 64 lanes x 16 B land at M0 + 16 * lane.
-// M0 is compiler-reserved, so the statement saves and restores it around the DMA.
-__device__ __forceinline__ void dma16(const void* src, uint32_t lds_dst) {
-  const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_dst);
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(src), "s"(dst)
-      : "memory");
-}
-
-// Tap table entry: dh (10-bit signed) | dw (10-bit signed) << 10 | weight tap (12-bit) << 20.
-// int32 (not short[]) because SMEM loads are dword-only on gfx950: a 16-bit table entry read
-// with a uniform index becomes a VMEM load whose s_waitcnt would also drain the DMA ring.
-__host__ __device__ inline int pack_tap(int dh, int dw, int wt) {
-  return (dh & 0x3ff) | ((dw & 0x3ff) << 10) | (wt << 20);
-}
-__device__ __forceinline__ int tap_dh(int v) { return (v << 22) >> 22; }
-__device__ __forceinline__ int tap_dw(int v) { return (v << 12) >> 22; }
-__device__ __forceinline__ int tap_wt(int v) { return static_cast<int>(static_cast<unsigned>(v) >> 20); }
-
-__device__ __forceinline__ bf16x8_t as_frag(uint4 v) { return __builtin_bit_cast(bf16x8_t, v); }
-
-__device__ __forceinline__ float epi_act(float v, int act) {
-  if (act == kActReLU) return fmaxf(v, 0.f);
-  if (act == kActReLU6) return fminf(fmaxf(v, 0.f), 6.f);
-  return v;
-}
-
-__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
-  return static_cast<uint32_t>(f32_to_bf16(lo)) | (static_cast<uint32_t>(f32_to_bf16(hi)) << 16);
-}
-
-template <int CTRL, int ROWS>
-__device__ __forceinline__ float dpp_f(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROWS, 0xF, false));
-}
-// Sum over each 32-lane half of the wave; valid in lanes 16..31 and 48..63 (DPP only, no LDS):
-// quad swaps, half-row and row mirrors, then row 0 -> 1 / row 2 -> 3 broadcast of lane 15.
-__device__ __forceinline__ float half_wave_sum(float v) {
-  v += dpp_f<0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
-  v += dpp_f<0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
-  v += dpp_f<0x141, 0xF>(v);  // row_half_mirror
-  v += dpp_f<0x140, 0xF>(v);  // row_mirror
-  v += dpp_f<0x142, 0xA>(v);  // row_bcast15 into rows 1 and 3
-  return v;
-}
-
-// Bijective block -> logical id map that gives each XCD (blockIdx % 8 under round-robin
-// dispatch) a contiguous range of logical ids: neighbouring tiles share L2.  Speed only.
-__device__ __forceinline__ int xcd_logical(int b, int G) {
-  const int q = G / 8, r = G % 8, x = b % 8;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
-}
 
 struct IgArgs {
   const uint16_t* x;
@@ -161,12 +88,6 @@ struct IgArgs {
   int taps[kMaxTaps];     // packed tap: see pack_tap (32-bit so the scalar unit can load it)
 };
 
-__device__ __forceinline__ void bf16x4_unpack(uint2 r, float* f) {
-  f[0] = bf16_to_f32(static_cast<uint16_t>(r.x & 0xffff));
-  f[1] = bf16_to_f32(static_cast<uint16_t>(r.x >> 16));
-  f[2] = bf16_to_f32(static_cast<uint16_t>(r.y & 0xffff));
-  f[3] = bf16_to_f32(static_cast<uint16_t>(r.y >> 16));
-}
 
 // STATS: 0 = none, 1 = forward BN statistics of the output, 2 = BN-backward epilogue (IgArgs.bz)
 template <int BM, int BN, int WM, int WN, int NST, int EPI, int STATS>
@@ -865,6 +786,8 @@ bool conv_igemm_supported(const ConvGeom& g, int mode) {
   const int outc = mode == 1 ? g.cin : g.cout;
   if (red % 64 != 0 || outc % 8 != 0) return false;
   if (g.kh * g.kw > kMaxTaps) return false;
+  // tap offsets are packed as 8-bit signed values (pack_tap)
+  if ((g.kh - 1) * g.dh + g.ph > 127 || (g.kw - 1) * g.dw + g.pw > 127) return false;
   if (mode == 2 && (g.cout % 64 != 0)) return false;
   return true;
 }

@@ -12,6 +12,10 @@ each routed to our kernel or to MIOpen:
   longer re-reads the conv output;
 * data gradient: ``conv_igemm_dgrad`` -- the same gather kernel over dy with a flipped tap
   table (one launch per output phase for strided convs, no col2im, no zero-fill);
+* stride-1 3 x 3 convs (forward and data gradient) also have the
+  halo-tiled kernel ``conv_halo`` (``csrc/kernels/conv_halo.hip``): the input tile + halo of a
+  64-channel chunk is staged in LDS once and every tap reads a shifted window of it, instead of
+  re-gathering each pixel once per tap;
 * weight gradient: ``conv_igemm_wgrad`` -- split-K over pixels with transposed LDS reads, fp32
   partial tiles reduced deterministically straight into the fp32 weight-gradient layout
   (MIOpen's wrw needs a zero-filled output buffer every call);
@@ -21,7 +25,8 @@ each routed to our kernel or to MIOpen:
 Each pass of each layer shape is timed once against MIOpen the first time it runs
 (``cudnn.benchmark``-style; never during HIP-graph capture) and the faster one is kept --
 ``decisions()`` lists the outcomes.  ``RTSEG_CONV_MFMA=0`` disables our kernels, ``=1`` forces
-them wherever they apply.
+them wherever they apply; ``RTSEG_CONV_HALO=0`` drops the halo kernel from the candidates,
+``=1`` puts it first (so ``RTSEG_CONV_MFMA=1`` forces it where it applies).
 """
 from __future__ import annotations
 
@@ -38,6 +43,27 @@ _DECISIONS: dict = {}
 
 def _mode() -> str:
     return os.environ.get("RTSEG_CONV_MFMA", "auto")
+
+
+def _halo_mode() -> str:
+    return os.environ.get("RTSEG_CONV_HALO", "auto")
+
+
+def halo_ok(conv, reduce_c: int, out_c: int) -> bool:
+    """Shapes ``conv_halo`` takes: 3 x 3, stride 1, dilation 1, 64-channel multiples on both
+    sides (``reduce_c``: channels summed over, ``out_c``: produced)."""
+    if _halo_mode() == "0" or tuple(conv.stride) != (1, 1):
+        return False
+    if tuple(conv.kernel_size) != (3, 3) or tuple(conv.dilation) != (1, 1):
+        return False
+    return reduce_c % 64 == 0 and out_c % 64 == 0 and max(reduce_c, out_c) <= 8192
+
+
+def _order(cands):
+    """``RTSEG_CONV_HALO=1``: the halo candidate first (what ``RTSEG_CONV_MFMA=1`` forces)."""
+    if _halo_mode() == "1":
+        cands.sort(key=lambda c: c[0] != "halo" and not c[0].startswith("halo"))
+    return cands
 
 
 def _autocast_bf16(x: torch.Tensor) -> bool:
@@ -104,8 +130,10 @@ def _choose(key, candidates):
     if len(candidates) == 1 or _mode() == "1":
         return 0
     got = _DECISIONS.get(key)
-    if got is not None:
-        return got[0]
+    if got is not None:  # by name: the candidate list may differ (e.g. RTSEG_CONV_HALO changed)
+        names = [n for n, _ in candidates]
+        if got[1] in names:
+            return names.index(got[1])
     if torch.cuda.is_current_stream_capturing():
         return len(candidates) - 1  # MIOpen is last
     with torch.no_grad():
@@ -131,6 +159,8 @@ class _ConvFn(torch.autograd.Function):
             y, part = ops().conv_igemm(x, wk, stride, padding, dilation, stats, None, None, 0)
         elif impl == "igemm_nostats":  # short-K convs: the epilogue reduction costs more than a pass
             y, part = ops().conv_igemm(x, wk, stride, padding, dilation, False, None, None, 0)
+        elif impl == "halo":
+            y, part = ops().conv_halo(x, wk, stride, padding, dilation, stats, None, None, 0)
         elif impl == "mfma":
             y, part = ops().conv_mfma(x, wk, stride, padding, dilation, stats, None, None, 0)
         else:
@@ -190,6 +220,8 @@ def _fwd_impl(x, wk, conv, key, stats) -> str:
                 ops().bn_stats_sums(y)
 
             cands.append(("igemm_nostats", nostats))
+        if halo_ok(conv, cin, cout):
+            cands.append(("halo", lambda: ops().conv_halo(x, wk, stride, padding, dilation, stats, None, None, 0)))
     elif cin % 32 == 0 and cout % 8 == 0:
         cands.append(("mfma", lambda: ops().conv_mfma(x, wk, stride, padding, dilation, stats, None, None, 0)))
     if not cands:
@@ -201,7 +233,7 @@ def _fwd_impl(x, wk, conv, key, stats) -> str:
             ops().bn_stats_sums(y)  # the statistics pass our epilogue replaces
 
     cands.append(("miopen", miopen))
-    return cands[_choose(("fwd", stats) + key, cands)][0]
+    return cands[_choose(("fwd", stats) + key, _order(cands))][0]
 
 
 def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None):
@@ -218,15 +250,22 @@ def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None):
             wt.append(wk.permute(3, 1, 2, 0).contiguous())
         return ops().conv_igemm_dgrad(dy, wt[0], list(x.shape), stride, padding, dilation, None, addend)
 
+    def halo():
+        if not wt:
+            wt.append(wk.permute(3, 1, 2, 0).contiguous())
+        return ops().conv_halo_dgrad(dy, wt[0], list(x.shape), stride, padding, dilation, addend)
+
     def miopen():
         return torch.ops.aten.convolution_backward(dy, x, wk.permute(0, 3, 1, 2), None, stride, padding, dilation, False,
                                                    [0, 0], 1, [True, False, False])[0]
 
     cands = [("igemm", ours)] if cout % 64 == 0 and cin % 8 == 0 else []
+    if halo_ok(conv, cout, cin):
+        cands.append(("halo", halo))
     cands.append(("miopen", miopen))
-    name, fn = cands[_choose(("dgrad",) + key, cands)]
+    name, fn = cands[_choose(("dgrad",) + key, _order(cands))]
     dx = fn()
-    if addend is not None and name != "igemm":
+    if addend is not None and name not in ("igemm", "halo"):
         dx = dx + addend
     return dx
 

@@ -4,7 +4,8 @@ and weight gradient.
 Run on the GPU box:  python tools/bench_conv.py [--batch 32] [--iters 20] [--only fwd,dgrad,wgrad]
 One line per shape and pass: relative max error vs MIOpen, time (us) of MIOpen and of ours,
 TFLOP/s of both.  Ours: ``conv_igemm`` (+ its BN-statistics epilogue, ``fwd+st``),
-``conv_igemm_dgrad``, ``conv_igemm_wgrad``; MIOpen: ``F.conv2d`` / ``aten.convolution_backward``
+``conv_igemm_dgrad``, ``conv_igemm_wgrad``, and for stride-1 3x3 shapes the halo-tiled
+``conv_halo`` (``halo``, ``halo+st``) / ``conv_halo_dgrad`` (``halo_dg``); MIOpen: ``F.conv2d`` / ``aten.convolution_backward``
 (MIOpen find mode, i.e. its best solver per shape).
 """
 import argparse
@@ -82,6 +83,7 @@ def main():
         flop = 2.0 * n * ho * wo * cout * cin * k * k
         dy = torch.randn_like(y_ref).contiguous(memory_format=torch.channels_last)
         tag = f"{n}x{cin}x{h}x{w}->{cout} k{k}s{s}"
+        halo = s == 1 and k == 3 and cin % 64 == 0 and cout % 64 == 0 and os.environ.get("RTSEG_CONV_HALO") != "0"
         rows = []
         for cfg in cfgs:
             sfx = "" if cfg is None else f"@{cfg}"
@@ -97,6 +99,14 @@ def main():
                     t_os = timeit(lambda: torch.ops.rtseg.conv_igemm(x, wk, [s, s], [p, p], [1, 1], True, None, None,
                                                                      0), a.iters)
                     rows.append(("fwd+st", 0.0, t_m, t_os))
+                    if halo:  # the halo-tiled kernel (conv_halo.hip) on the same shape
+                        yh, _ = torch.ops.rtseg.conv_halo(x, wk, [s, s], [p, p], [1, 1], False, None, None, 0)
+                        t_h = timeit(lambda: torch.ops.rtseg.conv_halo(x, wk, [s, s], [p, p], [1, 1], False, None,
+                                                                       None, 0), a.iters)
+                        rows.append(("halo", relerr(yh, y_ref), t_m, t_h))
+                        t_hs = timeit(lambda: torch.ops.rtseg.conv_halo(x, wk, [s, s], [p, p], [1, 1], True, None,
+                                                                        None, 0), a.iters)
+                        rows.append(("halo+st", 0.0, t_m, t_hs))
             if "dgrad" in passes:
                 dx_ref = conv_bw(dy, x, wcl, None, [s, s], [p, p], [1, 1], False, [0, 0], 1, [True, False, False])[0]
                 dx = torch.ops.rtseg.conv_igemm_dgrad(dy, wtr, list(x.shape), [s, s], [p, p], [1, 1])
@@ -105,6 +115,11 @@ def main():
                 t_o = timeit(lambda: torch.ops.rtseg.conv_igemm_dgrad(dy, wtr, list(x.shape), [s, s], [p, p], [1, 1]),
                              a.iters)
                 rows.append(("dgrad" + sfx, relerr(dx, dx_ref), t_m, t_o))
+                if halo and cfg is None:
+                    dxh = torch.ops.rtseg.conv_halo_dgrad(dy, wtr, list(x.shape), [s, s], [p, p], [1, 1])
+                    t_h = timeit(lambda: torch.ops.rtseg.conv_halo_dgrad(dy, wtr, list(x.shape), [s, s], [p, p],
+                                                                         [1, 1]), a.iters)
+                    rows.append(("halo_dg", relerr(dxh, dx_ref), t_m, t_h))
             if "dgrad_bn" in passes and cin % 32 == 0:
                 # BN-backward reduction of the BN producing x: separate pass (ours dgrad + reduce,
                 # reported in the "miopen" column) vs fused into the dgrad epilogue
