@@ -29,6 +29,13 @@ RESNET_SPECS = {
     "resnet50": ("bottleneck", (3, 4, 6, 3)),
     "resnet101": ("bottleneck", (3, 4, 23, 3)),
     "resnet152": ("bottleneck", (3, 8, 36, 3)),
+    # ResNeXt (SMP / torchvision names): grouped 3x3 in every bottleneck, (groups, width per group)
+    "resnext50_32x4d": ("bottleneck", (3, 4, 6, 3), 32, 4),
+    "resnext101_32x4d": ("bottleneck", (3, 4, 23, 3), 32, 4),
+    "resnext101_32x8d": ("bottleneck", (3, 4, 23, 3), 32, 8),
+    "resnext101_32x16d": ("bottleneck", (3, 4, 23, 3), 32, 16),
+    "resnext101_32x32d": ("bottleneck", (3, 4, 23, 3), 32, 32),
+    "resnext101_32x48d": ("bottleneck", (3, 4, 23, 3), 32, 48),
 }
 
 
@@ -75,13 +82,14 @@ class BasicBlock(nn.Module):
 class Bottleneck(nn.Module):
     expansion = 4
 
-    def __init__(self, inplanes, planes, stride=1, downsample=None, dilation=1):
+    def __init__(self, inplanes, planes, stride=1, downsample=None, dilation=1, groups=1, base_width=64):
         super().__init__()
-        self.conv1 = nn.Conv2d(inplanes, planes, 1, bias=False)
-        self.bn1 = nn.BatchNorm2d(planes)
-        self.conv2 = nn.Conv2d(planes, planes, 3, stride, dilation, dilation=dilation, bias=False)
-        self.bn2 = nn.BatchNorm2d(planes)
-        self.conv3 = nn.Conv2d(planes, planes * 4, 1, bias=False)
+        width = int(planes * (base_width / 64.0)) * groups  # torchvision's ResNeXt width rule
+        self.conv1 = nn.Conv2d(inplanes, width, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.conv2 = nn.Conv2d(width, width, 3, stride, dilation, dilation=dilation, groups=groups, bias=False)
+        self.bn2 = nn.BatchNorm2d(width)
+        self.conv3 = nn.Conv2d(width, planes * 4, 1, bias=False)
         self.bn3 = nn.BatchNorm2d(planes * 4)
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
@@ -113,7 +121,8 @@ class ResNet(nn.Module):
         super().__init__()
         if resnet_type not in RESNET_SPECS:
             raise ValueError(f"Unsupported ResNet type: {resnet_type}.\n")
-        kind, layers = RESNET_SPECS[resnet_type]
+        kind, layers, *gw = RESNET_SPECS[resnet_type]
+        self._groups, self._base_width = gw if gw else (1, 64)
         block = BasicBlock if kind == "basic" else Bottleneck
         self.resnet_type = resnet_type
         self.inplanes, self.dilation = 64, 1
@@ -145,9 +154,10 @@ class ResNet(nn.Module):
         if stride != 1 or self.inplanes != planes * block.expansion:
             downsample = _ConvBN(nn.Conv2d(self.inplanes, planes * block.expansion, 1, stride, bias=False),
                                  nn.BatchNorm2d(planes * block.expansion))
-        layers = [block(self.inplanes, planes, stride, downsample, prev_dil)]
+        kw = {} if block is BasicBlock else {"groups": self._groups, "base_width": self._base_width}
+        layers = [block(self.inplanes, planes, stride, downsample, prev_dil, **kw)]
         self.inplanes = planes * block.expansion
-        layers += [block(self.inplanes, planes, dilation=self.dilation) for _ in range(1, blocks)]
+        layers += [block(self.inplanes, planes, dilation=self.dilation, **kw) for _ in range(1, blocks)]
         return nn.Sequential(*layers)
 
     def stem(self, x):

@@ -4,7 +4,7 @@ Parity: reference models/__init__.py:42-44 (``decoder_hub``), :67-81
 (``smp`` branch incl. the ``mit_b*`` special cases) and :102-122 (teacher).
 segmentation_models_pytorch is not installed in this environment, so the nine
 decoders are native re-implementations with SMP's module layout (see
-``base.py``); encoders: ResNet-18/34/50/101/152, MobileNetV2.
+``base.py``); encoders: ResNet-18/34/50/101/152, ResNeXt-50/101, MobileNetV2, MiT-B0..B5.
 """
 from __future__ import annotations
 
@@ -29,6 +29,9 @@ def build_smp_model(decoder, encoder, encoder_weights=None, num_class=1, in_chan
     encoder = encoder or "resnet18"
     if encoder.startswith("mit_b") and decoder in ("deeplabv3", "deeplabv3p", "linknet", "unetpp"):
         raise ValueError(f"Encoder `{encoder}` is not supported for `{decoder}")
+    if encoder.startswith("mit_b") and decoder == "pan":  # reference models/__init__.py:69-73
+        return DECODER_HUB[decoder](encoder_name=encoder, encoder_weights=encoder_weights, encoder_output_stride=32,
+                                    in_channels=in_channels, classes=num_class)
     return DECODER_HUB[decoder](encoder_name=encoder, encoder_weights=encoder_weights, in_channels=in_channels,
                                 classes=num_class)
 

@@ -1,4 +1,5 @@
-"""SMP-style encoders: ResNet-18/34/50/101/152 and MobileNetV2.
+"""SMP-style encoders: ResNet-18/34/50/101/152, ResNeXt-50/101 (32xNd), MobileNetV2 and the
+Mix Transformers MiT-B0..B5 (``mit.py``).
 
 Behavioural target: SMP's ``ResNetEncoder`` / ``MobileNetV2Encoder`` (the
 torchvision networks with the classifier removed; ``forward`` returns the
@@ -14,6 +15,7 @@ import torch.nn as nn
 
 from ... import ops
 from ..backbone import RESNET_SPECS, ResNet, load_pretrained, mobilenet_v2_features
+from .mit import MIT_SPECS, MixVisionTransformerEncoder
 
 _RESNET_CHANNELS = {"basic": (3, 64, 64, 128, 256, 512), "bottleneck": (3, 64, 256, 512, 1024, 2048)}
 
@@ -91,14 +93,21 @@ class MobileNetV2Encoder(_EncoderMixin, nn.Module):
         return self.get_stages()[1:]
 
 
-ENCODERS = tuple(RESNET_SPECS) + ("mobilenet_v2",)
+ENCODERS = tuple(RESNET_SPECS) + ("mobilenet_v2",) + tuple(MIT_SPECS)
 
 
 def get_encoder(name, in_channels=3, depth=5, weights=None, output_stride=32):
     if name is None:
         raise ValueError("config.encoder must be set for model='smp'")
-    if name.startswith("mit_b"):
-        raise NotImplementedError(f"Encoder `{name}` (Mix Transformer) is not available in this framework.")
+    if name in MIT_SPECS:
+        # SMP's MixVisionTransformerEncoder: 3 input channels only, no dilated mode
+        if in_channels != 3:
+            raise ValueError("MixVisionTransformer encoder does not support in_channels setting other than 3")
+        enc = MixVisionTransformerEncoder(name, depth)
+        if weights is not None:
+            load_pretrained(enc, name)
+        enc.make_dilated(output_stride)
+        return enc
     if name in RESNET_SPECS:
         enc = ResNetEncoder(name, depth)
     elif name == "mobilenet_v2":

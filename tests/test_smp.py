@@ -61,8 +61,10 @@ def test_encoder_strides_and_smp_dilation_rule():
 
 
 def test_unsupported_encoders_raise():
-    with pytest.raises(NotImplementedError):
-        get_encoder("mit_b0")
+    with pytest.raises(ValueError):  # SMP: MiT has no dilated mode and only 3 input channels
+        get_encoder("mit_b0", output_stride=16)
+    with pytest.raises(ValueError):
+        get_encoder("mit_b0", in_channels=4)
     with pytest.raises(ValueError):
         build_smp_model("unetpp", "mit_b0", None, 19)
     with pytest.raises(ValueError):
@@ -99,3 +101,48 @@ def test_smp_bf16_train_step_gpu(decoder):
     loss.backward()
     assert torch.isfinite(loss)
     assert all(torch.isfinite(p.grad).all() for p in m.parameters() if p.grad is not None)
+
+
+def test_mit_encoder_contract():
+    """SMP's MixVisionTransformerEncoder contract: [x, 0-channel stride-2 placeholder, /4, /8, /16,
+    /32] with MiT-B0's widths; SMP checkpoint key layout (incl. the unused ImageNet head)."""
+    e = get_encoder("mit_b0", depth=5)
+    feats = e(torch.randn(2, 3, 64, 96))
+    assert [tuple(f.shape[1:]) for f in feats] == [(3, 64, 96), (0, 32, 48), (32, 16, 24), (64, 8, 12),
+                                                   (160, 4, 6), (256, 2, 3)]
+    assert e.out_channels == (3, 0, 32, 64, 160, 256)
+    keys = set(e.state_dict())
+    for k in ("patch_embed1.proj.weight", "patch_embed4.norm.bias", "block1.1.attn.sr.weight",
+              "block1.0.attn.norm.weight", "block3.1.mlp.dwconv.dwconv.weight", "block4.1.attn.kv.weight",
+              "norm4.weight", "head.weight"):
+        assert k in keys, k
+    assert not any(k.startswith("block4.0.attn.sr") for k in keys)  # stage 4: sr ratio 1
+    assert len(e.block3) == 2 and len(get_encoder("mit_b2").block3) == 6
+    # an ImageNet checkpoint without its classifier still loads strictly
+    sd = {k: v for k, v in e.state_dict().items() if not k.startswith("head.")}
+    e.load_state_dict(sd)
+
+
+@pytest.mark.parametrize("decoder", ["unet", "fpn", "pspnet", "manet", "pan"])
+def test_mit_with_supported_decoders(decoder):
+    torch.manual_seed(0)
+    m = build_smp_model(decoder, "mit_b0", None, 19).train()
+    hw = 256 if decoder == "pan" else 64  # PAN's FPA pools the stride-32 map 8x further
+    x = torch.randn(2, 3, hw, hw)
+    y = m(x)
+    assert y.shape == (2, 19, hw, hw)
+    y.float().square().mean().backward()
+    assert m.encoder.patch_embed1.proj.weight.grad is not None
+    if decoder == "pan":  # reference models/__init__.py:69-73: MiT + PAN at encoder output stride 32
+        assert m.encoder.output_stride == 32
+
+
+def test_resnext_encoder_matches_torchvision_layout():
+    e = get_encoder("resnext50_32x4d", depth=5)
+    assert e.layer1[0].conv2.groups == 32 and e.layer1[0].conv2.in_channels == 128
+    assert e.layer4[0].conv2.out_channels == 1024 and e.layer4[0].conv3.out_channels == 2048
+    # torchvision resnext50_32x4d has 25,028,904 parameters, 2,049,000 of them in the fc head
+    assert sum(p.numel() for p in e.parameters()) == 25_028_904 - 2_049_000
+    feats = e(torch.randn(1, 3, 64, 64))
+    assert [f.shape[1] for f in feats] == [3, 64, 256, 512, 1024, 2048]
+    assert get_encoder("resnext101_32x8d").layer3[22].conv2.groups == 32
