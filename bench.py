@@ -152,7 +152,7 @@ def main():
 
     cfg = make_config(a, world)
     cfg.cudnn_benchmark = not a.no_cudnn_benchmark
-    configure_backend(cfg.cudnn_benchmark)
+    configure_backend(cfg.cudnn_benchmark, model=cfg.model, exclude_naive=True)
     ops.load()
     trainer = SegTrainer(cfg)
     trainer.parallel_model(cfg)

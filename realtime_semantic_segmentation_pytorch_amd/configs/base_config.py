@@ -125,8 +125,11 @@ class BaseConfig:
         self.fused_optimizer = True      # HIP multi-tensor optimizer step that also writes the EMA
         self.hip_depthwise = True        # depth-wise convs on the HIP kernels (else MIOpen)
         self.hip_pooling = True          # avg / max / adaptive pooling on the HIP kernels
+        self.hip_activations = True      # PReLU / ELU / SELU / Hardswish / SiLU / ... on the HIP kernels
         self.ddp_bucket_mb = 32          # RCCL all-reduce bucket: ~3 buckets for DDRNet-23 (84 MB), overlapped with backward
         self.ddp_static_graph = True
+        self.spawn_procs = None          # main.py without torchrun: worker processes (None: one per visible GPU)
+        self.gpu_aug = False             # training augmentation on the GPU (ops/augment.py): workers only decode
         self.synthetic_data = False      # device-generated synthetic batches (benchmarks)
         self.synthetic_len = 64          # images per epoch of the synthetic dataset
         self.synthetic_size = None       # (H, W) of synthetic images (default: crop)

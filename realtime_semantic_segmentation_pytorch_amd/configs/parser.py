@@ -42,7 +42,7 @@ _SPEC = [
     ("dice_loss_coef", float, {}), ("bce_loss_coef", float, {}),
     # training
     ("total_epoch", int, {}), ("base_lr", float, {}), ("train_bs", int, {}),
-    ("use_aux", "true", {}), ("aux_coef", "list", {}), ("logger_name", str, {}),
+    ("use_aux", "true", {}), ("no_aux", "true", {"dest": "no_aux"}), ("aux_coef", "list", {}), ("logger_name", str, {}),
     # validating
     ("val_bs", int, {}), ("begin_val_epoch", int, {}), ("val_interval", int, {}),
     # testing
@@ -79,7 +79,7 @@ _SPEC = [
     ("amp_dtype", str, {"choices": ["bf16", "fp16"]}), ("no_channels_last", "true",
                                                         {"dest": "no_channels_last"}),
     ("no_fused_loss", "true", {"dest": "no_fused_loss"}), ("ddp_bucket_mb", int, {}),
-    ("synthetic_data", "true", {}), ("synthetic_len", int, {}), ("max_train_itrs", int, {}),
+    ("gpu_aug", "true", {}), ("spawn_procs", int, {}), ("synthetic_data", "true", {}), ("synthetic_len", int, {}), ("max_train_itrs", int, {}),
     ("log_interval", int, {}), ("device", str, {}),
     ("no_fused_optimizer", "true", {"dest": "no_fused_optimizer"}),
 ]
@@ -114,6 +114,8 @@ def load_parser(config, argv=None):
             continue
         if k == "no_channels_last":
             config.channels_last = not v
+        elif k == "no_aux":
+            config.use_aux = not v
         elif k == "no_fused_loss":
             config.fused_loss = not v
         elif k == "no_fused_optimizer":

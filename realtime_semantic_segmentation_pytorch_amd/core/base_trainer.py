@@ -27,6 +27,21 @@ from ..utils.runtime import configure_backend
 from .loss import get_loss_fn
 
 
+def inject_fault(epoch: int):
+    """Failure injection for restart tests (tests/test_elastic_cpu.py): with
+    ``RTSEG_FAULT_EPOCH=e`` and ``RTSEG_FAULT_SENTINEL=path``, the LAST rank dies (exit 17) when
+    epoch ``e`` starts -- once: the sentinel file marks that the fault has fired, so the restarted
+    job (torchrun ``--max-restarts``) resumes from ``last.pth`` and runs through."""
+    want, sentinel = os.environ.get("RTSEG_FAULT_EPOCH"), os.environ.get("RTSEG_FAULT_SENTINEL")
+    if want is None or sentinel is None or int(want) != epoch or os.path.exists(sentinel):
+        return
+    rank, _, world = dist_env()
+    if rank == max(world - 1, 0) or rank == -1:
+        with open(sentinel, "w") as f:
+            f.write(f"rank {rank} killed at epoch {epoch}\n")
+        os._exit(17)
+
+
 class BaseTrainer:
     def __init__(self, config):
         self.rank, self.local_rank, self.world_size = dist_env()
@@ -35,7 +50,8 @@ class BaseTrainer:
         if hasattr(config, "init_dependent_config"):
             config.init_dependent_config()  # idempotent; main.py calls it too
         self.logger = get_logger(config, self.main_rank)
-        configure_backend(getattr(config, "cudnn_benchmark", True))  # same MIOpen setup as bench.py
+        # same find-mode policy as bench.py (which alone also drops the naive solvers)
+        configure_backend(getattr(config, "cudnn_benchmark", True), model=config.model)
         self.device = set_device(config, self.local_rank)
         self.amp_dtype = torch.float16 if getattr(config, "amp_dtype", "bf16") == "fp16" else torch.bfloat16
         use_scaler = bool(config.amp_training) and self.amp_dtype == torch.float16 and self.device.type == "cuda"
@@ -77,6 +93,7 @@ class BaseTrainer:
             log_config(config, self.logger)
         for cur_epoch in range(self.cur_epoch, config.total_epoch):
             self.cur_epoch = cur_epoch
+            inject_fault(cur_epoch)
             self.train_one_epoch(config)
             if cur_epoch >= config.begin_val_epoch and cur_epoch % config.val_interval == 0:
                 val_score = self.validate(config)

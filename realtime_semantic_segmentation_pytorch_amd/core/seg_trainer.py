@@ -60,6 +60,14 @@ class SegTrainer(BaseTrainer):
         masks = masks.to(self.device, dtype=torch.long, non_blocking=True)
         return images, masks
 
+    def _gpu_augment(self, img, msk, params):
+        """Raw uint8 batch from a ``gpu_aug`` dataset -> augmented (images, masks) on the device."""
+        ds = self.train_loader.dataset
+        cl = bool(getattr(self.config, "channels_last", False)) and self.device.type == "cuda"
+        img = img.to(self.device, non_blocking=True)
+        msk = msk.to(self.device, non_blocking=True)
+        return ops.augment_batch(img, msk, params, ds.aug_lut, ds.aug_spec, channels_last=cl)
+
     def compute_loss(self, images, masks):
         """Forward + total loss. Returns (loss, main_preds, extras dict)."""
         cfg = self.config
@@ -124,11 +132,11 @@ class SegTrainer(BaseTrainer):
         sampler_set_epoch(config, self.train_loader, self.cur_epoch)
         log_every = max(1, int(getattr(config, "log_interval", 20)))
         max_itrs = getattr(config, "max_train_itrs", None)
-        for cur_itrs, (images, masks) in enumerate(self.train_loader):
+        for cur_itrs, batch in enumerate(self.train_loader):
             if max_itrs is not None and cur_itrs >= max_itrs:
                 break
             self.cur_itrs = cur_itrs
-            images, masks = self._prep(images, masks)
+            images, masks = self._gpu_augment(*batch) if len(batch) == 3 else self._prep(*batch)
             loss, extras = self.train_step(images, masks)
             if self.main_rank and (cur_itrs % log_every == 0):
                 lv = float(loss)

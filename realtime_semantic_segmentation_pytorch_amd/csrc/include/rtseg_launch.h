@@ -272,4 +272,68 @@ struct TapConvGeo {
 void launch_tapconv(const void* x, const float* w, const float* bias, void* y, const TapConvGeo& g, int ci, int co,
                     int dtype, hipStream_t st);
 
+// ---- augment.hip --------------------------------------------------------------
+// Per-sample parameter row (fp32 [N, kAugParams]): scaled size, centred-pad offsets, crop origin,
+// flip, jitter op count + order code (2 bits per op: 0 brightness, 1 contrast, 2 saturation,
+// 3 hue), jitter factors.  Drawn on the host by ops/augment.py.
+enum AugParam : int {
+  kAugNh = 0, kAugNw, kAugTop, kAugLeft, kAugCy, kAugCx, kAugFlip, kAugNops, kAugCode,
+  kAugBright, kAugContrast, kAugSat, kAugHue, kAugParams
+};
+struct AugArgs {
+  const uint8_t* img;     // [N, H, W, 3] uint8
+  const uint8_t* msk;     // [N, H, W] uint8 raw labels, or null
+  const float* params;    // [N, kAugParams]
+  const uint8_t* lut;     // [256] raw label -> training label
+  const float* norm;      // [6] mean[3], std[3] (on [0, 1] pixels)
+  float* part;            // [N, augment_stat_blocks] contrast statistics workspace, or null
+  Tensor4 out;            // [N, 3, ch, cw] fp32 / bf16 / fp16, any strides
+  void* mout;             // [N, ch, cw] int64 or uint8, or null
+  int mask_bytes;
+  int n, h, w, ch, cw;
+  float pad_value;
+  int mask_pad;
+};
+int augment_stat_blocks(int ch, int cw);
+void launch_augment(const AugArgs& a, hipStream_t st);
+
+// ---- act.hip ------------------------------------------------------------------
+enum ActKind : int {
+  kActPReLU = 0, kActLeaky, kActELU, kActCELU, kActSELU, kActHardswish, kActHardtanh, kActSiLU,
+  kActSigmoid, kActTanh, kActGELU, kActGELUTanh
+};
+// forward: out = f(x); backward (bwd): out = dx = dy * f'(x).  PReLU with a weight tensor w
+// (C = 1 for a scalar slope): channel of element i = (i / inner) % C (inner = 1: channels-last
+// or flat; inner = H*W: contiguous NCHW); its backward also writes dw [C] through `part`
+// (act_prelu_plan(a).blocks * C floats, or blocks floats in planes mode).  Other kinds: slope /
+// alpha / min in `a`, max in `b`.
+struct ActArgs {
+  const void* x;
+  const void* dy;
+  void* out;
+  const float* w;
+  float* part;
+  float* dw;
+  int dtype, kind;
+  bool bwd;
+  int64_t n;
+  int C;
+  int64_t inner;
+  float a, b;
+};
+struct ActPreluPlan {
+  bool planes;
+  int blocks, slices, tx;
+  int64_t rows_per_block;
+};
+ActPreluPlan act_prelu_plan(const ActArgs& a);
+void launch_act(const ActArgs& a, hipStream_t st);
+
+// ---- shuffle.hip --------------------------------------------------------------
+// out (contiguous NCHW, or channels-last when out_cl) <- remap of in (any strides):
+// kShufPixel: PixelShuffle(r); kShufPixelInv: PixelUnshuffle(r); kShufChannel: channel shuffle
+// with r groups.  fp32 / bf16 / fp16.
+enum ShufMode : int { kShufPixel = 0, kShufPixelInv = 1, kShufChannel = 2 };
+void launch_shuffle(const Tensor4& in, const Tensor4& out, int mode, int r, bool out_cl, hipStream_t st);
+
 }  // namespace rtseg

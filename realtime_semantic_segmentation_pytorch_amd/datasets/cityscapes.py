@@ -44,6 +44,24 @@ def sample_rng(seed: int, epoch: int, index: int) -> np.random.Generator:
     return np.random.default_rng([int(seed) % (2 ** 63), int(epoch), int(index)])
 
 
+def aug_spec(transform):
+    """Static crop / pad / normalisation of a training pipeline (for ops.augment_batch)."""
+    from ..ops.augment import draw_params
+
+    big = 1 << 15  # any source larger than the crop: the spec does not depend on the draws
+    return draw_params(transform, big, big, np.random.default_rng(0))[1]
+
+
+def raw_sample(transform, image, mask, rng):
+    """GPU-augmentation sample: (uint8 [H, W, 3] image, uint8 [H, W] raw labels, fp32 params)
+    with the parameters drawn from ``rng`` exactly as ``transform`` would draw them."""
+    from ..ops.augment import draw_params
+
+    params, _ = draw_params(transform, image.shape[0], image.shape[1], rng)
+    return (torch.from_numpy(np.require(image, np.uint8, ["C", "W"])),
+            torch.from_numpy(np.require(mask, np.uint8, ["C", "W"])), torch.from_numpy(params))
+
+
 class Cityscapes(Dataset):
     id_to_train_id = np.array(_TRAIN_IDS)
     # uint8 lookup (255 for anything unknown) used by encode_target
@@ -61,6 +79,11 @@ class Cityscapes(Dataset):
         self.mode = mode
         self.seed = int(getattr(config, "random_seed", 1))
         self.transform = T.train_transform(config) if mode == "train" else T.val_transform(config)
+        # GPU augmentation (ops/augment.py): __getitem__ returns the decoded raw image and label
+        # ids plus the drawn parameters; the trainer runs the pixel work on the device
+        self.gpu_aug = mode == "train" and bool(getattr(config, "gpu_aug", False))
+        self.aug_lut = torch.from_numpy(self._lut.copy())
+        self.aug_spec = aug_spec(self.transform) if self.gpu_aug else None
         self.images, self.masks = [], []
         for city in sorted(os.listdir(img_dir)):
             for name in sorted(os.listdir(os.path.join(img_dir, city))):
@@ -75,6 +98,8 @@ class Cityscapes(Dataset):
         index, epoch = split_key(key)
         image = np.asarray(Image.open(self.images[index]).convert("RGB"))
         mask = np.asarray(Image.open(self.masks[index]).convert("L"))
+        if self.gpu_aug:
+            return raw_sample(self.transform, image, mask, sample_rng(self.seed, epoch, index))
         image, mask = self.transform(image, mask, sample_rng(self.seed, epoch, index))
         return T.to_tensor(image), torch.from_numpy(self.encode_target(mask).astype(np.int64))
 

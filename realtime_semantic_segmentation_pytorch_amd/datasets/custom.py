@@ -15,7 +15,7 @@ from PIL import Image
 from torch.utils.data import Dataset
 
 from . import transforms as T
-from .cityscapes import sample_rng, split_key
+from .cityscapes import aug_spec, raw_sample, sample_rng, split_key
 
 
 class Custom(Dataset):
@@ -42,6 +42,12 @@ class Custom(Dataset):
             self.transform = T.train_transform(config, norm, square_size=config.train_size)
         else:
             self.transform = T.val_transform(config, norm, square_size=config.test_size)
+        # GPU augmentation needs one source size per batch: not with ResizeToSquare (train_size)
+        self.gpu_aug = mode == "train" and bool(getattr(config, "gpu_aug", False))
+        if self.gpu_aug and config.train_size is not None:
+            raise ValueError("gpu_aug does not support train_size (ResizeToSquare); unset one of them")
+        self.aug_lut = torch.arange(256, dtype=torch.uint8)  # masks already hold class ids
+        self.aug_spec = aug_spec(self.transform) if self.gpu_aug else None
         self.images, self.masks = [], []
         for name in sorted(os.listdir(img_dir)):
             self.images.append(os.path.join(img_dir, name))
@@ -54,5 +60,7 @@ class Custom(Dataset):
         index, epoch = split_key(key)
         image = np.asarray(Image.open(self.images[index]).convert("RGB"))
         mask = np.asarray(Image.open(self.masks[index]).convert("L"))
+        if self.gpu_aug:
+            return raw_sample(self.transform, image, mask, sample_rng(self.seed, epoch, index))
         image, mask = self.transform(image, mask, sample_rng(self.seed, epoch, index))
         return T.to_tensor(image), torch.from_numpy(np.asarray(mask, np.int64))

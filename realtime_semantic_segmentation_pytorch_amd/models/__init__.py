@@ -81,6 +81,9 @@ def get_model(config):
         ops.convert_dilated_group_convs(model)
     if getattr(config, "hip_deconv", True):
         ops.convert_transposed_convs(model)
+    if getattr(config, "hip_activations", True):
+        ops.convert_activations(model)
+    ops.convert_pixel_shuffle(model)
     return model
 
 

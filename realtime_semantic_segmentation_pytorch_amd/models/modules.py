@@ -40,9 +40,9 @@ def conv1x1(in_channels, out_channels, stride=1, bias=False):
 
 
 def channel_shuffle(x: torch.Tensor, groups: int = 2) -> torch.Tensor:
-    """ShuffleNet channel shuffle: [N, g*k, H, W] -> interleave the g groups."""
-    n, c, h, w = x.shape
-    return x.reshape(n, groups, c // groups, h, w).transpose(1, 2).reshape(n, c, h, w)
+    """ShuffleNet channel shuffle: [N, g*k, H, W] -> interleave the g groups (one HIP gather
+    pass on GPU tensors, ``ops.channel_shuffle``)."""
+    return ops.channel_shuffle(x, groups)
 
 
 _ACTIVATIONS = {

@@ -94,7 +94,7 @@ class _FusedMixin:
         slot and a replaced state buffer can never leave a stale pointer behind."""
         key = tuple((r[0].data_ptr(), r[1].data_ptr(), r[2].data_ptr() if r[2] is not None else 0,
                      r[3].data_ptr() if r[3] is not None else 0, r[4].data_ptr() if r[4] is not None else 0,
-                     r[5]) for r in rows)
+                     r[5], r[0].numel(), r[1].dtype) for r in rows)
         cache = self._tables
         if cache.get(slot, (None,))[0] != key:
             cache[slot] = (key, build_table(rows, rows[0][0].device))
@@ -211,7 +211,8 @@ def ema_lerp_(pairs, weight: float):
     rows = [(s, s, None, None, e, False) for s, e in pairs]
     if not rows:
         return
-    key = tuple((r[0].data_ptr(), r[4].data_ptr()) for r in rows)
+    # sizes too: a later set of tensors may reuse the same addresses with other shapes
+    key = tuple((r[0].data_ptr(), r[4].data_ptr(), r[0].numel()) for r in rows)
     tab = _EMA_TABLES.get(key)
     if tab is None:
         if len(_EMA_TABLES) > 16:

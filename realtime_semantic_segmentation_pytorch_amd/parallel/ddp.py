@@ -10,8 +10,11 @@ utils/parallel.py:7-53).
   over all 7 xGMI links) that overlap with the rest of backward.  Buckets are
   views of the gradients (``gradient_as_bucket_view``), BN buffers are not
   re-broadcast every forward when SyncBN already makes them identical.
-* single-process multi-GPU ``nn.DataParallel`` is deliberately not recreated:
-  non-DDP runs use one device ("DP" row).
+* single-process multi-GPU ``nn.DataParallel`` is deliberately not recreated: a launcher-less
+  run that sees several GPUs is turned into single-node DDP by ``main.py`` (one spawned worker
+  per device, SURVEY 2.10 "DP" row);
+* a torchrun restart (``--max-restarts``) re-joins through a per-generation store prefix
+  (``_restart_store``) and the trainer resumes from ``last.pth``.
 """
 from __future__ import annotations
 
@@ -77,11 +80,15 @@ def set_device(config, local_rank=None):
             device = torch.device("cpu")
             backend = "gloo"
         if not is_dist():
-            kw = dict(backend=backend, init_method="env://",
+            kw = dict(backend=backend,
                       timeout=datetime.timedelta(minutes=int(os.getenv("RTSEG_PG_TIMEOUT_MIN", 30))))
             if backend == "nccl":
                 kw["device_id"] = device
-            dist.init_process_group(**kw)
+            store = _restart_store(rank, world, kw["timeout"])
+            if store is None:
+                dist.init_process_group(init_method="env://", **kw)
+            else:
+                dist.init_process_group(store=store, rank=rank, world_size=world, **kw)
         config.gpu_num = dist.get_world_size()
         config.global_rank = dist.get_rank()
     else:
@@ -92,6 +99,19 @@ def set_device(config, local_rank=None):
         config.global_rank = 0
     config.num_workers = int(config.base_workers)  # per rank
     return device
+
+
+def _restart_store(rank, world, timeout):
+    """After a torchrun restart (``--max-restarts``), a key space of this generation's own on the
+    launcher's store: the default env:// rendezvous would read the previous generation's
+    (dead) peer addresses left in the store and fail to connect.  None on a first start."""
+    gen = int(os.getenv("TORCHELASTIC_RESTART_COUNT", "0") or 0)
+    if gen == 0:
+        return None
+    agent = os.getenv("TORCHELASTIC_USE_AGENT_STORE", "False") == "True"
+    base = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world,
+                         is_master=(not agent and rank == 0), timeout=timeout)
+    return dist.PrefixStore(f"rtseg_gen{gen}", base)
 
 
 _SYNCBN_PG = None

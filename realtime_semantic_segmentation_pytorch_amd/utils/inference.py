@@ -18,6 +18,8 @@ from typing import Optional, Sequence
 import torch
 import torch.nn as nn
 
+from ..ops.act import _HipAct
+
 from .. import ops
 
 
@@ -37,7 +39,9 @@ class InferenceEngine:
             for m in model.modules():
                 # isinstance: the rtseg conv subclasses (DilatedGroupConv2d, DepthwiseConv2d, ...)
                 # carry fp32 weights too
-                if isinstance(m, (nn.Conv2d, nn.ConvTranspose2d, nn.Linear, nn.PReLU)):
+                # (the HIP activation kernels read an fp32 PReLU weight directly: no autocast cast)
+                if isinstance(m, (nn.Conv2d, nn.ConvTranspose2d, nn.Linear)) or (
+                        isinstance(m, nn.PReLU) and not isinstance(m, _HipAct)):
                     m.to(dtype)
         self.model = model.eval().to(self.device)
         if channels_last:

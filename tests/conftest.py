@@ -22,3 +22,16 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _isolate_miopen_find_mode():
+    """A trainer built by one test turns MIOpen find mode on for the process (utils/runtime.py);
+    it must not leak into later tests, whose models may have geometries find mode is not
+    verified on (LEDNet / CFPNet degenerate dilated convs)."""
+    import torch
+
+    saved = torch.backends.cudnn.benchmark
+    torch.backends.cudnn.benchmark = False
+    yield
+    torch.backends.cudnn.benchmark = saved
