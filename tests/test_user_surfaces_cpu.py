@@ -239,3 +239,29 @@ def test_cos_warmup_cycles_momentum(optimizer_type):
     assert moms[-1] == pytest.approx(0.95, abs=1e-3)
     with pytest.raises(ValueError):  # stepping past total_itrs raises, as in the reference
         s.step()
+
+
+def test_miopen_find_mode_only_on_verified_models(monkeypatch):
+    """MIOpen's exhaustive solver search faulted the GPU on degenerate dilated convs (CFPNet at
+    1024x512, LEDNet's dilation-17 (3,1) convs on a 16-row map at 128x256 once a trainer had
+    switched find mode on for the whole pytest process): find mode is per model and the naive
+    solvers -- the fallback for those geometries -- are only excluded by bench.py."""
+    import torch
+
+    from realtime_semantic_segmentation_pytorch_amd.utils.runtime import _NAIVE, configure_backend
+
+    for k in _NAIVE:  # set-then-delete so monkeypatch restores the original state afterwards
+        monkeypatch.setenv(k, "1")
+        monkeypatch.delenv(k)
+    saved = torch.backends.cudnn.benchmark
+    try:
+        configure_backend(True, model="ddrnet")
+        assert torch.backends.cudnn.benchmark
+        for key in ("lednet", "cfpnet", "enet", "smp"):
+            configure_backend(True, model=key)
+            assert not torch.backends.cudnn.benchmark, key
+        assert all(k not in os.environ for k in _NAIVE)  # trainers keep the naive solvers
+        configure_backend(True, model="ddrnet", exclude_naive=True)  # bench.py only
+        assert all(os.environ[k] == "0" for k in _NAIVE)
+    finally:
+        torch.backends.cudnn.benchmark = saved
