@@ -92,6 +92,8 @@ def make_config(a, world):
         c.kd_training = True
         c.teacher_model, c.teacher_encoder, c.teacher_decoder = "smp", "resnet101", "deeplabv3p"
         c.teacher_random_init = True
+        c.kd_teacher_graph = os.environ.get("RTSEG_KD_EAGER", "0") != "1"  # A/B: eager teacher
+    c.hip_activations = os.environ.get("RTSEG_DISABLE_ACT", "0") != "1"  # A/B: torch activations
     c.is_testing = False
     c.use_ema = True
     return c

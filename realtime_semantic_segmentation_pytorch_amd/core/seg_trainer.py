@@ -68,6 +68,27 @@ class SegTrainer(BaseTrainer):
         msk = msk.to(self.device, non_blocking=True)
         return ops.augment_batch(img, msk, params, ds.aug_lut, ds.aug_spec, channels_last=cl)
 
+    def _teacher_forward(self, images):
+        """Frozen KD teacher.  On the GPU it runs as a captured HIP graph with its weights cast to
+        the autocast dtype once (utils/inference.py InferenceEngine): one copy + one graph launch
+        per step instead of an eager forward of a few hundred kernels and per-forward weight casts
+        (``kd_teacher_graph=False``: eager).  Rebuilt if the batch shape changes."""
+        cfg = self.config
+        if self.device.type != "cuda" or not getattr(cfg, "kd_teacher_graph", True):
+            return self.teacher_model(images)
+        key = (tuple(images.shape), images.dtype)
+        eng = getattr(self, "_teacher_engine", None)
+        if eng is None or eng[0] != key:
+            from ..utils.inference import InferenceEngine
+
+            dtype = self.amp_dtype if cfg.amp_training else torch.float32
+            with torch.autocast(self.device.type, enabled=False):
+                engine = InferenceEngine(self.teacher_model, tuple(images.shape), dtype=dtype,
+                                         channels_last=bool(getattr(cfg, "channels_last", False)), warmup=2,
+                                         device=self.device)
+            self._teacher_engine = eng = (key, engine)
+        return eng[1](images)
+
     def compute_loss(self, images, masks):
         """Forward + total loss. Returns (loss, main_preds, extras dict)."""
         cfg = self.config
@@ -103,7 +124,7 @@ class SegTrainer(BaseTrainer):
                 loss = self.loss_fn(preds, labels)
             if cfg.kd_training:
                 with torch.no_grad(), ops.defer_final_upsample(False):
-                    teacher_preds = self.teacher_model(images)
+                    teacher_preds = self._teacher_forward(images)
                 loss_kd = kd_loss_fn(cfg, preds, teacher_preds)
                 extras["loss_main"] = loss
                 loss = loss + cfg.kd_loss_coefficient * loss_kd
