@@ -75,7 +75,6 @@ struct IgArgs {
   const uint8_t* bmask;   // activation-derivative bits (1 per element, channels-last order)
   int bmode;              // kBnMaskNone / kBnMaskBits
   int bdbg;               // experiment knobs (RTSEG_BN_EPI_DBG), 0 in production
-  int stagger;            // 1: waves NW/2.. issue their ring stage after the first MFMA sub-step
   int act;
   int H, W, C;            // gathered operand [N][H][W][C]
   int Hv, Wv;             // virtual output grid
@@ -429,10 +428,6 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
       if (p < total) stage();
 
     int kk = 0, ord = 0, buf = 0, pend_mt = -1;
-    // stagger: the two waves sharing a SIMD (wid and wid + NW/2) split the DMA-issue phase: the
-    // early one issues its stage before its MFMAs, the late one after its first sub-step, so one
-    // wave's address math / DMA issue runs under its partner's MFMAs instead of both idling the pipe
-    const bool late = a.stagger != 0 && wid >= NW / 2;
     for (int gs = 0; gs < total; ++gs) {
       if (NST >= 3 && gs + 1 < total) {
         vm_wait<(NST - 2) * PER>();
@@ -445,8 +440,7 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
         pack_tile(pend_mt);
         pend_mt = -1;
       }
-      const bool do_stage = gs + NST - 1 < total;
-      if (do_stage && !late) stage();
+      if (gs + NST - 1 < total) stage();
 
       const uint4* Wt = lds + buf * STAGE + (wn * (BN / WN) + frow) * 8;
       const uint4* Pt = lds + buf * STAGE + BN * 8 + (wm * (BM / WM) + frow) * 8;
@@ -478,7 +472,6 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
           for (int tj = 0; tj < TJ; ++tj)
             acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[sl][ti], bfg[sl][tj], acc[ti][tj], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
-        if (s == 0 && do_stage && late) stage();
       }
       if (++buf == NST) buf = 0;
       if (++kk == nk) {
@@ -777,12 +770,9 @@ __global__ void slab_compact_kernel(const float* __restrict__ in, int rows, int 
   out[static_cast<int64_t>(blockIdx.x) * width + c] = ctr ? s - center[c - half] * s0 : s;
 }
 
-void launch_gather(const IgArgs& k0, const Cfg& c, hipStream_t st) {
-  const int grid = persistent_grid(k0.mtiles, k0.ntiles);
+void launch_gather(const IgArgs& k, const Cfg& c, hipStream_t st) {
+  const int grid = persistent_grid(k.mtiles, k.ntiles);
   if (grid <= 0) return;
-  static const int stagger = std::getenv("RTSEG_IGEMM_STAGGER") ? std::atoi(std::getenv("RTSEG_IGEMM_STAGGER")) : 0;
-  IgArgs k = k0;
-  k.stagger = stagger;
   if (k.ss != nullptr) launch_cfg<1, 0>(k, c, grid, st);
   else if (k.part != nullptr && k.bz != nullptr) launch_cfg<0, 2>(k, c, grid, st);
   else if (k.part != nullptr) launch_cfg<0, 1>(k, c, grid, st);
