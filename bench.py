@@ -50,6 +50,8 @@ def parse():
     p.add_argument("--kd", action="store_true",
                    help="knowledge distillation from an SMP DeepLabV3+/ResNet-101 teacher (random init)")
     p.add_argument("--no-infer", action="store_true", help="skip the inference-FPS measurement")
+    p.add_argument("--graph-step", action="store_true",
+                   help="replay forward+loss+backward from one captured HIP graph (SegTrainer.graph_step)")
     p.add_argument("--fp32", action="store_true", help="disable bf16 autocast (diagnostic)")
     p.add_argument("--no-fused-loss", action="store_true")
     p.add_argument("--nchw", action="store_true")
@@ -94,6 +96,7 @@ def make_config(a, world):
         c.teacher_random_init = True
         c.kd_teacher_graph = os.environ.get("RTSEG_KD_EAGER", "0") != "1"  # A/B: eager teacher
     c.hip_activations = os.environ.get("RTSEG_DISABLE_ACT", "0") != "1"  # A/B: torch activations
+    c.graph_step = bool(a.graph_step) and world == 1
     c.is_testing = False
     c.use_ema = True
     return c

@@ -129,6 +129,8 @@ class BaseConfig:
         self.ddp_bucket_mb = 32          # RCCL all-reduce bucket: ~3 buckets for DDRNet-23 (84 MB), overlapped with backward
         self.ddp_static_graph = True
         self.spawn_procs = None          # main.py without torchrun: worker processes (None: one per visible GPU)
+        self.graph_step = False          # replay forward+loss+backward from one captured HIP graph (small batches)
+        self.graph_warmup = 3            # eager steps per input shape before the capture
         self.kd_teacher_graph = True     # KD teacher as a captured HIP graph with pre-cast weights
         self.gpu_aug = False             # training augmentation on the GPU (ops/augment.py): workers only decode
         self.synthetic_data = False      # device-generated synthetic batches (benchmarks)

@@ -131,10 +131,58 @@ class SegTrainer(BaseTrainer):
                 extras["loss_kd"] = loss_kd
         return loss, preds, extras
 
+    def _graph_step_ok(self, images):
+        cfg = self.config
+        return (bool(getattr(cfg, "graph_step", False)) and images.is_cuda and not cfg.DDP
+                and not cfg.kd_training and not self.scaler.is_enabled())
+
+    def _graphed_forward_backward(self, images, masks):
+        """Forward + loss + backward replayed from ONE captured HIP graph (``graph_step``).
+
+        Small per-GPU batches are launch-bound: a training step is ~900 kernels, each paying the
+        host's launch cost.  After ``graph_warmup`` eager steps (per-shape kernel autotune, MIOpen
+        find, optimizer state) the forward, the loss and the backward -- including the zeroing of
+        the persistent gradient buffers -- are captured once per input shape; a step is then two
+        input copies, one graph launch and the (eager, single-launch) fused optimizer, whose
+        per-step learning rate / EMA weight therefore stay live.  Non-DDP, non-KD, no GradScaler.
+        Returns None while warming up (the caller runs the eager step)."""
+        key = (tuple(images.shape), images.dtype, tuple(masks.shape), masks.dtype)
+        st = getattr(self, "_gstep", None)
+        if st is None or st["key"] != key:
+            st = self._gstep = {"key": key, "seen": 0, "graph": None}
+        if st["graph"] is None:
+            st["seen"] += 1
+            if st["seen"] <= int(getattr(self.config, "graph_warmup", 3)):
+                return None
+            params = [p for p in self.model.parameters() if p.requires_grad]
+            for p in params:  # persistent gradient buffers the graph writes in place
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
+            grads = [p.grad for p in params]
+            sx, sy = images.clone(), masks.clone()
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                torch._foreach_zero_(grads)
+                loss, _, extras = self.compute_loss(sx, sy)
+                loss.backward()
+            st.update(graph=g, x=sx, y=sy, loss=loss, extras=extras)
+        st["x"].copy_(images, non_blocking=True)
+        st["y"].copy_(masks, non_blocking=True)
+        st["graph"].replay()
+        return st["loss"], st["extras"]
+
     def train_step(self, images, masks):
-        self.optimizer.zero_grad(set_to_none=True)
-        loss, _, extras = self.compute_loss(images, masks)
-        self.scaler.scale(loss).backward()
+        done = self._graphed_forward_backward(images, masks) if self._graph_step_ok(images) else None
+        if done is not None:
+            loss, extras = done
+        else:
+            if getattr(self, "_gstep", None) is None or self._gstep.get("graph") is None:
+                self.optimizer.zero_grad(set_to_none=True)
+            else:  # a shape change after capture: keep the graph's gradient buffers
+                self.optimizer.zero_grad(set_to_none=False)
+            loss, _, extras = self.compute_loss(images, masks)
+            self.scaler.scale(loss).backward()
         if self.ema_fused:  # the fused optimizer writes the parameter EMAs in its own launch
             self.optimizer.ema_weight = 1.0 - self.ema_model.decay(self.train_itrs + 1)
         self.scaler.step(self.optimizer)

@@ -323,7 +323,7 @@ struct ActArgs {
 };
 struct ActPreluPlan {
   bool planes;
-  int blocks, slices, tx;
+  int blocks, slices, tx, vec;  // vec: channels per lane (16-byte vectors) in rows mode
   int64_t rows_per_block;
 };
 ActPreluPlan act_prelu_plan(const ActArgs& a);

@@ -171,6 +171,63 @@ __global__ void __launch_bounds__(kActBlock) prelu_bwd_rows_kernel(const T* __re
   }
 }
 
+// 16-byte-vector forms for channels-last with C % V == 0: a lane owns V consecutive channels
+template <typename T>
+__global__ void __launch_bounds__(kActBlock) prelu_fwd_vec_kernel(const T* __restrict__ x, const float* __restrict__ w,
+                                                                  T* __restrict__ y, uint32_t nv, FastDiv fcv) {
+  constexpr int V = Vec<T>::N;
+  typedef typename Vec<T>::type VT;
+  for (uint32_t i = blockIdx.x * kActBlock + threadIdx.x; i < nv; i += gridDim.x * kActBlock) {
+    uint32_t cg;
+    fcv.divmod(i, cg);  // channel group of vector i
+    float v[V];
+    unpack<T, V>(reinterpret_cast<const VT*>(x)[i], v);
+#pragma unroll
+    for (int e = 0; e < V; ++e) v[e] = v[e] > 0.f ? v[e] : w[cg * V + e] * v[e];
+    reinterpret_cast<VT*>(y)[i] = pack<T, V>(v);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kActBlock) prelu_bwd_rows_vec_kernel(const T* __restrict__ x,
+                                                                       const T* __restrict__ dy,
+                                                                       const float* __restrict__ w, T* __restrict__ dx,
+                                                                       float* __restrict__ part, int64_t M, int C,
+                                                                       int64_t rows_per_block, int TX) {
+  constexpr int V = Vec<T>::N;
+  typedef typename Vec<T>::type VT;
+  extern __shared__ float acc[];  // [TY][C]
+  const int CG = C / V, TY = kActBlock / TX;
+  const int tx = threadIdx.x % TX, ty = threadIdx.x / TX;
+  const bool live = ty < TY;
+  if (live)
+    for (int g = tx; g < CG; g += TX)
+#pragma unroll
+      for (int e = 0; e < V; ++e) acc[ty * C + g * V + e] = 0.f;
+  const int64_t r0 = blockIdx.x * rows_per_block, r1 = live ? min(r0 + rows_per_block, M) : r0;
+  for (int64_t r = r0 + ty; r < r1; r += TY) {
+    for (int g = tx; g < CG; g += TX) {
+      const int64_t i = r * CG + g;  // vector index
+      float v[V], d[V], o[V];
+      unpack<T, V>(reinterpret_cast<const VT*>(x)[i], v);
+      unpack<T, V>(reinterpret_cast<const VT*>(dy)[i], d);
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const bool pos = v[e] > 0.f;
+        o[e] = pos ? d[e] : w[g * V + e] * d[e];
+        if (!pos) acc[ty * C + g * V + e] += d[e] * v[e];
+      }
+      reinterpret_cast<VT*>(dx)[i] = pack<T, V>(o);
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += kActBlock) {
+    float s = 0.f;
+    for (int k = 0; k < TY; ++k) s += acc[k * C + c];
+    part[static_cast<int64_t>(blockIdx.x) * C + c] = s;
+  }
+}
+
 // PReLU backward, contiguous [N, C, HW]: one block per (n, c) plane slice
 template <typename T>
 __global__ void __launch_bounds__(kActBlock) prelu_bwd_planes_kernel(const T* __restrict__ x, const T* __restrict__ dy,
@@ -241,8 +298,13 @@ template <typename T>
 void launch_typed(const ActArgs& a, hipStream_t st) {
   const int grid = stream_grid((a.n + 7) / 8, kActBlock);
   const bool channel_w = a.kind == kActPReLU && a.w != nullptr;
+  const ActPreluPlan p = act_prelu_plan(a);
   if (!a.bwd) {
-    if (channel_w) {
+    if (channel_w && p.vec > 1) {
+      const uint32_t nv = static_cast<uint32_t>(a.n / p.vec);
+      prelu_fwd_vec_kernel<T><<<stream_grid(nv, kActBlock), kActBlock, 0, st>>>(
+          static_cast<const T*>(a.x), a.w, static_cast<T*>(a.out), nv, FastDiv::make(static_cast<uint32_t>(a.C / p.vec)));
+    } else if (channel_w) {
       prelu_fwd_kernel<T><<<stream_grid(a.n, kActBlock), kActBlock, 0, st>>>(
           static_cast<const T*>(a.x), a.w, static_cast<T*>(a.out), static_cast<uint32_t>(a.n),
           FastDiv::make(static_cast<uint32_t>(a.inner)), FastDiv::make(static_cast<uint32_t>(a.C)));
@@ -258,14 +320,18 @@ void launch_typed(const ActArgs& a, hipStream_t st) {
   const T* x = static_cast<const T*>(a.x);
   const T* dy = static_cast<const T*>(a.dy);
   T* dx = static_cast<T*>(a.out);
-  const ActPreluPlan p = act_prelu_plan(a);
   if (p.planes) {
     prelu_bwd_planes_kernel<T><<<p.blocks, kActBlock, 0, st>>>(x, dy, a.w, dx, a.part, a.C, a.inner, p.slices);
     act_prelu_wfinal<<<(a.C + 255) / 256, 256, 0, st>>>(a.part, a.dw, a.C, p.blocks, p.slices);
   } else {
     const int TY = kActBlock / p.tx;
-    prelu_bwd_rows_kernel<T><<<p.blocks, kActBlock, static_cast<size_t>(TY) * a.C * sizeof(float), st>>>(
-        x, dy, a.w, dx, a.part, a.n / a.C, a.C, p.rows_per_block, p.tx);
+    const size_t lds = static_cast<size_t>(TY) * a.C * sizeof(float);
+    if (p.vec > 1)
+      prelu_bwd_rows_vec_kernel<T><<<p.blocks, kActBlock, lds, st>>>(x, dy, a.w, dx, a.part, a.n / a.C, a.C,
+                                                                       p.rows_per_block, p.tx);
+    else
+      prelu_bwd_rows_kernel<T><<<p.blocks, kActBlock, lds, st>>>(x, dy, a.w, dx, a.part, a.n / a.C, a.C,
+                                                                   p.rows_per_block, p.tx);
     act_prelu_wfinal<<<(a.C + 255) / 256, 256, 0, st>>>(a.part, a.dw, a.C, p.blocks, 0);
   }
 }
@@ -280,9 +346,12 @@ ActPreluPlan act_prelu_plan(const ActArgs& a) {
     p.slices = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>((2048 + planes - 1) / planes,
                                                                        (a.inner + 4095) / 4096)));
     p.blocks = static_cast<int>(planes * p.slices);
-  } else {  // [M, C] rows
+  } else {  // [M, C] rows; 16-byte channel vectors when C allows (channels-last, C > 1)
     const int64_t M = a.n / a.C;
-    p.tx = a.C >= 64 ? 64 : a.C;
+    const int v = a.dtype == kF32 ? 4 : 8;
+    p.vec = (a.C > 1 && a.C % v == 0) ? v : 1;
+    const int groups = a.C / p.vec;
+    p.tx = groups >= 64 ? 64 : groups;
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(2048, (M + 63) / 64));
     p.rows_per_block = (M + blocks - 1) / blocks;
     p.blocks = static_cast<int>((M + p.rows_per_block - 1) / p.rows_per_block);
