@@ -40,6 +40,53 @@ from ._ext import ops, use_hip
 
 _DECISIONS: dict = {}
 
+# Persistent tuning database: per-shape winners of earlier runs on this GPU architecture, so a
+# fresh process skips the timing (a 1024x2048 DDRNet-23 step tunes ~70 pass shapes).  Read from
+# RTSEG_TUNE_DB (default: the in-tree miopen_db/rtseg_conv_decisions.json, next to MIOpen's find
+# database); new decisions are written to RTSEG_TUNE_DB_OUT when set.  RTSEG_TUNE_DB=none: off.
+_DB_DEFAULT = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                           "miopen_db", "rtseg_conv_decisions.json")
+_DB = None
+
+
+def _arch() -> str:
+    try:
+        return torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName.split(":")[0]
+    except Exception:  # noqa: BLE001 - no device: nothing to look up
+        return ""
+
+
+def _tune_db() -> dict:
+    global _DB
+    if _DB is None:
+        _DB = {}
+        path = os.environ.get("RTSEG_TUNE_DB", _DB_DEFAULT)
+        if path != "none" and os.path.isfile(path):
+            import json
+
+            try:
+                with open(path) as f:
+                    data = json.load(f)
+                if data.get("arch") == _arch():
+                    _DB = dict(data.get("decisions", {}))
+            except (OSError, ValueError):
+                _DB = {}
+    return _DB
+
+
+def _db_record(key, name):
+    out = os.environ.get("RTSEG_TUNE_DB_OUT")
+    if not out:
+        return
+    import json
+
+    db = _tune_db()
+    db[repr(key)] = name
+    tmp = f"{out}.{os.getpid()}.tmp"
+    with open(tmp, "w") as f:
+        json.dump({"arch": _arch(), "decisions": dict(sorted(db.items()))}, f, indent=0)
+    os.replace(tmp, out)
+
 
 def _mode() -> str:
     return os.environ.get("RTSEG_CONV_MFMA", "auto")
@@ -129,17 +176,22 @@ def _choose(key, candidates):
     ``candidates``: [(name, fn)] with ours first; ``RTSEG_CONV_MFMA=1`` forces index 0."""
     if len(candidates) == 1 or _mode() == "1":
         return 0
+    names = [n for n, _ in candidates]
     got = _DECISIONS.get(key)
     if got is not None:  # by name: the candidate list may differ (e.g. RTSEG_CONV_HALO changed)
-        names = [n for n, _ in candidates]
         if got[1] in names:
             return names.index(got[1])
+    saved = _tune_db().get(repr(key))
+    if saved in names:  # an earlier run's winner for this shape (persistent tuning database)
+        _DECISIONS[key] = (names.index(saved), saved, [])
+        return names.index(saved)
     if torch.cuda.is_current_stream_capturing():
         return len(candidates) - 1  # MIOpen is last
     with torch.no_grad():
         times = [_time(fn) for _, fn in candidates]
     best = min(range(len(times)), key=times.__getitem__)
     _DECISIONS[key] = (best, candidates[best][0], [round(t, 4) for t in times])
+    _db_record(key, candidates[best][0])
     return best
 
 

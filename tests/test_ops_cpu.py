@@ -221,3 +221,26 @@ def test_convert_activations_keeps_state_and_cpu_semantics():
     assert type(net[5]) is nn.ReLU6  # ReLU6 stays: the BN / conv epilogues fuse it
     assert net.state_dict().keys() == ref.keys()
     assert torch.equal(net(x), y0)  # CPU tensors run the module's own forward
+
+
+def test_conv_tuning_db_roundtrip(tmp_path, monkeypatch):
+    """Per-shape conv winners persist across processes (ops/conv.py tuning database) and are
+    only reused on the architecture that measured them."""
+    import json
+
+    from realtime_semantic_segmentation_pytorch_amd.ops import conv as C
+
+    out = tmp_path / "db.json"
+    monkeypatch.setenv("RTSEG_TUNE_DB_OUT", str(out))
+    monkeypatch.setenv("RTSEG_TUNE_DB", str(out))
+    monkeypatch.setattr(C, "_DB", None)
+    key = ("dgrad", (32, 64, 256, 512), 64, 3, 3, (1, 1), (1, 1), (1, 1))
+    C._db_record(key, "igemm")
+    monkeypatch.setattr(C, "_DB", None)
+    assert C._tune_db()[repr(key)] == "igemm"
+    data = json.loads(out.read_text())
+    data["arch"] = "gfx000"  # another architecture's measurements are ignored
+    out.write_text(json.dumps(data))
+    monkeypatch.setattr(C, "_DB", None)
+    assert C._tune_db() == {}
+    monkeypatch.setattr(C, "_DB", None)

@@ -1,8 +1,6 @@
 #!/bin/bash
-# per-GPU batch sweep of the headline bench, then the default bench + rocprofv3 steady profile
+# round-end style verification (new-kernel tests, GPU suite, smoke, bench) + rocprofv3 steady profile
 mkdir -p gpurun_out
-for b in 48 64; do
-  timeout -k 10 400 python -u bench.py --batch $b --steps 10 --warmup 4 --no-infer > gpurun_out/f_bench_b$b.json 2> gpurun_out/f_bench_b$b.err || { tail -20 gpurun_out/f_bench_b$b.err; exit 1; }
-  cat gpurun_out/f_bench_b$b.json
-done
-bash tools/gpu_bench.sh b32
+bash tools/gpu_verify2.sh || exit 1
+PROF_SKIP=4 bash tools/profile_bench.sh gpurun_out/prof_final --steps 6 --warmup 4 || exit 1
+head -12 gpurun_out/prof_final/steady.txt
