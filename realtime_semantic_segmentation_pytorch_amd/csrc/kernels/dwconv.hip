@@ -239,10 +239,12 @@ __global__ void __launch_bounds__(kDwBlock) dw_wgrad_kernel(DwGeom g, DwDivs fd,
         float xv[VEC];
         if constexpr (MT == 1) {
           Vec<T, VEC>::load(xp + co, xv);
-        } else {  // <= 4 distinct inputs (mult >= 2, VEC <= 8): 4 scalar loads + selects
+        } else {  // <= 4 distinct inputs (mult >= 2, VEC <= 8): scalar loads + selects; a
+          // VEC-aligned group of 8 outputs spans only 2 inputs for mult 4 / 6 (BiSeNetV2's x6)
+          constexpr int NIN = (MT == 4 || MT == 6) && VEC <= 8 ? 2 : 4;
           float xs[4];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) xs[k] = Io<T>::ld(xp + min(base + k, g.cin - 1));
+          for (int k = 0; k < 4; ++k) xs[k] = k < NIN ? Io<T>::ld(xp + min(base + k, g.cin - 1)) : 0.f;
 #pragma unroll
           for (int v = 0; v < VEC; ++v)
             xv[v] = rel[v] == 0 ? xs[0] : rel[v] == 1 ? xs[1] : rel[v] == 2 ? xs[2] : xs[3];
