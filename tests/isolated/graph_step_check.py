@@ -1,9 +1,6 @@
 """Graph-captured training step (SegTrainer.graph_step): forward + loss + backward replayed from
 one HIP graph must train like the eager step (reference core/seg_trainer.py:38-119 step)."""
-import pytest
 import torch
-
-pytestmark = pytest.mark.gpu
 
 
 def _trainer(tmp_path, graph, model="ddrnet"):
@@ -26,7 +23,6 @@ def _trainer(tmp_path, graph, model="ddrnet"):
     return SegTrainer(c)
 
 
-@pytest.mark.parametrize("model", ["ddrnet", "enet"])
 def test_graph_step_trains_like_eager(tmp_path, model):
     torch.manual_seed(0)
     xs = [torch.randn(4, 3, 256, 512, device="cuda").contiguous(memory_format=torch.channels_last) for _ in range(6)]
@@ -50,3 +46,15 @@ def test_graph_step_trains_like_eager(tmp_path, model):
     num = sum(float((se[k] - sg[k]).norm() ** 2) for k in se if se[k].is_floating_point())
     den = sum(float(se[k].norm() ** 2) for k in se if se[k].is_floating_point())
     assert (num / den) ** 0.5 < 1e-2
+
+
+if __name__ == "__main__":  # run in a child process by tests/test_isolated_gpu.py
+    import pathlib
+    import sys
+    import tempfile
+
+    sys.path.insert(0, str(pathlib.Path(__file__).resolve().parents[2]))
+    with tempfile.TemporaryDirectory() as d:
+        for model in ("ddrnet", "enet"):
+            test_graph_step_trains_like_eager(pathlib.Path(d), model)
+            print(f"graph step {model}: ok", flush=True)

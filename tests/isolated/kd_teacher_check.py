@@ -1,9 +1,6 @@
 """KD teacher as a captured HIP graph (SegTrainer._teacher_forward) == the eager teacher.
 Reference: core/seg_trainer.py:94-101 (teacher forward under no_grad, KD loss)."""
-import pytest
 import torch
-
-pytestmark = pytest.mark.gpu
 
 
 def _trainer(tmp_path, graph):
@@ -41,3 +38,14 @@ def test_graph_teacher_matches_eager(tmp_path):
     loss, _, extras = tr.compute_loss(x, y)
     loss.backward()
     assert torch.isfinite(loss) and torch.isfinite(extras["loss_kd"])
+
+
+if __name__ == "__main__":  # run in a child process by tests/test_isolated_gpu.py
+    import pathlib
+    import sys
+    import tempfile
+
+    sys.path.insert(0, str(pathlib.Path(__file__).resolve().parents[2]))
+    with tempfile.TemporaryDirectory() as d:
+        test_graph_teacher_matches_eager(pathlib.Path(d))
+        print("kd teacher graph: ok", flush=True)
