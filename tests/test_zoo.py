@@ -96,9 +96,9 @@ def _rel(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-6)).item()
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("key", KEYS)
-def test_zoo_hip_matches_torch_path_gpu(key, monkeypatch):
+# The two GPU checks below run for every zoo model in ONE child process
+# (tests/isolated/zoo_gpu_check.py via tests/test_isolated_gpu.py), not in the pytest process.
+def check_zoo_hip_matches_torch_path(key, monkeypatch):
     """Eval forward: HIP path == torch path (tight).  Train fwd/bwd: both GPU paths are
     scored against a CPU fp64 run of the same model -- several zoo models have fp32
     gradient errors of ~1e-3 on either path (ill-conditioned tiny-batch BatchNorm,
@@ -148,9 +148,7 @@ def test_zoo_hip_matches_torch_path_gpu(key, monkeypatch):
     assert err(cat(g_h), cat(g_r)) <= max(4 * gt, 1e-2)
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("key", KEYS)
-def test_zoo_bf16_channels_last_train_step_gpu(key):
+def check_zoo_bf16_channels_last_train_step(key):
     m = _model(key, use_aux=True).cuda().to(memory_format=torch.channels_last).train()
     x = torch.randn(2, 3, *HW, device="cuda").contiguous(memory_format=torch.channels_last)
     labels = torch.randint(0, 19, (2, *HW), device="cuda", dtype=torch.uint8)
