@@ -213,7 +213,9 @@ def main():
     extra = {"loss_last": loss_val, "per_gpu_batch": a.batch,
              "peak_mem_gb": torch.cuda.max_memory_allocated(dev) / 2 ** 30,
              "hip_ext_loaded": bool(ops.load()), "channels_last": cfg.channels_last,
-             "fused_loss": cfg.fused_loss}
+             "fused_loss": cfg.fused_loss,
+             # the optimizer step (+ parameter EMA) ran as the single fused HIP launch
+             "fused_optimizer_step": bool(getattr(trainer.optimizer, "last_step_fused", False))}
     from realtime_semantic_segmentation_pytorch_amd.ops.conv import decisions
 
     picks = {}
