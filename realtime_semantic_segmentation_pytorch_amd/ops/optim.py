@@ -54,20 +54,13 @@ def _dense(t: torch.Tensor) -> bool:
     return True
 
 
-def same_layout(a: torch.Tensor, b: torch.Tensor) -> bool:
-    """Same shape and the same memory order: strides must agree on every dim of size > 1 (a
-    size-1 dim's stride is arbitrary -- a 1x1 conv weight converted to channels-last reports
-    strides (C, 1, C, C) while its contiguous gradient reports (C, 1, 1, 1), one memory layout)."""
-    return a.shape == b.shape and all(sa == sb for n, sa, sb in zip(a.shape, a.stride(), b.stride()) if n > 1)
-
-
 def _dense_ok(p) -> bool:
     """The kernel walks every tensor of a row linearly in MEMORY order, so param, grad, state
     and EMA only need to be dense with identical strides (channels-last conv weights are fine)."""
     g = p.grad
     return (p.is_cuda and p.dtype == torch.float32 and _dense(p) and g is not None
             and not g.is_sparse and g.dtype in (torch.float32, torch.bfloat16)
-            and same_layout(g, p))
+            and g.shape == p.shape and g.stride() == p.stride())
 
 
 class _FusedMixin:
@@ -83,7 +76,7 @@ class _FusedMixin:
 
     def attach_ema(self, pairs):
         """pairs: iterable of (model_param, ema_tensor) of identical shape/dtype/strides."""
-        self._ema_of = {p: e for p, e in pairs if same_layout(e, p) and e.dtype == p.dtype}
+        self._ema_of = {p: e for p, e in pairs if e.stride() == p.stride() and e.dtype == p.dtype}
         self._tables = {}
 
     def _can_fuse(self, group) -> bool:
@@ -140,7 +133,7 @@ class FusedSGD(_FusedMixin, SGD):
                     if buf is None:
                         buf = st["momentum_buffer"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                         first = True
-                    elif not same_layout(buf, p):  # e.g. loaded from a checkpoint in another layout
+                    elif buf.stride() != p.stride():  # e.g. loaded from a checkpoint in another layout
                         buf = st["momentum_buffer"] = torch.empty_like(p).copy_(buf)
                 rows.append((p, p.grad, buf, None, self._ema_of.get(p) if ema_w is not None else None, first))
             if not rows:
@@ -176,7 +169,7 @@ class _FusedAdamBase(_FusedMixin):
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 for k in ("exp_avg", "exp_avg_sq"):  # checkpoint-loaded state may be in another layout
-                    if not same_layout(st[k], p):
+                    if st[k].stride() != p.stride():
                         st[k] = torch.empty_like(p).copy_(st[k])
                 st["step"] += 1
                 by_step.setdefault(float(st["step"]), []).append(

@@ -244,15 +244,3 @@ def test_conv_tuning_db_roundtrip(tmp_path, monkeypatch):
     monkeypatch.setattr(C, "_DB", None)
     assert C._tune_db() == {}
     monkeypatch.setattr(C, "_DB", None)
-
-
-def test_optimizer_layout_check_ignores_size_one_dims():
-    """A channels-last 1x1 conv weight and its contiguous gradient share one memory layout: the
-    fused optimizer must accept the pair (it fell back to the stock step on DDRNet-23 before)."""
-    from realtime_semantic_segmentation_pytorch_amd.ops.optim import same_layout
-
-    w = torch.empty_strided((128, 64, 1, 1), (64, 1, 64, 64))  # what model.to(channels_last) gives
-    g = torch.randn(128, 64, 1, 1)
-    assert w.stride() != g.stride() and same_layout(w, g)
-    w3 = torch.randn(8, 4, 3, 3).contiguous(memory_format=torch.channels_last)
-    assert not same_layout(w3, torch.randn(8, 4, 3, 3))
