@@ -219,7 +219,8 @@ std::tuple<at::Tensor, at::Tensor> conv_igemm_dgrad_bn(
 
 // x [N,Cin,H,W], dy [N,Cout,Ho,Wo] (CL bf16) -> dw fp32 [Cout,Cin,KH,KW]
 at::Tensor conv_igemm_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t kh, int64_t kw,
-                            at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation) {
+                            at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
+                            bool channels_last) {
   check_act(x, "input");
   check_act(dy, "grad_output");
   ConvGeom g = geom(x.size(0), x.size(1), x.size(2), x.size(3), dy.size(1), kh, kw, stride, padding, dilation);
@@ -229,8 +230,10 @@ at::Tensor conv_igemm_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t k
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   g.x = x.data_ptr(); g.y = dy.data_ptr();
   at::Tensor ws = at::empty({conv_igemm_wgrad_ws_elems(g)}, x.options().dtype(at::kFloat));
-  at::Tensor dw = at::empty({g.cout, g.cin, g.kh, g.kw}, x.options().dtype(at::kFloat));
-  launch_conv_igemm_wgrad(g, ws.data_ptr<float>(), dw.data_ptr<float>(), cur_stream());
+  at::Tensor dw = at::empty({g.cout, g.cin, g.kh, g.kw},
+                            x.options().dtype(at::kFloat).memory_format(channels_last ? at::MemoryFormat::ChannelsLast
+                                                                                      : at::MemoryFormat::Contiguous));
+  launch_conv_igemm_wgrad(g, ws.data_ptr<float>(), dw.data_ptr<float>(), channels_last, cur_stream());
   return dw;
 }
 
@@ -249,8 +252,8 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
   m.def("conv_igemm_dgrad_bn(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
         "Tensor? addend, Tensor z, Tensor? mask, Tensor mean_invstd, int mode) "
         "-> (Tensor, Tensor)");
-  m.def("conv_igemm_wgrad(Tensor x, Tensor dy, int kh, int kw, int[] stride, int[] padding, int[] dilation) "
-        "-> Tensor");
+  m.def("conv_igemm_wgrad(Tensor x, Tensor dy, int kh, int kw, int[] stride, int[] padding, int[] dilation, "
+        "bool channels_last=False) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {

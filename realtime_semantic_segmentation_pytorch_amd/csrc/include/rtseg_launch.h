@@ -183,7 +183,7 @@ void launch_conv_igemm_dgrad(const ConvGeom& g, hipStream_t st);
 // g.x = x [N,H,W,Cin], g.y = dy [N,Ho,Wo,Cout]; ws fp32 of conv_igemm_wgrad_ws_elems(g);
 // dw fp32 [Cout][Cin][KH][KW]
 int64_t conv_igemm_wgrad_ws_elems(const ConvGeom& g);
-void launch_conv_igemm_wgrad(const ConvGeom& g, float* ws, float* dw, hipStream_t st);
+void launch_conv_igemm_wgrad(const ConvGeom& g, float* ws, float* dw, bool krsc, hipStream_t st);
 
 // ---- conv_halo.hip ------------------------------------------------------------
 // Halo-tiled stride-1 conv (taps within a 3 x 3 footprint, Cin % 64 == 0, Cout % 64 == 0):

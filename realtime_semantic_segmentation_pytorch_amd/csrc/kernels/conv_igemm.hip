@@ -677,6 +677,10 @@ __global__ void igemm_wgrad_reduce16(const float4* __restrict__ ws, float4* __re
   out[blockIdx.y * plane4 + c] = acc;
 }
 
+// KRSC: dw in the slab's own [Cout][KH][KW][Cin] order -- the memory order of a channels-last
+// [Cout, Cin, KH, KW] parameter, so the gradient already has the parameter's strides (what the
+// fused optimizer and DDP's bucket views need); otherwise the NCHW order [Cout][Cin][KH][KW].
+template <bool KRSC>
 __global__ void igemm_wgrad_reduce(const float* __restrict__ ws, float* __restrict__ dw, int rows, int cout,
                                    int C, int kt) {
   const int64_t kp = static_cast<int64_t>(kt) * C;
@@ -686,10 +690,14 @@ __global__ void igemm_wgrad_reduce(const float* __restrict__ ws, float* __restri
     float s = 0.f;
 #pragma unroll 16
     for (int sp = 0; sp < rows; ++sp) s += ws[sp * plane + e];
-    const int64_t co = e / kp;
-    const int64_t r = e - co * kp;
-    const int64_t t = r / C, ci = r - t * C;
-    dw[(co * C + ci) * kt + t] = s;
+    if constexpr (KRSC) {
+      dw[e] = s;
+    } else {
+      const int64_t co = e / kp;
+      const int64_t r = e - co * kp;
+      const int64_t t = r / C, ci = r - t * C;
+      dw[(co * C + ci) * kt + t] = s;
+    }
   }
 }
 
@@ -947,8 +955,9 @@ int64_t conv_igemm_wgrad_ws_elems(const ConvGeom& g) {
   return plane * (p.splits + (p.splits > 16 ? (p.splits + 15) / 16 : 0));
 }
 
-// g.x = x [N,H,W,Cin], g.y = dy [N,Ho,Wo,Cout] (bf16); dw fp32 [Cout][Cin][KH][KW]
-void launch_conv_igemm_wgrad(const ConvGeom& g, float* ws, float* dw, hipStream_t st) {
+// g.x = x [N,H,W,Cin], g.y = dy [N,Ho,Wo,Cout] (bf16); dw fp32 [Cout][Cin][KH][KW], or
+// [Cout][KH][KW][Cin] (krsc: a channels-last weight's memory order)
+void launch_conv_igemm_wgrad(const ConvGeom& g, float* ws, float* dw, bool krsc, hipStream_t st) {
   const WgPlan p = wgrad_plan(g);
   WgArgs k{};
   k.x = static_cast<const uint16_t*>(g.x);
@@ -989,7 +998,8 @@ void launch_conv_igemm_wgrad(const ConvGeom& g, float* ws, float* dw, hipStream_
     rows = (rows + 15) / 16;
   }
   const int rg = static_cast<int>(std::min<int64_t>((plane + 255) / 256, 4096));
-  igemm_wgrad_reduce<<<rg, 256, 0, st>>>(src, dw, rows, g.cout, g.cin, g.kh * g.kw);
+  if (krsc) igemm_wgrad_reduce<true><<<rg, 256, 0, st>>>(src, dw, rows, g.cout, g.cin, g.kh * g.kw);
+  else igemm_wgrad_reduce<false><<<rg, 256, 0, st>>>(src, dw, rows, g.cout, g.cin, g.kh * g.kw);
 }
 
 }  // namespace rtseg

@@ -209,6 +209,18 @@ class SegHead(nn.Sequential):
                          conv1x1(hid_channels, num_class))
 
 
+def _sync_group(bn):
+    """The process group a SyncBatchNorm synchronises over (None: local statistics)."""
+    if not isinstance(bn, nn.SyncBatchNorm):
+        return None
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()):
+        return None
+    pg = bn.process_group or dist.group.WORLD
+    return pg if dist.get_world_size(pg) > 1 else None
+
+
 def pooled_conv_bn_act(block: nn.Sequential, pooled: torch.Tensor, spatial: int) -> torch.Tensor:
     """``block`` (Sequential conv1x1, BN, act) applied to ``pooled`` [N, C, 1, 1]
     *as if* it had been broadcast to ``spatial`` = H*W positions first.
@@ -227,14 +239,36 @@ def pooled_conv_bn_act(block: nn.Sequential, pooled: torch.Tensor, spatial: int)
     out_dtype = y.dtype
     if bn.training or not bn.track_running_stats or bn.running_mean is None:
         y32 = y.float()
-        mean = y32.mean(dim=(0, 2, 3))
-        var = y32.var(dim=(0, 2, 3), unbiased=False)
+        pg = _sync_group(bn)
+        if pg is None:
+            mean = y32.mean(dim=(0, 2, 3))
+            var = y32.var(dim=(0, 2, 3), unbiased=False)
+            n_vec = y.shape[0]
+        else:
+            # SyncBatchNorm (reference utils/parallel.py:36-37 converts these too): the batch
+            # statistics are over every rank's pooled vectors -- one differentiable all-reduce of
+            # (sum, sum of squares, count) in fp64; its backward all-reduces the gradients, as
+            # torch's SyncBatchNorm backward does
+            from torch.distributed.nn.functional import all_reduce
+
+            y64 = y32.double()
+            c = y.shape[1]
+            packed = torch.cat([y64.sum(dim=(0, 2, 3)), (y64 * y64).sum(dim=(0, 2, 3)),
+                                y64.new_full((1,), float(y.shape[0] * y.shape[2] * y.shape[3]))])
+            packed = all_reduce(packed, group=pg)
+            tot = packed[2 * c]
+            mean64 = packed[:c] / tot
+            var = (packed[c:2 * c] / tot - mean64 * mean64).clamp_min(0.0).float()
+            mean = mean64.float()
+            n_vec = tot.detach().float()  # a device scalar: no host sync
         if bn.training and bn.track_running_stats and bn.running_mean is not None:
             with torch.no_grad():
-                count = y.shape[0] * spatial
+                count = n_vec * spatial
                 mom = bn.momentum if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked + 1)
                 bn.running_mean.mul_(1 - mom).add_(mean.detach(), alpha=mom)
-                bn.running_var.mul_(1 - mom).add_(var.detach() * count / max(count - 1, 1), alpha=mom)
+                unbias = (count / (count - 1).clamp_min(1) if isinstance(count, torch.Tensor)
+                          else count / max(count - 1, 1))
+                bn.running_var.mul_(1 - mom).add_(var.detach() * unbias, alpha=mom)
                 bn.num_batches_tracked.add_(1)
         inv = torch.rsqrt(var + bn.eps)
         y = (y32 - mean[None, :, None, None]) * inv[None, :, None, None]

@@ -49,6 +49,21 @@ def load(build_if_missing: bool = True) -> bool:
     return _loaded
 
 
+# Raw-pointer writers (the fused optimizer step, the EMA lerp) update parameters, EMA weights
+# and BN running statistics without bumping their autograd ``_version`` counters.  Every cache
+# keyed on (data_ptr, _version) -- the bf16 weight copies of ops.conv, BN eval coefficients of
+# ops.bn -- also folds in this generation, which those writers advance after each launch.
+_WRITE_GEN = [0]
+
+
+def bump_write_generation() -> None:
+    _WRITE_GEN[0] += 1
+
+
+def write_generation() -> int:
+    return _WRITE_GEN[0]
+
+
 def library_path() -> str:
     return _build.LIB_PATH
 
@@ -64,5 +79,47 @@ def use_hip(t: torch.Tensor) -> bool:
     return True
 
 
+class _TracedOps:
+    """``RTSEG_TRACE_OPS=<file>``: every rtseg op call is logged (name, tensor shapes/dtypes,
+    data pointers) to ``<file>`` BEFORE it launches and the device is synchronised after it,
+    so the last line written before a GPU fault names the faulting op (used with the
+    guard-page allocator, ``utils/guard.py``)."""
+
+    def __init__(self, path):
+        self._f = open(path, "a", buffering=1)
+        self._n = 0
+
+    def __getattr__(self, name):
+        fn = getattr(torch.ops.rtseg, name)
+
+        def call(*args, **kw):
+            self._n += 1
+            desc = []
+            for a in list(args) + list(kw.values()):
+                if isinstance(a, torch.Tensor):
+                    desc.append(f"T{tuple(a.shape)}{str(a.dtype)[6:]}@{a.data_ptr():x}"
+                                f"{'' if a.is_contiguous() else '/cl' if a.dim() == 4 and a.is_contiguous(memory_format=torch.channels_last) else '/nc'}")
+                elif isinstance(a, (int, float, bool)) or a is None:
+                    desc.append(repr(a))
+                else:
+                    desc.append(type(a).__name__)
+            self._f.write(f"{self._n} {name}({', '.join(desc)})\n")
+            os.fsync(self._f.fileno())
+            out = fn(*args, **kw)
+            torch.cuda.synchronize()
+            return out
+
+        return call
+
+
+_traced = None
+
+
 def ops():
+    global _traced
+    path = os.environ.get("RTSEG_TRACE_OPS")
+    if path:
+        if _traced is None:
+            _traced = _TracedOps(path)
+        return _traced
     return torch.ops.rtseg

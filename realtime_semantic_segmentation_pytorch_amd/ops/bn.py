@@ -22,7 +22,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-from ._ext import use_hip, ops
+from ._ext import use_hip, ops, write_generation
 
 ACT_NONE, ACT_RELU, ACT_RELU6 = 0, 1, 2
 MASK_NONE, MASK_FROM_Y, MASK_FROM_X, MASK_BITS = 0, 1, 2, 3
@@ -177,7 +177,8 @@ def eval_coeffs(bn):
     the module until any of weight / bias / running stats changes (an inference forward --
     and its HIP graph -- then has no per-layer coefficient kernel)."""
     ts = (bn.weight, bn.bias, bn.running_mean, bn.running_var)
-    key = tuple((t.data_ptr(), t._version) if t is not None else None for t in ts) + (float(bn.eps),)
+    key = tuple((t.data_ptr(), t._version) if t is not None else None for t in ts) + (float(bn.eps),
+                                                                                     write_generation())
     hit = getattr(bn, "_rtseg_eval_coeffs", None)
     if hit is not None and hit[0] == key:
         return hit[1]

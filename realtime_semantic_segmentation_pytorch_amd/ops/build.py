@@ -29,6 +29,7 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 BUILD_DIR = os.path.join(CSRC, "build")
 LIB_DIR = os.path.join(PKG_DIR, "_C")
 LIB_PATH = os.path.join(LIB_DIR, "librtseg_hip.so")
+GUARD_LIB_PATH = os.path.join(LIB_DIR, "librtseg_guard.so")
 ARCH = os.environ.get("RTSEG_OFFLOAD_ARCH", "gfx950")
 
 
@@ -156,6 +157,33 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
     return LIB_PATH
 
 
+def build_guard(verbose: bool = False) -> str:
+    """Build ``_C/librtseg_guard.so``: the guard-page debugging allocator
+    (``csrc/tools/guard_alloc.cpp``, host code over the HIP virtual-memory API)."""
+    os.makedirs(LIB_DIR, exist_ok=True)
+    src = os.path.join(CSRC, "tools", "guard_alloc.cpp")
+    flags = ["-shared", "-fPIC", "-O2", "-std=c++17", "-D__HIP_PLATFORM_AMD__=1", "-I", "/opt/rocm/include"]
+    tag = _digest([src], flags)
+    stamp = GUARD_LIB_PATH + ".stamp"
+    if os.path.exists(GUARD_LIB_PATH) and os.path.exists(stamp):
+        with open(stamp) as f:
+            if f.read().strip() == tag:
+                return GUARD_LIB_PATH
+    tmp = GUARD_LIB_PATH + ".tmp"
+    cmd = [os.environ.get("CXX", "g++")] + flags + ["-o", tmp, src, "-L", "/opt/rocm/lib", "-lamdhip64",
+                                                      "-Wl,-rpath,/opt/rocm/lib"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"guard allocator build failed\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, GUARD_LIB_PATH)
+    with open(stamp, "w") as f:
+        f.write(tag)
+    return GUARD_LIB_PATH
+
+
 if __name__ == "__main__":
     p = build(verbose="-v" in sys.argv, force="--force" in sys.argv)
     print(p)
+    print(build_guard(verbose="-v" in sys.argv))

@@ -36,7 +36,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ._ext import ops, use_hip
+from ._ext import ops, use_hip, write_generation
 
 _DECISIONS: dict = {}
 
@@ -75,16 +75,29 @@ def _tune_db() -> dict:
 
 
 def _db_record(key, name):
+    """Add one decision to RTSEG_TUNE_DB_OUT: merged with what the file already holds (other
+    processes' or earlier runs' entries survive), written atomically, by global rank 0 only
+    (every DDP rank times the same shapes)."""
+    db = _tune_db()
+    db[repr(key)] = name
     out = os.environ.get("RTSEG_TUNE_DB_OUT")
-    if not out:
+    if not out or os.environ.get("RANK", "0") != "0":
         return
     import json
 
-    db = _tune_db()
-    db[repr(key)] = name
+    merged = {}
+    if os.path.isfile(out):
+        try:
+            with open(out) as f:
+                data = json.load(f)
+            if data.get("arch") == _arch():
+                merged = dict(data.get("decisions", {}))
+        except (OSError, ValueError):
+            merged = {}
+    merged.update(db)
     tmp = f"{out}.{os.getpid()}.tmp"
     with open(tmp, "w") as f:
-        json.dump({"arch": _arch(), "decisions": dict(sorted(db.items()))}, f, indent=0)
+        json.dump({"arch": _arch(), "decisions": dict(sorted(merged.items()))}, f, indent=0)
     os.replace(tmp, out)
 
 
@@ -144,7 +157,7 @@ def _cached(conv, attr, make):
     w = conv.weight
     if conv.training and torch.is_grad_enabled():
         return make(w.detach())
-    key = (w.data_ptr(), w._version)
+    key = (w.data_ptr(), w._version, write_generation())
     hit = getattr(conv, attr, None)
     if hit is not None and hit[0] == key:
         return hit[1]
@@ -188,7 +201,10 @@ def _choose(key, candidates):
     if torch.cuda.is_current_stream_capturing():
         return len(candidates) - 1  # MIOpen is last
     with torch.no_grad():
-        times = [_time(fn) for _, fn in candidates]
+        # three interleaved rounds, best of each: one noisy round (clock ramp, a neighbour's
+        # allocation) no longer flips the pick from run to run
+        rounds = [[_time(fn, reps=4) for _, fn in candidates] for _ in range(3)]
+        times = [min(r[i] for r in rounds) for i in range(len(candidates))]
     best = min(range(len(times)), key=times.__getitem__)
     _DECISIONS[key] = (best, candidates[best][0], [round(t, 4) for t in times])
     _db_record(key, candidates[best][0])
@@ -256,7 +272,9 @@ class _ConvFn(torch.autograd.Function):
             else:
                 dx = _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend)
         if want_dw:
-            dw = _wgrad(x, dy, wk, conv, key, stride, padding, dilation).to(ctx.wdtype)
+            dw = _wgrad(x, dy, wk, conv, key, stride, padding, dilation)
+            if dw.dtype != ctx.wdtype:
+                dw = like_param(dw.to(ctx.wdtype), conv.weight)
         return dx, dw, None, None
 
 
@@ -363,12 +381,39 @@ def find_conv_consumer(t: torch.Tensor, r: torch.Tensor, max_nodes: int = 64):
     return None
 
 
+def like_param(g: torch.Tensor, p: torch.Tensor) -> torch.Tensor:
+    """``g`` with exactly the strides of parameter ``p``: a free re-stride when both are dense in
+    the same memory order (e.g. the (C,1,1,1) vs (C,1,C,C) strides of a 1x1 conv weight), else a
+    copy.  The fused optimizer walks param / grad / state linearly in memory and DDP's
+    gradient-bucket views want the parameter's strides (no "grad strides do not match bucket
+    view strides" copies)."""
+    if g.stride() == p.stride():
+        return g
+    if g.shape == p.shape and _dense(g) and _dense(p):
+        big = [i for i in range(g.dim()) if g.shape[i] > 1]
+        if sorted(big, key=lambda i: -g.stride(i)) == sorted(big, key=lambda i: -p.stride(i)):
+            return g.as_strided(p.shape, p.stride())
+    return torch.empty_like(p, dtype=g.dtype).copy_(g)
+
+
+def _dense(t: torch.Tensor) -> bool:
+    """Non-overlapping and dense: the size>1 dims tile memory exactly."""
+    expected = 1
+    for st, sz in sorted((st, sz) for sz, st in zip(t.shape, t.stride()) if sz != 1):
+        if st != expected:
+            return False
+        expected *= sz
+    return True
+
+
 def _wgrad(x, dy, wk, conv, key, stride, padding, dilation):
     cin, cout = conv.in_channels, conv.out_channels
     kh, kw = conv.kernel_size
+    w = conv.weight
+    cl = w.dim() == 4 and w.is_contiguous(memory_format=torch.channels_last) and not w.is_contiguous()
 
     def ours():
-        return ops().conv_igemm_wgrad(x, dy, kh, kw, stride, padding, dilation)
+        return ops().conv_igemm_wgrad(x, dy, kh, kw, stride, padding, dilation, cl or (kh == 1 and kw == 1))
 
     def miopen():
         return torch.ops.aten.convolution_backward(dy, x, wk.permute(0, 3, 1, 2), None, stride, padding, dilation,
@@ -377,7 +422,7 @@ def _wgrad(x, dy, wk, conv, key, stride, padding, dilation):
     cands = [("igemm", ours)] if cin % 64 == 0 and cout % 64 == 0 else []
     cands.append(("miopen", miopen))
     dw = cands[_choose(("wgrad",) + key, cands)][1]()
-    return dw.contiguous()
+    return like_param(dw, w)
 
 
 # ----------------------------------------------------------------------------- public entry points
@@ -433,7 +478,8 @@ def conv_forward(x: torch.Tensor, conv: nn.Module) -> torch.Tensor:
     if (type(conv) is nn.Conv2d and not conv.training and not torch.is_grad_enabled() and x.is_cuda
             and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16):
         w = conv.weight
-        key = (w.data_ptr(), w._version, None if conv.bias is None else (conv.bias.data_ptr(), conv.bias._version))
+        key = (w.data_ptr(), w._version, write_generation(),
+               None if conv.bias is None else (conv.bias.data_ptr(), conv.bias._version))
         hit = getattr(conv, "_rtseg_w16", None)
         if hit is None or hit[0] != key:
             b16 = conv.bias.detach().to(torch.bfloat16) if conv.bias is not None else None

@@ -18,7 +18,7 @@ import math
 import torch
 from torch.optim import SGD, Adam, AdamW
 
-from ._ext import ops, use_hip
+from ._ext import bump_write_generation, ops, use_hip
 
 MODE_SGD, MODE_ADAM, MODE_ADAMW = 0, 1, 2
 META_FIELDS = 8
@@ -54,13 +54,26 @@ def _dense(t: torch.Tensor) -> bool:
     return True
 
 
+def same_layout(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Same shape, both dense, and the same MEMORY order of their size>1 dims -- i.e. walking both
+    linearly visits the same elements.  Strides of size-1 dims are irrelevant: a 1x1 conv weight
+    is (C,1,C,C) after ``.to(channels_last)`` but (C,1,1,1) when freshly allocated."""
+    if a.shape != b.shape:
+        return False
+    if a.stride() == b.stride():
+        return _dense(a)
+    if not (_dense(a) and _dense(b)):
+        return False
+    big = [i for i in range(a.dim()) if a.shape[i] > 1]
+    return sorted(big, key=lambda i: -a.stride(i)) == sorted(big, key=lambda i: -b.stride(i))
+
+
 def _dense_ok(p) -> bool:
     """The kernel walks every tensor of a row linearly in MEMORY order, so param, grad, state
-    and EMA only need to be dense with identical strides (channels-last conv weights are fine)."""
+    and EMA only need to be dense in the same memory order (channels-last conv weights are fine)."""
     g = p.grad
-    return (p.is_cuda and p.dtype == torch.float32 and _dense(p) and g is not None
-            and not g.is_sparse and g.dtype in (torch.float32, torch.bfloat16)
-            and g.shape == p.shape and g.stride() == p.stride())
+    return (p.is_cuda and p.dtype == torch.float32 and g is not None and not g.is_sparse
+            and g.dtype in (torch.float32, torch.bfloat16) and same_layout(g, p))
 
 
 class _FusedMixin:
@@ -72,11 +85,12 @@ class _FusedMixin:
         self._ema_of = {}          # param -> EMA tensor
         self.ema_weight = None     # 1 - decay for the NEXT step (set by the trainer); None => no fused EMA
         self._tables = {}
-        self.last_step_fused = False
+        self.last_step_fused = False  # parameter EMAs written by this step's launch
+        self.fused_steps = 0          # steps that ran the fused kernel (vs the stock torch step)
 
     def attach_ema(self, pairs):
         """pairs: iterable of (model_param, ema_tensor) of identical shape/dtype/strides."""
-        self._ema_of = {p: e for p, e in pairs if e.stride() == p.stride() and e.dtype == p.dtype}
+        self._ema_of = {p: e for p, e in pairs if same_layout(e, p) and e.dtype == p.dtype}
         self._tables = {}
 
     def _can_fuse(self, group) -> bool:
@@ -100,6 +114,7 @@ class _FusedMixin:
             cache[slot] = (key, build_table(rows, rows[0][0].device))
         meta, nt, nb = cache[slot][1]
         ops().fused_opt_step(meta, nt, nb, self._mode, *hp)
+        bump_write_generation()
 
 
 class FusedSGD(_FusedMixin, SGD):
@@ -133,7 +148,7 @@ class FusedSGD(_FusedMixin, SGD):
                     if buf is None:
                         buf = st["momentum_buffer"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                         first = True
-                    elif buf.stride() != p.stride():  # e.g. loaded from a checkpoint in another layout
+                    elif not same_layout(buf, p):  # e.g. loaded from a checkpoint in another layout
                         buf = st["momentum_buffer"] = torch.empty_like(p).copy_(buf)
                 rows.append((p, p.grad, buf, None, self._ema_of.get(p) if ema_w is not None else None, first))
             if not rows:
@@ -143,6 +158,7 @@ class FusedSGD(_FusedMixin, SGD):
                   0.0, 0.0, 0.0, 0.0, 0.0, 1.0, float(ema_w) if ema_w is not None else 0.0)
             self._launch(gi, rows, hp)
         self.last_step_fused = ema_w is not None and bool(self._ema_of)
+        self.fused_steps += 1
         return loss
 
 
@@ -169,7 +185,7 @@ class _FusedAdamBase(_FusedMixin):
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 for k in ("exp_avg", "exp_avg_sq"):  # checkpoint-loaded state may be in another layout
-                    if st[k].stride() != p.stride():
+                    if not same_layout(st[k], p):
                         st[k] = torch.empty_like(p).copy_(st[k])
                 st["step"] += 1
                 by_step.setdefault(float(st["step"]), []).append(
@@ -184,6 +200,7 @@ class _FusedAdamBase(_FusedMixin):
                       lr / bc1, 1.0 / math.sqrt(bc2), 1.0, float(ema_w) if ema_w is not None else 0.0)
                 self._launch((gi, bi), rows, hp)
         self.last_step_fused = ema_w is not None and bool(self._ema_of)
+        self.fused_steps += 1
         return loss
 
 
@@ -220,3 +237,4 @@ def ema_lerp_(pairs, weight: float):
         tab = _EMA_TABLES[key] = build_table(rows, rows[0][0].device)
     meta, nt, nb = tab
     ops().ema_lerp(meta, nt, nb, float(weight))
+    bump_write_generation()

@@ -11,12 +11,28 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP kernels on cuda:0)")
     config.addinivalue_line("markers", "slow: long-running test")
+    config.addinivalue_line("markers", "no_guard: cannot run under the guard-page allocator (graph capture)")
+    # RTSEG_GUARD=tail|head: every device tensor borders an unmapped guard page, so any
+    # out-of-bounds kernel access faults deterministically (utils/guard.py)
+    mode = os.environ.get("RTSEG_GUARD")
+    if mode:
+        import torch
+
+        if torch.cuda.is_available():
+            from realtime_semantic_segmentation_pytorch_amd.utils import guard
+
+            guard.install(mode)
 
 
 def pytest_collection_modifyitems(config, items):
     import torch
 
     if torch.cuda.is_available():
+        if os.environ.get("RTSEG_GUARD"):
+            skip = pytest.mark.skip(reason="graph capture / child processes: not under the guard allocator")
+            for item in items:
+                if "no_guard" in item.keywords:
+                    item.add_marker(skip)
         return
     skip = pytest.mark.skip(reason="no GPU in this environment")
     for item in items:

@@ -15,6 +15,11 @@ import test_zoo as Z  # noqa: E402
 
 
 def main():
+    if os.environ.get("RTSEG_GUARD"):  # guard-page allocator: OOB accesses fault deterministically
+        from realtime_semantic_segmentation_pytorch_amd.utils import guard
+
+        guard.install(os.environ["RTSEG_GUARD"])
+        print(f"guard allocator: {os.environ['RTSEG_GUARD']}", flush=True)
     only = [k for k in os.environ.get("ZOO_ONLY", "").split(",") if k]
     bad = []
     for key in only or Z.KEYS:
@@ -36,6 +41,10 @@ def main():
         else:
             continue
         break
+    if os.environ.get("RTSEG_GUARD"):
+        from realtime_semantic_segmentation_pytorch_amd.utils import guard
+
+        print(f"guard stats: {guard.stats()}", flush=True)
     print(f"zoo checks done: {len(bad)} failed {bad}", flush=True)
     return 1 if bad else 0
 

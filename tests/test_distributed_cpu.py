@@ -81,3 +81,59 @@ def test_ddp_gloo_two_ranks(tmp_path, variant):
     assert os.path.isfile(os.path.join(save_dir, "best.pth"))
     ck = torch.load(os.path.join(save_dir, "last.pth"), weights_only=True)
     assert ck["cur_epoch"] == 1 and not any(k.startswith("module.") for k in ck["state_dict"])
+
+
+def _arm_worker(rank, world, port, out_dir):
+    """STDC / BiSeNetV1 attention refinement (pooled conv1x1 + SyncBN + sigmoid gate) on half
+    the batch per rank, SyncBN over gloo."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    import torch.distributed as dist
+    import torch.nn as nn
+
+    from realtime_semantic_segmentation_pytorch_amd.models.bisenetv1 import AttentionRefinementModule
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    arm = nn.SyncBatchNorm.convert_sync_batchnorm(AttentionRefinementModule(8)).train()
+    x = torch.randn(4, 8, 6, 10) * 2 + 0.3
+    gy = torch.randn(4, 8, 6, 10)
+    sl = slice(rank * 2, rank * 2 + 2)
+    xs = x[sl].clone().requires_grad_(True)
+    y = arm(xs)
+    y.backward(gy[sl])
+    grads = {n: p.grad.clone() for n, p in arm.named_parameters()}
+    for g in grads.values():
+        dist.all_reduce(g)  # what DDP sums (then averages)
+    torch.save({"y": y.detach(), "dx": xs.grad, "grads": grads, "rm": arm.conv[1].running_mean.clone(),
+                "rv": arm.conv[1].running_var.clone()}, os.path.join(out_dir, f"arm{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_syncbn_pooled_attention_two_ranks_matches_full_batch(tmp_path):
+    """The pooled ARM/FFM attention BN (models/modules.py pooled_conv_bn_act) must synchronise its
+    statistics under SyncBN like every other BN (reference utils/parallel.py:36-37 converts them
+    all; bisenetv1.py:76-88, reused by stdc.py:13): 2 ranks x half batch == 1 process x full batch."""
+    import torch.nn as nn
+
+    from realtime_semantic_segmentation_pytorch_amd.models.bisenetv1 import AttentionRefinementModule
+
+    mp.spawn(_arm_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    got = [torch.load(os.path.join(tmp_path, f"arm{r}.pt"), weights_only=True) for r in (0, 1)]
+    torch.manual_seed(0)
+    arm = AttentionRefinementModule(8).train()
+    x = (torch.randn(4, 8, 6, 10) * 2 + 0.3).requires_grad_(True)
+    gy = torch.randn(4, 8, 6, 10)
+    y = arm(x)
+    y.backward(gy)
+    torch.testing.assert_close(torch.cat([got[0]["y"], got[1]["y"]]), y.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(torch.cat([got[0]["dx"], got[1]["dx"]]), x.grad, rtol=1e-4, atol=1e-6)
+    for n, p in arm.named_parameters():
+        for r in (0, 1):
+            torch.testing.assert_close(got[r]["grads"][n], p.grad, rtol=1e-4, atol=1e-6, msg=n)
+    for r in (0, 1):
+        torch.testing.assert_close(got[r]["rm"], arm.conv[1].running_mean, rtol=1e-5, atol=1e-7)
+        torch.testing.assert_close(got[r]["rv"], arm.conv[1].running_var, rtol=1e-5, atol=1e-7)
+    assert isinstance(nn.SyncBatchNorm.convert_sync_batchnorm(AttentionRefinementModule(8)).conv[1],
+                      nn.SyncBatchNorm)

@@ -176,6 +176,7 @@ def test_tap_conv_gpu_vs_cpu_fp64(axis, d, dt, cin, cout):
     torch.testing.assert_close(gw.float().cpu(), gwr.float(), **dict(tol, atol=tol["atol"] * 20))
 
 
+@pytest.mark.no_guard
 @pytest.mark.parametrize("key", ["cgnet", "dabnet", "ddrnet"])
 def test_inference_engine_bf16_matches_eager_autocast(key):
     """utils/inference.py: the graph engine (weights pre-cast to bf16 on a private copy) gives

@@ -4,11 +4,11 @@ CPU: every registered model runs a train step through the trainer's path
 (deferred final upsample -> fused-loss formulation -> backward) and the deferred
 logits materialise to exactly the model's normal output.
 
-GPU: every model in fp32 channels-last runs forward + loss + backward once on
-the HIP kernels and once with ``RTSEG_DISABLE_HIP=1`` (PyTorch formulation of
-the same ops); outputs, loss and all parameter gradients must agree.  A second
-GPU test runs the production configuration (bf16 autocast, channels-last, OHEM)
-and checks for finite loss/gradients.
+GPU (in the pytest process): every model in fp32 channels-last runs forward + loss + backward
+on the HIP kernels, scored against a CPU fp64 run with the CPU fp32 run and the GPU NCHW torch
+path as yardsticks, with frozen and with batch-statistics BatchNorm
+(``check_zoo_hip_matches_torch_path``).  A second GPU test runs the production configuration
+(bf16 autocast, channels-last, OHEM) and checks for finite loss/gradients.
 """
 import copy
 
@@ -96,18 +96,29 @@ def _rel(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-6)).item()
 
 
-# The two GPU checks below run for every zoo model in ONE child process
-# (tests/isolated/zoo_gpu_check.py via tests/test_isolated_gpu.py), not in the pytest process.
+def _freeze_bn(m):
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.modules.batchnorm._BatchNorm):
+            mod.eval()
+    return m
+
+
 def check_zoo_hip_matches_torch_path(key, monkeypatch):
-    """Eval forward: HIP path == torch path (tight).  Train fwd/bwd: both GPU paths are
-    scored against a CPU fp64 run of the same model -- several zoo models have fp32
-    gradient errors of ~1e-3 on either path (ill-conditioned tiny-batch BatchNorm,
-    MIOpen algorithm choice), so the HIP path must be as accurate as the torch path.
-    "As accurate" allows a factor 4: on the ill-conditioned models (DFANet, CANet,
-    FarSeeNet) the fp32 paths differ from fp64 by 1e-3..1 relative and which of two
-    equally exact fp32 summation orders lands closer is a coin toss
-    (tools/probe_zoo_err.py: e.g. DFANet grad error 0.86 HIP vs 1.77 torch, CANet 8.6e-3
-    vs 3.0e-3 on one run)."""
+    """Eval forward: HIP path == torch path (tight).  Training step (forward, loss, backward): the
+    HIP path (channels-last) is scored against a CPU fp64 run of the same step, with two
+    yardsticks measured in the same test -- the CPU fp32 run and the GPU torch path in NCHW.
+
+    Measured on MI355X (tools/probe_zoo_gpu_err.py, profiles/r3_zoo_numerics): MIOpen's fp32
+    channels-last convolutions are ~1e-2 off fp64 even with frozen BatchNorm, NCHW ones ~1e-5,
+    so the channels-last torch path is NOT a usable yardstick (round 2 used it and had to skip 7
+    models).  Two passes, no skips:
+    * frozen BatchNorm (running statistics): every model's whole HIP training path -- convs,
+      depth-wise convs, pooling, interpolation, gating, activations, the loss -- must be within
+      10x the CPU fp32 error (floor 1e-3);
+    * batch-statistics BatchNorm at batch 2: within 4x the better of the two yardsticks (floor
+      1e-2).  Where even CPU fp32 is > 0.1 off fp64 (DFANet, Lite-HRNet, MiniNetV2: BN over a
+      handful of values at batch 2, gradients of ~1e8), the step is only checked for finite
+      gradients; the frozen pass above still pins their numerics."""
     torch.manual_seed(0)
     cpu = _model(key)
     for mod in cpu.modules():  # CPU and GPU RNG streams differ: compare without dropout
@@ -126,26 +137,43 @@ def check_zoo_hip_matches_torch_path(key, monkeypatch):
         e_t = _main(ev(xg)).float()
         monkeypatch.delenv("RTSEG_DISABLE_HIP", raising=False)
     assert _rel(e_h, e_t) < 2e-5
-    # train: accuracy against fp64
-    y_r, l_r, g_r = _run_gpu(copy.deepcopy(cpu).train().double(), x.double(), labels, False, monkeypatch)
-    base.train()
-    y_h, l_h, g_h = _run_gpu(copy.deepcopy(base), xg, labels.cuda(), False, monkeypatch)
-    y_t, l_t, g_t = _run_gpu(copy.deepcopy(base), xg, labels.cuda(), True, monkeypatch)
-    assert g_h.keys() == g_t.keys() == g_r.keys()
-    cat = lambda g: torch.cat([g[n].flatten().double().cpu() for n in g_r])  # noqa: E731
     err = lambda a, b: ((a.double().cpu() - b.double().cpu()).norm() / (b.double().cpu().norm() + 1e-30)).item()  # noqa: E731
-    # train-mode fp32 forward vs fp64: MIOpen's solver choice moves either path's error
-    # within ~1e-5 .. 1.2e-4 run to run (BiSeNetV2, tools/probe_zoo_err.py: HIP 2.0e-5 /
-    # 5.0e-5 vs torch 6.8e-5 / 7.5e-5 on two runs; 8.4e-5 vs 1.8e-5 on a third)
-    assert err(y_h, y_r) <= max(4 * err(y_t, y_r), 2e-4)
-    gt = err(cat(g_t), cat(g_r))
-    assert torch.isfinite(cat(g_h)).all()
-    if gt > 0.1:  # DFANet: fp32 gradients of ~1e8 that differ from fp64 by O(1) on any path
-        pytest.skip(f"{key}: fp32 training step not meaningful vs fp64 (torch-path grad error {gt:.2f})")
-    # floors: MIOpen's atomic weight-gradient kernels make either GPU path's error vary ~8x
-    # run to run on these tiny batches (ShelfNet torch path: 6.5e-4 .. 5.1e-3)
-    assert abs(l_h.item() - l_r.item()) <= max(4 * abs(l_t.item() - l_r.item()), 1e-3 * abs(l_r.item()))
-    assert err(cat(g_h), cat(g_r)) <= max(4 * gt, 1e-2)
+    for frozen in (True, False):
+        prep = _freeze_bn if frozen else (lambda m: m)
+        y_r, l_r, g_r = _run_gpu(prep(copy.deepcopy(cpu).train().double()), x.double(), labels, False, monkeypatch)
+        y_c, l_c, g_c = _run_gpu(prep(copy.deepcopy(cpu).train()), x, labels, False, monkeypatch)
+        y_h, l_h, g_h = _run_gpu(prep(copy.deepcopy(base).train()), xg, labels.cuda(), False, monkeypatch)
+        assert g_h.keys() == g_c.keys() == g_r.keys()
+        cat = lambda g: torch.cat([g[n].flatten().double().cpu() for n in g_r])  # noqa: E731
+        hg, cg = err(cat(g_h), cat(g_r)), err(cat(g_c), cat(g_r))
+        assert torch.isfinite(cat(g_h)).all()
+        tag = f"{key} {'frozen-BN' if frozen else 'train-BN'}: HIP grad err {hg:.2e}, CPU fp32 {cg:.2e}"
+        if frozen:
+            assert err(y_h, y_r) <= max(10 * err(y_c, y_r), 1e-4), tag
+            assert abs(l_h.item() - l_r.item()) <= max(10 * abs(l_c.item() - l_r.item()), 1e-4 * abs(l_r.item())), tag
+            assert hg <= max(10 * cg, 1e-3), tag
+            continue
+        if cg > 0.1:
+            continue  # ill-conditioned at batch 2 on any path (see docstring); finiteness checked
+        nchw = copy.deepcopy(cpu).cuda().train()
+        _, l_t, g_t = _run_gpu(nchw, x.cuda(), labels.cuda(), True, monkeypatch)
+        tg = err(cat(g_t), cat(g_r))
+        tag += f", GPU torch NCHW {tg:.2e}"
+        assert abs(l_h.item() - l_r.item()) <= max(4 * min(abs(l_t.item() - l_r.item()), abs(l_c.item() - l_r.item())),
+                                                   1e-3 * abs(l_r.item())), tag
+        assert hg <= max(4 * min(tg, cg), 1e-2), tag
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key", KEYS)
+def test_zoo_hip_matches_torch_path_gpu(key, monkeypatch):
+    check_zoo_hip_matches_torch_path(key, monkeypatch)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key", KEYS)
+def test_zoo_bf16_channels_last_train_step_gpu(key):
+    check_zoo_bf16_channels_last_train_step(key)
 
 
 def check_zoo_bf16_channels_last_train_step(key):
