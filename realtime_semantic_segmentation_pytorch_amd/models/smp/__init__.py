@@ -4,7 +4,9 @@ Parity: reference models/__init__.py:42-44 (``decoder_hub``), :67-81
 (``smp`` branch incl. the ``mit_b*`` special cases) and :102-122 (teacher).
 segmentation_models_pytorch is not installed in this environment, so the nine
 decoders are native re-implementations with SMP's module layout (see
-``base.py``); encoders: ResNet-18/34/50/101/152, ResNeXt-50/101, MobileNetV2, MiT-B0..B5.
+``base.py``); encoders: ResNet-18/34/50/101/152, ResNeXt-50/101, MobileNetV2, MiT-B0..B5,
+VGG-11/13/16/19(+BN), DenseNet-121/161/169/201, EfficientNet-B0..B7, SE-ResNet-50/101/152 and
+SE-ResNeXt-50/101 (``encoders_extra.py``).
 """
 from __future__ import annotations
 

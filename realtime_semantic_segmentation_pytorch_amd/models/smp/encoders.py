@@ -1,5 +1,6 @@
-"""SMP-style encoders: ResNet-18/34/50/101/152, ResNeXt-50/101 (32xNd), MobileNetV2 and the
-Mix Transformers MiT-B0..B5 (``mit.py``).
+"""SMP-style encoders: ResNet-18/34/50/101/152, ResNeXt-50/101 (32xNd), MobileNetV2, the
+Mix Transformers MiT-B0..B5 (``mit.py``) and VGG / DenseNet / EfficientNet-B0..B7 / SE-ResNet /
+SE-ResNeXt (``encoders_extra.py``).
 
 Behavioural target: SMP's ``ResNetEncoder`` / ``MobileNetV2Encoder`` (the
 torchvision networks with the classifier removed; ``forward`` returns the
@@ -93,7 +94,18 @@ class MobileNetV2Encoder(_EncoderMixin, nn.Module):
         return self.get_stages()[1:]
 
 
-ENCODERS = tuple(RESNET_SPECS) + ("mobilenet_v2",) + tuple(MIT_SPECS)
+def _extra():
+    from . import encoders_extra
+
+    return encoders_extra
+
+
+ENCODERS = tuple(RESNET_SPECS) + ("mobilenet_v2",) + tuple(MIT_SPECS) + (
+    "vgg11", "vgg11_bn", "vgg13", "vgg13_bn", "vgg16", "vgg16_bn", "vgg19", "vgg19_bn",
+    "densenet121", "densenet161", "densenet169", "densenet201",
+    "efficientnet-b0", "efficientnet-b1", "efficientnet-b2", "efficientnet-b3",
+    "efficientnet-b4", "efficientnet-b5", "efficientnet-b6", "efficientnet-b7",
+    "se_resnet50", "se_resnet101", "se_resnet152", "se_resnext50_32x4d", "se_resnext101_32x4d")
 
 
 def get_encoder(name, in_channels=3, depth=5, weights=None, output_stride=32):
@@ -112,6 +124,8 @@ def get_encoder(name, in_channels=3, depth=5, weights=None, output_stride=32):
         enc = ResNetEncoder(name, depth)
     elif name == "mobilenet_v2":
         enc = MobileNetV2Encoder(depth)
+    elif name in ENCODERS:
+        enc = _extra().build_extra_encoder(name, depth)
     else:
         raise ValueError(f"Unsupported encoder `{name}`; available: {', '.join(ENCODERS)}")
     if weights is not None:

@@ -146,3 +146,38 @@ def test_resnext_encoder_matches_torchvision_layout():
     feats = e(torch.randn(1, 3, 64, 64))
     assert [f.shape[1] for f in feats] == [3, 64, 256, 512, 1024, 2048]
     assert get_encoder("resnext101_32x8d").layer3[22].conv2.groups == 32
+
+
+# encoders beyond ResNet / MobileNetV2 / MiT (models/smp/encoders_extra.py): parameter counts of
+# the published backbones without their classifier heads (torchvision vgg / densenet,
+# EfficientNet-PyTorch, pretrainedmodels SENet) and SMP's stage channels
+_EXTRA = {"vgg16": 14.71, "vgg19_bn": 20.04, "densenet121": 6.95, "densenet161": 26.47, "densenet201": 18.09,
+          "efficientnet-b0": 4.01, "efficientnet-b4": 17.55, "efficientnet-b7": 63.79, "se_resnet50": 26.04,
+          "se_resnext50_32x4d": 25.51}
+
+
+@pytest.mark.parametrize("name", sorted(_EXTRA))
+def test_extra_encoders_params_and_stages(name):
+    from realtime_semantic_segmentation_pytorch_amd.models.smp import get_encoder
+
+    enc = get_encoder(name)
+    assert abs(sum(p.numel() for p in enc.parameters()) / 1e6 - _EXTRA[name]) < 0.01
+    x = torch.randn(1, 3, 64, 64)
+    with torch.no_grad():
+        feats = enc(x)
+    assert [f.shape[1] for f in feats] == list(enc.out_channels)
+    assert [f.shape[-1] for f in feats] == [64 >> i for i in range(6)]
+
+
+@pytest.mark.parametrize("enc", ["efficientnet-b0", "densenet121", "se_resnext50_32x4d", "vgg11_bn"])
+def test_unet_with_extra_encoder_trains(enc):
+    from realtime_semantic_segmentation_pytorch_amd.models.smp import build_smp_model
+
+    m = build_smp_model("unet", enc, None, 19).train()
+    y = m(torch.randn(2, 3, 64, 64))
+    assert y.shape == (2, 19, 64, 64)
+    y.float().mean().backward()
+    # EfficientNet keeps its (unused) _conv_head / _bn1 in the state dict, as SMP does
+    missing = [n for n, p in m.named_parameters() if p.grad is None and "_conv_head" not in n and ".encoder._bn1" not in
+               "." + n]
+    assert not missing, missing[:5]
