@@ -20,13 +20,17 @@ constexpr int kWave = 64;  // CDNA wavefront width
 __device__ __forceinline__ float bf16_to_f32(uint16_t v) {
   return __uint_as_float(static_cast<uint32_t>(v) << 16);
 }
+// Round-to-nearest-even, NaN stays NaN: the plain conversion is gfx950's v_cvt_pk_bf16_f32
+// (one instruction; the integer-arithmetic form costs a compare + select per value)
+typedef __bf16 rtseg_bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float rtseg_f32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u) {  // inf / nan: keep a quiet nan
-    return static_cast<uint16_t>((u >> 16) | ((u & 0xffffu) ? 0x40u : 0u));
-  }
-  u += 0x7fffu + ((u >> 16) & 1u);  // round to nearest even
-  return static_cast<uint16_t>(u >> 16);
+  return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f));
+}
+// two values -> one packed dword (lo | hi << 16) in a single v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t f32x2_to_bf16x2(float lo, float hi) {
+  const rtseg_f32x2_t v = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, rtseg_bf16x2_t));
 }
 
 template <typename T> struct Io;

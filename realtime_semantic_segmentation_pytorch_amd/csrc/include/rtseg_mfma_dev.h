@@ -63,9 +63,7 @@ __device__ __forceinline__ float epi_act(float v, int act) {
   return v;
 }
 
-__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
-  return static_cast<uint32_t>(f32_to_bf16(lo)) | (static_cast<uint32_t>(f32_to_bf16(hi)) << 16);
-}
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) { return f32x2_to_bf16x2(lo, hi); }
 
 template <int CTRL, int ROWS>
 __device__ __forceinline__ float dpp_f(float v) {

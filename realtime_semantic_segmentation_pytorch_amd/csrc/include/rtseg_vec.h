@@ -26,8 +26,7 @@ template <> struct Vec<uint16_t, 8> {
     uint4 r;
     unsigned w[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      w[i] = static_cast<unsigned>(f32_to_bf16(v[2 * i])) | (static_cast<unsigned>(f32_to_bf16(v[2 * i + 1])) << 16);
+    for (int i = 0; i < 4; ++i) w[i] = f32x2_to_bf16x2(v[2 * i], v[2 * i + 1]);
     r.x = w[0]; r.y = w[1]; r.z = w[2]; r.w = w[3];
     *reinterpret_cast<uint4*>(p) = r;
   }
@@ -40,8 +39,8 @@ template <> struct Vec<uint16_t, 4> {
   }
   __device__ __forceinline__ static void store(uint16_t* p, const float* v) {
     uint2 r;
-    r.x = static_cast<unsigned>(f32_to_bf16(v[0])) | (static_cast<unsigned>(f32_to_bf16(v[1])) << 16);
-    r.y = static_cast<unsigned>(f32_to_bf16(v[2])) | (static_cast<unsigned>(f32_to_bf16(v[3])) << 16);
+    r.x = f32x2_to_bf16x2(v[0], v[1]);
+    r.y = f32x2_to_bf16x2(v[2], v[3]);
     *reinterpret_cast<uint2*>(p) = r;
   }
 };
@@ -51,8 +50,7 @@ template <> struct Vec<uint16_t, 2> {
     v[0] = __uint_as_float(r << 16); v[1] = __uint_as_float(r & 0xffff0000u);
   }
   __device__ __forceinline__ static void store(uint16_t* p, const float* v) {
-    *reinterpret_cast<unsigned*>(p) =
-        static_cast<unsigned>(f32_to_bf16(v[0])) | (static_cast<unsigned>(f32_to_bf16(v[1])) << 16);
+    *reinterpret_cast<unsigned*>(p) = f32x2_to_bf16x2(v[0], v[1]);
   }
 };
 template <int VEC> struct VecF {  // fp32 and fp16 via element loops the compiler merges

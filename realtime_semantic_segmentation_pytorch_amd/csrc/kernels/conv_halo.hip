@@ -268,14 +268,12 @@ __global__ void __launch_bounds__(WM* WN * 64) halo_conv_kernel(const HaloArgs a
           pk.x = pack2(v[0], v[1]);
           pk.y = pack2(v[2], v[3]);
           if (sok && !(a.dbg & 1)) *reinterpret_cast<uint2*>(a.y + pend_off[tj] + co) = pk;
-          if constexpr (STATS) {
-            float q[4];
-            bf16x4_unpack(pk, q);  // statistics of the values as stored
+          if constexpr (STATS) {  // statistics of the fp32 outputs (the accumulators)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const float u = sok ? q[e] : 0.f;
+              const float u = sok ? v[e] : 0.f;  // halo rows past the image are not zero
               ts[ti][4 * g + e] += u;
-              tq[ti][4 * g + e] += u * u;
+              tq[ti][4 * g + e] = fmaf(u, u, tq[ti][4 * g + e]);
             }
           }
         }

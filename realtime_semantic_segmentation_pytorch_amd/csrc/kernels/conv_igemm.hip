@@ -85,12 +85,36 @@ struct IgArgs {
   int ntap, cch, nk;      // taps, 64-channel chunks per tap, K-steps per tile
   int M, mtiles, ntiles;
   FastDiv fwv, fhv;
+  uint32_t xbytes;        // bytes of the gathered operand (<= 2^31: buffer range, GB kernels)
   int taps[kMaxTaps];     // packed tap: see pack_tap (32-bit so the scalar unit can load it)
 };
 
+// Two LDS-DMA gathers through a buffer resource (range-checked: a voffset past the buffer's
+// size returns zeros -- the image border / padding needs no per-lane select of a zero source):
+// 64 lanes x 16 B land at M0 + 16 * lane.  Inline asm (opaque to hipcc's waitcnt pass, see dma16);
+// M0 is compiler-reserved, so it is saved and restored around the pair.
+__device__ __forceinline__ void bdma16x2(__amdgpu_buffer_rsrc_t r, uint32_t v0, uint32_t d0, uint32_t v1,
+                                         uint32_t d1) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %4\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %5\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(v0), "v"(v1), "s"(r), "s"(d0), "s"(d1)
+      : "memory");
+}
+
 
 // STATS: 0 = none, 1 = forward BN statistics of the output, 2 = BN-backward epilogue (IgArgs.bz)
-template <int BM, int BN, int WM, int WN, int NST, int EPI, int STATS>
+// GB: gather the activation rows through a buffer resource (range-checked voffsets, the
+// border handled by the range check) instead of 64-bit flat addresses with a zero source.
+template <int BM, int BN, int WM, int WN, int NST, int EPI, int STATS, int GB>
 __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs a) {
   constexpr int NW = WM * WN;
   constexpr int TI = BN / WN / 32;  // 32-channel MFMA tiles per wave
@@ -100,6 +124,7 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
   static_assert(TI >= 1 && TJ >= 1 && TI * WN * 32 == BN && TJ * WM * 32 == BM, "wave tiling");
   static_assert(WI >= 1 && PI >= 1 && WI * NW * 8 == BN && PI * NW * 8 == BM, "DMA tiling");
   static_assert(NST >= 2 && NST <= 4, "ring depth");
+  static_assert(PI % 2 == 0, "gather DMAs are issued in pairs");
   constexpr int PER = WI + PI;
   __shared__ uint4 lds[NST * STAGE];
 
@@ -133,7 +158,12 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
     const int row = (wid * PI + e) * 8 + lr8;
     plc[e] = lch ^ ((row >> 1) & 7);
   }
-  const uint16_t* pbase[PI];
+  // gathered rows.  GB: byte offset of the row's (n, hv*sh, wv*sw) pixel + chunk (u32 voffset
+  // of a buffer resource over x) and the pixel's (h, w); else a 64-bit base pointer
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.x), 0, static_cast<int>(a.xbytes), 0x00020000);
+  uint32_t roff[GB ? PI : 1];
+  const uint16_t* pbase[GB ? 1 : PI];
   int phb[PI], pwb[PI];
   auto set_rows = [&](int mt) {
 #pragma unroll
@@ -145,7 +175,11 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
       const uint32_t n = a.fhv.divmod(t, hv);
       phb[e] = ok ? static_cast<int>(hv) * a.sh : -(1 << 28);
       pwb[e] = static_cast<int>(wv) * a.sw;
-      pbase[e] = a.x + static_cast<int64_t>(n) * a.H * a.W * a.C + plc[e] * 8;
+      if constexpr (GB) {
+        roff[e] = static_cast<uint32_t>(((static_cast<int>(n) * a.H + phb[e]) * a.W + pwb[e]) * a.C + plc[e] * 8) * 2u;
+      } else {
+        pbase[e] = a.x + static_cast<int64_t>(n) * a.H * a.W * a.C + plc[e] * 8;
+      }
     }
   };
 
@@ -164,14 +198,32 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
       const void* src = wok[e] ? static_cast<const void*>(wsrc[e] + woff) : static_cast<const void*>(g_igemm_zero);
       dma16(src, base + (wid * WI + e) * 1024);
     }
+    if constexpr (GB) {
+      // uniform tap delta; an out-of-image tap moves the voffset past the buffer (zeros)
+      const uint32_t delta = static_cast<uint32_t>((dh * a.W + dw) * a.C + c0) * 2u;
+      const uint32_t pb = base + BN * 128 + wid * PI * 1024;
 #pragma unroll
-    for (int e = 0; e < PI; ++e) {
-      const int hi = phb[e] + dh, wi = pwb[e] + dw;
-      const bool ok = static_cast<unsigned>(hi) < static_cast<unsigned>(a.H) &&
-                      static_cast<unsigned>(wi) < static_cast<unsigned>(a.W);
-      const uint16_t* s = pbase[e] + static_cast<int64_t>(hi * a.W + wi) * a.C + c0;
-      dma16(ok ? static_cast<const void*>(s) : static_cast<const void*>(g_igemm_zero),
-            base + BN * 128 + (wid * PI + e) * 1024);
+      for (int e = 0; e < PI; e += 2) {
+        uint32_t v[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const bool ok = static_cast<unsigned>(phb[e + q] + dh) < static_cast<unsigned>(a.H) &&
+                          static_cast<unsigned>(pwb[e + q] + dw) < static_cast<unsigned>(a.W);
+          v[q] = ok ? roff[e + q] + delta : 0x80000000u;
+        }
+        bdma16x2(xr, v[0], __builtin_amdgcn_readfirstlane(pb + e * 1024), v[1],
+                 __builtin_amdgcn_readfirstlane(pb + (e + 1) * 1024));
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < PI; ++e) {
+        const int hi = phb[e] + dh, wi = pwb[e] + dw;
+        const bool ok = static_cast<unsigned>(hi) < static_cast<unsigned>(a.H) &&
+                        static_cast<unsigned>(wi) < static_cast<unsigned>(a.W);
+        const uint16_t* src = pbase[e] + static_cast<int64_t>(hi * a.W + wi) * a.C + c0;
+        dma16(ok ? static_cast<const void*>(src) : static_cast<const void*>(g_igemm_zero),
+              base + BN * 128 + (wid * PI + e) * 1024);
+      }
     }
     if (++st_buf == NST) st_buf = 0;
     if (++st_c == a.cch) {
@@ -374,15 +426,15 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
             pk.y = pack2(v[2], v[3]);
             if (ok && co < a.cout) *reinterpret_cast<uint2*>(a.y + pend_off[tj] + co) = pk;
             if constexpr (STATS) {
-              const bool sok = ok && co < a.cout;
-              const float q0 = sok ? bf16_to_f32(static_cast<uint16_t>(pk.x & 0xffff)) : 0.f;
-              const float q1 = sok ? bf16_to_f32(static_cast<uint16_t>(pk.x >> 16)) : 0.f;
-              const float q2 = sok ? bf16_to_f32(static_cast<uint16_t>(pk.y & 0xffff)) : 0.f;
-              const float q3 = sok ? bf16_to_f32(static_cast<uint16_t>(pk.y >> 16)) : 0.f;
-              ts[ti][4 * g + 0] += q0; tq[ti][4 * g + 0] += q0 * q0;
-              ts[ti][4 * g + 1] += q1; tq[ti][4 * g + 1] += q1 * q1;
-              ts[ti][4 * g + 2] += q2; tq[ti][4 * g + 2] += q2 * q2;
-              ts[ti][4 * g + 3] += q3; tq[ti][4 * g + 3] += q3 * q3;
+              // statistics of the fp32 conv outputs, straight from the accumulators: STATS == 1
+              // launches (training forward) carry no bias / addend, and rows past M or channels
+              // past Cout accumulated exactly zero (zero DMA sources), so nothing needs masking --
+              // 2 VALU per value instead of a bf16 round trip + select
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                ts[ti][4 * g + q] += v[q];
+                tq[ti][4 * g + q] = fmaf(v[q], v[q], tq[ti][4 * g + q]);
+              }
             }
           }
           #pragma unroll
@@ -745,19 +797,32 @@ void fill_common(IgArgs& k, const Cfg& c, int n) {
   k.fhv = FastDiv::make(static_cast<uint32_t>(k.Hv));
 }
 
-template <int EPI, int STATS>
+template <int EPI, int STATS, int GB>
 void launch_cfg(const IgArgs& k, const Cfg& c, int grid, hipStream_t st) {
   switch (c.id) {
-    case 0: igemm_gather_kernel<256, 64, 4, 2, 3, EPI, STATS><<<grid, 512, 0, st>>>(k); break;
-    case 2: igemm_gather_kernel<512, 64, 8, 1, 2, EPI, STATS><<<grid, 512, 0, st>>>(k); break;
+    case 0: igemm_gather_kernel<256, 64, 4, 2, 3, EPI, STATS, GB><<<grid, 512, 0, st>>>(k); break;
+    case 2: igemm_gather_kernel<512, 64, 8, 1, 2, EPI, STATS, GB><<<grid, 512, 0, st>>>(k); break;
     case 3:
-      if constexpr (EPI == 0 && STATS != 2) igemm_gather_kernel<256, 256, 2, 4, 2, 0, STATS><<<grid, 512, 0, st>>>(k);
+      if constexpr (EPI == 0 && STATS != 2) igemm_gather_kernel<256, 256, 2, 4, 2, 0, STATS, GB><<<grid, 512, 0, st>>>(k);
       break;
     case 4:
-      if constexpr (EPI == 0 && STATS != 2) igemm_gather_kernel<512, 128, 4, 2, 2, 0, STATS><<<grid, 512, 0, st>>>(k);
+      if constexpr (EPI == 0 && STATS != 2) igemm_gather_kernel<512, 128, 4, 2, 2, 0, STATS, GB><<<grid, 512, 0, st>>>(k);
       break;
-    default: igemm_gather_kernel<256, 128, 4, 2, 3, EPI, STATS><<<grid, 512, 0, st>>>(k); break;
+    default: igemm_gather_kernel<256, 128, 4, 2, 3, EPI, STATS, GB><<<grid, 512, 0, st>>>(k); break;
   }
+}
+
+// the buffer gather needs the gathered operand within a 2^31-byte range; RTSEG_IGEMM_GATHER=0
+// forces the flat-address gather (A/B)
+bool use_buffer_gather(const IgArgs& k) {
+  static const int mode = std::getenv("RTSEG_IGEMM_GATHER") ? std::atoi(std::getenv("RTSEG_IGEMM_GATHER")) : 1;
+  return mode != 0 && k.xbytes != 0 && k.xbytes <= 0x80000000u;
+}
+
+template <int EPI, int STATS>
+void launch_cfg(const IgArgs& k, const Cfg& c, int grid, hipStream_t st) {
+  if (use_buffer_gather(k)) launch_cfg<EPI, STATS, 1>(k, c, grid, st);
+  else launch_cfg<EPI, STATS, 0>(k, c, grid, st);
 }
 
 // out[r][c] = sum_{i < chunk} in[r * chunk + i][c] (rows past `rows` count as zero).
@@ -848,9 +913,11 @@ void launch_conv_igemm_fwd(const ConvGeom& g, hipStream_t st) {
   k.wrow = g.kh * g.kw * g.cin;
   k.cch = g.cin / 64;
   k.ntap = 0;
+  const int64_t xb = static_cast<int64_t>(g.n) * g.h * g.w_in * g.cin * 2;
+  k.xbytes = xb <= (int64_t{1} << 31) ? static_cast<uint32_t>(xb) : 0u;  // 0: flat gather
   for (int i = 0; i < g.kh; ++i)
     for (int j = 0; j < g.kw; ++j) {
-      k.taps[k.ntap++] = pack_tap(i * g.dh - g.ph, j * g.dw - g.pw, i * g.kw + j);
+      k.taps[k.ntap++] = pack_tap(i * g.dh - g.ph, j * g.dw - g.pw, i * g.kw + j, i, j);
     }
   Cfg c = pick_cfg(g.cout, static_cast<int64_t>(g.n) * g.ho * g.wo);
   // the inference BN epilogue (scale/shift/residual loads) spills on the 64 x 128 wave tiles
@@ -888,13 +955,15 @@ void launch_conv_igemm_dgrad(const ConvGeom& g, hipStream_t st) {
       k.wrow = g.kh * g.kw * g.cout;
       k.cch = g.cout / 64;
       k.ntap = 0;
+      const int64_t xb = static_cast<int64_t>(g.n) * g.ho * g.wo * g.cout * 2;
+      k.xbytes = xb <= (int64_t{1} << 31) ? static_cast<uint32_t>(xb) : 0u;  // 0: flat gather
       for (int i = 0; i < g.kh; ++i) {
         const int vh = a + g.ph - i * g.dh;
         if (((vh % g.sh) + g.sh) % g.sh != 0) continue;
         for (int j = 0; j < g.kw; ++j) {
           const int vw = b + g.pw - j * g.dw;
           if (((vw % g.sw) + g.sw) % g.sw != 0) continue;
-          k.taps[k.ntap++] = pack_tap(vh / g.sh, vw / g.sw, i * g.kw + j);
+          k.taps[k.ntap++] = pack_tap(vh / g.sh, vw / g.sw, i * g.kw + j, i, j);
         }
       }
       fill_common(k, c, g.n);

@@ -26,6 +26,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ._ext import ops, use_hip
+from .conv import like_param
 
 
 def _out_size(x, m):
@@ -82,12 +83,15 @@ class _DeconvFn(torch.autograd.Function):
                 dx = torch.ops.aten.convolution_backward(
                     dy, x, w16, None, st, pd, dl, True, list(m.output_padding), 1, [True, False, False])[0]
         if ctx.needs_input_grad[1]:
+            w = m.weight
+            cl = w.is_contiguous(memory_format=torch.channels_last) and not w.is_contiguous()
             if cout_t % 64 == 0 and cin_t % 64 == 0:
-                dw = ops().conv_igemm_wgrad(dy, x, kh, kw, st, pd, dl)  # [Cin_t][Cout_t][kh][kw]
+                # [Cin_t][Cout_t][kh][kw], in the parameter's memory order
+                dw = ops().conv_igemm_wgrad(dy, x, kh, kw, st, pd, dl, cl or (kh == 1 and kw == 1))
             else:
                 dw = torch.ops.aten.convolution_backward(
                     dy, x, w16, None, st, pd, dl, True, list(m.output_padding), 1, [False, True, False])[1]
-            dw = dw.to(ctx.wdtype)
+            dw = like_param(dw.to(ctx.wdtype), w)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = dy.float().sum((0, 2, 3))
         return dx, dw, db, None

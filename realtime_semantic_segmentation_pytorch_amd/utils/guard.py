@@ -29,6 +29,10 @@ def install(mode: str = "tail") -> str:
     os.environ["RTSEG_GUARD_MODE"] = mode
     alloc = torch.cuda.memory.CUDAPluggableAllocator(path, "rtseg_guard_malloc", "rtseg_guard_free")
     torch.cuda.memory.change_current_allocator(alloc)
+    # MIOpen's convolutions return garbage on memory of the HIP virtual-memory API (measured:
+    # tools/probe_guard_diff.py, profiles/r3_fault/README.md), so under the guard the stock
+    # convolutions run on PyTorch's own implementation instead; our kernels are what is guarded
+    torch.backends.cudnn.enabled = False
     _installed = mode
     return mode
 

@@ -147,3 +147,80 @@ def test_hip_syncbn_two_ranks_matches_full_batch_bn(tmp_path):
                                                msg="conv weight grad")
     finally:
         os.environ.pop("RTSEG_CONV_MFMA", None)
+
+
+# ------------------------------------------------------------------ pooled attention / [N,C,1,1] BNs
+def _block(kind):
+    from realtime_semantic_segmentation_pytorch_amd.models.bisenetv1 import AttentionRefinementModule
+    from realtime_semantic_segmentation_pytorch_amd.models.bisenetv2 import ContextEmbeddingBlock
+
+    torch.manual_seed(3)
+    return AttentionRefinementModule(C) if kind == "arm" else ContextEmbeddingBlock(C, C)
+
+
+def _block_run(m, x, gy):
+    x = x.cuda().contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    y = m(x)
+    y.backward(gy.cuda().contiguous(memory_format=torch.channels_last))
+    bns = [b for b in m.modules() if isinstance(b, torch.nn.modules.batchnorm._BatchNorm)]
+    return (y.detach().float().cpu(), x.grad.float().cpu(),
+            {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None},
+            [(b.running_mean.cpu(), b.running_var.cpu()) for b in bns])
+
+
+def _block_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    import torch.nn as nn
+
+    from realtime_semantic_segmentation_pytorch_amd.ops import convert_batchnorm
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pg = dist.new_group(ranks=list(range(world)))
+    x, _, gy, *_ = _data()
+    sl = slice(rank * N // world, (rank + 1) * N // world)
+    res = {}
+    for kind in ("arm", "ce"):
+        m = nn.SyncBatchNorm.convert_sync_batchnorm(_block(kind), process_group=pg)
+        convert_batchnorm(m)
+        m = m.cuda().to(memory_format=torch.channels_last).train()
+        y, dx, grads, stats = _block_run(m, x[sl], gy[sl])
+        for g in grads.values():
+            dist.all_reduce(g)
+        res[kind] = dict(y=y, dx=dx, grads={k: v.cpu() for k, v in grads.items()}, stats=stats)
+    torch.save(res, os.path.join(out, f"blk{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_syncbn_pooled_attention_and_context_embedding_two_ranks():
+    """SyncBN in the pooled attention branch (BiSeNetV1 / STDC ARM: pooled_conv_bn_act) and in
+    BiSeNetV2's context-embedding BN on [N, C, 1, 1]: 2 ranks x half batch == one process over
+    the whole batch (reference utils/parallel.py:36-37 syncs every BN)."""
+    import tempfile
+
+    from realtime_semantic_segmentation_pytorch_amd import ops
+    from realtime_semantic_segmentation_pytorch_amd.ops import convert_batchnorm
+
+    assert ops.load()
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.spawn(_block_worker, args=(2, _port(), tmp), nprocs=2, join=True)
+        got = [torch.load(os.path.join(tmp, f"blk{r}.pt"), weights_only=True) for r in (0, 1)]
+    x, _, gy, *_ = _data()
+    for kind in ("arm", "ce"):
+        m = _block(kind)
+        convert_batchnorm(m)
+        m = m.cuda().to(memory_format=torch.channels_last).train()
+        y, dx, grads, stats = _block_run(m, x, gy)
+        tol = dict(rtol=1e-4, atol=2e-4)
+        torch.testing.assert_close(torch.cat([got[0][kind]["y"], got[1][kind]["y"]]), y, **tol, msg=f"{kind}: y")
+        torch.testing.assert_close(torch.cat([got[0][kind]["dx"], got[1][kind]["dx"]]), dx, **tol, msg=f"{kind}: dx")
+        for r in (0, 1):
+            for n, g in grads.items():
+                torch.testing.assert_close(got[r][kind]["grads"][n], g.cpu(), rtol=1e-3, atol=1e-3,
+                                           msg=f"{kind}: grad {n}")
+            for (rm, rv), (rm2, rv2) in zip(got[r][kind]["stats"], stats):
+                torch.testing.assert_close(rm, rm2, rtol=1e-3, atol=1e-4, msg=f"{kind}: running mean")
+                torch.testing.assert_close(rv, rv2, rtol=2e-3, atol=1e-4, msg=f"{kind}: running var")
