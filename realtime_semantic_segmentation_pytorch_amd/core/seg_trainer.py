@@ -154,11 +154,11 @@ class SegTrainer(BaseTrainer):
             st["seen"] += 1
             if st["seen"] <= int(getattr(self.config, "graph_warmup", 3)):
                 return None
-            params = [p for p in self.model.parameters() if p.requires_grad]
-            for p in params:  # persistent gradient buffers the graph writes in place
-                if p.grad is None:
-                    p.grad = torch.zeros_like(p)
-            grads = [p.grad for p in params]
+            # persistent gradient buffers the graph writes in place: exactly the parameters the
+            # last eager step gave a gradient -- a built-but-unused head (aux / detail off) keeps
+            # grad None, so the optimizer skips it exactly as in eager training (no weight decay,
+            # momentum or Adam-moment updates on a zero gradient)
+            grads = [p.grad for p in self.model.parameters() if p.requires_grad and p.grad is not None]
             sx, sy = images.clone(), masks.clone()
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()

@@ -36,7 +36,8 @@ def test_graph_step_trains_like_eager(tmp_path, model):
                 if isinstance(m, torch.nn.modules.dropout._DropoutNd):
                     m.p = 0.0
         losses = [float(tr.train_step(x, y)[0]) for x, y in zip(xs, ys)]
-        out[graph] = (losses, {k: v.detach().float().clone() for k, v in tr.model.state_dict().items()})
+        out[graph] = (losses, {k: v.detach().float().clone() for k, v in tr.model.state_dict().items()},
+                      {n for n, p in tr.model.named_parameters() if p.grad is None})
         if graph:
             assert tr._gstep["graph"] is not None  # steps 3.. replayed the captured graph
     le, lg = out[False][0], out[True][0]
@@ -46,6 +47,9 @@ def test_graph_step_trains_like_eager(tmp_path, model):
     num = sum(float((se[k] - sg[k]).norm() ** 2) for k in se if se[k].is_floating_point())
     den = sum(float(se[k].norm() ** 2) for k in se if se[k].is_floating_point())
     assert (num / den) ** 0.5 < 1e-2
+    # parameters without a gradient stay without one under graph capture (no persistent zero
+    # gradient that weight decay / momentum would then act on)
+    assert out[False][2] == out[True][2], (out[False][2] ^ out[True][2])
 
 
 if __name__ == "__main__":  # run in a child process by tests/test_isolated_gpu.py
