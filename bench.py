@@ -142,6 +142,10 @@ def _heartbeat(period=30.0):
 def main():
     a = parse()
     hb = _heartbeat()
+    if os.environ.get("RTSEG_STACK_DUMP"):  # diagnose a stuck step: Python stacks every N s
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["RTSEG_STACK_DUMP"]), repeat=True)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1 and "LOCAL_RANK" not in os.environ:
         raise SystemExit("N>1 must be launched with torchrun (one process per GPU)")

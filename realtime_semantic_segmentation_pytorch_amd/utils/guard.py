@@ -4,7 +4,13 @@
 makes it START right after one, so an out-of-bounds access of any kernel faults on the first
 launch that does it instead of depending on what the caching allocator placed next to the
 tensor.  Must run before the process allocates its first CUDA tensor.  Combine with
-``RTSEG_TRACE_OPS=<file>`` (``ops/_ext.py``) to name the op that faulted."""
+``RTSEG_TRACE_OPS=<file>`` (``ops/_ext.py``) to name the op that faulted.
+
+Limitation (measured on MI355X, profiles/r3_fault/README.md): the vendor libraries do not work
+on memory of the HIP virtual-memory API -- a hipBLASLt/rocBLAS ``mm`` returns wrong results
+(tools/guard_sanity.py: relative error 0.30) and MIOpen convolutions garbage -- so the guard
+is only meaningful for workloads made of our kernels and elementwise ATen ops.  It is NOT part
+of the test suite (a wrong GEMM upstream can turn into an index kernel's fault downstream)."""
 from __future__ import annotations
 
 import ctypes
@@ -30,8 +36,7 @@ def install(mode: str = "tail") -> str:
     alloc = torch.cuda.memory.CUDAPluggableAllocator(path, "rtseg_guard_malloc", "rtseg_guard_free")
     torch.cuda.memory.change_current_allocator(alloc)
     # MIOpen's convolutions return garbage on memory of the HIP virtual-memory API (measured:
-    # tools/probe_guard_diff.py, profiles/r3_fault/README.md), so under the guard the stock
-    # convolutions run on PyTorch's own implementation instead; our kernels are what is guarded
+    # tools/probe_guard_diff.py); PyTorch's own convolutions are correct there (GEMMs are not)
     torch.backends.cudnn.enabled = False
     _installed = mode
     return mode
