@@ -159,64 +159,6 @@ at::Tensor conv_halo_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntAr
   return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, std::nullopt, addend, true);
 }
 
-// dgrad with the BN-backward epilogue: dx is the gradient of y = act(BN(z) [+ r]) where y is the
-// conv's input.  Returns (g = (dx [+ addend]) * mask bit, slab [G, 2*Cin] of
-// (sum g, sum g * (z - mean))).  mask: 0 none (act none), 3 the forward's bit mask (`mask` =
-// uint8 bits, one bit per element, channels-last order); Cin % 32 == 0.
-std::tuple<at::Tensor, at::Tensor> conv_igemm_dgrad_bn(
-    const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size, at::IntArrayRef stride,
-    at::IntArrayRef padding, at::IntArrayRef dilation, const std::optional<at::Tensor>& addend,
-    const at::Tensor& z, const std::optional<at::Tensor>& mask, const at::Tensor& mean_invstd, int64_t mode) {
-  check_act(dy, "grad_output");
-  check_act(z, "bn_input");
-  TORCH_CHECK(x_size.size() == 4, "rtseg.conv_igemm_dgrad_bn: x_size must be [N, Cin, H, W]");
-  TORCH_CHECK(wt.is_cuda() && wt.dim() == 4 && wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() &&
-                  wt.size(0) == x_size[1] && wt.size(3) == dy.size(1),
-              "rtseg.conv_igemm_dgrad_bn: weights must be contiguous bf16 [Cin, KH, KW, Cout]");
-  ConvGeom g = geom(x_size[0], x_size[1], x_size[2], x_size[3], dy.size(1), wt.size(1), wt.size(2), stride, padding,
-                    dilation);
-  TORCH_CHECK(g.ho == dy.size(2) && g.wo == dy.size(3) && g.n == dy.size(0),
-              "rtseg.conv_igemm_dgrad_bn: grad_output does not match the geometry");
-  TORCH_CHECK(conv_igemm_supported(g, 1), "rtseg.conv_igemm_dgrad_bn: needs Cout % 64 == 0, Cin % 8 == 0");
-  TORCH_CHECK(z.size(0) == x_size[0] && z.size(1) == x_size[1] && z.size(2) == x_size[2] && z.size(3) == x_size[3],
-              "rtseg.conv_igemm_dgrad_bn: BN input must match dx");
-  TORCH_CHECK(mean_invstd.is_cuda() && mean_invstd.scalar_type() == at::kFloat && mean_invstd.is_contiguous() &&
-                  mean_invstd.numel() == 2 * g.cin,
-              "rtseg.conv_igemm_dgrad_bn: mean_invstd must be fp32 [2*Cin]");
-  TORCH_CHECK(mode == kBnMaskNone || mode == kBnMaskBits,
-              "rtseg.conv_igemm_dgrad_bn: mask must be none or the bit mask");
-  TORCH_CHECK(g.cin % 32 == 0, "rtseg.conv_igemm_dgrad_bn: needs Cin % 32 == 0");
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
-  at::Tensor dx = at::empty({g.n, g.cin, g.h, g.w_in}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
-  g.x = dy.data_ptr(); g.w = wt.data_ptr(); g.y = dx.data_ptr();
-  g.scale_shift = nullptr;
-  g.res = nullptr;
-  if (addend.has_value() && addend->defined()) {
-    check_act(*addend, "addend");
-    TORCH_CHECK(addend->sizes() == dx.sizes(), "rtseg.conv_igemm_dgrad_bn: addend must match dx");
-    g.res = addend->data_ptr();
-  }
-  g.bn_z = z.data_ptr();
-  g.bn_mode = static_cast<int>(mode);
-  g.bn_mask = nullptr;
-  if (mode == kBnMaskBits) {
-    TORCH_CHECK(mask.has_value() && mask->defined() && mask->is_cuda() && mask->scalar_type() == at::kByte &&
-                    mask->is_contiguous() && mask->numel() * 8 == dx.numel(),
-                "rtseg.conv_igemm_dgrad_bn: bit mask must be uint8 [numel / 8]");
-    g.bn_mask = mask->data_ptr();
-  }
-  at::Tensor part = at::empty({conv_igemm_dgrad_slabs(g), 2 * g.cin}, dy.options().dtype(at::kFloat));
-  g.part = part.data_ptr<float>();
-  launch_conv_igemm_dgrad(g, cur_stream());
-  // fold the per-tile rows (so the BN finalize stays cheap) and centre them: sum g z -> sum g (z - mean)
-  const int rows = static_cast<int>(part.size(0));
-  const int chunk = (rows + 255) / 256;
-  at::Tensor small = at::empty({(rows + chunk - 1) / chunk, 2 * g.cin}, part.options());
-  launch_slab_compact(part.data_ptr<float>(), rows, 2 * g.cin, chunk, small.data_ptr<float>(), cur_stream(),
-                      mean_invstd.data_ptr<float>());
-  return {dx, small};
-}
-
 // x [N,Cin,H,W], dy [N,Cout,Ho,Wo] (CL bf16) -> dw fp32 [Cout,Cin,KH,KW]
 at::Tensor conv_igemm_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t kh, int64_t kw,
                             at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
@@ -249,9 +191,6 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
         "Tensor? scale_shift, Tensor? residual, int act) -> (Tensor, Tensor)");
   m.def("conv_halo_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
         "Tensor? addend=None) -> Tensor");
-  m.def("conv_igemm_dgrad_bn(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
-        "Tensor? addend, Tensor z, Tensor? mask, Tensor mean_invstd, int mode) "
-        "-> (Tensor, Tensor)");
   m.def("conv_igemm_wgrad(Tensor x, Tensor dy, int kh, int kw, int[] stride, int[] padding, int[] dilation, "
         "bool channels_last=False) -> Tensor");
 }
@@ -261,6 +200,5 @@ TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
   m.impl("conv_igemm_dgrad", &rtseg::conv_igemm_dgrad);
   m.impl("conv_halo", &rtseg::conv_halo);
   m.impl("conv_halo_dgrad", &rtseg::conv_halo_dgrad);
-  m.impl("conv_igemm_dgrad_bn", &rtseg::conv_igemm_dgrad_bn);
   m.impl("conv_igemm_wgrad", &rtseg::conv_igemm_wgrad);
 }

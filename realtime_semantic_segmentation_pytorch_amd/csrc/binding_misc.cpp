@@ -269,6 +269,26 @@ static at::Tensor dw_conv_fwd(const at::Tensor& x, const at::Tensor& wt, const s
   return y;
 }
 
+// forward + per-block BN statistics slab [rows, 2*Cout] (empty slab: unsupported multiplier)
+static std::tuple<at::Tensor, at::Tensor> dw_conv_fwd_stats(const at::Tensor& x, const at::Tensor& wt, int64_t cout,
+                                                            int64_t kh, int64_t kw, int64_t sh, int64_t sw,
+                                                            int64_t ph, int64_t pw, int64_t dh, int64_t dw) {
+  check_cl(x, "input");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  DwGeom g = dw_geom(x.size(0), x.size(1), x.size(2), x.size(3), cout, kh, kw, sh, sw, ph, pw, dh, dw);
+  check_wt(wt, kh * kw, cout);
+  at::Tensor y = at::empty({x.size(0), cout, g.ho, g.wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int rows = dw_fwd_stats_rows(g, dtype_code(x));
+  at::Tensor part = at::empty({rows, 2 * cout}, x.options().dtype(at::kFloat));
+  if (rows == 0) {
+    launch_dw_fwd(g, dtype_code(x), x.data_ptr(), wt.data_ptr<float>(), nullptr, y.data_ptr(), cur_stream());
+  } else {
+    launch_dw_fwd_stats(g, dtype_code(x), x.data_ptr(), wt.data_ptr<float>(), y.data_ptr(), part.data_ptr<float>(),
+                        cur_stream());
+  }
+  return {y, part};
+}
+
 static at::Tensor dw_conv_dgrad(const at::Tensor& dy, const at::Tensor& wt, int64_t cin, int64_t h, int64_t w,
                                 int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh,
                                 int64_t dw) {
@@ -307,6 +327,8 @@ static at::Tensor dw_conv_wgrad(const at::Tensor& dy, const at::Tensor& x, int64
 TORCH_LIBRARY_FRAGMENT(rtseg, m) {
   m.def("dw_conv_fwd(Tensor x, Tensor wt, Tensor? bias, int cout, int kh, int kw, int sh, int sw, int ph, int pw, "
         "int dh, int dw) -> Tensor");
+  m.def("dw_conv_fwd_stats(Tensor x, Tensor wt, int cout, int kh, int kw, int sh, int sw, int ph, int pw, "
+        "int dh, int dw) -> (Tensor, Tensor)");
   m.def("dw_conv_dgrad(Tensor dy, Tensor wt, int cin, int h, int w, int kh, int kw, int sh, int sw, int ph, "
         "int pw, int dh, int dw) -> Tensor");
   m.def("dw_conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw) -> Tensor");
@@ -314,6 +336,7 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
 
 TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
   m.impl("dw_conv_fwd", &rtseg::dw_conv_fwd);
+  m.impl("dw_conv_fwd_stats", &rtseg::dw_conv_fwd_stats);
   m.impl("dw_conv_dgrad", &rtseg::dw_conv_dgrad);
   m.impl("dw_conv_wgrad", &rtseg::dw_conv_wgrad);
 }

@@ -128,6 +128,11 @@ struct DwWgradPlan {
 };
 int dw_vec(int dtype, int c);
 DwWgradPlan dw_wgrad_plan(const DwGeom& g, int dtype);
+// forward + BN statistics slab (fp32 [rows, 2*Cout]); rows = dw_fwd_stats_rows (0: unsupported
+// channel multiplier -> use launch_dw_fwd + a statistics pass)
+int dw_fwd_stats_rows(const DwGeom& g, int dtype);
+void launch_dw_fwd_stats(const DwGeom& g, int dtype, const void* x, const float* wt, void* y, float* part,
+                         hipStream_t st);
 void launch_dw_fwd(const DwGeom& g, int dtype, const void* x, const float* wt, const float* bias, void* y,
                    hipStream_t st);
 void launch_dw_dgrad(const DwGeom& g, int dtype, const void* dy, const float* wt, void* dx, hipStream_t st);
@@ -148,11 +153,6 @@ struct ConvGeom {
   const void* res;
   int act;
   int n, h, w_in, cin, ho, wo, cout, kh, kw, sh, sw, ph, pw, dh, dw;
-  // conv_igemm dgrad only: BN-backward epilogue for the BatchNorm(+act) whose output is this
-  // conv's input (see launch_conv_igemm_dgrad)
-  const void* bn_z;
-  const void* bn_mask;
-  int bn_mode;
 };
 // BN activation-derivative sources (= ops/bn.py MASK_*)
 enum BnMaskMode : int { kBnMaskNone = 0, kBnMaskFromY = 1, kBnMaskFromX = 2, kBnMaskBits = 3 };
@@ -167,18 +167,11 @@ bool conv_igemm_supported(const ConvGeom& g, int mode);
 // rows of the BN statistics slab [rows, 2*Cout] written by the forward when g.part != nullptr
 // (one per M tile and pixel wave); launch_slab_compact sums groups of `chunk` rows
 int conv_igemm_slabs(const ConvGeom& g);
-// center: optional [C] mean for BN-backward slabs [sum g | sum g z] -> [sum g | sum g (z - mean)]
-void launch_slab_compact(const float* in, int rows, int width, int chunk, float* out, hipStream_t st,
-                         const float* center = nullptr);
+void launch_slab_compact(const float* in, int rows, int width, int chunk, float* out, hipStream_t st);
 void launch_conv_igemm_fwd(const ConvGeom& g, hipStream_t st);
 // g.x = dy [N,Ho,Wo,Cout], g.w = [Cin][KH][KW][Cout] bf16, g.y = dx [N,H,W,Cin];
 // g.scale_shift, when set, is a [Cin] bias added to dx (the forward of a transposed conv);
 // g.res, when set, is a bf16 tensor of dx's layout added to dx (a residual branch's gradient);
-// g.bn_z, when set: dx is the gradient of y = act(BN(z) [+ r]); the kernel stores
-// g = (dx [+ res]) * mask-bit and writes per-(tile, wave) rows [sum g | sum g z] into g.part
-// (conv_igemm_dgrad_slabs(g) rows of 2*Cin floats; launch_slab_compact(center = mean) centres
-// them); bn_mode kBnMaskNone or kBnMaskBits, Cin % 32 == 0
-int conv_igemm_dgrad_slabs(const ConvGeom& g);
 void launch_conv_igemm_dgrad(const ConvGeom& g, hipStream_t st);
 // g.x = x [N,H,W,Cin], g.y = dy [N,Ho,Wo,Cout]; ws fp32 of conv_igemm_wgrad_ws_elems(g);
 // dw fp32 [Cout][Cin][KH][KW]

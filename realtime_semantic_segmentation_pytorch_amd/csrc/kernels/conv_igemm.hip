@@ -68,13 +68,6 @@ struct IgArgs {
   const uint16_t* res;
   const float* bias;      // [cout] added to the accumulators first (transposed conv), or null
   const uint16_t* addend; // bf16 tensor of the output's layout added in the epilogue, or null
-  // BN-backward epilogue (STATS == 2; dgrad of the conv that consumes a BN(+act) output y):
-  // g = dx * act'(.) is stored instead of dx, and per-channel (sum g, sum g * z) of the BN
-  // input z go to `part` -- the BatchNorm backward then has no reduction pass
-  const uint16_t* bz;     // BN input z, dx's layout
-  const uint8_t* bmask;   // activation-derivative bits (1 per element, channels-last order)
-  int bmode;              // kBnMaskNone / kBnMaskBits
-  int bdbg;               // experiment knobs (RTSEG_BN_EPI_DBG), 0 in production
   int act;
   int H, W, C;            // gathered operand [N][H][W][C]
   int Hv, Wv;             // virtual output grid
@@ -111,7 +104,7 @@ __device__ __forceinline__ void bdma16x2(__amdgpu_buffer_rsrc_t r, uint32_t v0, 
 }
 
 
-// STATS: 0 = none, 1 = forward BN statistics of the output, 2 = BN-backward epilogue (IgArgs.bz)
+// STATS: 0 = none, 1 = forward BN statistics of the output
 // GB: gather the activation rows through a buffer resource (range-checked voffsets, the
 // border handled by the range check) instead of 64-bit flat addresses with a zero source.
 template <int BM, int BN, int WM, int WN, int NST, int EPI, int STATS, int GB>
@@ -254,121 +247,7 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
   const int co_lane = co0 + wn * (BN / WN) + 4 * fhi;  // + ti*32 + 8g
 
   auto pack_tile = [&](int mt) __attribute__((always_inline)) {
-    if constexpr (STATS == 2) {
-      // BN-backward epilogue: g = (acc [+ addend]) * bit(y) is stored, and per channel
-      // (sum g, sum g * z) is reduced (the binding subtracts mean * sum g).  Every load of the
-      // tile (z, the bit mask, the addend) is issued first: one exposed memory round trip per
-      // tile instead of one per 4-channel group.
-      static_assert(TJ >= 2, "statistics fold into two accumulator tiles");
-      bool okj[TJ];
-#pragma unroll
-      for (int tj = 0; tj < TJ; ++tj) {
-        const int m = mt * BM + wm * (BM / WM) + tj * 32 + frow;
-        okj[tj] = m < a.M;
-        uint32_t wv, hv;
-        const uint32_t t = a.fwv.divmod(static_cast<uint32_t>(okj[tj] ? m : 0), wv);
-        const uint32_t n = a.fhv.divmod(t, hv);
-        const int ho = static_cast<int>(hv) * a.osh + a.oph, wo = static_cast<int>(wv) * a.osw + a.opw;
-        pend_off[tj] = ((static_cast<int64_t>(n) * a.Ho + ho) * a.Wo + wo) * a.cout;
-      }
-      const bool has_add = a.addend != nullptr, has_bits = a.bmode == kBnMaskBits && !(a.bdbg & 2);
-      const bool load_z = !(a.bdbg & 1);
-      uint2 zr[TI][TJ][4], ad[TI][TJ][4];
-      uint32_t mb[TI][TJ];
-#pragma unroll
-      for (int ti = 0; ti < TI; ++ti) {
-        const bool tok = co_lane - 4 * fhi + ti * 32 < a.cout;  // Cout % 32 == 0: whole 32-row block
-#pragma unroll
-        for (int tj = 0; tj < TJ; ++tj) {
-          const bool ok = okj[tj] && tok;
-          const int64_t ob = pend_off[tj] + co_lane + ti * 32;  // + 8 g
-          // 4 consecutive mask bytes (channels co_lane - 4 fhi + ti*32 .. +31), 4-byte aligned
-          mb[ti][tj] = ok && has_bits ? *reinterpret_cast<const uint32_t*>(a.bmask + (ob >> 3))
-                                      : 0xffffffffu;
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            zr[ti][tj][g] = ok && load_z ? *reinterpret_cast<const uint2*>(a.bz + ob + 8 * g) : make_uint2(0, 0);
-            ad[ti][tj][g] = ok && has_add ? *reinterpret_cast<const uint2*>(a.addend + ob + 8 * g) : make_uint2(0, 0);
-          }
-        }
-      }
-      // one 4-channel group of MFMA tile (ti, tj): store g, return q = g (as stored) and q * z
-      auto grp = [&](int ti, int tj, int g, bool ok, float* q, float* qz) __attribute__((always_inline)) {
-        const uint32_t bits = mb[ti][tj] >> (4 * fhi + 8 * g);
-        float v[4], r[4], z[4];
-        bf16x4_unpack(ad[ti][tj][g], r);
-        bf16x4_unpack(zr[ti][tj][g], z);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = ((bits >> e) & 1u) ? acc[ti][tj][4 * g + e] + r[e] : 0.f;
-        uint2 pk;
-        pk.x = pack2(v[0], v[1]);
-        pk.y = pack2(v[2], v[3]);
-        if (ok && !(a.bdbg & 16)) *reinterpret_cast<uint2*>(a.y + pend_off[tj] + co_lane + ti * 32 + 8 * g) = pk;
-        bf16x4_unpack(pk, q);  // statistics of the values as stored
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          q[e] = ok ? q[e] : 0.f;
-          qz[e] = q[e] * z[e];
-        }
-      };
-      // per channel row ti, the lane's TJ pixels fold into the dead accumulator tiles acc[ti][0]
-      // (sum) / acc[ti][1] (sum * z) -- no extra registers -- then the 32 pixel lanes of each
-      // half-wave reduce by DPP: lanes 31 / 63 hold the tile's sums for channels
-      // (r & 3) + 8 (r >> 2) + 4 * half.  One slab row per (M tile, pixel wave), no atomics.
-      float* prow = a.part + (static_cast<int64_t>(mt) * WM + wm) * 2 * a.cout;
-#pragma unroll
-      for (int ti = 0; ti < TI; ++ti) {
-        const bool tok = co_lane - 4 * fhi + ti * 32 < a.cout;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          float q0[4], z0[4], q1[4], z1[4];
-          grp(ti, 0, g, okj[0] && tok, q0, z0);
-          grp(ti, 1, g, okj[1] && tok, q1, z1);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            acc[ti][0][4 * g + e] = q0[e] + q1[e];
-            acc[ti][1][4 * g + e] = z0[e] + z1[e];
-          }
-        }
-#pragma unroll
-        for (int tj = 2; tj < TJ; ++tj) {
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            float q[4], qz[4];
-            grp(ti, tj, g, okj[tj] && tok, q, qz);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              acc[ti][0][4 * g + e] += q[e];
-              acc[ti][1][4 * g + e] += qz[e];
-            }
-          }
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[ti][tj][r] = 0.f;
-        }
-        if (!(a.bdbg & 4)) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            acc[ti][0][r] = half_wave_sum(acc[ti][0][r]);
-            acc[ti][1][r] = half_wave_sum(acc[ti][1][r]);
-          }
-        }
-        if (frow == 31 && tok && !(a.bdbg & 8)) {
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int co = co_lane + ti * 32 + 8 * g;
-            *reinterpret_cast<float4*>(prow + co) =
-                make_float4(acc[ti][0][4 * g], acc[ti][0][4 * g + 1], acc[ti][0][4 * g + 2], acc[ti][0][4 * g + 3]);
-            *reinterpret_cast<float4*>(prow + a.cout + co) =
-                make_float4(acc[ti][1][4 * g], acc[ti][1][4 * g + 1], acc[ti][1][4 * g + 2], acc[ti][1][4 * g + 3]);
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          acc[ti][0][r] = 0.f;
-          acc[ti][1][r] = 0.f;
-        }
-      }
-    } else {  // no BN-backward epilogue    } else {  // no BN-backward epilogue
+    {
       // BN statistics of this tile: per-lane partial sums over the lane's TJ pixels
       float ts[STATS ? TI : 1][16], tq[STATS ? TI : 1][16];
       if constexpr (STATS) {
@@ -803,10 +682,10 @@ void launch_cfg(const IgArgs& k, const Cfg& c, int grid, hipStream_t st) {
     case 0: igemm_gather_kernel<256, 64, 4, 2, 3, EPI, STATS, GB><<<grid, 512, 0, st>>>(k); break;
     case 2: igemm_gather_kernel<512, 64, 8, 1, 2, EPI, STATS, GB><<<grid, 512, 0, st>>>(k); break;
     case 3:
-      if constexpr (EPI == 0 && STATS != 2) igemm_gather_kernel<256, 256, 2, 4, 2, 0, STATS, GB><<<grid, 512, 0, st>>>(k);
+      if constexpr (EPI == 0) igemm_gather_kernel<256, 256, 2, 4, 2, 0, STATS, GB><<<grid, 512, 0, st>>>(k);
       break;
     case 4:
-      if constexpr (EPI == 0 && STATS != 2) igemm_gather_kernel<512, 128, 4, 2, 2, 0, STATS, GB><<<grid, 512, 0, st>>>(k);
+      if constexpr (EPI == 0) igemm_gather_kernel<512, 128, 4, 2, 2, 0, STATS, GB><<<grid, 512, 0, st>>>(k);
       break;
     default: igemm_gather_kernel<256, 128, 4, 2, 3, EPI, STATS, GB><<<grid, 512, 0, st>>>(k); break;
   }
@@ -826,28 +705,20 @@ void launch_cfg(const IgArgs& k, const Cfg& c, int grid, hipStream_t st) {
 }
 
 // out[r][c] = sum_{i < chunk} in[r * chunk + i][c] (rows past `rows` count as zero).
-// center != null (BN-backward slabs [sum g | sum g z]): the second half becomes
-// sum g (z - mean) = sum g z - mean * sum g, row by row (linear, so exact per row).
 __global__ void slab_compact_kernel(const float* __restrict__ in, int rows, int width, int chunk,
-                                    const float* __restrict__ center, float* __restrict__ out) {
+                                    float* __restrict__ out) {
   const int c = blockIdx.y * blockDim.x + threadIdx.x;
   if (c >= width) return;
-  const int half = width / 2;
-  const bool ctr = center != nullptr && c >= half;
   const int r0 = blockIdx.x * chunk, r1 = min(r0 + chunk, rows);
-  float s = 0.f, s0 = 0.f;
-  for (int r = r0; r < r1; ++r) {
-    s += in[static_cast<int64_t>(r) * width + c];
-    if (ctr) s0 += in[static_cast<int64_t>(r) * width + c - half];
-  }
-  out[static_cast<int64_t>(blockIdx.x) * width + c] = ctr ? s - center[c - half] * s0 : s;
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += in[static_cast<int64_t>(r) * width + c];
+  out[static_cast<int64_t>(blockIdx.x) * width + c] = s;
 }
 
 void launch_gather(const IgArgs& k, const Cfg& c, hipStream_t st) {
   const int grid = persistent_grid(k.mtiles, k.ntiles);
   if (grid <= 0) return;
   if (k.ss != nullptr) launch_cfg<1, 0>(k, c, grid, st);
-  else if (k.part != nullptr && k.bz != nullptr) launch_cfg<0, 2>(k, c, grid, st);
   else if (k.part != nullptr) launch_cfg<0, 1>(k, c, grid, st);
   else launch_cfg<0, 0>(k, c, grid, st);
 }
@@ -874,28 +745,12 @@ int conv_igemm_slabs(const ConvGeom& g) {
 // the BN-backward epilogue does not fit the registers of the 64 x 128 wave tiles (it spills):
 // those layers take the 64 x 64 wave tiles of config 1 instead
 static Cfg dgrad_cfg(const ConvGeom& g) {
-  const Cfg c = pick_cfg(g.cin, static_cast<int64_t>(g.n) * g.h * g.w_in / (g.sh * g.sw));
-  return g.bn_z != nullptr && (c.id == 3 || c.id == 4) ? kCfgs[1] : c;
+  return pick_cfg(g.cin, static_cast<int64_t>(g.n) * g.h * g.w_in / (g.sh * g.sw));
 }
 
-// dgrad: one launch per output phase (a, b), each with its own virtual grid
-int conv_igemm_dgrad_slabs(const ConvGeom& g) {
-  const Cfg c = dgrad_cfg(g);
-  int rows = 0;
-  for (int a = 0; a < g.sh; ++a)
-    for (int b = 0; b < g.sw; ++b) {
-      const int64_t hv = (g.h - a + g.sh - 1) / g.sh, wv = (g.w_in - b + g.sw - 1) / g.sw;
-      if (hv <= 0 || wv <= 0) continue;
-      const int64_t M = g.n * hv * wv;
-      rows += static_cast<int>((M + c.bm - 1) / c.bm) * c.wm;
-    }
-  return rows;
-}
-
-void launch_slab_compact(const float* in, int rows, int width, int chunk, float* out, hipStream_t st,
-                         const float* center) {
+void launch_slab_compact(const float* in, int rows, int width, int chunk, float* out, hipStream_t st) {
   const dim3 grid((rows + chunk - 1) / chunk, (width + 255) / 256);
-  slab_compact_kernel<<<grid, 256, 0, st>>>(in, rows, width, chunk, center, out);
+  slab_compact_kernel<<<grid, 256, 0, st>>>(in, rows, width, chunk, out);
 }
 
 void launch_conv_igemm_fwd(const ConvGeom& g, hipStream_t st) {
@@ -929,18 +784,9 @@ void launch_conv_igemm_fwd(const ConvGeom& g, hipStream_t st) {
 // g: forward geometry; g.x = dy [N,Ho,Wo,Cout], g.w = wt [Cin][KH][KW][Cout], g.y = dx [N,H,W,Cin]
 void launch_conv_igemm_dgrad(const ConvGeom& g, hipStream_t st) {
   const Cfg c = dgrad_cfg(g);
-  int slab_row = 0;
   for (int a = 0; a < g.sh; ++a)
     for (int b = 0; b < g.sw; ++b) {
       IgArgs k{};
-      if (g.bn_z != nullptr) {  // BN-backward epilogue: this phase's rows of the slab
-        k.bz = static_cast<const uint16_t*>(g.bn_z);
-        k.bmask = static_cast<const uint8_t*>(g.bn_mask);
-        k.bmode = g.bn_mode;
-        static const int dbg = std::getenv("RTSEG_BN_EPI_DBG") ? std::atoi(std::getenv("RTSEG_BN_EPI_DBG")) : 0;
-        k.bdbg = dbg;
-        k.part = g.part + static_cast<int64_t>(slab_row) * 2 * g.cin;
-      }
       k.x = static_cast<const uint16_t*>(g.x);
       k.w = static_cast<const uint16_t*>(g.w);
       k.y = static_cast<uint16_t*>(g.y);
@@ -967,7 +813,6 @@ void launch_conv_igemm_dgrad(const ConvGeom& g, hipStream_t st) {
         }
       }
       fill_common(k, c, g.n);
-      slab_row += k.mtiles * c.wm;
       launch_gather(k, c, st);
     }
 }

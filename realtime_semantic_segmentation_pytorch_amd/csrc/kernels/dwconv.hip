@@ -23,6 +23,7 @@
 #include "rtseg_launch.h"
 #include "rtseg_vec.h"
 
+#include <algorithm>
 #include <type_traits>
 
 namespace rtseg {
@@ -64,13 +65,24 @@ __device__ __forceinline__ void load_wvec(const float* p, float* w) {
 // which hipcc lowers to a branch + s_waitcnt around every single load.
 
 // ---------------------------------------------------------------- forward
-template <typename T, int VEC, int MT, int KS>
+// STATS: also the per-channel (sum, sum of squares) of the fp32 outputs for a training BatchNorm
+// (one [2 * Cout] row per block of `part`, reduced by bn_finalize_slab) -- the BN forward then
+// never re-reads y.  Deterministic: the host makes gridDim.x * kDwBlock a multiple of the
+// channel-vector count, so each thread keeps ONE channel vector for all its iterations and
+// accumulates it in registers; the block then sums its threads in a fixed order through LDS.
+template <typename T, int VEC, int MT, int KS, bool STATS = false>
 __global__ void __launch_bounds__(kDwBlock) dw_fwd_kernel(DwGeom g, DwDivs fd, const T* __restrict__ x,
                                                           const float* __restrict__ wt,
-                                                          const float* __restrict__ bias, T* __restrict__ y) {
+                                                          const float* __restrict__ bias, T* __restrict__ y,
+                                                          float* __restrict__ part = nullptr) {
   constexpr int OV = MT > 1 ? VEC * MT : VEC;  // output channels per thread
   const int cv_n = MT > 1 ? g.cin / VEC : g.cout / VEC;
   const uint32_t total = static_cast<uint32_t>(g.n) * g.ho * g.wo * cv_n;  // < 2^31 (host splits)
+  float ssum[STATS ? OV : 1], ssq[STATS ? OV : 1];
+  if constexpr (STATS) {
+#pragma unroll
+    for (int e = 0; e < OV; ++e) ssum[e] = ssq[e] = 0.f;
+  }
   for (uint32_t it = blockIdx.x * kDwBlock + threadIdx.x; it < total; it += gridDim.x * kDwBlock) {
     uint32_t cvu, wou, hou;
     const uint32_t pix = fd.c.divmod(it, cvu);
@@ -117,6 +129,46 @@ __global__ void __launch_bounds__(kDwBlock) dw_fwd_kernel(DwGeom g, DwDivs fd, c
     T* yp = y + ((static_cast<int64_t>(n) * g.ho + ho) * g.wo + wo) * g.cout + co;
 #pragma unroll
     for (int q = 0; q < OV / VEC; ++q) Vec<T, VEC>::store(yp + q * VEC, acc + q * VEC);
+    if constexpr (STATS) {
+#pragma unroll
+      for (int e = 0; e < OV; ++e) {
+        ssum[e] += acc[e];
+        ssq[e] = fmaf(acc[e], acc[e], ssq[e]);
+      }
+    }
+  }
+  if constexpr (STATS) {
+    // block reduction in 8-channel chunks: thread t owns channel vector (base + t) % cv_n
+    __shared__ float red[2][8][kDwBlock];
+    const int t = threadIdx.x;
+    const int base = static_cast<int>((static_cast<uint64_t>(blockIdx.x) * kDwBlock) % cv_n);
+    float* prow = part + static_cast<int64_t>(blockIdx.x) * 2 * g.cout;
+#pragma unroll
+    for (int k = 0; k < (OV + 7) / 8; ++k) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[0][e][t] = k * 8 + e < OV ? ssum[(k * 8 + e) % OV] : 0.f;
+        red[1][e][t] = k * 8 + e < OV ? ssq[(k * 8 + e) % OV] : 0.f;
+      }
+      __syncthreads();
+      // (channel vector cv, output e of this chunk): sum over the threads holding cv
+      for (int r = t; r < cv_n * 8; r += kDwBlock) {
+        const int cv = r >> 3, e = r & 7;
+        if (k * 8 + e < OV) {
+          int t0 = cv - base;
+          t0 = ((t0 % cv_n) + cv_n) % cv_n;
+          float a = 0.f, b = 0.f;
+          for (int tt = t0; tt < kDwBlock; tt += cv_n) {
+            a += red[0][e][tt];
+            b += red[1][e][tt];
+          }
+          const int c = cv * OV + k * 8 + e;
+          prow[c] = a;
+          prow[g.cout + c] = b;
+        }
+      }
+      __syncthreads();
+    }
   }
 }
 
@@ -377,6 +429,61 @@ void launch_dw_fwd(const DwGeom& g0, int dtype, const void* x, const float* wt, 
       dw_fwd_kernel<T, V, M, 0><<<grid, kDwBlock, 0, st>>>(g, fd, reinterpret_cast<const T*>(xb), wt, bias,
                                                              reinterpret_cast<T*>(yb));
     });
+  }
+}
+
+// grid of one stats launch: a multiple of cv_n / gcd(cv_n, kDwBlock) blocks (every thread keeps
+// one channel vector), never more blocks than the work needs rounded up to that multiple
+static int dw_stats_grid(int64_t items, int cv_n) {
+  int gg = kDwBlock, a = cv_n;
+  while (a != 0) { const int r = gg % a; gg = a; a = r; }
+  const int m = cv_n / gg;
+  int grid = stream_grid(items, kDwBlock);
+  grid = std::max(m, (grid + m - 1) / m * m);
+  return grid;
+}
+
+static int dw_fwd_stats_vec(const DwGeom& g, int dtype) {
+  const int mt = mt_of(g.mult);
+  return mt > 1 ? dw_vec(dtype, g.cin) : dw_vec(dtype, g.cout);
+}
+
+int dw_fwd_stats_rows(const DwGeom& g0, int dtype) {
+  const int mt = mt_of(g0.mult);
+  if (mt == 0) return 0;
+  const int vec = dw_fwd_stats_vec(g0, dtype);
+  const int cv_n = (mt > 1 ? g0.cin : g0.cout) / vec;
+  const int64_t per_img = static_cast<int64_t>(g0.ho) * g0.wo * cv_n;
+  const int nb = batch_chunk(per_img, g0.n);
+  int rows = 0;
+  for (int n0 = 0; n0 < g0.n; n0 += nb) rows += dw_stats_grid(per_img * std::min(nb, g0.n - n0), cv_n);
+  return rows;
+}
+
+void launch_dw_fwd_stats(const DwGeom& g0, int dtype, const void* x, const float* wt, void* y, float* part,
+                         hipStream_t st) {
+  const int mt = mt_of(g0.mult);
+  const int vec = dw_fwd_stats_vec(g0, dtype);
+  const int cv_n = (mt > 1 ? g0.cin : g0.cout) / vec;
+  const int64_t per_img = static_cast<int64_t>(g0.ho) * g0.wo * cv_n;
+  const int nb = batch_chunk(per_img, g0.n);
+  const int64_t eb = elem_bytes(dtype);
+  for (int n0 = 0; n0 < g0.n; n0 += nb) {
+    DwGeom g = g0;
+    g.n = n0 + nb <= g0.n ? nb : g0.n - n0;
+    const char* xb = static_cast<const char*>(x) + static_cast<int64_t>(n0) * g.h * g.w * g.cin * eb;
+    char* yb = static_cast<char*>(y) + static_cast<int64_t>(n0) * g.ho * g.wo * g.cout * eb;
+    const DwDivs fd{FastDiv::make(cv_n), FastDiv::make(g.wo), FastDiv::make(g.ho)};
+    const int grid = dw_stats_grid(per_img * g.n, cv_n);
+    dw_dispatch(dtype, vec, g.mult, [&](auto t, auto v, auto m) {
+      using T = decltype(t);
+      constexpr int V = decltype(v)::value, M = decltype(m)::value;
+      if constexpr (M != 0) {
+        dw_fwd_kernel<T, V, M, 0, true><<<grid, kDwBlock, 0, st>>>(g, fd, reinterpret_cast<const T*>(xb), wt, nullptr,
+                                                                     reinterpret_cast<T*>(yb), part);
+      }
+    });
+    part += static_cast<int64_t>(grid) * 2 * g.cout;
   }
 }
 

@@ -84,6 +84,14 @@ class _FusedTail:
             y = self._mfma_tail(x, conv, bn, own, residual, act)
             if y is not None:
                 return y
+        elif (residual is None and isinstance(conv, ops.DepthwiseConv2d)
+              and isinstance(bn, (nn.BatchNorm2d, nn.SyncBatchNorm))
+              and (bn.training or not bn.track_running_stats or bn.running_mean is None)):
+            # depth-wise conv with the BN statistics in its epilogue (DWConvBNAct, K2)
+            out = ops.dw_conv_bn_stats(x, conv)
+            if out is not None:
+                y, part = out
+                return ops.bn_act(y, bn, own, act_module=own, part=part)
         y = ops.conv_forward(x, conv)
         if residual is None:
             return ops.bn_act(y, bn, own, act_module=own)

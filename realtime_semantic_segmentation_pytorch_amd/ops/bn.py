@@ -31,11 +31,6 @@ MASK_NONE, MASK_FROM_Y, MASK_FROM_X, MASK_BITS = 0, 1, 2, 3
 _USE_BITS = os.environ.get("RTSEG_BN_BITS", "1") != "0"
 # residual-gradient hand-off to the upstream conv's dgrad (RTSEG_RES_HANDOFF=0: off, for A/B)
 _HANDOFF = os.environ.get("RTSEG_RES_HANDOFF", "1") != "0"
-# BN-backward reduction in the dgrad epilogue of the conv consuming the BN output
-# (ops.conv._dgrad_bn).  Off by default: the epilogue runs while every wave of the CU waits at
-# the K-step barrier, and its z / mask loads cost more there than the separate, bandwidth-bound
-# reduction pass (profiles/r2_bn_fusion: 0.73-1.02x at batch 32); RTSEG_BN_BWD_FUSE=1 enables it.
-_BN_BWD_FUSE = os.environ.get("RTSEG_BN_BWD_FUSE", "0") == "1"
 
 
 def act_code(act) -> Optional[int]:
@@ -89,14 +84,9 @@ class _BNActFn(torch.autograd.Function):
         else:
             sums = None
             mi, ss = eval_coeffs(bn)
-        # what a consuming routed conv's dgrad epilogue can take over (ops.conv._dgrad_bn): the
-        # backward reduction of a bf16 BN with batch statistics, its activation derivative as
-        # the bit mask (8 channels per byte, 32-channel aligned)
-        linkable = (_BN_BWD_FUSE and use_batch_stats and x.dtype == torch.bfloat16 and x.shape[1] % 32 == 0
-                    and vec_width(x.dtype, x.shape[1]) == 8 and _USE_BITS)
         if act == ACT_NONE:
             mask = MASK_NONE
-        elif residual is None and not linkable:
+        elif residual is None:
             mask = MASK_FROM_X
         else:
             mask = MASK_BITS if _USE_BITS else MASK_FROM_Y
@@ -118,32 +108,24 @@ class _BNActFn(torch.autograd.Function):
             if node is not None and node.addend_slot is None:
                 node.addend_slot = ctx.handoff = []
         ctx.has_w = weight is not None
-        ctx.bn_link = (x, bits, mi, mask) if linkable else None
-        ctx.bwd_slabs = None
         ctx.save_for_backward(x, y if mask == MASK_FROM_Y else bits, mi, ss, sums, weight)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, y, mi, ss, sums, weight = ctx.saved_tensors
-        slab, mask = _take_slab(ctx, dy), ctx.mask
-        if slab is not None:  # dy is already g = dy * act'(.) and reduced (ops.conv._dgrad_bn)
-            y, mask = None, MASK_NONE
+        mask = ctx.mask
         dy = _aligned_cl(dy)
         bsums = local = None
         want_dres = ctx.has_res and ctx.needs_input_grad[3]
         want_dw = ctx.has_w and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
         if ctx.pg is not None:
-            if slab is not None:
-                bsums = ops().bn_slab_sums(slab, -1.0)[: 2 * x.shape[1]]
-                slab = None
-            else:
-                bsums = ops().bn_bwd_sums(dy, x, y, mi, ss, ctx.act, mask)
+            bsums = ops().bn_bwd_sums(dy, x, y, mi, ss, ctx.act, mask)
             if want_dw:
                 local = bsums.clone()
             dist.all_reduce(bsums, group=ctx.pg)
         dx, dres, dw, db = ops().bn_backward(dy, x, y, bsums, sums, mi, ss, weight, ctx.act,
-                                             mask, want_dres, ctx.batch_stats, want_dw, slab)
+                                             mask, want_dres, ctx.batch_stats, want_dw, None)
         if local is not None:
             # parameter gradients are this rank's contribution (DDP averages them), as in torch's
             # SyncBatchNorm; only the input-gradient coefficients use the all-reduced sums
@@ -155,21 +137,6 @@ class _BNActFn(torch.autograd.Function):
             dres = None
         return (dx, dw if want_dw else None, db if want_dw else None,
                 dres if want_dres else None, None, None, None, None, None)
-
-
-def _take_slab(ctx, dy):
-    """The backward reduction a consuming conv's dgrad epilogue produced for this node, if ``dy``
-    is exactly that conv's output (same storage, never accumulated into); otherwise None, and
-    the conv(s) stop producing it (the BN output has other consumers)."""
-    slabs, ctx.bwd_slabs = ctx.bwd_slabs, None
-    if not slabs:
-        return None
-    part, ptr, ver, _ = slabs[0]
-    if len(slabs) == 1 and dy.data_ptr() == ptr and dy._version == ver and dy.dtype == torch.bfloat16:
-        return part
-    for *_, conv in slabs:
-        conv._rtseg_bn_fuse_off = True
-    return None
 
 
 def eval_coeffs(bn):

@@ -242,13 +242,6 @@ class _ConvFn(torch.autograd.Function):
         # residual branch's gradient to fuse into the dgrad epilogue (see ops.bn)
         ctx.in_key = (x.data_ptr(), tuple(x.shape), x.dtype)
         ctx.addend_slot = None
-        # input produced by a fused BN(+act) node (ops.bn): our dgrad can do that BN's backward
-        # reduction in its epilogue.  Turned off per conv once it is seen to be wasted (the BN
-        # output had other consumers whose gradients autograd summed in)
-        ctx.bn_node = None
-        if x.requires_grad and not getattr(conv, "_rtseg_bn_fuse_off", False):
-            if getattr(x.grad_fn, "bn_link", None) is not None:
-                ctx.bn_node = x.grad_fn
         ctx.wdtype = weight.dtype
         if part is not None:
             ctx.mark_non_differentiable(part)
@@ -266,11 +259,7 @@ class _ConvFn(torch.autograd.Function):
         dx = dw = None
         addend = ctx.addend_slot.pop() if ctx.addend_slot else None
         if want_dx:
-            node = ctx.bn_node
-            if node is not None and getattr(node, "bn_link", None) is not None and _dgrad_bn_ok(conv):
-                dx = _dgrad_bn(x, dy, wk, conv, stride, padding, dilation, addend, node)
-            else:
-                dx = _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend)
+            dx = _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend)
         if want_dw:
             dw = _wgrad(x, dy, wk, conv, key, stride, padding, dilation)
             if dw.dtype != ctx.wdtype:
@@ -337,30 +326,6 @@ def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None):
     dx = fn()
     if addend is not None and name not in ("igemm", "halo"):
         dx = dx + addend
-    return dx
-
-
-def _dgrad_bn_ok(conv) -> bool:
-    return conv.out_channels % 64 == 0 and conv.in_channels % 32 == 0
-
-
-def _dgrad_bn(x, dy, wk, conv, stride, padding, dilation, addend, node):
-    """Our dgrad with the BN-backward epilogue of the BN(+act) node that produced ``x``: returns
-    g = dx * act'(.) and leaves the per-channel reduction (sum g, sum g (z - mean)) on the node,
-    tagged with g's identity -- :class:`ops.bn._BNActFn` uses it only if g reaches it unchanged
-    (no other gradient was accumulated into it)."""
-    z, bits, mi, mode = node.bn_link
-    if addend is not None:
-        addend = addend.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        if addend.data_ptr() % 16:
-            addend = addend.clone(memory_format=torch.channels_last)
-    wt = wk.permute(3, 1, 2, 0).contiguous()  # [Cin, KH, KW, Cout] bf16
-    dx, part = ops().conv_igemm_dgrad_bn(dy, wt, list(x.shape), stride, padding, dilation, addend, z,
-                                         bits if mode == 3 else None, mi, mode)
-    slabs = getattr(node, "bwd_slabs", None)
-    if slabs is None:
-        slabs = node.bwd_slabs = []
-    slabs.append((part, dx.data_ptr(), dx._version, conv))
     return dx
 
 

@@ -36,21 +36,34 @@ def _cl_aligned(t: torch.Tensor) -> torch.Tensor:
 
 
 class _DWConvFn(torch.autograd.Function):
+    """y = depth-wise conv(x); with ``stats`` also the BN-statistics slab of y (fp32 [rows, 2C],
+    produced in the forward kernel's epilogue; ``ops.bn_act(..., part=slab)`` consumes it)."""
+
     @staticmethod
-    def forward(ctx, x, weight, bias, geom):
+    def forward(ctx, x, weight, bias, geom, stats=False):
         cout, kh, kw, sh, sw, ph, pw, dh, dw = geom
         wt = weight.detach().float().reshape(cout, kh * kw).t().contiguous()
         b = bias.detach().float().contiguous() if bias is not None else None
         x = _cl_aligned(x)
-        y = ops().dw_conv_fwd(x, wt, b, cout, kh, kw, sh, sw, ph, pw, dh, dw)
+        part = None
+        if stats and b is None:
+            y, part = ops().dw_conv_fwd_stats(x, wt, cout, kh, kw, sh, sw, ph, pw, dh, dw)
+            if part.numel() == 0:
+                part = None
+        else:
+            y = ops().dw_conv_fwd(x, wt, b, cout, kh, kw, sh, sw, ph, pw, dh, dw)
         ctx.geom = geom
         ctx.has_bias = bias is not None
         ctx.wdtype = weight.dtype
         ctx.save_for_backward(x, wt)
-        return y
+        if not stats:
+            return y
+        if part is not None:
+            ctx.mark_non_differentiable(part)
+        return y, part
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, _dpart=None):
         x, wt = ctx.saved_tensors
         cout, kh, kw, sh, sw, ph, pw, dh, dw = ctx.geom
         dy = _cl_aligned(dy.to(x.dtype))
@@ -61,7 +74,7 @@ class _DWConvFn(torch.autograd.Function):
             dwt = ops().dw_conv_wgrad(dy, x, kh, kw, sh, sw, ph, pw, dh, dw).to(ctx.wdtype)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = dy.float().sum((0, 2, 3))
-        return dx, dwt, db, None
+        return dx, dwt, db, None, None
 
 
 def depthwise_ok(conv: nn.Conv2d) -> bool:
@@ -82,6 +95,22 @@ def dw_conv2d(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
                     conv.padding[1], conv.dilation[0], conv.dilation[1])
             return _DWConvFn.apply(x.to(dt), conv.weight, conv.bias, geom)
     return F.conv2d(x, conv.weight, conv.bias, conv.stride, conv.padding, conv.dilation, conv.groups)
+
+
+def dw_conv_bn_stats(x: torch.Tensor, conv: nn.Conv2d):
+    """Training forward of a depth-wise conv followed by a batch-statistics BN: (y, slab | None),
+    the slab holding the BN statistics of y from the conv kernel's epilogue; None -> the caller's
+    stock path (``conv(x)`` + ``ops.bn_act``)."""
+    if not (x.dim() == 4 and use_hip(x) and x.is_contiguous(memory_format=torch.channels_last)
+            and os.environ.get("RTSEG_DWCONV", "1") != "0" and conv.bias is None and depthwise_ok(conv)):
+        return None
+    dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
+    if dt not in _DTYPES or conv.weight.dtype not in _DTYPES:
+        return None
+    kh, kw = conv.kernel_size
+    geom = (conv.out_channels, kh, kw, conv.stride[0], conv.stride[1], conv.padding[0],
+            conv.padding[1], conv.dilation[0], conv.dilation[1])
+    return _DWConvFn.apply(x.to(dt), conv.weight, None, geom, True)
 
 
 def dw_conv2d_reference(x, weight, bias, stride, padding, dilation):

@@ -177,90 +177,3 @@ def test_residual_grad_handoff_matches_plain_add(monkeypatch):
     _close(res[True][1], res[False][1], 2e-2)
     for n, g in res[False][2].items():
         _close(res[True][2][n], g, 2e-2)
-
-
-def _cl_bits(mask):
-    """[N,C,H,W] bool -> the BN kernels' bit mask: bit j of byte i = element 8i+j in
-    channels-last memory order."""
-    flat = mask.permute(0, 2, 3, 1).reshape(-1, 8).to(torch.int32)
-    return (flat << torch.arange(8, device=mask.device, dtype=torch.int32)).sum(1).to(torch.uint8)
-
-
-# (n, cin, h, w, cout, k, stride): the BN-backward epilogue on plain / strided dgrad
-DGRAD_BN = [(2, 64, 17, 23, 64, 3, 1), (2, 128, 16, 20, 64, 3, 2), (1, 256, 9, 11, 128, 1, 1)]
-
-
-@pytest.mark.parametrize("geom", DGRAD_BN)
-@pytest.mark.parametrize("mode,act", [(0, 0), (3, 1), (3, 2)])
-@pytest.mark.parametrize("with_addend", [False, True])
-def test_igemm_dgrad_bn_epilogue(geom, mode, act, with_addend):
-    n, cin, h, w, cout, k, s = geom
-    x, wt = _case(n, cin, h, w, cout, k, s, 1, seed=21)
-    p = (k - 1) // 2
-    ho, wo = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
-    gen = torch.Generator(device="cpu").manual_seed(3)
-    cl = dict(memory_format=torch.channels_last)
-    dy = torch.randn(n, cout, ho, wo, generator=gen).to(DEV, torch.bfloat16).contiguous(**cl)
-    z = (torch.randn(n, cin, h, w, generator=gen) * 2 + 0.5).to(DEV, torch.bfloat16).contiguous(**cl)
-    mean = torch.randn(cin, generator=gen).to(DEV) * 0.3
-    invstd = torch.rand(cin, generator=gen).to(DEV) + 0.5
-    scale = torch.randn(cin, generator=gen).to(DEV)
-    shift = torch.randn(cin, generator=gen).to(DEV)
-    res = torch.randn(n, cin, h, w, generator=gen).to(DEV)
-    add = torch.randn(n, cin, h, w, generator=gen).to(DEV, torch.bfloat16).contiguous(**cl)
-    pre = z.float() * scale.view(1, -1, 1, 1) + shift.view(1, -1, 1, 1) + res.float()  # y = act(BN(z) + r)
-    if act == 1:
-        m = pre > 0
-    elif act == 2:
-        m = (pre > 0) & (pre < 6)
-    else:
-        m = torch.ones_like(pre, dtype=torch.bool)
-    mask_t = _cl_bits(m) if mode == 3 else None
-    g, part = torch.ops.rtseg.conv_igemm_dgrad_bn(
-        dy, wt.permute(1, 2, 3, 0).contiguous(), list(x.shape), [s, s], [p, p], [1, 1],
-        add if with_addend else None, z, mask_t, torch.cat([mean, invstd]).contiguous(), mode)
-    ref = torch.nn.grad.conv2d_input(x.shape, wt.float(), dy.float(), s, p, 1)
-    if with_addend:
-        ref = ref + add.float()
-    gref = ref * m.float() if mode != 0 else ref
-    assert g.shape == x.shape and g.is_contiguous(memory_format=torch.channels_last)
-    _close(g, gref, 2e-2)
-    sums = part.double().sum(0)
-    g64 = g.double()  # the kernel's statistics are of the stored bf16 values
-    s1 = g64.sum((0, 2, 3))
-    s2 = (g64 * (z.double() - mean.double().view(1, -1, 1, 1))).sum((0, 2, 3))
-    torch.testing.assert_close(sums[:cin], s1, atol=1e-3 * s1.abs().max().item() + 1e-3, rtol=1e-3)
-    torch.testing.assert_close(sums[cin:], s2, atol=1e-3 * s2.abs().max().item() + 1e-3, rtol=1e-3)
-
-
-def test_bn_backward_fusion_matches_unfused(monkeypatch):
-    """DDRNet RB chain: the BN backward reductions run in the consuming convs' dgrad epilogues
-    (ops/conv.py _dgrad_bn) -- gradients must match the separate-reduction path, and the fused
-    slabs must actually be consumed."""
-    from realtime_semantic_segmentation_pytorch_amd.models.ddrnet import RB
-    from realtime_semantic_segmentation_pytorch_amd.ops import bn as bn_mod
-
-    monkeypatch.setenv("RTSEG_CONV_MFMA", "1")
-    torch.manual_seed(1)
-    net = ops.convert_batchnorm(torch.nn.Sequential(RB(64, 128, stride=2), RB(128, 128), RB(128, 128)))
-    net = net.to(DEV).to(memory_format=torch.channels_last).train()
-    x0 = torch.randn(4, 64, 32, 48, device=DEV).contiguous(memory_format=torch.channels_last)
-    gy = torch.randn(4, 128, 16, 24, device=DEV)
-    used = []
-    take = bn_mod._take_slab
-    monkeypatch.setattr(bn_mod, "_take_slab", lambda ctx, dy: used.append(take(ctx, dy)) or used[-1])
-    res = {}
-    for on in (True, False):
-        monkeypatch.setattr(bn_mod, "_BN_BWD_FUSE", on)
-        used.clear()
-        net.zero_grad(set_to_none=True)
-        x = x0.to(torch.bfloat16).requires_grad_(True)
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            y = net(x)
-        (y.float() * gy).sum().backward()
-        res[on] = (sum(u is not None for u in used), x.grad.float().clone(),
-                   {n: p.grad.float().clone() for n, p in net.named_parameters() if p.grad is not None})
-    assert res[True][0] >= 5 and res[False][0] == 0, (res[True][0], res[False][0])
-    _close(res[True][1], res[False][1], 3e-2)
-    for n, g in res[False][2].items():
-        _close(res[True][2][n], g, 3e-2)

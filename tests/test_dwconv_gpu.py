@@ -79,3 +79,63 @@ def test_dwconv_autocast_module():
     with torch.no_grad():
         yr = F.relu(blk[1](F.conv2d(x, blk[0].weight, None, 1, 1, 1, 32)))
     torch.testing.assert_close(y.float(), yr, atol=5e-2, rtol=5e-2)
+
+
+# ------------------------------------------------------ forward + BN statistics epilogue (K2)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("geom", [g for g in GEOMS if g[1] in (1, 2, 3, 4, 6)] + [
+    (96, 1, (3, 3), 1, 1, (33, 17)),     # 12 channel vectors: grid rounded to a multiple of 3
+    (768, 1, (3, 3), 1, 1, (8, 16)),     # 96 channel vectors (> 8 * 256 / 8 chunks of work)
+    (48, 1, (3, 3), 1, 1, (200, 300)),   # many blocks
+])
+def test_dwconv_forward_stats_slab(dtype, geom):
+    cin, mult, k, s, d, hw = geom
+    torch.manual_seed(1)
+    pad = tuple((kk - 1) // 2 * d for kk in k)
+    cout = cin * mult
+    w = torch.randn(cout, 1, *k, device=DEV)
+    wt = w.reshape(cout, -1).t().contiguous()
+    x = torch.randn(3, cin, *hw, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    y, part = torch.ops.rtseg.dw_conv_fwd_stats(x, wt, cout, k[0], k[1], s, s, pad[0], pad[1], d, d)
+    y0 = torch.ops.rtseg.dw_conv_fwd(x, wt, None, cout, k[0], k[1], s, s, pad[0], pad[1], d, d)
+    assert torch.equal(y, y0)
+    assert part.dim() == 2 and part.shape[1] == 2 * cout and part.shape[0] > 0
+    ref = F.conv2d(x.double(), w.double(), None, s, pad, d, cin)  # fp32 accumulators ~ fp64
+    torch.testing.assert_close(part[:, :cout].double().sum(0), ref.sum((0, 2, 3)), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(part[:, cout:].double().sum(0), ref.square().sum((0, 2, 3)), rtol=1e-4, atol=1e-3)
+    part2 = torch.ops.rtseg.dw_conv_fwd_stats(x, wt, cout, k[0], k[1], s, s, pad[0], pad[1], d, d)[1]
+    assert torch.equal(part, part2)  # deterministic
+
+
+@pytest.mark.parametrize("mult", [1, 6])
+def test_dwconvbnact_training_uses_epilogue_stats(mult, monkeypatch):
+    """DWConvBNAct (models/modules.py) in training: the forward takes the statistics from the
+    depth-wise kernel (no separate BN statistics pass) and matches the PyTorch modules."""
+    from realtime_semantic_segmentation_pytorch_amd.models.modules import DWConvBNAct
+
+    torch.manual_seed(2)
+    m = DWConvBNAct(32, 32 * mult, 3, 2 if mult > 1 else 1).to(DEV)
+    ref = DWConvBNAct(32, 32 * mult, 3, 2 if mult > 1 else 1).to(DEV)
+    ref.load_state_dict(m.state_dict())
+    ops.convert_depthwise(m)
+    ops.convert_batchnorm(m)
+    calls = []
+    orig = ops.dw_conv_bn_stats
+    import realtime_semantic_segmentation_pytorch_amd.models.modules as M
+
+    monkeypatch.setattr(M.ops, "dw_conv_bn_stats", lambda *a: calls.append(1) or orig(*a))
+    x = torch.randn(4, 32, 24, 40, device=DEV).contiguous(memory_format=torch.channels_last)
+    xr = x.clone().requires_grad_(True)
+    x.requires_grad_(True)
+    y = m(x)
+    assert calls, "the depth-wise statistics path did not run"
+    monkeypatch.setenv("RTSEG_DISABLE_HIP", "1")
+    yr = ref(xr)
+    monkeypatch.delenv("RTSEG_DISABLE_HIP")
+    torch.testing.assert_close(y, yr, rtol=1e-4, atol=1e-4)
+    g = torch.randn_like(yr)
+    y.backward(g)
+    yr.backward(g)
+    torch.testing.assert_close(x.grad, xr.grad, rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(m[1].running_mean, ref[1].running_mean, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(m[1].running_var, ref[1].running_var, rtol=1e-4, atol=1e-5)

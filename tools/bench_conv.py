@@ -120,23 +120,6 @@ def main():
                     t_h = timeit(lambda: torch.ops.rtseg.conv_halo_dgrad(dy, wtr, list(x.shape), [s, s], [p, p],
                                                                          [1, 1]), a.iters)
                     rows.append(("halo_dg", relerr(dxh, dx_ref), t_m, t_h))
-            if "dgrad_bn" in passes and cin % 32 == 0:
-                # BN-backward reduction of the BN producing x: separate pass (ours dgrad + reduce,
-                # reported in the "miopen" column) vs fused into the dgrad epilogue
-                z = torch.randn_like(x)
-                bits = torch.randint(0, 256, (x.numel() // 8,), device=dev, dtype=torch.uint8)
-                mi = torch.cat([torch.randn(cin, device=dev) * 0.1, torch.rand(cin, device=dev) + 0.5])
-                ss = torch.cat([torch.ones(cin, device=dev), torch.zeros(cin, device=dev)])
-
-                def unfused():
-                    d = torch.ops.rtseg.conv_igemm_dgrad(dy, wtr, list(x.shape), [s, s], [p, p], [1, 1])
-                    torch.ops.rtseg.bn_bwd_sums(d, z, bits, mi, ss, 1, 3)
-
-                def fused():
-                    torch.ops.rtseg.conv_igemm_dgrad_bn(dy, wtr, list(x.shape), [s, s], [p, p], [1, 1], None, z,
-                                                        bits, mi, 3)
-
-                rows.append(("dgrad_bn" + sfx, 0.0, timeit(unfused, a.iters), timeit(fused, a.iters)))
         os.environ.pop("RTSEG_IGEMM_CFG", None)
         if "wgrad" in passes:
             dw_ref = conv_bw(dy, x, wcl, None, [s, s], [p, p], [1, 1], False, [0, 0], 1, [False, True, False])[1]
