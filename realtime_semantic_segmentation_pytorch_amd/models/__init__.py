@@ -67,7 +67,8 @@ def get_model(config):
     """Build the configured model; every BatchNorm2d, depth-wise conv and pooling
     module is routed through the HIP kernels (``ops.convert_batchnorm`` /
     ``ops.convert_depthwise`` / ``ops.convert_pooling``; module classes only --
-    parameters and checkpoint keys are unchanged)."""
+    parameters and checkpoint keys are unchanged), and every other spatial conv drops the
+    taps that only read padding at the current input size (``ops.convert_pruned_convs``)."""
     from .. import ops
 
     model = ops.convert_batchnorm(_build_model(config))
@@ -81,6 +82,7 @@ def get_model(config):
         ops.convert_dilated_group_convs(model)
     if getattr(config, "hip_deconv", True):
         ops.convert_transposed_convs(model)
+    ops.convert_pruned_convs(model)  # last: every remaining plain spatial conv
     if getattr(config, "hip_activations", True):
         ops.convert_activations(model)
     ops.convert_pixel_shuffle(model)
@@ -118,8 +120,8 @@ def get_teacher_model(config, device):
         raise ValueError(f"Unsupported teacher decoder type: {config.teacher_decoder}")
     from .. import ops
 
-    model = ops.convert_pooling(ops.convert_depthwise(ops.convert_batchnorm(
-        build_smp_model(config.teacher_decoder, config.teacher_encoder, None, config.num_class))))
+    model = ops.convert_pruned_convs(ops.convert_pooling(ops.convert_depthwise(ops.convert_batchnorm(
+        build_smp_model(config.teacher_decoder, config.teacher_encoder, None, config.num_class)))))
     ckpt_path = config.teacher_ckpt
     if ckpt_path:
         if not os.path.isfile(ckpt_path):

@@ -37,6 +37,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ._ext import ops, use_hip, write_generation
+from .dilated import PrunedConv2d, has_dead_taps
 
 _DECISIONS: dict = {}
 
@@ -131,15 +132,20 @@ def _autocast_bf16(x: torch.Tensor) -> bool:
     return dt == torch.bfloat16
 
 
+_ROUTED = (nn.Conv2d, PrunedConv2d)
+
+
 def conv_ok(x: torch.Tensor, conv: nn.Module) -> bool:
     """Convs this module routes (anything else stays ``conv(x)`` on MIOpen): dense, bias-free,
     channels-last bf16 activations.  Which kernel runs each pass is decided per shape."""
-    if type(conv) is not nn.Conv2d or conv.groups != 1 or conv.bias is not None:
+    if type(conv) not in _ROUTED or conv.groups != 1 or conv.bias is not None:
         return False
     if conv.padding_mode != "zeros" or isinstance(conv.padding, str):
         return False
     if x.dim() != 4 or not x.is_cuda or _mode() == "0" or not use_hip(x):
         return False
+    if has_dead_taps(x.shape[2:], conv.kernel_size, conv.stride, conv.padding, conv.dilation):
+        return False  # the module's own forward drops the dead taps (ops/dilated.py)
     if conv.kernel_size[0] * conv.kernel_size[1] > 49:
         return False
     return _autocast_bf16(x) and x.is_contiguous(memory_format=torch.channels_last)
@@ -440,7 +446,7 @@ def conv_bn_act_eval(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, act_code: 
 def conv_forward(x: torch.Tensor, conv: nn.Module) -> torch.Tensor:
     """``conv(x)``; in bf16-autocast inference the bf16 weight copy is cached on the module
     (autocast would re-cast the fp32 weight -- one extra kernel per conv -- every forward)."""
-    if (type(conv) is nn.Conv2d and not conv.training and not torch.is_grad_enabled() and x.is_cuda
+    if (type(conv) in _ROUTED and not conv.training and not torch.is_grad_enabled() and x.is_cuda
             and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16):
         w = conv.weight
         key = (w.data_ptr(), w._version, write_generation(),

@@ -20,6 +20,104 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+# ---------------------------------------------------------------------------------------------
+# Dead-tap pruning.
+#
+# A conv whose reach exceeds the feature map -- dilation >= the map extent (LEDNet's dilation-17
+# (3, 1) convs on a 16-row map, LiteSeg's dilation-12/18 branches and RegSeg's dilation-14
+# DBlocks at 1/16 scale, SMP ASPP rates 12/24/36) -- has taps that read nothing but zero
+# padding for EVERY output pixel.  Dropping them is exact: the output is unchanged and the
+# dropped weights' gradient is exactly 0.  It removes work (a 3x3 conv on a map shorter than its
+# dilation is a 1x3 conv) and it keeps such geometries away from MIOpen: MIOpen's NHWC solvers
+# have faulted the GPU on exactly these (round-1 find-mode search on LEDNet / CFPNet shapes, and
+# the intermittent round-2/3 fault in the single-process zoo checks, always on LEDNet, LiteSeg or
+# RegSeg backward in fp32, where every dense conv is MIOpen's).
+# ---------------------------------------------------------------------------------------------
+
+
+def _fmt(x: torch.Tensor):
+    cl = x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous()
+    return torch.channels_last if cl else torch.contiguous_format
+
+
+def _out_len(extent: int, k: int, s: int, p: int, d: int) -> int:
+    return (extent + 2 * p - d * (k - 1) - 1) // s + 1
+
+
+def live_taps(extent: int, k: int, s: int, p: int, d: int):
+    """``(lo, hi)``: the taps along one axis that read an in-range input for at least one output
+    position (a contiguous range), or None when no tap ever does."""
+    out = _out_len(extent, k, s, p, d)
+    if out <= 0:
+        return None
+    lo, hi = 0, k - 1
+    while lo <= hi and lo * d - p + (out - 1) * s < 0:  # tap only ever reads the left padding
+        lo += 1
+    while hi >= lo and hi * d - p >= extent:  # ... or only the right padding
+        hi -= 1
+    return (lo, hi) if lo <= hi else None
+
+
+def has_dead_taps(hw, kernel_size, stride, padding, dilation) -> bool:
+    """Whether a zero-padded conv over an ``hw`` map has taps that never read the map (cheap:
+    only the first and last tap of each axis can be dead first)."""
+    for e, k, s, p, d in zip(hw, kernel_size, stride, padding, dilation):
+        if k > 1 and (p > (_out_len(e, k, s, p, d) - 1) * s or (k - 1) * d - p >= e):
+            return True
+    return False
+
+
+def pruned_conv2d(x, weight, bias, stride, padding, dilation, groups):
+    """``F.conv2d`` with the dead taps of ``weight`` removed (exact; see above).  Padding that
+    becomes asymmetric is applied (or cropped) explicitly."""
+    stride, padding, dilation = tuple(stride), tuple(padding), tuple(dilation)
+    hw = tuple(x.shape[2:])
+    if not has_dead_taps(hw, weight.shape[2:], stride, padding, dilation):
+        return F.conv2d(x, weight, bias, stride, padding, dilation, groups)
+    spans = [live_taps(e, k, s, p, d)
+             for e, k, s, p, d in zip(hw, weight.shape[2:], stride, padding, dilation)]
+    if None in spans:  # an all-padding conv: nothing to keep, leave it as is
+        return F.conv2d(x, weight, bias, stride, padding, dilation, groups)
+    w = weight[:, :, spans[0][0]:spans[0][1] + 1, spans[1][0]:spans[1][1] + 1]
+    w = w.contiguous(memory_format=_fmt(x))
+    lr, dil = [], []
+    for (lo, hi), e, k, s, p, d in zip(spans, hw, weight.shape[2:], stride, padding, dilation):
+        kk = hi - lo + 1
+        dd = d if kk > 1 else 1
+        left = p - lo * d
+        right = (_out_len(e, k, s, p, d) - 1) * s + dd * (kk - 1) + 1 - e - left
+        lr.append((left, right))
+        dil.append(dd)
+    if all(a == b >= 0 for a, b in lr):
+        return F.conv2d(x, w, bias, stride, (lr[0][0], lr[1][0]), tuple(dil), groups)
+    xp = F.pad(x, (lr[1][0], lr[1][1], lr[0][0], lr[0][1]))
+    return F.conv2d(xp, w, bias, stride, 0, tuple(dil), groups)
+
+
+class PrunedConv2d(nn.Conv2d):
+    """``nn.Conv2d`` whose GPU forward drops dead taps for the current input size
+    (:func:`pruned_conv2d`); identical to ``nn.Conv2d`` whenever no tap is dead, and on CPU."""
+
+    def _conv_forward(self, input, weight, bias):
+        if (not input.is_cuda or self.padding_mode != "zeros"
+                or not has_dead_taps(input.shape[2:], self.kernel_size, self.stride, self.padding, self.dilation)):
+            return super()._conv_forward(input, weight, bias)
+        return pruned_conv2d(input, weight, bias, self.stride, self.padding, self.dilation, self.groups)
+
+
+def prunable(conv: nn.Module) -> bool:
+    return (type(conv) is nn.Conv2d and conv.padding_mode == "zeros" and not isinstance(conv.padding, str)
+            and max(conv.kernel_size) > 1)
+
+
+def convert_pruned_convs(model: nn.Module) -> nn.Module:
+    """Swap every remaining plain ``nn.Conv2d`` with a spatial kernel to :class:`PrunedConv2d`
+    (run after the other converters; parameters and checkpoint keys unchanged)."""
+    for m in model.modules():
+        if prunable(m):
+            m.__class__ = PrunedConv2d
+    return model
+
 
 def dilated_group_ok(conv: nn.Module) -> bool:
     if type(conv) is not nn.Conv2d or conv.groups == 1 or conv.groups == conv.in_channels:
@@ -46,13 +144,31 @@ def dilated_group_conv2d(x, weight, bias, dilation, groups):
     xs = xn.reshape(n, hs, dh, ws, dw, c).permute(0, 2, 4, 1, 3, 5).reshape(n * dh * dw, hs, ws, c)
     xs = xs.permute(0, 3, 1, 2)  # NCHW logical, channels-last physical
     kh, kw = weight.shape[2:]
-    ys = F.conv2d(xs, weight, bias, 1, ((kh - 1) // 2, (kw - 1) // 2), 1, groups)
+    ys = pruned_conv2d(xs, weight, bias, (1, 1), ((kh - 1) // 2, (kw - 1) // 2), (1, 1), groups)
     co = ys.shape[1]
     yn = ys.permute(0, 2, 3, 1).reshape(n, dh, dw, hs, ws, co).permute(0, 3, 1, 4, 2, 5).reshape(n, hp, wp, co)
     y = yn.permute(0, 3, 1, 2)
     if (hp, wp) != (h, w):
         y = y[:, :, :h, :w].contiguous(memory_format=torch.channels_last)
     return y
+
+
+def dilated_group_pruned(x, weight, bias, dilation, groups):
+    """:func:`dilated_group_conv2d` after dropping dead taps: a dilation >= the map extent
+    leaves only the centre tap on that axis, which then needs no space-to-batch along it (what
+    stays is still 'same' and symmetric)."""
+    w, dil = weight, list(dilation)
+    for a, (e, k, d) in enumerate(zip(x.shape[2:], weight.shape[2:], dilation)):
+        c = (k - 1) // 2
+        m = min(c, -(-e // d) - 1)
+        if m < c:
+            w = w.narrow(2 + a, c - m, 2 * m + 1)
+            dil[a] = d if m > 0 else 1
+    if max(dil) < 2:
+        kh, kw = w.shape[2:]
+        return F.conv2d(x, w.contiguous(memory_format=_fmt(x)), bias, 1,
+                        ((kh - 1) // 2, (kw - 1) // 2), 1, groups)
+    return dilated_group_conv2d(x, w, bias, tuple(dil), groups)
 
 
 class DilatedGroupConv2d(nn.Conv2d):
@@ -63,7 +179,7 @@ class DilatedGroupConv2d(nn.Conv2d):
 
         if not x.is_cuda or not use_hip(x):  # RTSEG_DISABLE_HIP=1: the stock conv, for A/B runs
             return super().forward(x)
-        return dilated_group_conv2d(x, self.weight, self.bias, tuple(self.dilation), self.groups)
+        return dilated_group_pruned(x, self.weight, self.bias, tuple(self.dilation), self.groups)
 
 
 def convert_dilated_group_convs(model: nn.Module) -> nn.Module:

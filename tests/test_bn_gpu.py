@@ -136,6 +136,10 @@ def test_fused_batchnorm_module_matches_torch(dtype, shape):
         ya.backward(g.to(dtype).contiguous(memory_format=torch.channels_last))
         yb.backward(g)
         torch.testing.assert_close(xa.grad.float(), xb.grad, atol=10 * tol, rtol=10 * tol)
+        # parameter gradients (accumulated over the train and eval passes on both sides)
+        for pa, pb in ((mod.weight, ref.weight), (mod.bias, ref.bias)):
+            torch.testing.assert_close(pa.grad, pb.grad, atol=10 * tol * max(1.0, pb.grad.abs().max().item()),
+                                       rtol=10 * tol)
     torch.testing.assert_close(mod.running_mean, ref.running_mean, atol=1e-4, rtol=1e-4)
 
 

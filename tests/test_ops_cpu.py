@@ -197,6 +197,63 @@ def test_dilated_group_conv_space_to_batch_cpu(hw, d, groups):
         torch.testing.assert_close(a, b)
 
 
+@pytest.mark.parametrize("hw,k,s,p,d", [
+    ((8, 16), (3, 3), (1, 1), (14, 14), (14, 14)),   # RegSeg DBlock at 1/16 of 128x256
+    ((16, 32), (3, 1), (1, 1), (17, 0), (17, 1)),    # LEDNet (3, 1), dilation 17
+    ((8, 16), (3, 3), (1, 1), (12, 12), (12, 12)),   # LiteSeg / ASPP branch
+    ((5, 7), (5, 3), (2, 1), (6, 1), (3, 1)),        # strided, asymmetric leftovers
+    ((1, 2), (3, 3), (1, 1), (1, 1), (1, 1)),        # 3x3 on a 1x2 map
+    ((3, 9), (7, 7), (1, 2), (9, 3), (2, 1)),
+    ((20, 24), (3, 3), (1, 1), (2, 2), (2, 2)),      # nothing dead: plain F.conv2d
+])
+def test_pruned_conv_drops_only_dead_taps_cpu(hw, k, s, p, d):
+    """ops/dilated.py: dead-tap pruning is exact (values and all three gradients; the dropped
+    taps' weight gradient is 0)."""
+    import torch.nn.functional as F
+    from realtime_semantic_segmentation_pytorch_amd.ops import has_dead_taps, pruned_conv2d
+
+    torch.manual_seed(0)
+    w = torch.randn(6, 4, *k, dtype=torch.float64, requires_grad=True)
+    b = torch.randn(6, dtype=torch.float64, requires_grad=True)
+    x = torch.randn(2, 4, *hw, dtype=torch.float64, requires_grad=True)
+    ref = F.conv2d(x, w, b, s, p, d)
+    got = pruned_conv2d(x, w, b, s, p, d, 1)
+    assert got.shape == ref.shape
+    torch.testing.assert_close(got, ref)
+    g = torch.randn_like(ref)
+    for a, r in zip(torch.autograd.grad(got, (x, w, b), g), torch.autograd.grad(ref, (x, w, b), g)):
+        torch.testing.assert_close(a, r)
+    assert has_dead_taps(hw, k, s, p, d) == (hw != (20, 24))
+
+
+@pytest.mark.parametrize("hw,d", [((8, 16), (14, 14)), ((8, 16), (4, 14)), ((3, 3), (5, 5)), ((9, 9), (2, 3))])
+def test_dilated_group_conv_prunes_then_space_to_batch_cpu(hw, d):
+    import torch.nn.functional as F
+    from realtime_semantic_segmentation_pytorch_amd.ops.dilated import dilated_group_pruned
+
+    torch.manual_seed(0)
+    w = torch.randn(32, 4, 3, 3, dtype=torch.float64, requires_grad=True)
+    x = torch.randn(2, 32, *hw, dtype=torch.float64, requires_grad=True)
+    ref = F.conv2d(x, w, None, 1, d, d, 8)
+    got = dilated_group_pruned(x, w, None, d, 8)
+    torch.testing.assert_close(got, ref)
+    g = torch.randn_like(ref)
+    for a, r in zip(torch.autograd.grad(got, (x, w), g), torch.autograd.grad(ref, (x, w), g)):
+        torch.testing.assert_close(a, r)
+
+
+def test_pruned_convs_converted_in_zoo_cpu():
+    from realtime_semantic_segmentation_pytorch_amd.configs import BaseConfig
+    from realtime_semantic_segmentation_pytorch_amd.models import get_model
+    from realtime_semantic_segmentation_pytorch_amd.ops import PrunedConv2d
+
+    c = BaseConfig()
+    c.model, c.num_class = "lednet", 19
+    m = get_model(c)
+    assert not any(type(x) is torch.nn.Conv2d and max(x.kernel_size) > 1 for x in m.modules())
+    assert any(type(x) is PrunedConv2d and max(x.dilation) > 1 for x in m.modules())
+
+
 def test_dilated_group_conv_converted_in_regseg_cpu():
     from realtime_semantic_segmentation_pytorch_amd.configs import BaseConfig
     from realtime_semantic_segmentation_pytorch_amd.models import get_model

@@ -220,10 +220,79 @@ def test_syncbn_pooled_attention_and_context_embedding_two_ranks():
         for r in (0, 1):
             for n, g in grads.items():
                 # relative to the tensor's norm: the context-embedding BNs normalise over N = 4
-                # pooled values, so single elements carry fp32 summation-order noise
+                # pooled values, so single elements carry fp32 summation-order noise.  The pooled
+                # BN's bias feeds a 1x1 conv followed by a training-mode BN, which cancels any
+                # per-channel constant: its true gradient is 0 and both sides hold only rounding
+                # noise, hence the absolute floor.
                 a, b = got[r][kind]["grads"][n].double(), g.cpu().double()
-                err = ((a - b).norm() / (b.norm() + 1e-12)).item()
-                assert err < 2e-3, f"{kind}: grad {n} relative error {err:.2e}"
+                diff, ref = (a - b).norm().item(), b.norm().item()
+                assert diff < 2e-3 * ref + 1e-5 * b.numel() ** 0.5, \
+                    f"{kind}: grad {n} |diff| {diff:.3e} vs |ref| {ref:.3e}"
             for (rm, rv), (rm2, rv2) in zip(got[r][kind]["stats"], stats):
                 torch.testing.assert_close(rm, rm2, rtol=1e-3, atol=1e-4, msg=f"{kind}: running mean")
                 torch.testing.assert_close(rv, rv2, rtol=2e-3, atol=1e-4, msg=f"{kind}: running var")
+
+
+def _pooled_bn_worker(rank, world, port, out, fused):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    import torch.nn as nn
+
+    from realtime_semantic_segmentation_pytorch_amd.ops import convert_batchnorm
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pg = dist.new_group(ranks=list(range(world)))
+    torch.manual_seed(5)
+    bn = nn.BatchNorm2d(C)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+    bn = nn.SyncBatchNorm.convert_sync_batchnorm(bn, process_group=pg)
+    if fused:
+        bn = convert_batchnorm(nn.Sequential(bn))[0]
+    bn = bn.cuda().train()
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn(4, C, 1, 1, generator=g) * 2 + 0.3
+    gy = torch.randn(4, C, 1, 1, generator=g)
+    sl = slice(rank * 2, rank * 2 + 2)
+    xs = x[sl].cuda().contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    y = bn(xs)
+    y.backward(gy[sl].cuda().contiguous(memory_format=torch.channels_last))
+    gw, gb = bn.weight.grad.clone(), bn.bias.grad.clone()
+    dist.all_reduce(gw)
+    dist.all_reduce(gb)
+    torch.save({"y": y.detach().cpu(), "dx": xs.grad.cpu(), "gw": gw.cpu(), "gb": gb.cpu()},
+               os.path.join(out, f"pbn{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("fused", [False, True])
+def test_syncbn_on_pooled_vectors_two_ranks(fused):
+    """SyncBN over [N, C, 1, 1] (BiSeNetV2 context embedding): 2 ranks x 2 vectors == 1 process x
+    4 vectors, for torch's SyncBatchNorm (fused=False: the reference semantics) and ours."""
+    import tempfile
+
+    import torch.nn as nn
+
+    torch.manual_seed(5)
+    bn = nn.BatchNorm2d(C)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+    bn = bn.cuda().train()
+    g = torch.Generator().manual_seed(6)
+    x = (torch.randn(4, C, 1, 1, generator=g) * 2 + 0.3).cuda().requires_grad_(True)
+    gy = torch.randn(4, C, 1, 1, generator=g).cuda()
+    y = bn(x)
+    y.backward(gy)
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.spawn(_pooled_bn_worker, args=(2, _port(), tmp, fused), nprocs=2, join=True)
+        got = [torch.load(os.path.join(tmp, f"pbn{r}.pt"), weights_only=True) for r in (0, 1)]
+    torch.testing.assert_close(torch.cat([got[0]["y"], got[1]["y"]]), y.detach().cpu(), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(torch.cat([got[0]["dx"], got[1]["dx"]]), x.grad.cpu(), rtol=1e-3, atol=1e-4)
+    for r in (0, 1):
+        torch.testing.assert_close(got[r]["gw"], bn.weight.grad.cpu(), rtol=1e-3, atol=1e-4, msg="weight grad")
+        torch.testing.assert_close(got[r]["gb"], bn.bias.grad.cpu(), rtol=1e-3, atol=1e-4, msg="bias grad")

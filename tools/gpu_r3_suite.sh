@@ -4,7 +4,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/r3_suite
 export PYTHONUNBUFFERED=1
-timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread \
+timeout -k 10 1120 python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread \
   > gpurun_out/r3_suite/pytest_gpu.log 2>&1
 rc=$?
 grep -E "passed|failed|error" gpurun_out/r3_suite/pytest_gpu.log | tail -3

@@ -66,7 +66,6 @@ static void check_conv_plans() {
               for (int mode = 0; mode < 3; ++mode) {
                 if (!conv_igemm_supported(g, mode)) continue;
                 if (mode == 0) CHECK(conv_igemm_slabs(g) > 0, "fwd slabs n=%d cin=%d cout=%d", n, cin, cout);
-                if (mode == 1) CHECK(conv_igemm_dgrad_slabs(g) > 0, "dgrad slabs cin=%d cout=%d", cin, cout);
                 if (mode == 2) {
                   const int64_t ws = conv_igemm_wgrad_ws_elems(g);
                   CHECK(ws >= static_cast<int64_t>(cout) * cin * k * k, "wgrad ws %lld", static_cast<long long>(ws));
