@@ -80,6 +80,66 @@ __device__ __forceinline__ float half_wave_sum(float v) {
   return v;
 }
 
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+
+// One reduce-scatter butterfly step over lane pairs that differ in lane bit `hi`: of the pair
+// (a, b) a lane keeps a (hi clear) or b (hi set) and adds its partner's copy of the same entry.
+template <int CTRL>
+__device__ __forceinline__ float rs_step(float a, float b, bool hi) {
+  return (hi ? b : a) + dpp_mov<CTRL>(hi ? a : b);
+}
+
+// Sums of the BN-statistics epilogue: ts / tq [TI][16] per lane -> per-channel sums over the 32
+// pixel lanes of each half-wave, stored to one slab row (prow[co] = sum, prow[cout + co] = sum of
+// squares; lane channel of entry (ti, r): co_lane + ti * 32 + 8 * (r >> 2) + (r & 3)).
+// A reduce-scatter instead of 2 * TI * 16 independent 5-step all-reduces: v_permlane16_swap
+// (lane bit 4), then DPP row_ror:8 / row_half_mirror / quad_perm xor 2 / xor 1 (bits 3, 2, 1, 0),
+// halving the live entries at every step -- about 3 * 2 * TI * 16 VALU instead of 15 per entry.
+// Lane l ends with entries 32 k + bitrev5(l & 31) of the flat list [ts..., tq...].
+template <int TI>
+__device__ __forceinline__ void stats_reduce_store(const float (&ts)[TI][16], const float (&tq)[TI][16], float* prow,
+                                                   int co_lane, int cout, int lane) {
+  constexpr int V = 2 * TI * 16;
+  float x[V];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      x[i * 16 + r] = ts[i][r];
+      x[TI * 16 + i * 16 + r] = tq[i][r];
+    }
+  float y[V / 2];
+#pragma unroll
+  for (int k = 0; k < V / 2; ++k) {  // lane bit 4: rows 0 <-> 1 and 2 <-> 3
+    const auto sw = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, x[2 * k]),
+                                                     __builtin_bit_cast(unsigned, x[2 * k + 1]), false, false);
+    y[k] = __builtin_bit_cast(float, static_cast<unsigned>(sw[0])) + __builtin_bit_cast(float, static_cast<unsigned>(sw[1]));
+  }
+  const bool b3 = lane & 8, b2 = lane & 4, b1 = lane & 2, b0 = lane & 1;
+  float z[V / 4];
+#pragma unroll
+  for (int k = 0; k < V / 4; ++k) z[k] = rs_step<0x128>(y[2 * k], y[2 * k + 1], b3);  // row_ror:8
+  float u[V / 8];
+#pragma unroll
+  for (int k = 0; k < V / 8; ++k) u[k] = rs_step<0x141>(z[2 * k], z[2 * k + 1], b2);  // row_half_mirror
+  float w[V / 16];
+#pragma unroll
+  for (int k = 0; k < V / 16; ++k) w[k] = rs_step<0x4E>(u[2 * k], u[2 * k + 1], b1);  // quad_perm xor 2
+  const int j = static_cast<int>(__builtin_bitreverse32(static_cast<unsigned>(lane & 31)) >> 27);
+#pragma unroll
+  for (int k = 0; k < V / 32; ++k) {
+    const float v = rs_step<0xB1>(w[2 * k], w[2 * k + 1], b0);  // quad_perm xor 1
+    const int e = 32 * k + j;                 // flat entry: [ts (TI*16) | tq (TI*16)]
+    const int sq = e >= TI * 16, slot = sq ? e - TI * 16 : e;
+    const int r = slot & 15;
+    const int co = co_lane + (slot >> 4) * 32 + 8 * (r >> 2) + (r & 3);
+    if (co < cout) prow[(sq ? cout : 0) + co] = v;
+  }
+}
+
 // Bijective block -> logical id map that gives each XCD (blockIdx % 8 under round-robin
 // dispatch) a contiguous range of logical ids: neighbouring tiles share L2.  Speed only.
 __device__ __forceinline__ int xcd_logical(int b, int G) {

@@ -282,30 +282,10 @@ __global__ void __launch_bounds__(WM* WN * 64) halo_conv_kernel(const HaloArgs a
       }
     }
     if constexpr (STATS) {
-      // DPP over the 32 pixel lanes of each half-wave: lanes 31 / 63 hold the tile's sums for
-      // channels (r & 3) + 8 (r >> 2) + 4 * half; one slab row per (M tile, pixel wave)
-#pragma unroll
-      for (int ti = 0; ti < TI; ++ti)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          ts[ti][r] = half_wave_sum(ts[ti][r]);
-          tq[ti][r] = half_wave_sum(tq[ti][r]);
-        }
-      if (frow == 31) {
-        float* prow = a.part + (static_cast<int64_t>(mt) * WM + wm) * 2 * a.cout;
-#pragma unroll
-        for (int ti = 0; ti < TI; ++ti)
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int co = co_lane + ti * 32 + 8 * g;
-            if (co < a.cout) {
-              *reinterpret_cast<float4*>(prow + co) =
-                  make_float4(ts[ti][4 * g], ts[ti][4 * g + 1], ts[ti][4 * g + 2], ts[ti][4 * g + 3]);
-              *reinterpret_cast<float4*>(prow + a.cout + co) =
-                  make_float4(tq[ti][4 * g], tq[ti][4 * g + 1], tq[ti][4 * g + 2], tq[ti][4 * g + 3]);
-            }
-          }
-      }
+      // reduce-scatter over the 32 pixel lanes of each half-wave (rtseg_mfma_dev.h); one slab
+      // row per (M tile, pixel wave)
+      stats_reduce_store<TI>(ts, tq, a.part + (static_cast<int64_t>(mt) * WM + wm) * 2 * a.cout, co_lane, a.cout,
+                             lane);
     }
   };
 

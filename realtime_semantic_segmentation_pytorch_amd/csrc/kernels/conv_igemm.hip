@@ -79,6 +79,7 @@ struct IgArgs {
   int M, mtiles, ntiles;
   FastDiv fwv, fhv;
   uint32_t xbytes;        // bytes of the gathered operand (<= 2^31: buffer range, GB kernels)
+  uint32_t ybytes;        // bytes of the output (<= 2^31 for GB kernels: range-checked stores)
   int taps[kMaxTaps];     // packed tap: see pack_tap (32-bit so the scalar unit can load it)
 };
 
@@ -106,7 +107,10 @@ __device__ __forceinline__ void bdma16x2(__amdgpu_buffer_rsrc_t r, uint32_t v0, 
 
 // STATS: 0 = none, 1 = forward BN statistics of the output
 // GB: gather the activation rows through a buffer resource (range-checked voffsets, the
-// border handled by the range check) instead of 64-bit flat addresses with a zero source.
+// border handled by the range check) instead of 64-bit flat addresses with a zero source, and
+// store / load the output-layout tensors (y, residual, addend) through range-checked buffer
+// resources too: a pixel past M or a channel past Cout gets an out-of-range offset (the store is
+// dropped, the load returns 0) instead of an exec-mask branch around every 8-byte access.
 template <int BM, int BN, int WM, int WN, int NST, int EPI, int STATS, int GB>
 __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs a) {
   constexpr int NW = WM * WN;
@@ -243,8 +247,13 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
   // A finished tile is packed and stored at the start of the NEXT K-step, after its barrier and
   // before its DMA issue: the accumulators are the deferred buffer (no extra registers), and the
   // stores get a whole compute step to retire before any counted vmcnt waits behind them.
-  int64_t pend_off[TJ];
+  int64_t pend_off[GB ? 1 : TJ];
+  uint32_t poff[GB ? TJ : 1];  // GB: byte offset of the pixel's row in y, or out of range
   const int co_lane = co0 + wn * (BN / WN) + 4 * fhi;  // + ti*32 + 8g
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(a.y, 0, static_cast<int>(a.ybytes), 0x00020000);
+  const uint16_t* side = EPI == 1 ? a.res : a.addend;  // an output-layout tensor read in the epilogue
+  const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(side), 0, side != nullptr ? static_cast<int>(a.ybytes) : 0, 0x00020000);
 
   auto pack_tile = [&](int mt) __attribute__((always_inline)) {
     {
@@ -264,7 +273,13 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
         const uint32_t t = a.fwv.divmod(static_cast<uint32_t>(ok ? m : 0), wv);
         const uint32_t n = a.fhv.divmod(t, hv);
         const int ho = static_cast<int>(hv) * a.osh + a.oph, wo = static_cast<int>(wv) * a.osw + a.opw;
-        pend_off[tj] = ((static_cast<int64_t>(n) * a.Ho + ho) * a.Wo + wo) * a.cout;
+        if constexpr (GB) {
+          poff[tj] = ok ? ((n * static_cast<uint32_t>(a.Ho) + ho) * static_cast<uint32_t>(a.Wo) + wo) *
+                              static_cast<uint32_t>(a.cout) * 2u
+                        : 0x80000000u;
+        } else {
+          pend_off[tj] = ((static_cast<int64_t>(n) * a.Ho + ho) * a.Wo + wo) * a.cout;
+        }
         #pragma unroll
         for (int ti = 0; ti < TI; ++ti) {
           #pragma unroll
@@ -273,16 +288,27 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
             float v[4];
             #pragma unroll
             for (int q = 0; q < 4; ++q) v[q] = acc[ti][tj][4 * g + q];
-            if (a.bias != nullptr) {
-              const float4 bb = *reinterpret_cast<const float4*>(a.bias + min(co, a.cout - 4));
-              v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+            // GB: the byte offset of these 4 channels, out of range past M or Cout
+            uint32_t voff = 0;
+            if constexpr (GB) voff = co < a.cout ? poff[tj] + static_cast<uint32_t>(co) * 2u : 0x80000000u;
+            float sv[4] = {0.f, 0.f, 0.f, 0.f};  // residual (EPI 1) / addend (EPI 0) values
+            if (side != nullptr && (EPI == 1 || STATS == 0)) {
+              if constexpr (GB) {
+                const auto r = __builtin_amdgcn_raw_buffer_load_b64(sr, voff, 0, 0);
+                bf16x4_unpack(make_uint2(r[0], r[1]), sv);
+              } else if (ok && co < a.cout) {
+                bf16x4_unpack(*reinterpret_cast<const uint2*>(side + pend_off[tj] + co), sv);
+              }
             }
-            if (a.addend != nullptr && ok && co < a.cout) {  // e.g. a residual branch's gradient
-              const uint2 r = *reinterpret_cast<const uint2*>(a.addend + pend_off[tj] + co);
-              v[0] += bf16_to_f32(static_cast<uint16_t>(r.x & 0xffff));
-              v[1] += bf16_to_f32(static_cast<uint16_t>(r.x >> 16));
-              v[2] += bf16_to_f32(static_cast<uint16_t>(r.y & 0xffff));
-              v[3] += bf16_to_f32(static_cast<uint16_t>(r.y >> 16));
+            if constexpr (EPI == 0 && STATS == 0) {
+              if (a.bias != nullptr) {  // transposed conv
+                const float4 bb = *reinterpret_cast<const float4*>(a.bias + min(co, a.cout - 4));
+                v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+              }
+              if (side != nullptr) {  // e.g. a residual branch's gradient
+                #pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] += sv[q];
+              }
             }
             if constexpr (EPI == 1) {
               const int cc = min(co, a.cout - 4);
@@ -290,12 +316,9 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
               const float4 sf = *reinterpret_cast<const float4*>(a.ss + a.cout + cc);
               v[0] = fmaf(v[0], sc.x, sf.x); v[1] = fmaf(v[1], sc.y, sf.y);
               v[2] = fmaf(v[2], sc.z, sf.z); v[3] = fmaf(v[3], sc.w, sf.w);
-              if (a.res != nullptr && ok && co < a.cout) {
-                const uint2 r = *reinterpret_cast<const uint2*>(a.res + pend_off[tj] + co);
-                v[0] += bf16_to_f32(static_cast<uint16_t>(r.x & 0xffff));
-                v[1] += bf16_to_f32(static_cast<uint16_t>(r.x >> 16));
-                v[2] += bf16_to_f32(static_cast<uint16_t>(r.y & 0xffff));
-                v[3] += bf16_to_f32(static_cast<uint16_t>(r.y >> 16));
+              if (side != nullptr) {
+                #pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] += sv[q];
               }
               #pragma unroll
               for (int q = 0; q < 4; ++q) v[q] = epi_act(v[q], a.act);
@@ -303,7 +326,12 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
             uint2 pk;
             pk.x = pack2(v[0], v[1]);
             pk.y = pack2(v[2], v[3]);
-            if (ok && co < a.cout) *reinterpret_cast<uint2*>(a.y + pend_off[tj] + co) = pk;
+            if constexpr (GB) {
+              typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+              __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pk.x, pk.y}, yr, voff, 0, 0);
+            } else if (ok && co < a.cout) {
+              *reinterpret_cast<uint2*>(a.y + pend_off[tj] + co) = pk;
+            }
             if constexpr (STATS) {
               // statistics of the fp32 conv outputs, straight from the accumulators: STATS == 1
               // launches (training forward) carry no bias / addend, and rows past M or channels
@@ -321,31 +349,10 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
         }
       }
       if constexpr (STATS) {
-        // reduce over the 32 pixel lanes of each half-wave (DPP, full rate): lanes 31 / 63 end
-        // up with the tile's sums for channels (r & 3) + 8 (r >> 2) + 4 * half; one slab row per
-        // (M tile, pixel wave) -> every entry written once, deterministic, no atomics
-        #pragma unroll
-        for (int ti = 0; ti < TI; ++ti)
-          #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            ts[ti][r] = half_wave_sum(ts[ti][r]);
-            tq[ti][r] = half_wave_sum(tq[ti][r]);
-          }
-        if (frow == 31) {
-          float* prow = a.part + (static_cast<int64_t>(mt) * WM + wm) * 2 * a.cout;
-          #pragma unroll
-          for (int ti = 0; ti < TI; ++ti)
-            #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-              const int co = co_lane + ti * 32 + 8 * g;
-              if (co < a.cout) {
-                *reinterpret_cast<float4*>(prow + co) =
-                    make_float4(ts[ti][4 * g], ts[ti][4 * g + 1], ts[ti][4 * g + 2], ts[ti][4 * g + 3]);
-                *reinterpret_cast<float4*>(prow + a.cout + co) =
-                    make_float4(tq[ti][4 * g], tq[ti][4 * g + 1], tq[ti][4 * g + 2], tq[ti][4 * g + 3]);
-              }
-            }
-        }
+        // reduce over the 32 pixel lanes of each half-wave (reduce-scatter, rtseg_mfma_dev.h);
+        // one slab row per (M tile, pixel wave) -> every entry written once, deterministic
+        stats_reduce_store<TI>(ts, tq, a.part + (static_cast<int64_t>(mt) * WM + wm) * 2 * a.cout, co_lane,
+                               a.cout, lane);
       }
     }
   };
@@ -695,7 +702,7 @@ void launch_cfg(const IgArgs& k, const Cfg& c, int grid, hipStream_t st) {
 // forces the flat-address gather (A/B)
 bool use_buffer_gather(const IgArgs& k) {
   static const int mode = std::getenv("RTSEG_IGEMM_GATHER") ? std::atoi(std::getenv("RTSEG_IGEMM_GATHER")) : 1;
-  return mode != 0 && k.xbytes != 0 && k.xbytes <= 0x80000000u;
+  return mode != 0 && k.xbytes != 0 && k.xbytes <= 0x80000000u && k.ybytes != 0 && k.ybytes <= 0x80000000u;
 }
 
 template <int EPI, int STATS>
@@ -770,6 +777,8 @@ void launch_conv_igemm_fwd(const ConvGeom& g, hipStream_t st) {
   k.ntap = 0;
   const int64_t xb = static_cast<int64_t>(g.n) * g.h * g.w_in * g.cin * 2;
   k.xbytes = xb <= (int64_t{1} << 31) ? static_cast<uint32_t>(xb) : 0u;  // 0: flat gather
+  const int64_t yb = static_cast<int64_t>(g.n) * g.ho * g.wo * g.cout * 2;
+  k.ybytes = yb <= (int64_t{1} << 31) ? static_cast<uint32_t>(yb) : 0u;
   for (int i = 0; i < g.kh; ++i)
     for (int j = 0; j < g.kw; ++j) {
       k.taps[k.ntap++] = pack_tap(i * g.dh - g.ph, j * g.dw - g.pw, i * g.kw + j, i, j);
@@ -803,6 +812,8 @@ void launch_conv_igemm_dgrad(const ConvGeom& g, hipStream_t st) {
       k.ntap = 0;
       const int64_t xb = static_cast<int64_t>(g.n) * g.ho * g.wo * g.cout * 2;
       k.xbytes = xb <= (int64_t{1} << 31) ? static_cast<uint32_t>(xb) : 0u;  // 0: flat gather
+      const int64_t yb = static_cast<int64_t>(g.n) * g.h * g.w_in * g.cin * 2;
+      k.ybytes = yb <= (int64_t{1} << 31) ? static_cast<uint32_t>(yb) : 0u;
       for (int i = 0; i < g.kh; ++i) {
         const int vh = a + g.ph - i * g.dh;
         if (((vh % g.sh) + g.sh) % g.sh != 0) continue;
