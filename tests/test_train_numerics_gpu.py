@@ -66,14 +66,28 @@ def _cos(g, ref):
             for n in ref if ref[n].norm() > 1e-8}
 
 
-def test_ddrnet23_bf16_step_vs_fp32_reference(tmp_path, monkeypatch):
+# BASELINE configs 2-4: DDRNet-23 + aux, BiSeNetV2 + 4 aux heads, STDC2 + detail head (OHEM).
+# Per model: (trainer overrides, HIP-fp32 loss tolerance, HIP-fp32 median / 10th-percentile
+# gradient cosine floors).
+_STEP_MODELS = {
+    "ddrnet23_aux": ({}, 1e-4, 0.995, 0.99),
+    "bisenetv2_aux": ({"model": "bisenetv2", "arch_type": None}, 1e-3, 0.99, 0.95),
+    "stdc2_detail": ({"model": "stdc", "arch_type": None, "encoder_type": "stdc2", "use_aux": False,
+                      "use_detail_head": True}, 1e-3, 0.99, 0.95),
+}
+
+
+@pytest.mark.parametrize("name", sorted(_STEP_MODELS))
+def test_bf16_step_vs_fp32_reference(tmp_path, monkeypatch, name):
     """One training step's gradients against a stock-PyTorch fp32 reference.  At random init the
     BN-heavy backward amplifies rounding noise layer by layer (two stock bf16 runs with different
     reduction orders already disagree on a few layers), so the bf16 yardstick is the stock bf16
     path's own distance to fp32: the HIP bf16 path (MFMA convs, fused BN, residual-gradient
-    hand-off, OHEM, interp) must be at least as close.  The HIP fp32 path (our BN / loss / interp
-    kernels around MIOpen convs) must agree with the fp32 reference tightly."""
-    tr = _trainer(tmp_path)
+    hand-off, depth-wise convs, OHEM / detail loss, interp) must be at least as close.  The HIP
+    fp32 path (our BN / loss / interp kernels around MIOpen convs) must agree with the fp32
+    reference tightly."""
+    kw, loss_tol, cos_med, cos_p10 = _STEP_MODELS[name]
+    tr = _trainer(tmp_path, **kw)
     imgs, masks = _batch(tr)
     monkeypatch.setenv("RTSEG_DISABLE_HIP", "1")
     loss_ref, g_ref = _grads(tr, imgs, masks, amp=False)
@@ -86,14 +100,17 @@ def test_ddrnet23_bf16_step_vs_fp32_reference(tmp_path, monkeypatch):
     assert set(g_hb) == set(g_ref) == set(g_hf)
     for loss in (loss_sb, loss_hb):
         assert abs(loss - loss_ref) <= 2e-2 * abs(loss_ref), (loss, loss_ref)
-    assert abs(loss_hf - loss_ref) <= 1e-4 * abs(loss_ref), (loss_hf, loss_ref)
+    assert abs(loss_hf - loss_ref) <= loss_tol * abs(loss_ref), (loss_hf, loss_ref)
     c_sb, c_hb, c_hf = (sorted(_cos(g, g_ref).values()) for g in (g_sb, g_hb, g_hf))
     med = len(c_sb) // 2
+    print(f"{name}: cos median stock-bf16 {c_sb[med]:.4f} hip-bf16 {c_hb[med]:.4f} hip-fp32 {c_hf[med]:.4f}; "
+          f"p10 hip-fp32 {c_hf[len(c_hf) // 10]:.4f}; <0.9: stock {sum(c < 0.9 for c in c_sb)} "
+          f"hip {sum(c < 0.9 for c in c_hb)} of {len(c_hb)}")
     assert c_hb[med] >= c_sb[med] - 5e-3, (c_hb[med], c_sb[med])
-    assert sum(c < 0.9 for c in c_hb) <= sum(c < 0.9 for c in c_sb) + len(c_hb) // 50
-    # measured on MI355X: median 0.9986, 10th percentile 0.9978 (fp32 reduction-order noise through
-    # ~70 BN backward passes at random init)
-    assert c_hf[med] > 0.995 and c_hf[len(c_hf) // 10] > 0.99, (c_hf[med], c_hf[len(c_hf) // 10])
+    assert sum(c < 0.9 for c in c_hb) <= sum(c < 0.9 for c in c_sb) + max(1, len(c_hb) // 50)
+    # DDRNet-23 measured on MI355X: median 0.9986, 10th percentile 0.9978 (fp32 reduction-order
+    # noise through ~70 BN backward passes at random init)
+    assert c_hf[med] > cos_med and c_hf[len(c_hf) // 10] > cos_p10, (c_hf[med], c_hf[len(c_hf) // 10])
 
 
 def test_ddrnet23_overfits_one_batch_with_hip_kernels(tmp_path):
