@@ -99,9 +99,11 @@ __device__ __forceinline__ float rs_step(float a, float b, bool hi) {
 // (lane bit 4), then DPP row_ror:8 / row_half_mirror / quad_perm xor 2 / xor 1 (bits 3, 2, 1, 0),
 // halving the live entries at every step -- about 3 * 2 * TI * 16 VALU instead of 15 per entry.
 // Lane l ends with entries 32 k + bitrev5(l & 31) of the flat list [ts..., tq...].
+// Stage 1 of the reduce-scatter (lane bit 4, v_permlane16_swap): the 2 * TI * 16 entries of
+// [ts..., tq...] -> TI * 16 half-reduced values.  Linear, so stage-1 outputs of several tiles may
+// be summed before stage 2 (the conv kernels keep that sum in registers across their tiles).
 template <int TI>
-__device__ __forceinline__ void stats_reduce_store(const float (&ts)[TI][16], const float (&tq)[TI][16], float* prow,
-                                                   int co_lane, int cout, int lane) {
+__device__ __forceinline__ void stats_stage1(const float (&ts)[TI][16], const float (&tq)[TI][16], float (&y)[TI * 16]) {
   constexpr int V = 2 * TI * 16;
   float x[V];
 #pragma unroll
@@ -111,13 +113,31 @@ __device__ __forceinline__ void stats_reduce_store(const float (&ts)[TI][16], co
       x[i * 16 + r] = ts[i][r];
       x[TI * 16 + i * 16 + r] = tq[i][r];
     }
-  float y[V / 2];
 #pragma unroll
   for (int k = 0; k < V / 2; ++k) {  // lane bit 4: rows 0 <-> 1 and 2 <-> 3
     const auto sw = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, x[2 * k]),
                                                      __builtin_bit_cast(unsigned, x[2 * k + 1]), false, false);
     y[k] = __builtin_bit_cast(float, static_cast<unsigned>(sw[0])) + __builtin_bit_cast(float, static_cast<unsigned>(sw[1]));
   }
+}
+
+// Which entry value k (0 <= k < 2 * TI * 16 / 32) of stats_stage2 a lane ends with: sq (0 = sum,
+// 1 = sum of squares) and the channel offset from co_lane (ti * 32 + 8 * (r >> 2) + (r & 3)).
+template <int TI>
+__device__ __forceinline__ void stats_slot(int k, int lane, int& sq, int& dc) {
+  const int j = static_cast<int>(__builtin_bitreverse32(static_cast<unsigned>(lane & 31)) >> 27);
+  const int e = 32 * k + j;  // flat entry: [ts (TI*16) | tq (TI*16)]
+  sq = e >= TI * 16;
+  const int slot = sq ? e - TI * 16 : e;
+  const int r = slot & 15;
+  dc = (slot >> 4) * 32 + 8 * (r >> 2) + (r & 3);
+}
+
+// Stage 2 (lane bits 3..0, DPP) and the scatter: put(k, sq, dc, value) for the lane's entries
+// k = 0 .. 2 * TI * 16 / 32 - 1 (stats_slot gives sq / dc).
+template <int TI, class Put>
+__device__ __forceinline__ void stats_stage2(const float (&y)[TI * 16], int lane, Put put) {
+  constexpr int V = 2 * TI * 16;
   const bool b3 = lane & 8, b2 = lane & 4, b1 = lane & 2, b0 = lane & 1;
   float z[V / 4];
 #pragma unroll
@@ -128,16 +148,24 @@ __device__ __forceinline__ void stats_reduce_store(const float (&ts)[TI][16], co
   float w[V / 16];
 #pragma unroll
   for (int k = 0; k < V / 16; ++k) w[k] = rs_step<0x4E>(u[2 * k], u[2 * k + 1], b1);  // quad_perm xor 2
-  const int j = static_cast<int>(__builtin_bitreverse32(static_cast<unsigned>(lane & 31)) >> 27);
 #pragma unroll
   for (int k = 0; k < V / 32; ++k) {
     const float v = rs_step<0xB1>(w[2 * k], w[2 * k + 1], b0);  // quad_perm xor 1
-    const int e = 32 * k + j;                 // flat entry: [ts (TI*16) | tq (TI*16)]
-    const int sq = e >= TI * 16, slot = sq ? e - TI * 16 : e;
-    const int r = slot & 15;
-    const int co = co_lane + (slot >> 4) * 32 + 8 * (r >> 2) + (r & 3);
-    if (co < cout) prow[(sq ? cout : 0) + co] = v;
+    int sq, dc;
+    stats_slot<TI>(k, lane, sq, dc);
+    put(k, sq, dc, v);
   }
+}
+
+template <int TI>
+__device__ __forceinline__ void stats_reduce_store(const float (&ts)[TI][16], const float (&tq)[TI][16], float* prow,
+                                                   int co_lane, int cout, int lane) {
+  float y[TI * 16];
+  stats_stage1<TI>(ts, tq, y);
+  stats_stage2<TI>(y, lane, [&](int, int sq, int dc, float v) {
+    const int co = co_lane + dc;
+    if (co < cout) prow[(sq ? cout : 0) + co] = v;
+  });
 }
 
 // Bijective block -> logical id map that gives each XCD (blockIdx % 8 under round-robin

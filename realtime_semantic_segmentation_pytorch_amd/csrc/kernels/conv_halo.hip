@@ -213,6 +213,11 @@ __global__ void __launch_bounds__(WM* WN * 64) halo_conv_kernel(const HaloArgs a
 
   int64_t pend_off[TJ];
   const int co_lane = co0 + wn * (BN / WN) + 4 * fhi;  // + ti*32 + 8g
+  // STATS: the lane's first-stage-reduced BN statistics summed over the block's tiles (they
+  // share the channel tile); the rest of the reduction runs once, at the end (as conv_igemm)
+  float pst[STATS ? TI * 16 : 1];
+#pragma unroll
+  for (int k = 0; k < (STATS ? TI * 16 : 1); ++k) pst[k] = 0.f;
 
   auto pack_tile = [&](int mt) __attribute__((always_inline)) {
     int n, oy0, ox0;
@@ -282,10 +287,10 @@ __global__ void __launch_bounds__(WM* WN * 64) halo_conv_kernel(const HaloArgs a
       }
     }
     if constexpr (STATS) {
-      // reduce-scatter over the 32 pixel lanes of each half-wave (rtseg_mfma_dev.h); one slab
-      // row per (M tile, pixel wave)
-      stats_reduce_store<TI>(ts, tq, a.part + (static_cast<int64_t>(mt) * WM + wm) * 2 * a.cout, co_lane, a.cout,
-                             lane);
+      float y1[TI * 16];
+      stats_stage1<TI>(ts, tq, y1);
+#pragma unroll
+      for (int k = 0; k < TI * 16; ++k) pst[k] += y1[k];
     }
   };
 
@@ -372,6 +377,23 @@ __global__ void __launch_bounds__(WM* WN * 64) halo_conv_kernel(const HaloArgs a
     }
   }
   if (pend_mt >= 0) pack_tile(pend_mt);
+
+  if constexpr (STATS) {
+    // one slab row per block: DPP stages per wave, the WM pixel waves summed in a fixed order
+    // through LDS (deterministic; every block has >= 1 tile, so no early return skips this)
+    __syncthreads();  // every wave is past its last fragment read; no DMA is in flight
+    float* red = reinterpret_cast<float*>(lds);  // [WM][2][BN]
+    const int cl = wn * (BN / WN) + 4 * fhi;
+    stats_stage2<TI>(pst, lane, [&](int, int sq, int dc, float v) { red[(wm * 2 + sq) * BN + cl + dc] = v; });
+    __syncthreads();
+    for (int e = tid; e < 2 * BN; e += NW * 64) {
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) s += red[w * 2 * BN + e];
+      const int sq = e >= BN, c = co0 + (sq ? e - BN : e);
+      if (c < a.cout) a.part[static_cast<int64_t>(mfirst) * 2 * a.cout + (sq ? a.cout : 0) + c] = s;
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------- host side
@@ -488,7 +510,10 @@ int conv_halo_slabs(const ConvGeom& g) {
   k.Ho = g.ho; k.Wo = g.wo; k.cout = g.cout;
   if (!fwd_taps(g, k)) return 0;
   fill_tiles(k, g.n);
-  return k.mtiles * halo_cfg(k.cout, k.ntap).wm;
+  // one row per block of a channel tile (see the end of halo_conv_kernel)
+  const int64_t tiles = static_cast<int64_t>(k.mtiles) * k.ntiles;
+  const int cap = std::max(k.ntiles, (256 / k.ntiles) * k.ntiles);
+  return static_cast<int>(tiles < cap ? tiles : cap) / k.ntiles;
 }
 
 void launch_conv_halo_fwd(const ConvGeom& g, hipStream_t st) {

@@ -254,6 +254,15 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
   const uint16_t* side = EPI == 1 ? a.res : a.addend;  // an output-layout tensor read in the epilogue
   const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint16_t*>(side), 0, side != nullptr ? static_cast<int>(a.ybytes) : 0, 0x00020000);
+  // STATS: this lane's BN statistics summed over all of the block's tiles (they share the channel
+  // tile).  SP1: kept after the first reduce-scatter stage (TI * 16 registers; per tile only the
+  // cheap stage 1), else -- the 512 x 128 tiles, which would spill -- after the whole per-tile
+  // reduction (2 * TI * 16 / 32 registers)
+  constexpr bool SP1 = BM * BN < 512 * 128;
+  constexpr int NPS = !STATS ? 1 : SP1 ? TI * 16 : TI;
+  float pst[NPS];
+#pragma unroll
+  for (int k = 0; k < NPS; ++k) pst[k] = 0.f;
 
   auto pack_tile = [&](int mt) __attribute__((always_inline)) {
     {
@@ -349,10 +358,16 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
         }
       }
       if constexpr (STATS) {
-        // reduce over the 32 pixel lanes of each half-wave (reduce-scatter, rtseg_mfma_dev.h);
-        // one slab row per (M tile, pixel wave) -> every entry written once, deterministic
-        stats_reduce_store<TI>(ts, tq, a.part + (static_cast<int64_t>(mt) * WM + wm) * 2 * a.cout, co_lane,
-                               a.cout, lane);
+        // first reduce-scatter stage only (rtseg_mfma_dev.h), summed over the block's tiles (all
+        // of them share the channel tile); the rest of the reduction runs once, at the end
+        float y1[TI * 16];
+        stats_stage1<TI>(ts, tq, y1);
+        if constexpr (SP1) {
+#pragma unroll
+          for (int k = 0; k < TI * 16; ++k) pst[k] += y1[k];
+        } else {
+          stats_stage2<TI>(y1, lane, [&](int k, int, int, float v) { pst[k] += v; });
+        }
       }
     }
   };
@@ -421,6 +436,32 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
     if (pend_mt >= 0) pack_tile(pend_mt);
   }
 
+  if constexpr (STATS) {
+    // finish the reduction once per block: DPP stages per wave, then the WM pixel waves of each
+    // channel range summed in a fixed order through LDS -> ONE slab row per block (row = the
+    // block's M-walk start, every (row, channel) written exactly once: deterministic, <= 256 rows)
+    __syncthreads();  // every wave is past its last fragment read; no DMA is in flight
+    float* red = reinterpret_cast<float*>(lds);  // [WM][2][BN]
+    const int cl = wn * (BN / WN) + 4 * fhi;
+    if constexpr (SP1) {
+      stats_stage2<TI>(pst, lane, [&](int, int sq, int dc, float v) { red[(wm * 2 + sq) * BN + cl + dc] = v; });
+    } else {
+#pragma unroll
+      for (int k = 0; k < NPS; ++k) {
+        int sq, dc;
+        stats_slot<TI>(k, lane, sq, dc);
+        red[(wm * 2 + sq) * BN + cl + dc] = pst[k];
+      }
+    }
+    __syncthreads();
+    for (int e = tid; e < 2 * BN; e += NW * 64) {
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) s += red[w * 2 * BN + e];
+      const int sq = e >= BN, c = co0 + (sq ? e - BN : e);
+      if (c < a.cout) a.part[static_cast<int64_t>(mfirst) * 2 * a.cout + (sq ? a.cout : 0) + c] = s;
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------- wgrad
@@ -743,10 +784,13 @@ bool conv_igemm_supported(const ConvGeom& g, int mode) {
   return true;
 }
 
+// BN-statistics slab rows of a forward launch: one per block of a channel tile (the blocks of a
+// persistent grid that walk the same channel tile), see the end of igemm_gather_kernel
 int conv_igemm_slabs(const ConvGeom& g) {
   const int64_t M = static_cast<int64_t>(g.n) * g.ho * g.wo;
   const Cfg c = pick_cfg(g.cout, M);
-  return static_cast<int>((M + c.bm - 1) / c.bm) * c.wm;
+  const int mtiles = static_cast<int>((M + c.bm - 1) / c.bm), ntiles = (g.cout + c.bn - 1) / c.bn;
+  return persistent_grid(mtiles, ntiles) / ntiles;
 }
 
 // the BN-backward epilogue does not fit the registers of the 64 x 128 wave tiles (it spills):

@@ -19,6 +19,12 @@ GEOMS = [
     (3, 64, 8, 64, 320, 3, 3, 1, 1),
     (1, 64, 10, 69, 128, 3, 3, 0, 0),
 ]
+# several tiles per block of the persistent grid (BN statistics summed per block before its one
+# slab row is written): 64- and 128-channel configs, a partial last tile row
+BIG_GEOMS = [
+    (8, 64, 130, 256, 64, 3, 3, 1, 1),
+    (8, 128, 66, 256, 128, 3, 3, 1, 1),
+]
 
 
 @pytest.fixture(autouse=True)
@@ -37,7 +43,7 @@ def _close(got, ref, tol):
     torch.testing.assert_close(got.float(), ref, atol=tol * ref.abs().max().item() + 1e-6, rtol=tol)
 
 
-@pytest.mark.parametrize("geom", GEOMS)
+@pytest.mark.parametrize("geom", GEOMS + BIG_GEOMS)
 def test_halo_forward_and_stats(geom):
     n, cin, h, w, cout, kh, kw, ph, pw = geom
     x, wt = _case(n, cin, h, w, cout, kh, kw)
@@ -49,6 +55,9 @@ def test_halo_forward_and_stats(geom):
     rf = ref.double()  # the slab holds the statistics of the fp32 outputs (the accumulators)
     torch.testing.assert_close(part[:, :cout].double().sum(0), rf.sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
     torch.testing.assert_close(part[:, cout:].double().sum(0), rf.square().sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+    assert part.shape[0] <= 256
+    _, p1 = torch.ops.rtseg.conv_halo(x, wk, [1, 1], [ph, pw], [1, 1], True, None, None, 0)
+    assert torch.equal(p1, part)  # deterministic
     y2, p2 = torch.ops.rtseg.conv_halo(x, wk, [1, 1], [ph, pw], [1, 1], False, None, None, 0)
     assert p2 is None or p2.numel() == 0
     torch.testing.assert_close(y2, y, rtol=0, atol=0)

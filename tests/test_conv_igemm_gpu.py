@@ -21,6 +21,14 @@ GEOMS = [
     (2, 128, 15, 21, 128, 1, 2, 1),
     (1, 192, 11, 13, 320, 3, 2, 1),
 ]
+# big enough that the persistent grid walks several M tiles per block (the BN statistics are
+# summed over a block's tiles before the one slab row per block is written), per tile config
+BIG_GEOMS = [
+    (8, 64, 128, 256, 64, 3, 1, 1),    # 512 x 64 tiles
+    (16, 128, 128, 128, 128, 3, 1, 1),  # 512 x 128
+    (16, 256, 64, 128, 256, 3, 1, 1),   # 256 x 256
+    (8, 64, 96, 128, 200, 3, 1, 1),     # 256 x 256, partial channel tile
+]
 
 
 @pytest.fixture(autouse=True)
@@ -39,7 +47,7 @@ def _close(got, ref, tol):
     torch.testing.assert_close(got.float(), ref, atol=tol * ref.abs().max().item() + 1e-6, rtol=tol)
 
 
-@pytest.mark.parametrize("geom", GEOMS)
+@pytest.mark.parametrize("geom", GEOMS + BIG_GEOMS)
 def test_igemm_forward_and_stats(geom):
     n, cin, h, w, cout, k, s, d = geom
     x, wt = _case(*geom)
@@ -51,8 +59,13 @@ def test_igemm_forward_and_stats(geom):
     _close(y, ref, 2e-2)
     # the slab holds the statistics of the fp32 conv outputs (the kernel's accumulators)
     rf = ref.double()
+    assert part.shape[0] <= 256 and part.shape[1] == 2 * cout
     torch.testing.assert_close(part[:, :cout].double().sum(0), rf.sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
     torch.testing.assert_close(part[:, cout:].double().sum(0), rf.square().sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+    # deterministic: a second launch gives the same bits
+    _, part2 = torch.ops.rtseg.conv_igemm(x, wt.permute(0, 2, 3, 1).contiguous(), [s, s], [p, p], [d, d], True,
+                                          None, None, 0)
+    assert torch.equal(part, part2)
 
 
 @pytest.mark.parametrize("act", [0, 1, 2])
