@@ -299,12 +299,57 @@ __device__ __forceinline__ void apply_one(const T* __restrict__ x, const T* __re
   if constexpr (BITS) bits[i] = static_cast<uint8_t>(b);  // vector i = byte i (off / V)
 }
 
+// Channel-stationary form (the channel-vector count cv divides the 256-thread block, i.e. C / V
+// is a power of two <= 256, every DDRNet / ResNet width): the grid stride is a whole number of
+// rows, so a thread keeps ONE channel vector for all its rows -- its per-channel coefficients
+// live in registers (no per-element LDS reads: with 32 or 64 distinct channel vectors per wave
+// those were 4-8-way bank-conflicted) and the row index advances by a constant (no 64-bit
+// division per vector).
+template <typename T, int V, int ACT, bool RES, bool BITS>
+__device__ __forceinline__ void apply_rows(const T* __restrict__ x, const T* __restrict__ res,
+                                           const float* __restrict__ scale_shift, T* __restrict__ y,
+                                           int64_t M, int C, uint8_t* __restrict__ bits) {
+  const int cv = C / V;
+  const int cvi = threadIdx.x % cv;
+  const int c0 = cvi * V;
+  float sc[V], sh[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) { sc[j] = scale_shift[c0 + j]; sh[j] = scale_shift[C + c0 + j]; }
+  const int64_t rstep = static_cast<int64_t>(gridDim.x) * (blockDim.x / cv);
+  auto one = [&](int64_t row) {
+    const int64_t off = row * C + c0;
+    float f[V], r[V];
+    VecIO<T, V>::load(x + off, f);
+    if constexpr (RES) VecIO<T, V>::load(res + off, r);
+    uint32_t b = 0;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      float z = fmaf(f[j], sc[j], sh[j]);
+      if constexpr (RES) z += r[j];
+      f[j] = act_fwd<ACT>(z);
+      if constexpr (BITS) b |= (act_grad_pre<ACT>(1.f, z) != 0.f ? 1u : 0u) << j;
+    }
+    VecIO<T, V>::store(y + off, f);
+    if constexpr (BITS) bits[row * cv + cvi] = static_cast<uint8_t>(b);
+  };
+  int64_t row = static_cast<int64_t>(blockIdx.x) * (blockDim.x / cv) + threadIdx.x / cv;
+  for (; row + rstep < M; row += 2 * rstep) {  // two rows in flight per thread
+    one(row);
+    one(row + rstep);
+  }
+  if (row < M) one(row);
+}
+
 template <typename T, int V, int ACT, bool RES, bool BITS = false>
 __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x,
                                                        const T* __restrict__ res,
                                                        const float* __restrict__ scale_shift,
                                                        T* __restrict__ y, int64_t M, int C,
                                                        uint8_t* __restrict__ bits = nullptr) {
+  if (blockDim.x % (C / V) == 0) {  // block-uniform
+    apply_rows<T, V, ACT, RES, BITS>(x, res, scale_shift, y, M, C, bits);
+    return;
+  }
   extern __shared__ __attribute__((aligned(16))) float coef[];  // [2][C]
   for (int c = threadIdx.x; c < 2 * C; c += blockDim.x) coef[c] = scale_shift[c];
   __syncthreads();
@@ -365,17 +410,20 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
 #pragma unroll
     for (int j = 0; j < V; ++j) m[j] = mu[c0 + j];
     int64_t r = r0 + g.my_r;
-    for (; r + g.rpi < r1; r += 2 * g.rpi) {  // two rows (4-6 loads) in flight
-      float ga[V], xa[V], gb[V], xb[V];
+    for (; r + 3 * g.rpi < r1; r += 4 * g.rpi) {  // four rows (8-12 loads) in flight
+      float ga[V], xa[V], gb[V], xb[V], gc[V], xc[V], gd[V], xd[V];
       load_g<T, V, ACT, MASK>(dy, x, y, coef, C, r * C + c0, c0, ga, xa);
       load_g<T, V, ACT, MASK>(dy, x, y, coef, C, (r + g.rpi) * C + c0, c0, gb, xb);
+      load_g<T, V, ACT, MASK>(dy, x, y, coef, C, (r + 2 * g.rpi) * C + c0, c0, gc, xc);
+      load_g<T, V, ACT, MASK>(dy, x, y, coef, C, (r + 3 * g.rpi) * C + c0, c0, gd, xd);
 #pragma unroll
       for (int j = 0; j < V; ++j) {
-        s[j] += ga[j] + gb[j];
-        q[j] += ga[j] * (xa[j] - m[j]) + gb[j] * (xb[j] - m[j]);
+        s[j] += (ga[j] + gb[j]) + (gc[j] + gd[j]);
+        q[j] += (ga[j] * (xa[j] - m[j]) + gb[j] * (xb[j] - m[j])) +
+                (gc[j] * (xc[j] - m[j]) + gd[j] * (xd[j] - m[j]));
       }
     }
-    if (r < r1) {
+    for (; r < r1; r += g.rpi) {
       float ga[V], xa[V];
       load_g<T, V, ACT, MASK>(dy, x, y, coef, C, r * C + c0, c0, ga, xa);
 #pragma unroll
@@ -437,11 +485,68 @@ __device__ __forceinline__ void bwd_apply_one(const T* dy, const T* x, const T* 
   VecIO<T, V>::store(dx + off, o);
 }
 
+// Channel-stationary backward apply (see apply_rows): dx = A*g + B*x + D per channel, with
+// A = k0, B = -k0*k2, D = k0*(k2*mean - k1) folded once per thread into registers.
+template <typename T, int V, int ACT, int MASK, bool DRES>
+__device__ __forceinline__ void bwd_apply_rows(const T* __restrict__ dy, const T* __restrict__ x,
+                                               const T* __restrict__ y, const float* __restrict__ mean_invstd,
+                                               const float* __restrict__ scale_shift,
+                                               const float* __restrict__ kcoef, T* __restrict__ dx,
+                                               T* __restrict__ dres, int64_t M, int C) {
+  const int cv = C / V;
+  const int c0 = (threadIdx.x % cv) * V;
+  float cf[2 * V], A[V], B[V], D[V];  // cf: scale | shift (pre-activation mask)
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    const int c = c0 + j;
+    const float k0 = kcoef[c], k1 = kcoef[C + c], k2 = kcoef[2 * C + c], mu = mean_invstd[c];
+    A[j] = k0;
+    B[j] = -k0 * k2;
+    D[j] = k0 * fmaf(k2, mu, -k1);
+    cf[j] = scale_shift[c];
+    cf[V + j] = scale_shift[C + c];
+  }
+  const int64_t rstep = static_cast<int64_t>(gridDim.x) * (blockDim.x / cv);
+  auto one = [&](int64_t row) {
+    const int64_t off = row * C + c0;
+    float g[V], xv[V], o[V];
+    VecIO<T, V>::load(dy + off, g);
+    VecIO<T, V>::load(x + off, xv);
+    if constexpr (MASK == kMaskFromY) {
+      float yv[V];
+      VecIO<T, V>::load(y + off, yv);
+#pragma unroll
+      for (int j = 0; j < V; ++j) g[j] = act_bwd_from_out<ACT>(g[j], yv[j]);
+    } else if constexpr (MASK == kMaskFromX) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) g[j] = act_grad_pre<ACT>(g[j], fmaf(xv[j], cf[j], cf[V + j]));
+    } else if constexpr (MASK == kMaskBits) {
+      const uint32_t b = reinterpret_cast<const uint8_t*>(y)[off / V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) g[j] = ((b >> j) & 1u) ? g[j] : 0.f;
+    }
+    if constexpr (DRES) VecIO<T, V>::store(dres + off, g);
+#pragma unroll
+    for (int j = 0; j < V; ++j) o[j] = fmaf(A[j], g[j], fmaf(B[j], xv[j], D[j]));
+    VecIO<T, V>::store(dx + off, o);
+  };
+  int64_t row = static_cast<int64_t>(blockIdx.x) * (blockDim.x / cv) + threadIdx.x / cv;
+  for (; row + rstep < M; row += 2 * rstep) {
+    one(row);
+    one(row + rstep);
+  }
+  if (row < M) one(row);
+}
+
 template <typename T, int V, int ACT, int MASK, bool DRES>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
     const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y,
     const float* __restrict__ mean_invstd, const float* __restrict__ scale_shift,
     const float* __restrict__ kcoef, T* __restrict__ dx, T* __restrict__ dres, int64_t M, int C) {
+  if (blockDim.x % (C / V) == 0) {  // block-uniform
+    bwd_apply_rows<T, V, ACT, MASK, DRES>(dy, x, y, mean_invstd, scale_shift, kcoef, dx, dres, M, C);
+    return;
+  }
   extern __shared__ __attribute__((aligned(16))) float sm[];  // coef[2C] | mu[C] | k[3C]
   float* coef = sm;
   float* mu = sm + 2 * C;
@@ -475,7 +580,9 @@ int bn_partial_grid(int64_t M, int C, int dtype) {
   const int V = bn_vec_width(dtype, C);
   const int rpi = 256 / (C / V);
   int64_t g = (M + static_cast<int64_t>(rpi) * 32 - 1) / (static_cast<int64_t>(rpi) * 32);
-  if (g > 512) g = 512;
+  // 4 blocks (16 waves) per CU: with 4 rows (8 x 16-B loads) in flight per lane that keeps
+  // ~64 KiB of reads outstanding per CU, what HBM3E latency x bandwidth needs
+  if (g > 1024) g = 1024;
   if (g < 1) g = 1;
   return static_cast<int>(g);
 }
