@@ -67,8 +67,9 @@ def get_model(config):
     """Build the configured model; every BatchNorm2d, depth-wise conv and pooling
     module is routed through the HIP kernels (``ops.convert_batchnorm`` /
     ``ops.convert_depthwise`` / ``ops.convert_pooling``; module classes only --
-    parameters and checkpoint keys are unchanged), and every other spatial conv drops the
-    taps that only read padding at the current input size (``ops.convert_pruned_convs``)."""
+    parameters and checkpoint keys are unchanged), every other spatial conv drops the
+    taps that only read padding at the current input size (``ops.convert_pruned_convs``), and
+    plain dense bias-free convs join the autotuned MFMA conv family (``ops.convert_routed_convs``)."""
     from .. import ops
 
     model = ops.convert_batchnorm(_build_model(config))
@@ -83,6 +84,8 @@ def get_model(config):
     if getattr(config, "hip_deconv", True):
         ops.convert_transposed_convs(model)
     ops.convert_pruned_convs(model)  # last: every remaining plain spatial conv
+    if getattr(config, "routed_convs", True):
+        ops.convert_routed_convs(model)  # plain dense bias-free convs -> the MFMA conv family
     if getattr(config, "hip_activations", True):
         ops.convert_activations(model)
     ops.convert_pixel_shuffle(model)

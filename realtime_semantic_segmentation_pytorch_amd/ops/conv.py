@@ -483,6 +483,41 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Module, bn: nn.Module, act="none", res
     return bn_act(conv_forward(x, conv), bn, act, residual=residual, act_module=act_module)
 
 
+class RoutedConv2d(PrunedConv2d):
+    """A dense, bias-free ``nn.Conv2d`` that a model calls as a plain module (not through a
+    ConvBNAct tail: e.g. ERFNet's last factorised conv, STDC's ``conv4`` / ``conv5``, decoder
+    projections).  In bf16 training its three passes go through :class:`_ConvFn` -- each pass
+    timed against MIOpen per shape like every other routed conv -- and in bf16 inference it
+    reuses the cached bf16 weight (:func:`conv_forward`); anything else is the stock forward
+    (dead taps dropped, :class:`PrunedConv2d`).  Same parameters and state-dict keys."""
+
+    def forward(self, x):
+        if (x.is_cuda and self.in_channels % 32 == 0 and self.out_channels % 8 == 0 and torch.is_grad_enabled()
+                and self.weight.requires_grad and conv_ok(x, self)):
+            return _ConvFn.apply(x.to(torch.bfloat16), self.weight, self, False)[0]
+        if (x.is_cuda and not self.training and not torch.is_grad_enabled() and torch.is_autocast_enabled("cuda")
+                and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+            return conv_forward(x, self)  # its cached-weight branch (never falls through to self(x))
+        return super().forward(x)
+
+
+def routable(conv: nn.Module) -> bool:
+    return (type(conv) in (nn.Conv2d, PrunedConv2d) and conv.groups == 1 and conv.bias is None
+            and conv.padding_mode == "zeros" and not isinstance(conv.padding, str))
+
+
+def convert_routed_convs(model: nn.Module) -> nn.Module:
+    """Swap every remaining plain dense bias-free conv to :class:`RoutedConv2d` (in place, run
+    after the other converters; parameters and checkpoint keys unchanged)."""
+    for m in model.modules():
+        if routable(m):
+            m.__class__ = RoutedConv2d
+    return model
+
+
+_ROUTED = (nn.Conv2d, PrunedConv2d, RoutedConv2d)
+
+
 def decisions() -> dict:
     """Per-shape kernel choices so far: key -> (index, name, [ms per candidate])."""
     return dict(_DECISIONS)

@@ -1,0 +1,75 @@
+"""Plain dense convs a model calls directly (``ops.RoutedConv2d``, ``ops.convert_routed_convs``):
+bf16 training forward + backward through the routed conv node vs an fp32 PyTorch conv of the same
+bf16-rounded operands, and bf16 inference through the cached bf16 weight.
+
+Reference sites: ERFNet's non-bottleneck-1D tail conv (reference models/erfnet.py), STDC's
+``conv4`` / ``conv5`` (reference models/stdc.py:13-101) -- ``nn.Conv2d`` modules outside any
+ConvBNAct."""
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from realtime_semantic_segmentation_pytorch_amd import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+# (n, cin, h, w, cout, kernel, stride, padding, dilation)
+GEOMS = [
+    (2, 64, 24, 40, 64, (1, 3), 1, (0, 2), (1, 2)),    # ERFNet factorised, dilated
+    (2, 128, 16, 32, 128, (3, 1), 1, (4, 0), (4, 1)),
+    (2, 512, 8, 16, 256, 1, 1, 0, 1),                  # STDC conv4
+    (1, 64, 33, 17, 128, 3, 2, 1, 1),
+    (2, 96, 20, 20, 64, 3, 1, 1, 1),                   # Cin % 64 != 0: the 16x16x32 family
+]
+
+
+@pytest.fixture(autouse=True)
+def _lib():
+    assert ops.load(), "HIP extension must load on the GPU box"
+
+
+def _close(got, ref, tol):
+    torch.testing.assert_close(got.float(), ref, atol=tol * ref.abs().max().item() + 1e-6, rtol=tol)
+
+
+@pytest.mark.parametrize("geom", GEOMS)
+def test_routed_conv_training_matches_fp32(geom):
+    n, cin, h, w, cout, k, s, p, d = geom
+    torch.manual_seed(0)
+    conv = nn.Conv2d(cin, cout, k, s, p, d, bias=False)
+    ops.convert_routed_convs(nn.Sequential(conv))
+    assert type(conv) is ops.RoutedConv2d
+    conv = conv.to(DEV).to(memory_format=torch.channels_last).train()
+    x = torch.randn(n, cin, h, w, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = conv(x)
+    assert y.grad_fn is not None and "ConvFn" in type(y.grad_fn).__name__, type(y.grad_fn).__name__
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr = x.detach().float().requires_grad_(True)
+    wr = conv.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+    ref = F.conv2d(xr, wr, None, s, p, d)
+    ref.backward(g.float())
+    _close(y, ref.detach(), 2e-2)
+    _close(x.grad, xr.grad, 3e-2)
+    _close(conv.weight.grad, wr.grad, 3e-2)
+    assert conv.weight.grad.stride() == conv.weight.stride()
+
+
+@pytest.mark.parametrize("geom", GEOMS[:3])
+def test_routed_conv_inference_uses_cached_bf16_weight(geom):
+    n, cin, h, w, cout, k, s, p, d = geom
+    conv = nn.Conv2d(cin, cout, k, s, p, d, bias=False)
+    ops.convert_routed_convs(nn.Sequential(conv))
+    conv = conv.to(DEV).to(memory_format=torch.channels_last).eval()
+    x = torch.randn(n, cin, h, w, device=DEV).contiguous(memory_format=torch.channels_last)
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        y = conv(x)
+        y2 = conv(x)
+    assert getattr(conv, "_rtseg_w16", None) is not None
+    ref = F.conv2d(x.to(torch.bfloat16).float(), conv.weight.to(torch.bfloat16).float(), None, s, p, d)
+    _close(y, ref, 2e-2)
+    torch.testing.assert_close(y, y2)

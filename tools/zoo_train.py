@@ -35,6 +35,9 @@ def config(key, a):
     c.base_workers, c.save_ckpt, c.use_tb, c.load_ckpt = 0, False, False, False
     c.save_dir = "/tmp/rtseg_zoo_train"
     c.use_ema, c.is_testing = True, False
+    # bf16 autocast like bench.py (BaseConfig's default is fp32, on which the MFMA conv kernels
+    # do not run: round 2's sweep measured fp32 by mistake); --fp32 for that column
+    c.amp_training, c.amp_dtype = not a.fp32, "bf16"
     c.init_dependent_config()
     return c
 
@@ -55,7 +58,7 @@ def run(key, a):
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
     return {"model": key, "images_per_s": round(a.batch / dt, 2), "ms_per_step": round(dt * 1e3, 2),
-            "loss": round(float(loss), 4), "aux": cfg.use_aux,
+            "loss": round(float(loss), 4), "aux": cfg.use_aux, "dtype": "fp32" if a.fp32 else "bf16",
             "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2)}
 
 
@@ -67,6 +70,7 @@ def main():
     ap.add_argument("--height", type=int, default=1024)
     ap.add_argument("--width", type=int, default=2048)
     ap.add_argument("--models", default="")
+    ap.add_argument("--fp32", action="store_true", help="no autocast (fp32 training)")
     ap.add_argument("--out", default="gpurun_out/zoo_train.jsonl")
     a = ap.parse_args()
     assert torch.cuda.is_available() and ops.load()
