@@ -253,20 +253,39 @@ __global__ void __launch_bounds__(kActBlock) prelu_bwd_planes_kernel(const T* __
 }
 
 // dw[c] = sum over the slab rows in fixed order.  rows layout: part[r * C + c] (rows mode) or
-// part[(n * C + c) * slices + s] (planes mode: rows = N * slices).
-__global__ void act_prelu_wfinal(const float* __restrict__ part, float* __restrict__ dw, int C, int rows,
-                                 int planes_slices) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// part[(n * C + c) * slices + s] (planes mode: rows = N * slices).  One block per 64 channels;
+// 16 waves take interleaved rows (independent loads in flight), then the 16 wave partials are
+// summed in wave order (deterministic).  A single thread per channel walking up to 2048 rows
+// serially took ~140 us per call (33 ms per CFPNet step, profiles/r3_models).
+constexpr int kWfWaves = 16;
+__global__ void __launch_bounds__(kWfWaves * 64) act_prelu_wfinal(const float* __restrict__ part,
+                                                                  float* __restrict__ dw, int C, int rows,
+                                                                  int planes_slices) {
+  __shared__ float red[kWfWaves][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   float s = 0.f;
-  if (planes_slices == 0) {
-    for (int r = 0; r < rows; ++r) s += part[static_cast<int64_t>(r) * C + c];
-  } else {
-    const int nb = rows / (planes_slices * C);  // batch entries
-    for (int i = 0; i < nb; ++i)
-      for (int k = 0; k < planes_slices; ++k) s += part[(static_cast<int64_t>(i) * C + c) * planes_slices + k];
+  if (c < C) {
+    if (planes_slices == 0) {
+#pragma unroll 4
+      for (int r = w; r < rows; r += kWfWaves) s += part[static_cast<int64_t>(r) * C + c];
+    } else {
+      const int n_items = rows / C;  // (batch entry, slice) pairs
+#pragma unroll 4
+      for (int it = w; it < n_items; it += kWfWaves) {
+        const int i = it / planes_slices, k = it - (it / planes_slices) * planes_slices;
+        s += part[(static_cast<int64_t>(i) * C + c) * planes_slices + k];
+      }
+    }
   }
-  dw[c] = s;
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && c < C) {
+    float t = 0.f;
+#pragma unroll
+    for (int u = 0; u < kWfWaves; ++u) t += red[u][lane];
+    dw[c] = t;
+  }
 }
 
 template <typename T, bool BWD>
@@ -322,7 +341,7 @@ void launch_typed(const ActArgs& a, hipStream_t st) {
   T* dx = static_cast<T*>(a.out);
   if (p.planes) {
     prelu_bwd_planes_kernel<T><<<p.blocks, kActBlock, 0, st>>>(x, dy, a.w, dx, a.part, a.C, a.inner, p.slices);
-    act_prelu_wfinal<<<(a.C + 255) / 256, 256, 0, st>>>(a.part, a.dw, a.C, p.blocks, p.slices);
+    act_prelu_wfinal<<<(a.C + 63) / 64, kWfWaves * 64, 0, st>>>(a.part, a.dw, a.C, p.blocks, p.slices);
   } else {
     const int TY = kActBlock / p.tx;
     const size_t lds = static_cast<size_t>(TY) * a.C * sizeof(float);
@@ -332,7 +351,7 @@ void launch_typed(const ActArgs& a, hipStream_t st) {
     else
       prelu_bwd_rows_kernel<T><<<p.blocks, kActBlock, lds, st>>>(x, dy, a.w, dx, a.part, a.n / a.C, a.C,
                                                                    p.rows_per_block, p.tx);
-    act_prelu_wfinal<<<(a.C + 255) / 256, 256, 0, st>>>(a.part, a.dw, a.C, p.blocks, 0);
+    act_prelu_wfinal<<<(a.C + 63) / 64, kWfWaves * 64, 0, st>>>(a.part, a.dw, a.C, p.blocks, 0);
   }
 }
 

@@ -485,8 +485,9 @@ __device__ __forceinline__ void bwd_apply_one(const T* dy, const T* x, const T* 
   VecIO<T, V>::store(dx + off, o);
 }
 
-// Channel-stationary backward apply (see apply_rows): dx = A*g + B*x + D per channel, with
-// A = k0, B = -k0*k2, D = k0*(k2*mean - k1) folded once per thread into registers.
+// Channel-stationary backward apply (see apply_rows): dx = k0 * (g - k1 - (x - mean) * k2) with
+// the per-channel k0, k1, k2, mean held in registers (x - mean first, as in bwd_apply_one: no
+// cancellation between separately rounded k2*x and k2*mean terms).
 template <typename T, int V, int ACT, int MASK, bool DRES>
 __device__ __forceinline__ void bwd_apply_rows(const T* __restrict__ dy, const T* __restrict__ x,
                                                const T* __restrict__ y, const float* __restrict__ mean_invstd,
@@ -495,14 +496,14 @@ __device__ __forceinline__ void bwd_apply_rows(const T* __restrict__ dy, const T
                                                T* __restrict__ dres, int64_t M, int C) {
   const int cv = C / V;
   const int c0 = (threadIdx.x % cv) * V;
-  float cf[2 * V], A[V], B[V], D[V];  // cf: scale | shift (pre-activation mask)
+  float cf[2 * V], k0[V], k1[V], k2[V], mu[V];  // cf: scale | shift (pre-activation mask)
 #pragma unroll
   for (int j = 0; j < V; ++j) {
     const int c = c0 + j;
-    const float k0 = kcoef[c], k1 = kcoef[C + c], k2 = kcoef[2 * C + c], mu = mean_invstd[c];
-    A[j] = k0;
-    B[j] = -k0 * k2;
-    D[j] = k0 * fmaf(k2, mu, -k1);
+    k0[j] = kcoef[c];
+    k1[j] = kcoef[C + c];
+    k2[j] = kcoef[2 * C + c];
+    mu[j] = mean_invstd[c];
     cf[j] = scale_shift[c];
     cf[V + j] = scale_shift[C + c];
   }
@@ -527,7 +528,7 @@ __device__ __forceinline__ void bwd_apply_rows(const T* __restrict__ dy, const T
     }
     if constexpr (DRES) VecIO<T, V>::store(dres + off, g);
 #pragma unroll
-    for (int j = 0; j < V; ++j) o[j] = fmaf(A[j], g[j], fmaf(B[j], xv[j], D[j]));
+    for (int j = 0; j < V; ++j) o[j] = k0[j] * (g[j] - k1[j] - (xv[j] - mu[j]) * k2[j]);
     VecIO<T, V>::store(dx + off, o);
   };
   int64_t row = static_cast<int64_t>(blockIdx.x) * (blockDim.x / cv) + threadIdx.x / cv;
@@ -566,6 +567,248 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
   if (i < total) bwd_apply_one<T, V, ACT, MASK, DRES>(dy, x, y, coef, mu, k, dx, dres, i, cv, C);
 }
 
+// ------------------------------------------ odd channel counts: flat chunks ---
+// An odd C (the 19-class heads of the 11 DeConvBNAct models, whose BN runs at full resolution)
+// has channel vectors of ONE element: 2-byte loads, a quarter of the bandwidth of the 16-byte
+// path.  Here the [M, C] tensor is walked as flat 16-byte chunks instead (E = 16 / sizeof(T)
+// elements; element e has channel e % C).  The grid has a multiple of C threads, so a thread
+// that starts at chunk t and strides by the thread count always sees the same E channels
+// ((E * t + j) % C): its coefficients and partial sums stay in registers ("phase-stationary"),
+// exactly like the channel-stationary kernels above.  Partial sums: one [2C] slab row per block,
+// each channel summed over the block's (thread, element) slots in a fixed order (deterministic).
+template <typename T>
+struct Flat {
+  static constexpr int E = 16 / static_cast<int>(sizeof(T));
+  int64_t n_el, n_chunks, nthreads, t;
+  int ch[E];
+  __device__ __forceinline__ Flat(int64_t M, int C) {
+    n_el = M * C;
+    n_chunks = n_el / E;
+    nthreads = static_cast<int64_t>(gridDim.x) * blockDim.x;
+    t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int base = static_cast<int>((E * t) % C);
+#pragma unroll
+    for (int j = 0; j < E; ++j) ch[j] = (base + j) % C;
+  }
+  // the thread that owns the partial last chunk (n_el % E trailing elements), if any
+  __device__ __forceinline__ bool owns_tail() const {
+    return n_chunks * E < n_el && t == n_chunks % nthreads;
+  }
+};
+
+// block partials of the phase-stationary layout -> one slab row: sum of slots f (= thread * E +
+// element) with (E * blockIdx.x * blockDim.x + f) % C == c, in increasing f
+template <int E>
+__device__ __forceinline__ void flat_partials_out(const float* s, const float* q, int C, float* __restrict__ part) {
+  __shared__ float red[2][256 * E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    red[0][threadIdx.x * E + j] = s[j];
+    red[1][threadIdx.x * E + j] = q[j];
+  }
+  __syncthreads();
+  const int b0 = static_cast<int>((static_cast<int64_t>(E) * blockIdx.x * blockDim.x) % C);
+  const int nslot = blockDim.x * E;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float a = 0.f, b = 0.f;
+    for (int f = ((c - b0) % C + C) % C; f < nslot; f += C) { a += red[0][f]; b += red[1][f]; }
+    part[static_cast<int64_t>(blockIdx.x) * 2 * C + c] = a;
+    part[static_cast<int64_t>(blockIdx.x) * 2 * C + C + c] = b;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) bn_stats_flat_kernel(const T* __restrict__ x, int64_t M, int C,
+                                                            float* __restrict__ part) {
+  constexpr int E = Flat<T>::E;
+  const Flat<T> fl(M, C);
+  float s[E], q[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) { s[j] = 0.f; q[j] = 0.f; }
+  auto acc = [&](const float* f) {
+#pragma unroll
+    for (int j = 0; j < E; ++j) { s[j] += f[j]; q[j] = fmaf(f[j], f[j], q[j]); }
+  };
+  int64_t i = fl.t;
+  for (; i + fl.nthreads < fl.n_chunks; i += 2 * fl.nthreads) {
+    float a[E], b[E];
+    VecIO<T, E>::load(x + i * E, a);
+    VecIO<T, E>::load(x + (i + fl.nthreads) * E, b);
+    acc(a);
+    acc(b);
+  }
+  if (i < fl.n_chunks) {
+    float a[E];
+    VecIO<T, E>::load(x + i * E, a);
+    acc(a);
+  }
+  if (fl.owns_tail()) {
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      const int64_t e = fl.n_chunks * E + j;
+      if (e < fl.n_el) {
+        const float v = to_f<T>(x[e]);
+        s[j] += v;
+        q[j] = fmaf(v, v, q[j]);
+      }
+    }
+  }
+  flat_partials_out<E>(s, q, C, part);
+}
+
+template <typename T, int ACT, bool RES, bool BITS>
+__global__ void __launch_bounds__(256) bn_apply_flat_kernel(const T* __restrict__ x, const T* __restrict__ res,
+                                                            const float* __restrict__ scale_shift, T* __restrict__ y,
+                                                            int64_t M, int C, uint8_t* __restrict__ bits) {
+  constexpr int E = Flat<T>::E;
+  const Flat<T> fl(M, C);
+  float sc[E], sh[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) { sc[j] = scale_shift[fl.ch[j]]; sh[j] = scale_shift[C + fl.ch[j]]; }
+  auto val = [&](int j, float f, float r, uint32_t& b) {
+    float z = fmaf(f, sc[j], sh[j]);
+    if constexpr (RES) z += r;
+    if constexpr (BITS) b |= (act_grad_pre<ACT>(1.f, z) != 0.f ? 1u : 0u) << (8 * (j & 3));
+    return act_fwd<ACT>(z);
+  };
+  auto one = [&](int64_t i) {
+    float f[E], r[E];
+    VecIO<T, E>::load(x + i * E, f);
+    if constexpr (RES) VecIO<T, E>::load(res + i * E, r);
+    uint32_t b[2] = {0u, 0u};  // one byte per element (channel vectors of one element)
+#pragma unroll
+    for (int j = 0; j < E; ++j) f[j] = val(j, f[j], RES ? r[j] : 0.f, b[j >> 2]);
+    VecIO<T, E>::store(y + i * E, f);
+    if constexpr (BITS) {
+      if constexpr (E == 8) *reinterpret_cast<uint2*>(bits + i * E) = make_uint2(b[0], b[1]);
+      else *reinterpret_cast<uint32_t*>(bits + i * E) = b[0];
+    }
+  };
+  int64_t i = fl.t;
+  for (; i + fl.nthreads < fl.n_chunks; i += 2 * fl.nthreads) {
+    one(i);
+    one(i + fl.nthreads);
+  }
+  if (i < fl.n_chunks) one(i);
+  if (fl.owns_tail()) {
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      const int64_t e = fl.n_chunks * E + j;
+      if (e < fl.n_el) {
+        uint32_t b = 0u;
+        y[e] = from_f<T>(val(j, to_f<T>(x[e]), RES ? to_f<T>(res[e]) : 0.f, b));
+        if constexpr (BITS) bits[e] = static_cast<uint8_t>(b >> (8 * (j & 3)));
+      }
+    }
+  }
+}
+
+// activation-masked gradient of element j (value g) given x (and y / the bit byte)
+template <typename T, int ACT, int MASK>
+__device__ __forceinline__ float flat_mask(float g, float xv, const T* y, int64_t e, float sc, float sh) {
+  if constexpr (MASK == kMaskFromY) return act_bwd_from_out<ACT>(g, to_f<T>(y[e]));
+  else if constexpr (MASK == kMaskFromX) return act_grad_pre<ACT>(g, fmaf(xv, sc, sh));
+  else if constexpr (MASK == kMaskBits) return reinterpret_cast<const uint8_t*>(y)[e] ? g : 0.f;
+  else return g;
+}
+
+template <typename T, int ACT, int MASK>
+__global__ void __launch_bounds__(256) bn_bwd_reduce_flat_kernel(
+    const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y,
+    const float* __restrict__ mean_invstd, const float* __restrict__ scale_shift, int64_t M, int C,
+    float* __restrict__ part) {
+  constexpr int E = Flat<T>::E;
+  const Flat<T> fl(M, C);
+  float m[E], sc[E], sh[E], s[E], q[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    m[j] = mean_invstd[fl.ch[j]];
+    sc[j] = scale_shift[fl.ch[j]];
+    sh[j] = scale_shift[C + fl.ch[j]];
+    s[j] = 0.f;
+    q[j] = 0.f;
+  }
+  auto one = [&](int64_t i) {
+    float g[E], xv[E];
+    VecIO<T, E>::load(dy + i * E, g);
+    VecIO<T, E>::load(x + i * E, xv);
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      const float gm = flat_mask<T, ACT, MASK>(g[j], xv[j], y, i * E + j, sc[j], sh[j]);
+      s[j] += gm;
+      q[j] = fmaf(gm, xv[j] - m[j], q[j]);
+    }
+  };
+  int64_t i = fl.t;
+  for (; i + fl.nthreads < fl.n_chunks; i += 2 * fl.nthreads) {
+    one(i);
+    one(i + fl.nthreads);
+  }
+  if (i < fl.n_chunks) one(i);
+  if (fl.owns_tail()) {
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      const int64_t e = fl.n_chunks * E + j;
+      if (e < fl.n_el) {
+        const float xv = to_f<T>(x[e]);
+        const float gm = flat_mask<T, ACT, MASK>(to_f<T>(dy[e]), xv, y, e, sc[j], sh[j]);
+        s[j] += gm;
+        q[j] = fmaf(gm, xv - m[j], q[j]);
+      }
+    }
+  }
+  flat_partials_out<E>(s, q, C, part);
+}
+
+template <typename T, int ACT, int MASK, bool DRES>
+__global__ void __launch_bounds__(256) bn_bwd_apply_flat_kernel(
+    const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y,
+    const float* __restrict__ mean_invstd, const float* __restrict__ scale_shift,
+    const float* __restrict__ kcoef, T* __restrict__ dx, T* __restrict__ dres, int64_t M, int C) {
+  constexpr int E = Flat<T>::E;
+  const Flat<T> fl(M, C);
+  float k0[E], k1[E], k2[E], mu[E], sc[E], sh[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    const int c = fl.ch[j];
+    k0[j] = kcoef[c];
+    k1[j] = kcoef[C + c];
+    k2[j] = kcoef[2 * C + c];
+    mu[j] = mean_invstd[c];
+    sc[j] = scale_shift[c];
+    sh[j] = scale_shift[C + c];
+  }
+  auto one = [&](int64_t i) {
+    float g[E], xv[E], o[E];
+    VecIO<T, E>::load(dy + i * E, g);
+    VecIO<T, E>::load(x + i * E, xv);
+#pragma unroll
+    for (int j = 0; j < E; ++j) g[j] = flat_mask<T, ACT, MASK>(g[j], xv[j], y, i * E + j, sc[j], sh[j]);
+    if constexpr (DRES) VecIO<T, E>::store(dres + i * E, g);
+#pragma unroll
+    for (int j = 0; j < E; ++j) o[j] = k0[j] * (g[j] - k1[j] - (xv[j] - mu[j]) * k2[j]);
+    VecIO<T, E>::store(dx + i * E, o);
+  };
+  int64_t i = fl.t;
+  for (; i + fl.nthreads < fl.n_chunks; i += 2 * fl.nthreads) {
+    one(i);
+    one(i + fl.nthreads);
+  }
+  if (i < fl.n_chunks) one(i);
+  if (fl.owns_tail()) {
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      const int64_t e = fl.n_chunks * E + j;
+      if (e < fl.n_el) {
+        const float xv = to_f<T>(x[e]);
+        const float g = flat_mask<T, ACT, MASK>(to_f<T>(dy[e]), xv, y, e, sc[j], sh[j]);
+        if constexpr (DRES) dres[e] = from_f<T>(g);
+        dx[e] = from_f<T>(k0[j] * (g - k1[j] - (xv - mu[j]) * k2[j]));
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------ launchers -----
 // Channel-vector width: the widest of {16 B, 8 B, 4 B, 1 element} that divides C
 // with at most 256 vectors per row (fp16 keeps the 16-byte path only).
@@ -576,7 +819,18 @@ int bn_vec_width(int dtype, int C) {
   return 0;
 }
 
+// odd channel counts take the flat, phase-stationary kernels (grids: multiples of C threads' blocks)
+static bool bn_flat(int dtype, int C) { return dtype != kF16 && C >= 3 && (C & 1) && bn_vec_width(dtype, C) == 1; }
+
+static int64_t round_up_to(int64_t g, int m) { return (g + m - 1) / m * m; }
+
 int bn_partial_grid(int64_t M, int C, int dtype) {
+  if (bn_flat(dtype, C)) {  // ~16 chunks per thread, <= ~1024 blocks, a multiple of C blocks
+    const int64_t chunks = M * C / (dtype == kF32 ? 4 : 8);
+    int64_t g = (chunks + 256 * 16 - 1) / (256 * 16);
+    g = g < 1 ? 1 : (g > 1024 ? 1024 : g);
+    return static_cast<int>(round_up_to(g, C));
+  }
   const int V = bn_vec_width(dtype, C);
   const int rpi = 256 / (C / V);
   int64_t g = (M + static_cast<int64_t>(rpi) * 32 - 1) / (static_cast<int64_t>(rpi) * 32);
@@ -607,6 +861,11 @@ static void with_tv(int dtype, int C, F&& f) {
 
 void launch_bn_stats(const void* x, int dtype, int64_t M, int C, float* part, int G,
                      hipStream_t st) {
+  if (bn_flat(dtype, C)) {  // G (bn_partial_grid) is a multiple of C
+    if (dtype == kF32) bn_stats_flat_kernel<float><<<G, 256, 0, st>>>(static_cast<const float*>(x), M, C, part);
+    else bn_stats_flat_kernel<uint16_t><<<G, 256, 0, st>>>(static_cast<const uint16_t*>(x), M, C, part);
+    return;
+  }
   with_tv(dtype, C, [&]<typename T, int V>() {
     const int rpi = 256 / (C / V);
     const size_t lds = sizeof(float) * 2 * rpi * C;
@@ -650,6 +909,31 @@ static int apply_grid(int64_t work) {
   return static_cast<int>(g);
 }
 
+// flat kernels: a multiple of C blocks (so of C threads), ~2 chunks per thread up to 2048 blocks
+static int flat_grid(int64_t M, int C, int dtype) {
+  return static_cast<int>(round_up_to(apply_grid(M * C / (dtype == kF32 ? 4 : 8)), C));
+}
+
+template <typename T, int ACT>
+static void apply_flat_t(const void* x, const void* res, const float* ss, void* y, uint8_t* bits, int64_t M,
+                         int C, int dtype, hipStream_t st) {
+  const int g = flat_grid(M, C, dtype);
+  const T* xp = static_cast<const T*>(x);
+  const T* rp = static_cast<const T*>(res);
+  T* yp = static_cast<T*>(y);
+  if (res != nullptr && bits != nullptr) bn_apply_flat_kernel<T, ACT, true, true><<<g, 256, 0, st>>>(xp, rp, ss, yp, M, C, bits);
+  else if (res != nullptr) bn_apply_flat_kernel<T, ACT, true, false><<<g, 256, 0, st>>>(xp, rp, ss, yp, M, C, bits);
+  else if (bits != nullptr) bn_apply_flat_kernel<T, ACT, false, true><<<g, 256, 0, st>>>(xp, rp, ss, yp, M, C, bits);
+  else bn_apply_flat_kernel<T, ACT, false, false><<<g, 256, 0, st>>>(xp, rp, ss, yp, M, C, bits);
+}
+
+template <int ACT>
+static void apply_flat(const void* x, const void* res, const float* ss, void* y, uint8_t* bits, int64_t M, int C,
+                       int dtype, hipStream_t st) {
+  if (dtype == kF32) apply_flat_t<float, ACT>(x, res, ss, y, bits, M, C, dtype, st);
+  else apply_flat_t<uint16_t, ACT>(x, res, ss, y, bits, M, C, dtype, st);
+}
+
 template <typename T, int V, int ACT>
 static void apply_t(const void* x, const void* res, const float* ss, void* y, int64_t M, int C,
                     hipStream_t st) {
@@ -680,6 +964,11 @@ static void apply_bits_t(const void* x, const void* res, const float* ss, void* 
 // bits holds M * C / V bytes, V = bn_vec_width(dtype, C).
 void launch_bn_apply_bits(const void* x, const void* res, const float* scale_shift, void* y,
                           uint8_t* bits, int dtype, int64_t M, int C, int act, hipStream_t st) {
+  if (bn_flat(dtype, C)) {
+    if (act == kActReLU6) apply_flat<kActReLU6>(x, res, scale_shift, y, bits, M, C, dtype, st);
+    else apply_flat<kActReLU>(x, res, scale_shift, y, bits, M, C, dtype, st);
+    return;
+  }
   with_tv(dtype, C, [&]<typename T, int V>() {
     if (act == kActReLU6) apply_bits_t<T, V, kActReLU6>(x, res, scale_shift, y, bits, M, C, st);
     else apply_bits_t<T, V, kActReLU>(x, res, scale_shift, y, bits, M, C, st);
@@ -688,6 +977,12 @@ void launch_bn_apply_bits(const void* x, const void* res, const float* scale_shi
 
 void launch_bn_apply(const void* x, const void* res, const float* scale_shift, void* y, int dtype,
                      int64_t M, int C, int act, hipStream_t st) {
+  if (bn_flat(dtype, C)) {
+    if (act == kActReLU) apply_flat<kActReLU>(x, res, scale_shift, y, nullptr, M, C, dtype, st);
+    else if (act == kActReLU6) apply_flat<kActReLU6>(x, res, scale_shift, y, nullptr, M, C, dtype, st);
+    else apply_flat<kActNone>(x, res, scale_shift, y, nullptr, M, C, dtype, st);
+    return;
+  }
   with_tv(dtype, C, [&]<typename T, int V>() {
     if (act == kActReLU) apply_t<T, V, kActReLU>(x, res, scale_shift, y, M, C, st);
     else if (act == kActReLU6) apply_t<T, V, kActReLU6>(x, res, scale_shift, y, M, C, st);
@@ -730,9 +1025,35 @@ static void bwd_apply_t(const void* dy, const void* x, const void* y, const floa
     }                                                                                   \
   } while (0)
 
+// flat (odd C) backward dispatch: T = fp32 or bf16, (act, mask) as RT_ACT_MASK_DISPATCH
+#define RT_FLAT_DISPATCH(...)                                                           \
+  do {                                                                                  \
+    auto run = [&]<typename T, int ACT, int MASK>() { __VA_ARGS__; };                   \
+    auto by_mask = [&]<typename T>() {                                                  \
+      if (act == kActNone || mask == kMaskNone) run.template operator()<T, kActNone, kMaskNone>(); \
+      else if (act == kActReLU) {                                                       \
+        if (mask == kMaskFromY) run.template operator()<T, kActReLU, kMaskFromY>();     \
+        else if (mask == kMaskBits) run.template operator()<T, kActReLU, kMaskBits>();  \
+        else run.template operator()<T, kActReLU, kMaskFromX>();                        \
+      } else {                                                                          \
+        if (mask == kMaskFromY) run.template operator()<T, kActReLU6, kMaskFromY>();    \
+        else if (mask == kMaskBits) run.template operator()<T, kActReLU6, kMaskBits>(); \
+        else run.template operator()<T, kActReLU6, kMaskFromX>();                       \
+      }                                                                                 \
+    };                                                                                  \
+    if (dtype == kF32) by_mask.template operator()<float>();                            \
+    else by_mask.template operator()<uint16_t>();                                       \
+  } while (0)
+
 void launch_bn_bwd_reduce(const void* dy, const void* x, const void* y, const float* mean_invstd,
                           const float* scale_shift, int dtype, int64_t M, int C, int act, int mask,
                           float* part, int G, hipStream_t st) {
+  if (bn_flat(dtype, C)) {  // G (bn_partial_grid) is a multiple of C
+    RT_FLAT_DISPATCH((bn_bwd_reduce_flat_kernel<T, ACT, MASK><<<G, 256, 0, st>>>(
+        static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(y), mean_invstd, scale_shift,
+        M, C, part)));
+    return;
+  }
   with_tv(dtype, C, [&]<typename T, int V>() {
     RT_ACT_MASK_DISPATCH(bwd_reduce_t, dy, x, y, mean_invstd, scale_shift, M, C, part, G, st);
   });
@@ -756,6 +1077,20 @@ static void bwd_apply_res(const void* dy, const void* x, const void* y, const fl
 void launch_bn_bwd_apply(const void* dy, const void* x, const void* y, const float* mean_invstd,
                          const float* scale_shift, const float* kcoef, void* dx, void* dres,
                          int dtype, int64_t M, int C, int act, int mask, hipStream_t st) {
+  if (bn_flat(dtype, C)) {
+    const int g = flat_grid(M, C, dtype);
+    RT_FLAT_DISPATCH({
+      if (dres != nullptr)
+        bn_bwd_apply_flat_kernel<T, ACT, MASK, true><<<g, 256, 0, st>>>(
+            static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(y), mean_invstd, scale_shift,
+            kcoef, static_cast<T*>(dx), static_cast<T*>(dres), M, C);
+      else
+        bn_bwd_apply_flat_kernel<T, ACT, MASK, false><<<g, 256, 0, st>>>(
+            static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(y), mean_invstd, scale_shift,
+            kcoef, static_cast<T*>(dx), static_cast<T*>(dres), M, C);
+    });
+    return;
+  }
   with_tv(dtype, C, [&]<typename T, int V>() {
     RT_ACT_MASK_DISPATCH(bwd_apply_res, dy, x, y, mean_invstd, scale_shift, kcoef, dx, dres, M, C,
                          st);

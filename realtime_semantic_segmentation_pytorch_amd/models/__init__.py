@@ -84,7 +84,7 @@ def get_model(config):
     if getattr(config, "hip_deconv", True):
         ops.convert_transposed_convs(model)
     ops.convert_pruned_convs(model)  # last: every remaining plain spatial conv
-    if getattr(config, "routed_convs", True):
+    if getattr(config, "routed_convs", True) and os.environ.get("RTSEG_ROUTED_CONVS", "1") != "0":
         ops.convert_routed_convs(model)  # plain dense bias-free convs -> the MFMA conv family
     if getattr(config, "hip_activations", True):
         ops.convert_activations(model)

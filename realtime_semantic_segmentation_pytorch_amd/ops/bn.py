@@ -223,6 +223,18 @@ def bn_act(x: torch.Tensor, bn, act=None, residual: Optional[torch.Tensor] = Non
     raise ValueError(f"unsupported activation {act!r}")
 
 
+def channel_sum(t: torch.Tensor) -> torch.Tensor:
+    """fp32 per-channel sum over (N, H, W) -- a bias gradient.  On channels-last GPU tensors it is
+    the BN statistics pass (one read, 16-byte chunks, fp64 totals): PyTorch's own reduction over
+    the outer dims of a channels-last [N, 19, 1024, 2048] tensor took 63 ms per call on MI355X
+    (the x8 transposed-conv heads of CANet / ADSCNet, profiles/r3_models)."""
+    if (use_hip(t) and t.dim() == 4 and t.dtype in (torch.float32, torch.bfloat16) and t.numel() > 0
+            and vec_width(t.dtype, t.shape[1]) and t.is_contiguous(memory_format=torch.channels_last)
+            and t.data_ptr() % 16 == 0):
+        return ops().bn_stats_sums(t)[: t.shape[1]].float()
+    return t.float().sum((0, 2, 3))
+
+
 # --------------------------------------------------------------------------
 # Module-level routing: every BatchNorm2d of a model through the fused kernels.
 # --------------------------------------------------------------------------

@@ -494,7 +494,10 @@ class RoutedConv2d(PrunedConv2d):
     def forward(self, x):
         if (x.is_cuda and self.in_channels % 32 == 0 and self.out_channels % 8 == 0 and torch.is_grad_enabled()
                 and self.weight.requires_grad and conv_ok(x, self)):
-            return _ConvFn.apply(x.to(torch.bfloat16), self.weight, self, False)[0]
+            x = x.to(torch.bfloat16)
+            if x.data_ptr() % 16:  # the kernels' 16-byte operand loads
+                x = x.clone(memory_format=torch.channels_last)
+            return _ConvFn.apply(x, self.weight, self, False)[0]
         if (x.is_cuda and not self.training and not torch.is_grad_enabled() and torch.is_autocast_enabled("cuda")
                 and torch.get_autocast_dtype("cuda") == torch.bfloat16):
             return conv_forward(x, self)  # its cached-weight branch (never falls through to self(x))

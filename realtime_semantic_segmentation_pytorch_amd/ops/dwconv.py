@@ -22,6 +22,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .bn import channel_sum
 from ._ext import ops, use_hip
 
 _DTYPES = (torch.float32, torch.bfloat16, torch.float16)
@@ -73,7 +74,7 @@ class _DWConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             dwt = ops().dw_conv_wgrad(dy, x, kh, kw, sh, sw, ph, pw, dh, dw).to(ctx.wdtype)
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = dy.float().sum((0, 2, 3))
+            db = channel_sum(dy)
         return dx, dwt, db, None, None
 
 

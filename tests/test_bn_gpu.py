@@ -168,3 +168,52 @@ def test_bn_residual_bitmask_matches_mask_from_y(monkeypatch, act, shape):
             torch.testing.assert_close(a, b, atol=0, rtol=0)
         else:  # relu6: the mask is taken from the fp32 pre-activation vs the bf16-rounded output
             assert ((a.float() - b.float()).abs() > 1e-2 * (1 + b.float().abs())).float().mean() < 1e-3
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("act,with_res", [("relu", False), ("relu", True), ("none", False)])
+@pytest.mark.parametrize("shape", [(2, 19, 61, 67), (2, 19, 128, 256), (3, 5, 33, 31)])
+def test_bn_odd_channels_flat_path(dtype, act, with_res, shape):
+    """Odd channel counts (the 19-class full-resolution heads) take the flat, phase-stationary
+    kernels: several 16-byte chunks per thread, a partial last chunk, all mask modes.  The fp32
+    reference runs on the CPU."""
+    assert ops.load()
+    torch.manual_seed(1)
+    c = shape[1]
+    bn = nn.BatchNorm2d(c)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    bn_ref = copy.deepcopy(bn)
+    bn = bn.to(DEV)
+    x0 = torch.randn(shape) * 2 + 0.5
+    r0 = torch.randn(shape) if with_res else None
+    x = x0.to(DEV, dtype).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    res = r0.to(DEV, dtype).contiguous(memory_format=torch.channels_last).requires_grad_(True) if with_res else None
+    assert ops.bn_fused_ok(x, bn, ops.bn_act_code(act))
+    y = ops.bn_act(x, bn, act, residual=res)
+    xr = x.detach().float().cpu().requires_grad_(True)
+    rr = res.detach().float().cpu().requires_grad_(True) if with_res else None
+    yr = _ref(xr, bn_ref, act, rr)
+    tol = 1e-4 if dtype == torch.float32 else 3e-2
+    if act == "relu":  # compare with the kernel's own activation mask (rounding at 0)
+        yr_cmp = torch.where((y.detach().float().cpu() > 0) | (yr <= 0), yr, torch.zeros_like(yr))
+    else:
+        yr_cmp = yr
+    torch.testing.assert_close(y.float().cpu(), yr_cmp.detach(), atol=tol, rtol=tol)
+    torch.testing.assert_close(bn.running_mean.cpu(), bn_ref.running_mean, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(bn.running_var.cpu(), bn_ref.running_var, atol=1e-3, rtol=1e-3)
+    g = torch.randn(shape)
+    y.backward(g.to(DEV, dtype).contiguous(memory_format=torch.channels_last))
+    yr.backward(g)
+    gt = 2e-3 if dtype == torch.float32 else 6e-2
+    scale = xr.grad.abs().max().item()
+    bad = ((x.grad.float().cpu() - xr.grad).abs() > gt * scale + gt * xr.grad.abs()).float().mean()
+    assert bad < (1e-5 if dtype == torch.float32 else 2e-3)
+    torch.testing.assert_close(bn.weight.grad.cpu(), bn_ref.weight.grad,
+                               atol=gt * bn_ref.weight.grad.abs().max().item(), rtol=gt)
+    torch.testing.assert_close(bn.bias.grad.cpu(), bn_ref.bias.grad,
+                               atol=gt * bn_ref.bias.grad.abs().max().item(), rtol=gt)
+    if with_res:
+        bad_r = ((res.grad.float().cpu() - rr.grad).abs() > gt * rr.grad.abs().max().item()).float().mean()
+        assert bad_r < 2e-3

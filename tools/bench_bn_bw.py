@@ -44,7 +44,8 @@ def main():
     assert ops.load(), "rtseg extension missing"
     o = torch.ops.rtseg
     n = a.batch
-    shapes = [(n, 64, 512, 1024), (n, 64, 256, 512), (n, 128, 128, 256), (n, 256, 64, 128), (n, 512, 32, 64)]
+    shapes = [(n, 64, 512, 1024), (n, 64, 256, 512), (n, 128, 128, 256), (n, 256, 64, 128), (n, 512, 32, 64),
+              (8, 19, 1024, 2048)]  # the full-resolution 19-class head of the DeConvBNAct models (batch 8)
     print(f"{'shape':>24} {'pass':>14} {'us':>9} {'GB/s':>7} {'copy GB/s':>9}")
     for shp in shapes:
         C = shp[1]
