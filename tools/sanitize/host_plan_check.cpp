@@ -84,7 +84,13 @@ static void check_bn_plans() {
       CHECK(C % v == 0 && C / v <= 256, "bn vec C=%d v=%d", C, v);
       for (int64_t M : {int64_t{1}, int64_t{2}, int64_t{255}, int64_t{65536}, int64_t{32} * 256 * 512}) {
         const int G = bn_partial_grid(M, C, dtype);
-        CHECK(G >= 1 && G <= 512, "bn grid M=%lld C=%d G=%d", static_cast<long long>(M), C, G);
+        // odd C (flat, phase-stationary kernels): a multiple of C blocks, at most one C past 1024
+        const bool flat = dtype != kF16 && C >= 3 && (C & 1) && v == 1;
+        if (flat) {
+          CHECK(G >= C && G % C == 0 && G < 1024 + C, "bn flat grid M=%lld C=%d G=%d", static_cast<long long>(M), C, G);
+        } else {
+          CHECK(G >= 1 && G <= 1024, "bn grid M=%lld C=%d G=%d", static_cast<long long>(M), C, G);
+        }
       }
     }
 }
