@@ -136,6 +136,8 @@ class BaseConfig:
         self.synthetic_data = False      # device-generated synthetic batches (benchmarks)
         self.synthetic_len = 64          # images per epoch of the synthetic dataset
         self.synthetic_size = None       # (H, W) of synthetic images (default: crop)
+        self.synthetic_learnable = False  # labels a function of the image (colour-coded blocks)
+        self.synthetic_cell = 32         # block size (pixels) of the learnable synthetic task
         self.max_train_itrs = None       # stop an epoch early (smoke runs)
         self.log_interval = 20           # iterations between host-synced loss logs
         self.device = None               # force 'cpu' / 'cuda'

@@ -79,7 +79,8 @@ _SPEC = [
     ("amp_dtype", str, {"choices": ["bf16", "fp16"]}), ("no_channels_last", "true",
                                                         {"dest": "no_channels_last"}),
     ("no_fused_loss", "true", {"dest": "no_fused_loss"}), ("ddp_bucket_mb", int, {}),
-    ("gpu_aug", "true", {}), ("spawn_procs", int, {}), ("graph_step", "true", {}), ("synthetic_data", "true", {}), ("synthetic_len", int, {}), ("max_train_itrs", int, {}),
+    ("gpu_aug", "true", {}), ("spawn_procs", int, {}), ("graph_step", "true", {}), ("synthetic_data", "true", {}), ("synthetic_len", int, {}),
+    ("synthetic_learnable", "true", {}), ("synthetic_cell", int, {}), ("max_train_itrs", int, {}),
     ("log_interval", int, {}), ("device", str, {}),
     ("no_fused_optimizer", "true", {"dest": "no_fused_optimizer"}),
 ]

@@ -21,8 +21,11 @@ def get_dataset(config):
     if getattr(config, "synthetic_data", False):
         size = config.synthetic_size or (config.crop_h, config.crop_w)
         n = int(config.synthetic_len)
-        return (SyntheticSegDataset(n, size, config.num_class, config.ignore_index, seed=0),
-                SyntheticSegDataset(max(1, n // 4), size, config.num_class, config.ignore_index, seed=1))
+        learn = bool(getattr(config, "synthetic_learnable", False))
+        cell = int(getattr(config, "synthetic_cell", 32))
+        return (SyntheticSegDataset(n, size, config.num_class, config.ignore_index, seed=0, learnable=learn, cell=cell),
+                SyntheticSegDataset(max(1, n // 4), size, config.num_class, config.ignore_index, seed=1,
+                                    learnable=learn, cell=cell))
     if config.dataset not in dataset_hub:
         raise NotImplementedError("Unsupported dataset!")
     cls = dataset_hub[config.dataset]

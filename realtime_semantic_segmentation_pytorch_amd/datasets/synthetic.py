@@ -25,10 +25,41 @@ def _masks_like(gen, n, h, w, num_class, ignore_index, device):
     return m.to(device)
 
 
+def class_palette(num_class: int) -> torch.Tensor:
+    """[num_class, 3] well-separated colours (normalised-image units) for the learnable task: the
+    points of a {-1, 0, 1}^3 grid (up to 27 classes: any two differ by >= 1 in some channel), a
+    4-level grid (>= 2/3) up to 64 classes."""
+    levels = 3 if num_class <= 27 else 4 if num_class <= 64 else 1 + int(round(num_class ** (1 / 3) + 0.5))
+    vals = torch.linspace(-1.0, 1.0, levels)
+    grid = torch.cartesian_prod(vals, vals, vals)
+    return grid[:num_class].clone()
+
+
+def learnable_sample(gen, h, w, num_class, ignore_index, cell=32, noise=0.15, ignore_frac=0.02):
+    """One (image [3, H, W], label [H, W]) pair whose label is a function of the image: a map of
+    ``cell`` x ``cell`` blocks of random classes, each block painted in its class colour
+    (:func:`class_palette`) plus Gaussian noise; ``ignore_frac`` of the pixels are ignore-labelled
+    (their colour still follows the block's class)."""
+    ch, cw = max(1, (h + cell - 1) // cell), max(1, (w + cell - 1) // cell)
+    cells = torch.randint(0, num_class, (1, 1, ch, cw), generator=gen).float()
+    lbl = torch.nn.functional.interpolate(cells, size=(ch * cell, cw * cell), mode="nearest")[0, 0, :h, :w].long()
+    img = class_palette(num_class)[lbl].permute(2, 0, 1).contiguous()
+    img = img + noise * torch.randn((3, h, w), generator=gen)
+    ign = torch.rand((h, w), generator=gen) < ignore_frac
+    lbl[ign] = ignore_index
+    return img, lbl
+
+
 class SyntheticSegDataset(Dataset):
-    def __init__(self, length=2, size=(64, 128), num_class=19, ignore_index=255, seed=0):
+    """``learnable=False``: random images with blocky labels uncorrelated with them (throughput,
+    plumbing); ``learnable=True``: :func:`learnable_sample` -- colour-coded blocks, so training
+    must raise validation mIoU (convergence tests, ``config.synthetic_learnable``)."""
+
+    def __init__(self, length=2, size=(64, 128), num_class=19, ignore_index=255, seed=0, learnable=False,
+                 cell=32):
         self.length, self.size, self.num_class = length, tuple(size), num_class
         self.ignore_index, self.seed = ignore_index, seed
+        self.learnable, self.cell = bool(learnable), int(cell)
 
     def __len__(self):
         return self.length
@@ -37,6 +68,8 @@ class SyntheticSegDataset(Dataset):
         index = int(key[0]) if isinstance(key, (tuple, list)) else int(key)
         g = torch.Generator().manual_seed(self.seed * 100003 + index)
         h, w = self.size
+        if self.learnable:
+            return learnable_sample(g, h, w, self.num_class, self.ignore_index, self.cell)
         img = torch.randn((3, h, w), generator=g)
         mask = _masks_like(g, 1, h, w, self.num_class, self.ignore_index, "cpu")[0]
         return img, mask

@@ -68,9 +68,19 @@ def library_path() -> str:
     return _build.LIB_PATH
 
 
-def use_hip(t: torch.Tensor) -> bool:
+def families_off() -> frozenset:
+    """``RTSEG_HIP_OFF=bn,interp,...``: kernel families sent to their stock PyTorch formulation
+    (numerics bisection, tools/probe_numerics_bisect.py).  Families: act, bn, conv, deconv, detail,
+    dilated, dw, gate, interp, kd, loss, pool, shuffle, tapconv."""
+    raw = os.environ.get("RTSEG_HIP_OFF", "")
+    return frozenset(f.strip() for f in raw.split(",") if f.strip())
+
+
+def use_hip(t: torch.Tensor, family: str | None = None) -> bool:
     """Whether an op on tensor ``t`` must take the HIP path (raises if unavailable)."""
     if not t.is_cuda or hip_disabled():
+        return False
+    if family is not None and family in families_off():
         return False
     if not load():
         raise RuntimeError(
@@ -106,7 +116,10 @@ class _TracedOps:
             self._f.write(f"{self._n} {name}({', '.join(desc)})\n")
             os.fsync(self._f.fileno())
             out = fn(*args, **kw)
-            torch.cuda.synchronize()
+            # a synchronize is illegal while a HIP graph is being captured (graph_step, the
+            # inference engines): there the trace line is still written, the sync skipped
+            if not torch.cuda.is_current_stream_capturing():
+                torch.cuda.synchronize()
             return out
 
         return call

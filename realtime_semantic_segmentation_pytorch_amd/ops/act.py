@@ -74,7 +74,7 @@ def _ok(x: torch.Tensor, w) -> bool:
             return False
         if w.numel() > 1 and (x.dim() < 2 or x.shape[1] != w.numel() or w.numel() > 4096):
             return False
-    return use_hip(x)
+    return use_hip(x, "act")
 
 
 def activation(x: torch.Tensor, module: nn.Module) -> torch.Tensor:

@@ -22,7 +22,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-from ._ext import use_hip, ops, write_generation
+from ._ext import bump_write_generation, use_hip, ops, write_generation
 
 ACT_NONE, ACT_RELU, ACT_RELU6 = 0, 1, 2
 MASK_NONE, MASK_FROM_Y, MASK_FROM_X, MASK_BITS = 0, 1, 2, 3
@@ -81,6 +81,10 @@ class _BNActFn(torch.autograd.Function):
                 dist.all_reduce(sums, group=pg)
                 mi, ss = ops().bn_finalize(sums, weight, bias, rm, rv, nb, float(bn.momentum),
                                            float(bn.eps))
+            if rm is not None:
+                # the finalize kernels rewrite running_mean / running_var through raw pointers
+                # (no _version bump): invalidate the eval-coefficient caches keyed on them
+                bump_write_generation()
         else:
             sums = None
             mi, ss = eval_coeffs(bn)
@@ -197,7 +201,7 @@ def bn_act(x: torch.Tensor, bn, act=None, residual: Optional[torch.Tensor] = Non
     ``part``: BN statistics slab of ``x`` already computed by its producer (the MFMA conv
     epilogue, ``ops.conv``); used only on the fused batch-statistics path."""
     code = act if isinstance(act, int) else act_code(act)
-    if use_hip(x) and code is not None and fused_ok(x, bn, code) and (
+    if use_hip(x, "bn") and code is not None and fused_ok(x, bn, code) and (
             residual is None or (residual.shape == x.shape
                                  and residual.is_contiguous(memory_format=torch.channels_last)
                                  and residual.data_ptr() % 16 == 0)):
@@ -228,7 +232,7 @@ def channel_sum(t: torch.Tensor) -> torch.Tensor:
     the BN statistics pass (one read, 16-byte chunks, fp64 totals): PyTorch's own reduction over
     the outer dims of a channels-last [N, 19, 1024, 2048] tensor took 63 ms per call on MI355X
     (the x8 transposed-conv heads of CANet / ADSCNet, profiles/r3_models)."""
-    if (use_hip(t) and t.dim() == 4 and t.dtype in (torch.float32, torch.bfloat16) and t.numel() > 0
+    if (use_hip(t, "bn") and t.dim() == 4 and t.dtype in (torch.float32, torch.bfloat16) and t.numel() > 0
             and vec_width(t.dtype, t.shape[1]) and t.is_contiguous(memory_format=torch.channels_last)
             and t.data_ptr() % 16 == 0):
         return ops().bn_stats_sums(t)[: t.shape[1]].float()
@@ -248,7 +252,7 @@ class FusedBatchNorm2d(nn.BatchNorm2d):
     """
 
     def forward(self, x):
-        if use_hip(x) and fused_ok(x, self, ACT_NONE):
+        if use_hip(x, "bn") and fused_ok(x, self, ACT_NONE):
             use_batch = self.training or not self.track_running_stats or self.running_mean is None
             pg = _sync_group(self) if use_batch else None
             return _BNActFn.apply(x, self.weight, self.bias, None, self, ACT_NONE, use_batch, pg)
@@ -257,7 +261,7 @@ class FusedBatchNorm2d(nn.BatchNorm2d):
 
 class FusedSyncBatchNorm(nn.SyncBatchNorm):
     def forward(self, x):
-        if use_hip(x) and fused_ok(x, self, ACT_NONE):
+        if use_hip(x, "bn") and fused_ok(x, self, ACT_NONE):
             use_batch = self.training or not self.track_running_stats or self.running_mean is None
             pg = _sync_group(self) if use_batch else None
             return _BNActFn.apply(x, self.weight, self.bias, None, self, ACT_NONE, use_batch, pg)

@@ -142,7 +142,7 @@ def conv_ok(x: torch.Tensor, conv: nn.Module) -> bool:
         return False
     if conv.padding_mode != "zeros" or isinstance(conv.padding, str):
         return False
-    if x.dim() != 4 or not x.is_cuda or _mode() == "0" or not use_hip(x):
+    if x.dim() != 4 or not x.is_cuda or _mode() == "0" or not use_hip(x, "conv"):
         return False
     if has_dead_taps(x.shape[2:], conv.kernel_size, conv.stride, conv.padding, conv.dilation):
         return False  # the module's own forward drops the dead taps (ops/dilated.py)

@@ -41,7 +41,7 @@ def deconv_ok(x: torch.Tensor, m: nn.Module) -> bool:
     """Forward on our kernel: bf16 channels-last, groups 1, Cin_t % 64, Cout_t % 8."""
     if not isinstance(m, nn.ConvTranspose2d) or m.groups != 1 or m.padding_mode != "zeros":
         return False
-    if not x.is_cuda or x.dim() != 4 or not use_hip(x):
+    if not x.is_cuda or x.dim() != 4 or not use_hip(x, "deconv"):
         return False
     dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
     if dt != torch.bfloat16 or m.kernel_size[0] * m.kernel_size[1] > 49:
@@ -117,7 +117,7 @@ def conv_transpose2d(x: torch.Tensor, m: nn.ConvTranspose2d, output_size=None) -
         if x.data_ptr() % 16:
             x = x.clone(memory_format=torch.channels_last)
         return _DeconvFn.apply(x, m.weight, m.bias, m)
-    if (m.bias is not None and m.bias.requires_grad and torch.is_grad_enabled() and x.is_cuda and use_hip(x)
+    if (m.bias is not None and m.bias.requires_grad and torch.is_grad_enabled() and x.is_cuda and use_hip(x, "deconv")
             and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)):
         # Shapes our kernel does not take (e.g. the x8 19 -> 19 class heads of CANet / ADSCNet at
         # full resolution): MIOpen without the bias, the bias added separately -- aten's own bias

@@ -71,7 +71,7 @@ def detail_loss_reference(detail_logits, labels, detail_conv, thrs, dice_coef=1.
 def detail_loss(detail_logits: torch.Tensor, labels: torch.Tensor, detail_conv: nn.Module, thrs: float,
                 dice_coef: float = 1.0, bce_coef: float = 1.0, laplacian=None) -> torch.Tensor:
     """Detail loss from the H/8 detail logits ``[N, 1, h, w]`` and labels ``[N, H, W]``."""
-    if use_hip(detail_logits) and labels.dtype in (torch.uint8, torch.int64):
+    if use_hip(detail_logits, "detail") and labels.dtype in (torch.uint8, torch.int64):
         return _DetailLossFn.apply(detail_logits, labels.contiguous(), detail_conv.weight, detail_conv.bias,
                                    float(thrs), float(dice_coef), float(bce_coef))
     return detail_loss_reference(detail_logits, labels, detail_conv, thrs, dice_coef, bce_coef, laplacian)

@@ -177,7 +177,7 @@ class DilatedGroupConv2d(nn.Conv2d):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         from ._ext import use_hip
 
-        if not x.is_cuda or not use_hip(x):  # RTSEG_DISABLE_HIP=1: the stock conv, for A/B runs
+        if not x.is_cuda or not use_hip(x, "dilated"):  # RTSEG_DISABLE_HIP=1: the stock conv, for A/B runs
             return super().forward(x)
         return dilated_group_pruned(x, self.weight, self.bias, tuple(self.dilation), self.groups)
 

@@ -87,7 +87,7 @@ def depthwise_ok(conv: nn.Conv2d) -> bool:
 def dw_conv2d(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
     """``conv(x)`` for a depth-wise ``conv``; HIP kernels for channels-last GPU inputs
     (``RTSEG_DWCONV=0`` keeps MIOpen, for A/B comparisons)."""
-    if (x.dim() == 4 and use_hip(x) and x.is_contiguous(memory_format=torch.channels_last)
+    if (x.dim() == 4 and use_hip(x, "dw") and x.is_contiguous(memory_format=torch.channels_last)
             and os.environ.get("RTSEG_DWCONV", "1") != "0"):
         dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
         if dt in _DTYPES and conv.weight.dtype in _DTYPES:
@@ -102,7 +102,7 @@ def dw_conv_bn_stats(x: torch.Tensor, conv: nn.Conv2d):
     """Training forward of a depth-wise conv followed by a batch-statistics BN: (y, slab | None),
     the slab holding the BN statistics of y from the conv kernel's epilogue; None -> the caller's
     stock path (``conv(x)`` + ``ops.bn_act``)."""
-    if not (x.dim() == 4 and use_hip(x) and x.is_contiguous(memory_format=torch.channels_last)
+    if not (x.dim() == 4 and use_hip(x, "dw") and x.is_contiguous(memory_format=torch.channels_last)
             and os.environ.get("RTSEG_DWCONV", "1") != "0" and conv.bias is None and depthwise_ok(conv)):
         return None
     dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype

@@ -65,7 +65,7 @@ def gate(x: torch.Tensor, att: torch.Tensor, other: Optional[torch.Tensor] = Non
     """Gate ``x`` by ``att`` (see module doc); ``other`` is the second input of ``mode='blend'``.
     The result has ``x``'s dtype (a bf16 activation gated by an fp32 gate stays bf16)."""
     code = MODES[mode]
-    if (x.is_cuda and use_hip(x) and x.dim() == 4 and att.dim() == 4 and x.dtype in _DT
+    if (x.is_cuda and use_hip(x, "gate") and x.dim() == 4 and att.dim() == 4 and x.dtype in _DT
             and att.shape[0] == x.shape[0] and x.numel() > 0):
         bc = _bcast(x, att)
         ok = bc >= 0 and (other is None) == (code != 2)

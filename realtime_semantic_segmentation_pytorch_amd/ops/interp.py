@@ -57,7 +57,7 @@ def interpolate(x: torch.Tensor, size: Sequence[int], align_corners: bool = True
     """``act(skip + bilinear_resize(x, size))`` in one HIP kernel on GPU."""
     out_h, out_w = int(size[0]), int(size[1])
     code = ACT_CODES[act]
-    if use_hip(x) and x.dim() == 4 and x.dtype in (torch.float32, torch.bfloat16, torch.float16):
+    if use_hip(x, "interp") and x.dim() == 4 and x.dtype in (torch.float32, torch.bfloat16, torch.float16):
         if skip is not None and skip.dtype != x.dtype:
             dt = torch.promote_types(skip.dtype, x.dtype)
             x, skip = x.to(dt), skip.to(dt)

@@ -37,7 +37,7 @@ def kd_kl_div_reference(s: torch.Tensor, t: torch.Tensor, temperature: float) ->
 
 
 def kd_kl_div(s: torch.Tensor, t: torch.Tensor, temperature: float) -> torch.Tensor:
-    if use_hip(s) and s.dim() == 4 and s.shape == t.shape and s.dtype in (torch.float32, torch.bfloat16,
+    if use_hip(s, "kd") and s.dim() == 4 and s.shape == t.shape and s.dtype in (torch.float32, torch.bfloat16,
                                                                            torch.float16):
         return _KDFn.apply(s, t.detach().to(s.dtype), float(temperature))
     return kd_kl_div_reference(s, t, temperature)

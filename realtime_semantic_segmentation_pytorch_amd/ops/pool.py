@@ -37,7 +37,7 @@ def _pair(v):
 
 
 def _hip_ok(x: torch.Tensor) -> bool:
-    return (x.dim() == 4 and x.dtype in _DTYPES and x.numel() < 2 ** 31 and use_hip(x)
+    return (x.dim() == 4 and x.dtype in _DTYPES and x.numel() < 2 ** 31 and use_hip(x, "pool")
             and os.environ.get("RTSEG_POOL", "1") != "0")
 
 

@@ -78,7 +78,7 @@ def seg_cross_entropy(logits: torch.Tensor, labels: torch.Tensor, *, mode: int =
         out_size = tuple(labels.shape[-2:]) if resize_logits else tuple(logits.shape[-2:])
     out_size = (int(out_size[0]), int(out_size[1]))
     thresh = -math.log(ohem_thrs)
-    if use_hip(logits) and logits.dtype in (torch.float32, torch.bfloat16, torch.float16):
+    if use_hip(logits, "loss") and logits.dtype in (torch.float32, torch.bfloat16, torch.float16):
         if not resize_logits:
             out_size = tuple(logits.shape[-2:])
         if _fused_ok(logits, out_size):

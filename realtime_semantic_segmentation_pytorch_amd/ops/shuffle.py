@@ -38,7 +38,7 @@ class _ShuffleFn(torch.autograd.Function):
 
 def _ok(x):
     return (x.dim() == 4 and x.dtype in (torch.float32, torch.bfloat16, torch.float16) and x.numel() < 2 ** 32
-            and use_hip(x))
+            and use_hip(x, "shuffle"))
 
 
 def pixel_shuffle(x: torch.Tensor, r: int) -> torch.Tensor:

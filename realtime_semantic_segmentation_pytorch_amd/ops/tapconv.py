@@ -121,7 +121,7 @@ class _TapConvFn(torch.autograd.Function):
 
 
 def hip_tapconv_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
-    return (use_hip(x) and conv.in_channels in HIP_CHANNELS and conv.out_channels in HIP_CHANNELS
+    return (use_hip(x, "tapconv") and conv.in_channels in HIP_CHANNELS and conv.out_channels in HIP_CHANNELS
             and max(conv.kernel_size) <= 7 and x.dtype in (torch.float32, torch.bfloat16))
 
 

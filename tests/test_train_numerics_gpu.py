@@ -1,13 +1,15 @@
 """Model-level numerics of the bench configuration on the GPU.
 
-* one DDRNet-23 (+aux) training step in bf16 / channels-last with every HIP kernel on (MFMA
-  conv fwd/dgrad/wgrad, fused BN, fused OHEM, interp) and the same step in stock bf16
-  (``RTSEG_DISABLE_HIP=1``), both against the stock fp32 step (tools/probe_train_numerics.py
-  prints the per-layer table);
+* one training step of BASELINE configs 2-4 (DDRNet-23 + aux, BiSeNetV2 + aux, STDC2 + detail)
+  in bf16 / channels-last with every HIP kernel on (MFMA conv fwd/dgrad/wgrad, fused BN, fused
+  OHEM, interp, ...), in HIP fp32 and in stock bf16 (``RTSEG_DISABLE_HIP=1``), all against the
+  same step in fp64 on the CPU (tools/probe_numerics_bisect.py prints the per-family bisection
+  and the per-parameter table);
 * 200 steps overfitting one synthetic batch with every HIP kernel on: the loss must fall;
 * an fp16 + GradScaler step (``amp_dtype='fp16'``, reference core/base_trainer.py:30).
 Reference training step: core/seg_trainer.py:38-119.
 """
+import copy
 import os
 
 import pytest
@@ -57,75 +59,81 @@ def _grads(tr, imgs, masks, amp=True):
     tr.model.zero_grad(set_to_none=True)
     loss, _, _ = tr.compute_loss(imgs, masks)
     loss.backward()
-    g = {n: p.grad.detach().float().clone() for n, p in tr.model.named_parameters() if p.grad is not None}
-    return float(loss), g
+    g = {n: p.grad.detach().double().cpu() for n, p in tr.model.named_parameters() if p.grad is not None}
+    return float(loss.detach()), g
 
 
-def _cos(g, ref):
-    return {n: float(torch.nn.functional.cosine_similarity(g[n].flatten(), ref[n].flatten(), dim=0))
-            for n in ref if ref[n].norm() > 1e-8}
+def _grads_fp64_cpu(tr, imgs, masks):
+    """The same step in fp64 on the CPU (NCHW, stock PyTorch formulation of every op): the
+    yardstick.  The stock fp32 GPU step is NOT exact -- PyTorch's channels-last avg_pool2d
+    backward misplaces the gradient of padded windows on this ROCm build (README, ``pool.hip``),
+    which alone puts 12 of BiSeNetV2's gradients below cosine 0.9 (profiles/r4_numerics)."""
+    model = tr.model
+    tr.model = copy.deepcopy(model).cpu().double().to(memory_format=torch.contiguous_format)
+    try:
+        return _grads(tr, imgs.detach().cpu().double().contiguous(), masks.cpu(), amp=False)
+    finally:
+        tr.model = model
+
+
+def _cos(g, ref, live):
+    return {n: float(torch.dot(g[n].flatten(), ref[n].flatten()) / (g[n].norm() * ref[n].norm()))
+            for n in live}
 
 
 # BASELINE configs 2-4: DDRNet-23 + aux, BiSeNetV2 + 4 aux heads, STDC2 + detail head (OHEM).
-# Per model: (trainer overrides, HIP-fp32 loss tolerance, HIP-fp32 median / 10th-percentile
-# gradient cosine floors, HIP-bf16 vs stock-bf16 slack: median cosine, share of parameters < 0.9).
-# BiSeNetV2 (measured on MI355X at three commits of round 3, profiles/r3_numerics): the HIP bf16
-# path's median cosine to fp32 is 0.898-0.901 against stock bf16's 0.916-0.923, and 86-93 of
-# its 176 parameter gradients are < 0.9 against 66-70 -- a known gap of the bf16 path on this
-# model (its HIP fp32 path matches fp32 at median 1.0000), pinned here so it cannot grow.  Its HIP
-# fp32 10th-percentile cosine is 0.8773-0.8775 at all three commits (the floor of 0.95 it was
-# committed with never held): pinned at 0.85.
+# Measured on MI355X against the fp64 CPU step (profiles/r4_numerics/bisect.txt), median cosine /
+# parameters < 0.9: DDRNet-23 stock bf16 0.828 / 124, HIP bf16 0.838 / 122; BiSeNetV2 0.896 / 86 vs
+# 0.926 / 52; STDC2 + detail 0.394 / 151 vs 0.414 / 147 (random-init BN chains amplify bf16
+# rounding; two stock bf16 runs already differ).  HIP fp32: median 0.99998+, p10 0.9999 on all three.
 _STEP_MODELS = {
-    "ddrnet23_aux": ({}, 1e-4, 0.995, 0.99, 5e-3, 0.02),
-    "bisenetv2_aux": ({"model": "bisenetv2", "arch_type": None}, 1e-3, 0.99, 0.85, 0.035, 0.2),
-    "stdc2_detail": ({"model": "stdc", "arch_type": None, "encoder_type": "stdc2", "use_aux": False,
-                      "use_detail_head": True}, 1e-3, 0.99, 0.95, 5e-3, 0.02),
+    "ddrnet23_aux": {},
+    "bisenetv2_aux": {"model": "bisenetv2", "arch_type": None},
+    "stdc2_detail": {"model": "stdc", "arch_type": None, "encoder_type": "stdc2", "use_aux": False,
+                     "use_detail_head": True},
 }
 
 
-_OPEN = {
-    # round-3 final run on MI355X: a bf16 loss 2.3 % off the fp32 loss (8.766 vs 8.970; the check
-    # allows 2 %) -- the detail head's Dice / BCE at random init; its gradient-cosine criteria were
-    # never reached.  Open: profiles/r3_numerics/README.md
-    "stdc2_detail": "bf16 loss 2.3 % off fp32 in the round-3 final run (Dice/BCE detail head at random init)",
-}
+@pytest.mark.parametrize("name", sorted(_STEP_MODELS))
+def test_bf16_step_vs_fp64_reference(tmp_path, monkeypatch, name):
+    """One training step's loss and gradients against the fp64 CPU step.
 
-
-@pytest.mark.parametrize("name", [pytest.param(n, marks=pytest.mark.xfail(reason=_OPEN[n], strict=False))
-                                  if n in _OPEN else n for n in sorted(_STEP_MODELS)])
-def test_bf16_step_vs_fp32_reference(tmp_path, monkeypatch, name):
-    """One training step's gradients against a stock-PyTorch fp32 reference.  At random init the
-    BN-heavy backward amplifies rounding noise layer by layer (two stock bf16 runs with different
-    reduction orders already disagree on a few layers), so the bf16 yardstick is the stock bf16
-    path's own distance to fp32: the HIP bf16 path (MFMA convs, fused BN, residual-gradient
-    hand-off, depth-wise convs, OHEM / detail loss, interp) must be at least as close.  The HIP
-    fp32 path (our BN / loss / interp kernels around MIOpen convs) must agree with the fp32
-    reference tightly."""
-    kw, loss_tol, cos_med, cos_p10, med_slack, low_slack = _STEP_MODELS[name]
-    tr = _trainer(tmp_path, **kw)
+    * HIP fp32 (our BN / loss / pooling / interp / depth-wise kernels around MIOpen convs) is
+      exact to fp32: loss within 1e-5, gradient cosine median > 0.9999 and p10 > 0.999;
+    * HIP bf16 (MFMA convs, fused BN, residual-gradient hand-off, OHEM / detail loss, ...) is at
+      least as close as stock PyTorch bf16 on the same step: median cosine >= stock's - 5e-3, no
+      more parameters below 0.9 than stock (+2 %), loss within 2 % of fp64.
+    Parameters whose fp64 gradient is numerically zero (norm < 1e-4 x the median norm: BN weights
+    of GatherExpansion branches whose output feeds a scale-invariant BN) are not judged -- their
+    cosine is rounding noise on any path.  The stock bf16 loss is reported, not judged: on STDC2 it
+    is 2.3 % off fp64 because the reference formulation thresholds the detail target computed in
+    bf16 under autocast (core/seg_trainer.py:72-76); ours computes it exactly (0.27 %)."""
+    tr = _trainer(tmp_path, **_STEP_MODELS[name])
     imgs, masks = _batch(tr)
+    loss_64, g_64 = _grads_fp64_cpu(tr, imgs, masks)
     monkeypatch.setenv("RTSEG_DISABLE_HIP", "1")
-    loss_ref, g_ref = _grads(tr, imgs, masks, amp=False)
     loss_sb, g_sb = _grads(tr, imgs, masks)
     monkeypatch.delenv("RTSEG_DISABLE_HIP")
     monkeypatch.setenv("RTSEG_CONV_MFMA", "1")  # our conv kernels on every eligible layer
     loss_hb, g_hb = _grads(tr, imgs, masks)
     monkeypatch.delenv("RTSEG_CONV_MFMA")
     loss_hf, g_hf = _grads(tr, imgs, masks, amp=False)
-    assert set(g_hb) == set(g_ref) == set(g_hf)
-    for loss in (loss_sb, loss_hb):
-        assert abs(loss - loss_ref) <= 2e-2 * abs(loss_ref), (loss, loss_ref)
-    assert abs(loss_hf - loss_ref) <= loss_tol * abs(loss_ref), (loss_hf, loss_ref)
-    c_sb, c_hb, c_hf = (sorted(_cos(g, g_ref).values()) for g in (g_sb, g_hb, g_hf))
-    med = len(c_sb) // 2
-    print(f"{name}: cos median stock-bf16 {c_sb[med]:.4f} hip-bf16 {c_hb[med]:.4f} hip-fp32 {c_hf[med]:.4f}; "
-          f"p10 hip-fp32 {c_hf[len(c_hf) // 10]:.4f}; <0.9: stock {sum(c < 0.9 for c in c_sb)} "
-          f"hip {sum(c < 0.9 for c in c_hb)} of {len(c_hb)}")
-    assert c_hb[med] >= c_sb[med] - med_slack, (c_hb[med], c_sb[med])
-    assert sum(c < 0.9 for c in c_hb) <= sum(c < 0.9 for c in c_sb) + max(1, int(len(c_hb) * low_slack))
-    # DDRNet-23 measured on MI355X: median 0.9986, 10th percentile 0.9978 (fp32 reduction-order
-    # noise through ~70 BN backward passes at random init)
-    assert c_hf[med] > cos_med and c_hf[len(c_hf) // 10] > cos_p10, (c_hf[med], c_hf[len(c_hf) // 10])
+    assert set(g_hb) == set(g_64) == set(g_hf) == set(g_sb)
+    norms = sorted(float(g.norm()) for g in g_64.values())
+    live = [n for n, g in g_64.items() if float(g.norm()) > 1e-4 * norms[len(norms) // 2]]
+    assert len(live) >= 0.95 * len(g_64), (len(live), len(g_64))
+    c_sb, c_hb, c_hf = (sorted(_cos(g, g_64, live).values()) for g in (g_sb, g_hb, g_hf))
+    med, p10 = len(live) // 2, len(live) // 10
+    rel = {k: (v - loss_64) / abs(loss_64) for k, v in (("stock_bf16", loss_sb), ("hip_bf16", loss_hb),
+                                                       ("hip_fp32", loss_hf))}
+    print(f"{name}: loss rel. error vs fp64 {rel}; cos median stock-bf16 {c_sb[med]:.4f} hip-bf16 {c_hb[med]:.4f} "
+          f"hip-fp32 {c_hf[med]:.6f}; p10 hip-fp32 {c_hf[p10]:.6f}; <0.9: stock {sum(c < 0.9 for c in c_sb)} "
+          f"hip {sum(c < 0.9 for c in c_hb)} of {len(live)}")
+    assert abs(rel["hip_fp32"]) <= 1e-5, rel
+    assert c_hf[med] > 0.9999 and c_hf[p10] > 0.999, (c_hf[med], c_hf[p10])
+    assert abs(rel["hip_bf16"]) <= 2e-2, rel
+    assert c_hb[med] >= c_sb[med] - 5e-3, (c_hb[med], c_sb[med])
+    assert sum(c < 0.9 for c in c_hb) <= sum(c < 0.9 for c in c_sb) + max(1, int(0.02 * len(live)))
 
 
 def test_ddrnet23_overfits_one_batch_with_hip_kernels(tmp_path):
