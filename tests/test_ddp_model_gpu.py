@@ -1,0 +1,174 @@
+"""Model-level multi-GPU rehearsal on the one-GPU pool: 2 ranks (gloo, sharing the GPU) run the
+production ``SegTrainer.train_step`` under DDP -- HIP SyncBN (conv-epilogue statistics slabs, fp64
+all-reduce on its own process group), the pooled-vector SyncBN of the attention branches, DDP
+gradient-bucket views, the fused SGD + EMA step -- for 2 steps on their halves of a global batch,
+against ONE process stepping the concatenated batch.
+
+* fp32 (HIP BN / pooling / loss / interp kernels, MIOpen convs): parameters, EMA weights and BN
+  running statistics of the 2-rank run equal the 1-process run's (SyncBN makes every BN see the
+  global batch; DDP averages the per-rank mean gradients, equal halves);
+* bf16 (+ our MFMA convs): replicas stay identical, the fused step ran, no gradient-stride
+  warning, and the update direction agrees with the 1-process run (bf16 rounding at random init
+  moves individual layers, not the whole update).
+
+Reference wiring: utils/parallel.py:34-43 (SyncBN conversion + DDP), core/seg_trainer.py:38-119.
+RCCL itself needs one GPU per rank and runs on the driver's 8-GPU node; gloo exercises the same
+code paths here (``RTSEG_DIST_BACKEND=gloo``, parallel/ddp.py:set_device).
+"""
+import os
+import socket
+import warnings
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+MODELS = {
+    "stdc2_aux": {"model": "stdc", "arch_type": None, "encoder_type": "stdc2", "use_aux": True},
+    "bisenetv2_aux": {"model": "bisenetv2", "arch_type": None, "use_aux": True},
+}
+GLOBAL_BS, SIZE, STEPS = 4, (128, 256), 2
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _batches():
+    from realtime_semantic_segmentation_pytorch_amd.datasets.synthetic import _masks_like
+
+    g = torch.Generator().manual_seed(7)
+    out = []
+    for _ in range(STEPS):
+        img = torch.randn(GLOBAL_BS, 3, *SIZE, generator=g)
+        out.append((img, _masks_like(g, GLOBAL_BS, SIZE[0], SIZE[1], 19, 255, "cpu")))
+    return out
+
+
+def _run(rank, world, port, out, name, amp):
+    """One rank (world > 1: under DDP) -> its state after STEPS steps, saved to ``out``."""
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "RTSEG_DISABLE_HIP", "RTSEG_CONV_MFMA"):
+        os.environ.pop(k, None)
+    if world > 1:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), LOCAL_RANK=str(rank),
+                          WORLD_SIZE=str(world), RTSEG_DIST_BACKEND="gloo")
+    from realtime_semantic_segmentation_pytorch_amd import ops
+    from realtime_semantic_segmentation_pytorch_amd.configs import BaseConfig
+    from realtime_semantic_segmentation_pytorch_amd.core import SegTrainer
+    from realtime_semantic_segmentation_pytorch_amd.parallel import de_parallel
+
+    assert ops.load()
+    c = BaseConfig()
+    c.dataset, c.num_class = "cityscapes", 19
+    for k, v in MODELS[name].items():
+        setattr(c, k, v)
+    c.synthetic_data, c.synthetic_len, c.synthetic_size = True, 8, SIZE
+    c.crop_size, c.crop_h, c.crop_w = SIZE[0], SIZE[0], SIZE[1]
+    c.train_bs, c.val_bs, c.total_epoch = GLOBAL_BS // world, GLOBAL_BS // world, 4
+    c.amp_training, c.amp_dtype, c.channels_last = amp, "bf16", True
+    c.base_workers, c.use_tb, c.save_ckpt, c.load_ckpt, c.use_ema = 0, False, False, False, True
+    c.optimizer_type, c.lr_policy = "sgd", "cos_warmup"
+    c.save_dir = os.path.join(out, f"save{world}_{rank}")
+    c.init_dependent_config()
+    tr = SegTrainer(c)
+    tr.parallel_model(c)
+    sl = slice(rank * GLOBAL_BS // world, (rank + 1) * GLOBAL_BS // world)
+    fused, losses = [], []
+    with warnings.catch_warnings(record=True) as caught:
+        warnings.simplefilter("always")
+        for img, msk in _batches():
+            imgs, masks = tr._prep(img[sl], msk[sl])
+            loss, _ = tr.train_step(imgs, masks)
+            losses.append(float(loss))
+            fused.append(bool(getattr(tr.optimizer, "last_step_fused", False)))
+        torch.cuda.synchronize()
+    stride_warn = [str(w.message) for w in caught if "stride" in str(w.message).lower()]
+    model = de_parallel(tr.model)
+    state = {"params": {n: p.detach().float().cpu() for n, p in model.named_parameters()},
+             "buffers": {n: b.detach().float().cpu() for n, b in model.named_buffers()},
+             "ema": {n: v.detach().float().cpu() for n, v in tr.ema_model.ema.state_dict().items()},
+             "fused": fused, "ema_fused": tr.ema_fused, "losses": losses, "stride_warn": stride_warn,
+             "synced_bn": sum(isinstance(m, torch.nn.SyncBatchNorm) for m in model.modules())}
+    torch.save(state, os.path.join(out, f"{name}_{int(amp)}_w{world}_r{rank}.pt"))
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _init_params(name, out):
+    """Initial parameters (same seed as the runs) for update deltas."""
+    from realtime_semantic_segmentation_pytorch_amd.configs import BaseConfig
+    from realtime_semantic_segmentation_pytorch_amd.models import get_model
+    from realtime_semantic_segmentation_pytorch_amd.utils import set_seed
+
+    c = BaseConfig()
+    c.num_class = 19
+    for k, v in MODELS[name].items():
+        setattr(c, k, v)
+    set_seed(c.random_seed)
+    return {n: p.detach().float() for n, p in get_model(c).named_parameters()}
+
+
+def _spawn(world, port, out, name, amp):
+    ctx = mp.get_context("spawn")
+    ps = [ctx.Process(target=_run, args=(r, world, port, out, name, amp)) for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(240)
+    for p in ps:
+        if p.is_alive():
+            p.kill()
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+
+
+def _flat(d, keys):
+    return torch.cat([d[k].flatten().double() for k in keys])
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("name", sorted(MODELS))
+def test_ddp_two_ranks_match_one_process(tmp_path, name):
+    out = str(tmp_path)
+    init = _init_params(name, out)
+    res = {}
+    for amp in (False, True):
+        _spawn(1, _port(), out, name, amp)
+        _spawn(2, _port(), out, name, amp)
+        one = torch.load(os.path.join(out, f"{name}_{int(amp)}_w1_r0.pt"), weights_only=True)
+        r0, r1 = (torch.load(os.path.join(out, f"{name}_{int(amp)}_w2_r{r}.pt"), weights_only=True)
+                  for r in range(2))
+        assert r0["synced_bn"] > 0 and one["synced_bn"] == 0
+        for st in (one, r0, r1):
+            assert all(st["fused"]) and st["ema_fused"], (st["fused"], st["ema_fused"])
+            assert not st["stride_warn"], st["stride_warn"]
+            assert all(torch.isfinite(torch.tensor(st["losses"])))
+        # DDP replicas: identical parameters, EMA and buffers on both ranks
+        for part in ("params", "ema", "buffers"):
+            for k in r0[part]:
+                torch.testing.assert_close(r0[part][k], r1[part][k], rtol=0, atol=0, msg=f"{part} {k}")
+        keys = sorted(init)
+        d1 = _flat(one["params"], keys) - _flat(init, keys)
+        d2 = _flat(r0["params"], keys) - _flat(init, keys)
+        cos = float(torch.dot(d1, d2) / (d1.norm() * d2.norm()))
+        rel = float((d1 - d2).norm() / d1.norm())
+        ema_keys = sorted(k for k in one["ema"] if one["ema"][k].is_floating_point() and k in init)
+        e1 = _flat(one["ema"], ema_keys) - _flat(init, ema_keys)
+        e2 = _flat(r0["ema"], ema_keys) - _flat(init, ema_keys)
+        ema_rel = float((e1 - e2).norm() / e1.norm())
+        rm = [k for k in one["buffers"] if k.endswith("running_mean") or k.endswith("running_var")]
+        bn_rel = float((_flat(one["buffers"], rm) - _flat(r0["buffers"], rm)).norm() / _flat(one["buffers"], rm).norm())
+        res[amp] = (cos, rel, ema_rel, bn_rel)
+        print(f"{name} amp={amp}: update cos {cos:.6f} rel {rel:.2e}; EMA rel {ema_rel:.2e}; BN stats rel {bn_rel:.2e}; "
+              f"losses 1-proc {one['losses']} 2-rank {r0['losses']}/{r1['losses']}")
+    cos, rel, ema_rel, bn_rel = res[False]
+    # fp32: only reduction order (SyncBN fp64 sums, DDP averaging of equal halves) differs
+    assert cos > 0.9999 and rel < 2e-2 and ema_rel < 2e-2 and bn_rel < 1e-4, res[False]
+    cos, rel, ema_rel, bn_rel = res[True]
+    assert cos > 0.95 and bn_rel < 2e-2, res[True]

@@ -1,18 +1,22 @@
 #!/bin/bash
-# PMC passes (one counter set per run) over conv kernels: MFMA busy vs waits vs issue
+# PMC passes (one counter set per run) over conv kernels: MFMA busy vs waits vs issue.
+# usage: tools/gpu_pmc.sh OUTDIR kind:cin,h,w,cout [...]   (kinds: tools/conv_probe.py --kind)
 set -o pipefail
-mkdir -p gpurun_out/pmc
-cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
+OUT=$R/$1; shift
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp
 P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA"
 P2="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM"
-for kind in halo igemm; do
-  for shape in 128,128,256,128 64,256,512,64; do
-    i=0
-    for P in "$P1" "$P2"; do
-      i=$((i+1))
-      timeout -s KILL 90 rocprofv3 --pmc $P -d $R/gpurun_out/pmc/${kind}_${shape//,/x}_p$i -o run -- python3 $R/tools/conv_probe.py --kind $kind --shape $shape --iters 10 > $R/gpurun_out/pmc/${kind}_${shape//,/x}_p$i.log 2>&1 || { echo "FAIL $kind $shape $i"; tail -5 $R/gpurun_out/pmc/${kind}_${shape//,/x}_p$i.log; exit 1; }
-    done
+for spec in "$@"; do
+  kind=${spec%%:*}; shape=${spec#*:}
+  extra=""
+  if [[ $kind == *+st ]]; then kind=${kind%+st}; extra="--stats"; fi
+  tag=${spec//[:,+]/_}
+  i=0
+  for P in "$P1" "$P2"; do
+    i=$((i+1))
+    timeout -s KILL 90 rocprofv3 --pmc $P -d $OUT/${tag}_p$i -o run -- python3 $R/tools/conv_probe.py --kind $kind --shape $shape --iters 10 $extra > $OUT/${tag}_p$i.log 2>&1 || { echo "FAIL $spec pass $i"; tail -5 $OUT/${tag}_p$i.log; exit 1; }
   done
 done
-echo ok
+python3 $R/tools/pmc_summary.py $OUT/*_p? > $OUT/summary.txt && echo ok
