@@ -121,7 +121,9 @@ def test_bf16_step_vs_fp64_reference(tmp_path, monkeypatch, name):
     assert set(g_hb) == set(g_64) == set(g_hf) == set(g_sb)
     norms = sorted(float(g.norm()) for g in g_64.values())
     live = [n for n, g in g_64.items() if float(g.norm()) > 1e-4 * norms[len(norms) // 2]]
-    assert len(live) >= 0.95 * len(g_64), (len(live), len(g_64))
+    # BiSeNetV2: 157 of 189 (conv biases ahead of a BN and BN weights ahead of a scale-invariant BN
+    # have mathematically zero gradients)
+    assert len(live) >= 0.75 * len(g_64), (len(live), len(g_64))
     c_sb, c_hb, c_hf = (sorted(_cos(g, g_64, live).values()) for g in (g_sb, g_hb, g_hf))
     med, p10 = len(live) // 2, len(live) // 10
     rel = {k: (v - loss_64) / abs(loss_64) for k, v in (("stock_bf16", loss_sb), ("hip_bf16", loss_hb),
