@@ -41,7 +41,8 @@ ConvGeom geom(int64_t N, int64_t Cin, int64_t H, int64_t W, int64_t Cout, int64_
 std::tuple<at::Tensor, at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::Tensor& wk, at::IntArrayRef stride,
                                                  at::IntArrayRef padding, at::IntArrayRef dilation, bool stats,
                                                  const std::optional<at::Tensor>& scale_shift,
-                                                 const std::optional<at::Tensor>& residual, int64_t act, bool halo) {
+                                                 const std::optional<at::Tensor>& residual, int64_t act, int kind) {
+  const bool halo = kind == 1, wres = kind == 2;
   check_act(x, "input");
   TORCH_CHECK(wk.is_cuda() && wk.dim() == 4 && wk.scalar_type() == at::kBFloat16 && wk.is_contiguous() &&
                   wk.size(3) == x.size(1),
@@ -52,6 +53,9 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::
   if (halo) {
     TORCH_CHECK(conv_halo_supported(g, 0),
                 "rtseg.conv_halo: needs stride 1, taps within 3 x 3, Cin % 64 == 0, Cout % 64 == 0");
+  } else if (wres) {
+    TORCH_CHECK(conv_wres_supported(g, 0), "rtseg.conv_wres: needs 3 x 3 / stride 1 / pad 1, Cin == 64, Cout % 64 == 0");
+    TORCH_CHECK(!(scale_shift.has_value() && scale_shift->defined()), "rtseg.conv_wres: no inference BN epilogue");
   } else {
     TORCH_CHECK(conv_igemm_supported(g, 0), "rtseg.conv_igemm: needs Cin % 64 == 0, Cout % 8 == 0, <= 49 taps");
   }
@@ -61,7 +65,8 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::
   g.part = nullptr; g.scale_shift = nullptr; g.res = nullptr; g.act = static_cast<int>(act);
   at::Tensor part;
   if (stats) {
-    part = at::empty({halo ? conv_halo_slabs(g) : conv_igemm_slabs(g), 2 * g.cout}, x.options().dtype(at::kFloat));
+    part = at::empty({halo ? conv_halo_slabs(g) : wres ? conv_wres_slabs(g) : conv_igemm_slabs(g), 2 * g.cout},
+                     x.options().dtype(at::kFloat));
     g.part = part.data_ptr<float>();
   }
   if (scale_shift.has_value() && scale_shift->defined()) {
@@ -80,6 +85,7 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::
                 "rtseg.conv_igemm: residual / activation need the BN epilogue (scale_shift)");
   }
   if (halo) launch_conv_halo_fwd(g, cur_stream());
+  else if (wres) launch_conv_wres_fwd(g, cur_stream());
   else launch_conv_igemm_fwd(g, cur_stream());
   if (stats && part.size(0) > 256) {  // fold the per-tile rows so the BN finalize stays cheap
     const int rows = static_cast<int>(part.size(0));
@@ -95,7 +101,7 @@ std::tuple<at::Tensor, at::Tensor> conv_igemm(const at::Tensor& x, const at::Ten
                                               at::IntArrayRef padding, at::IntArrayRef dilation, bool stats,
                                               const std::optional<at::Tensor>& scale_shift,
                                               const std::optional<at::Tensor>& residual, int64_t act) {
-  return conv_fwd_impl(x, wk, stride, padding, dilation, stats, scale_shift, residual, act, false);
+  return conv_fwd_impl(x, wk, stride, padding, dilation, stats, scale_shift, residual, act, 0);
 }
 
 // the halo-tiled kernel (conv_halo.hip): stride-1 convs whose taps fit a 3 x 3 footprint
@@ -103,13 +109,20 @@ std::tuple<at::Tensor, at::Tensor> conv_halo(const at::Tensor& x, const at::Tens
                                              at::IntArrayRef padding, at::IntArrayRef dilation, bool stats,
                                              const std::optional<at::Tensor>& scale_shift,
                                              const std::optional<at::Tensor>& residual, int64_t act) {
-  return conv_fwd_impl(x, wk, stride, padding, dilation, stats, scale_shift, residual, act, true);
+  return conv_fwd_impl(x, wk, stride, padding, dilation, stats, scale_shift, residual, act, 1);
+}
+
+// the weights-resident halo kernel (conv_wres.hip): 3 x 3 stride-1 convs with Cin == 64
+std::tuple<at::Tensor, at::Tensor> conv_wres(const at::Tensor& x, const at::Tensor& wk, at::IntArrayRef stride,
+                                             at::IntArrayRef padding, at::IntArrayRef dilation, bool stats) {
+  return conv_fwd_impl(x, wk, stride, padding, dilation, stats, std::nullopt, std::nullopt, 0, 2);
 }
 
 // dy [N,Cout,Ho,Wo] CL bf16, wt [Cin,KH,KW,Cout] bf16 -> dx [N,Cin,H,W] CL bf16
 at::Tensor conv_dgrad_impl(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
                            at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
-                           const std::optional<at::Tensor>& bias, const std::optional<at::Tensor>& addend, bool halo) {
+                           const std::optional<at::Tensor>& bias, const std::optional<at::Tensor>& addend, int kind) {
+  const bool halo = kind == 1, wres = kind == 2;
   check_act(dy, "grad_output");
   TORCH_CHECK(x_size.size() == 4, "rtseg.conv_igemm_dgrad: x_size must be [N, Cin, H, W]");
   TORCH_CHECK(wt.is_cuda() && wt.dim() == 4 && wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() &&
@@ -123,6 +136,9 @@ at::Tensor conv_dgrad_impl(const at::Tensor& dy, const at::Tensor& wt, at::IntAr
     TORCH_CHECK(conv_halo_supported(g, 1),
                 "rtseg.conv_halo_dgrad: needs stride 1, taps within 3 x 3, Cin % 64 == 0, Cout % 64 == 0");
     TORCH_CHECK(!(bias.has_value() && bias->defined()), "rtseg.conv_halo_dgrad: no bias");
+  } else if (wres) {
+    TORCH_CHECK(conv_wres_supported(g, 1), "rtseg.conv_wres_dgrad: needs 3 x 3 / stride 1 / pad 1, Cout == 64, Cin % 64 == 0");
+    TORCH_CHECK(!(bias.has_value() && bias->defined()), "rtseg.conv_wres_dgrad: no bias");
   } else {
     TORCH_CHECK(conv_igemm_supported(g, 1), "rtseg.conv_igemm_dgrad: needs Cout % 64 == 0, Cin % 8 == 0");
   }
@@ -143,6 +159,7 @@ at::Tensor conv_dgrad_impl(const at::Tensor& dy, const at::Tensor& wt, at::IntAr
     g.res = addend->data_ptr();
   }
   if (halo) launch_conv_halo_dgrad(g, cur_stream());
+  else if (wres) launch_conv_wres_dgrad(g, cur_stream());
   else launch_conv_igemm_dgrad(g, cur_stream());
   return dx;
 }
@@ -150,13 +167,19 @@ at::Tensor conv_dgrad_impl(const at::Tensor& dy, const at::Tensor& wt, at::IntAr
 at::Tensor conv_igemm_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
                             at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
                             const std::optional<at::Tensor>& bias, const std::optional<at::Tensor>& addend) {
-  return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, bias, addend, false);
+  return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, bias, addend, 0);
 }
 
 at::Tensor conv_halo_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
                            at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
                            const std::optional<at::Tensor>& addend) {
-  return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, std::nullopt, addend, true);
+  return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, std::nullopt, addend, 1);
+}
+
+at::Tensor conv_wres_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
+                           at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
+                           const std::optional<at::Tensor>& addend) {
+  return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, std::nullopt, addend, 2);
 }
 
 // x [N,Cin,H,W], dy [N,Cout,Ho,Wo] (CL bf16) -> dw fp32 [Cout,Cin,KH,KW]
@@ -191,6 +214,9 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
         "Tensor? scale_shift, Tensor? residual, int act) -> (Tensor, Tensor)");
   m.def("conv_halo_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
         "Tensor? addend=None) -> Tensor");
+  m.def("conv_wres(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats) -> (Tensor, Tensor)");
+  m.def("conv_wres_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
+        "Tensor? addend=None) -> Tensor");
   m.def("conv_igemm_wgrad(Tensor x, Tensor dy, int kh, int kw, int[] stride, int[] padding, int[] dilation, "
         "bool channels_last=False) -> Tensor");
 }
@@ -200,5 +226,7 @@ TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
   m.impl("conv_igemm_dgrad", &rtseg::conv_igemm_dgrad);
   m.impl("conv_halo", &rtseg::conv_halo);
   m.impl("conv_halo_dgrad", &rtseg::conv_halo_dgrad);
+  m.impl("conv_wres", &rtseg::conv_wres);
+  m.impl("conv_wres_dgrad", &rtseg::conv_wres_dgrad);
   m.impl("conv_igemm_wgrad", &rtseg::conv_igemm_wgrad);
 }

@@ -187,6 +187,15 @@ int conv_halo_slabs(const ConvGeom& g);
 void launch_conv_halo_fwd(const ConvGeom& g, hipStream_t st);
 void launch_conv_halo_dgrad(const ConvGeom& g, hipStream_t st);
 
+// ---- conv_wres.hip ------------------------------------------------------------
+// Weights-resident halo conv: 3 x 3, stride 1, pad 1, dilation 1, 64 reduction channels
+// (forward: Cin == 64; data gradient: Cout == 64), output channels % 64 == 0; forward (+ BN
+// statistics slab of conv_wres_slabs(g) rows) and data gradient (g.res = optional addend).
+bool conv_wres_supported(const ConvGeom& g, int mode);
+int conv_wres_slabs(const ConvGeom& g);
+void launch_conv_wres_fwd(const ConvGeom& g, hipStream_t st);
+void launch_conv_wres_dgrad(const ConvGeom& g, hipStream_t st);
+
 // ---- gate.hip -----------------------------------------------------------------
 // out = x * s (mul), x * (1 + s) (residual), x * s + y * (1 - s) (blend); s = att or
 // sigmoid(att), broadcast per (n, c) (att fp32 [N, C]), per pixel (fp32 [N, H*W]) or full (x's

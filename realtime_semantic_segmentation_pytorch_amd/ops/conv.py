@@ -16,6 +16,9 @@ each routed to our kernel or to MIOpen:
   halo-tiled kernel ``conv_halo`` (``csrc/kernels/conv_halo.hip``): the input tile + halo of a
   64-channel chunk is staged in LDS once and every tap reads a shifted window of it, instead of
   re-gathering each pixel once per tap;
+* 3 x 3 stride-1 convs that sum over exactly 64 channels (forward Cin = 64, data gradient of
+  Cout = 64 -- DDRNet's layer1 at 256 x 512) also have ``conv_wres`` (``csrc/kernels/conv_wres.hip``):
+  the block's whole 64 x 9 x 64 weight slice stays in LDS and only the input halo streams;
 * weight gradient: ``conv_igemm_wgrad`` -- split-K over pixels with transposed LDS reads, fp32
   partial tiles reduced deterministically straight into the fp32 weight-gradient layout
   (MIOpen's wrw needs a zero-filled output buffer every call);
@@ -26,7 +29,8 @@ Each pass of each layer shape is timed once against MIOpen the first time it run
 (``cudnn.benchmark``-style; never during HIP-graph capture) and the faster one is kept --
 ``decisions()`` lists the outcomes.  ``RTSEG_CONV_MFMA=0`` disables our kernels, ``=1`` forces
 them wherever they apply; ``RTSEG_CONV_HALO=0`` drops the halo kernel from the candidates,
-``=1`` puts it first (so ``RTSEG_CONV_MFMA=1`` forces it where it applies).
+``=1`` puts it first (so ``RTSEG_CONV_MFMA=1`` forces it where it applies); ``RTSEG_CONV_WRES``
+likewise for ``conv_wres``.
 """
 from __future__ import annotations
 
@@ -120,10 +124,22 @@ def halo_ok(conv, reduce_c: int, out_c: int) -> bool:
     return reduce_c % 64 == 0 and out_c % 64 == 0 and max(reduce_c, out_c) <= 8192
 
 
+def wres_ok(conv, reduce_c: int, out_c: int) -> bool:
+    """Shapes ``conv_wres`` takes (``csrc/kernels/conv_wres.hip``): 3 x 3, stride 1, pad 1,
+    dilation 1, exactly 64 channels summed over, a multiple of 64 produced."""
+    if os.environ.get("RTSEG_CONV_WRES", "auto") == "0":
+        return False
+    return (tuple(conv.kernel_size) == (3, 3) and tuple(conv.stride) == (1, 1) and tuple(conv.padding) == (1, 1)
+            and tuple(conv.dilation) == (1, 1) and reduce_c == 64 and out_c % 64 == 0)
+
+
 def _order(cands):
-    """``RTSEG_CONV_HALO=1``: the halo candidate first (what ``RTSEG_CONV_MFMA=1`` forces)."""
+    """``RTSEG_CONV_HALO=1`` / ``RTSEG_CONV_WRES=1``: that candidate first (what
+    ``RTSEG_CONV_MFMA=1`` forces)."""
     if _halo_mode() == "1":
         cands.sort(key=lambda c: c[0] != "halo" and not c[0].startswith("halo"))
+    if os.environ.get("RTSEG_CONV_WRES") == "1":
+        cands.sort(key=lambda c: c[0] != "wres")
     return cands
 
 
@@ -200,8 +216,8 @@ def _choose(key, candidates):
     if got is not None:  # by name: the candidate list may differ (e.g. RTSEG_CONV_HALO changed)
         if got[1] in names:
             return names.index(got[1])
-    saved = _tune_db().get(repr(key))
-    if saved in names:  # an earlier run's winner for this shape (persistent tuning database)
+    saved = _db_pick(_tune_db().get(repr(key)), names)
+    if saved is not None:  # an earlier run's winner for this shape (persistent tuning database)
         _DECISIONS[key] = (names.index(saved), saved, [])
         return names.index(saved)
     if torch.cuda.is_current_stream_capturing():
@@ -213,8 +229,24 @@ def _choose(key, candidates):
         times = [min(r[i] for r in rounds) for i in range(len(candidates))]
     best = min(range(len(times)), key=times.__getitem__)
     _DECISIONS[key] = (best, candidates[best][0], [round(t, 4) for t in times])
-    _db_record(key, candidates[best][0])
+    _db_record(key, candidates[best][0] + "@" + "+".join(sorted(names)))
     return best
+
+
+# candidates of the round-3 tuning database, whose entries are bare winner names
+_LEGACY_CANDS = {"igemm", "igemm_nostats", "halo", "mfma", "miopen"}
+
+
+def _db_pick(entry, names):
+    """The tuning-database winner for a candidate list, or None: an entry ``winner@c1+c2+...``
+    counts only for the same candidate set (a new kernel family re-times the shapes it applies
+    to); a bare legacy entry only when every candidate predates the record format."""
+    if not entry:
+        return None
+    win, _, among = entry.partition("@")
+    if among:
+        return win if win in names and sorted(among.split("+")) == sorted(names) else None
+    return win if win in names and set(names) <= _LEGACY_CANDS else None
 
 
 # ----------------------------------------------------------------------------- autograd node
@@ -235,6 +267,8 @@ class _ConvFn(torch.autograd.Function):
             y, part = ops().conv_igemm(x, wk, stride, padding, dilation, False, None, None, 0)
         elif impl == "halo":
             y, part = ops().conv_halo(x, wk, stride, padding, dilation, stats, None, None, 0)
+        elif impl == "wres":
+            y, part = ops().conv_wres(x, wk, stride, padding, dilation, stats)
         elif impl == "mfma":
             y, part = ops().conv_mfma(x, wk, stride, padding, dilation, stats, None, None, 0)
         else:
@@ -287,6 +321,8 @@ def _fwd_impl(x, wk, conv, key, stats) -> str:
             cands.append(("igemm_nostats", nostats))
         if halo_ok(conv, cin, cout):
             cands.append(("halo", lambda: ops().conv_halo(x, wk, stride, padding, dilation, stats, None, None, 0)))
+        if wres_ok(conv, cin, cout):
+            cands.append(("wres", lambda: ops().conv_wres(x, wk, stride, padding, dilation, stats)))
     elif cin % 32 == 0 and cout % 8 == 0:
         cands.append(("mfma", lambda: ops().conv_mfma(x, wk, stride, padding, dilation, stats, None, None, 0)))
     if not cands:
@@ -320,6 +356,11 @@ def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None):
             wt.append(wk.permute(3, 1, 2, 0).contiguous())
         return ops().conv_halo_dgrad(dy, wt[0], list(x.shape), stride, padding, dilation, addend)
 
+    def wres():
+        if not wt:
+            wt.append(wk.permute(3, 1, 2, 0).contiguous())
+        return ops().conv_wres_dgrad(dy, wt[0], list(x.shape), stride, padding, dilation, addend)
+
     def miopen():
         return torch.ops.aten.convolution_backward(dy, x, wk.permute(0, 3, 1, 2), None, stride, padding, dilation, False,
                                                    [0, 0], 1, [True, False, False])[0]
@@ -327,10 +368,12 @@ def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None):
     cands = [("igemm", ours)] if cout % 64 == 0 and cin % 8 == 0 else []
     if halo_ok(conv, cout, cin):
         cands.append(("halo", halo))
+    if wres_ok(conv, cout, cin):
+        cands.append(("wres", wres))
     cands.append(("miopen", miopen))
     name, fn = cands[_choose(("dgrad",) + key, _order(cands))]
     dx = fn()
-    if addend is not None and name not in ("igemm", "halo"):
+    if addend is not None and name not in ("igemm", "halo", "wres"):
         dx = dx + addend
     return dx
 

@@ -7,7 +7,12 @@ run and the benchmark use the same MIOpen configuration.
   (they take tens of seconds per shape at 1024x2048 and never win there, but they are the
   fallback for the zoo's degenerate dilated convs, so a trainer process keeps them);
 * ``torch.backends.cudnn.benchmark`` (MIOpen find mode) for the convs that stay on MIOpen
-  (``config.cudnn_benchmark``, default on) on the models it is verified for.
+  (``config.cudnn_benchmark``) on the models it is verified for.  OFF by default since round 4:
+  a BiSeNetV2 training run at a new shape (batch 8, 256 x 512) left the GPU faulted in its first
+  backward, where find mode runs MIOpen's exhaustive solver search on every new shape (the
+  fault class of rounds 1-3, profiles/r3_fault).  bench.py turns it on for its one config,
+  whose shapes have run the search without a fault in every round; elsewhere MIOpen runs in
+  immediate mode (the find database in ``miopen_db/`` where it has the shape, else heuristics).
 
 Environment variables already set by the user win.  Must run before the first convolution.
 """

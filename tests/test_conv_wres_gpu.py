@@ -1,0 +1,125 @@
+"""Weights-resident halo conv (csrc/kernels/conv_wres.hip) vs fp32 PyTorch: forward (+ BN-statistics
+slab) of 3x3 / stride-1 / pad-1 convs with Cin = 64 and the data gradient (+ residual-gradient
+addend) of such convs with Cout = 64 -- partial tiles (H % 8, W % 32), several 64-channel output
+slices, fewer tiles than blocks, and many tiles per block (statistics summed over a block's tiles
+before its slab row).  Reference layers: DDRNet-23 layer1 RB blocks (ddrnet.py:168-191)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from realtime_semantic_segmentation_pytorch_amd import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+# forward geometries (n, h, w, cout), Cin = 64
+FWD = [(2, 17, 70, 64), (3, 8, 64, 128), (1, 5, 7, 64), (8, 130, 256, 64), (2, 33, 97, 192)]
+# data-gradient geometries (n, h, w, cin) of forward convs with Cout = 64
+DGRAD = [(2, 17, 70, 64), (3, 9, 40, 128), (8, 66, 256, 64), (1, 6, 33, 192)]
+
+
+@pytest.fixture(autouse=True)
+def _lib():
+    assert ops.load(), "HIP extension must load on the GPU box"
+
+
+def _t(shape, g, scale=1.0):
+    return (torch.randn(shape, generator=g) * scale).to(DEV, torch.bfloat16)
+
+
+def _close(got, ref, tol):
+    torch.testing.assert_close(got.float(), ref, atol=tol * ref.abs().max().item() + 1e-6, rtol=tol)
+
+
+@pytest.mark.parametrize("geom", FWD)
+def test_wres_forward_and_stats(geom):
+    n, h, w, cout = geom
+    g = torch.Generator().manual_seed(0)
+    x = _t((n, 64, h, w), g).contiguous(memory_format=torch.channels_last)
+    wt = _t((cout, 64, 3, 3), g, 1 / 24)
+    wk = wt.permute(0, 2, 3, 1).contiguous()
+    y, part = torch.ops.rtseg.conv_wres(x, wk, [1, 1], [1, 1], [1, 1], True)
+    ref = F.conv2d(x.float(), wt.float(), None, 1, 1)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    _close(y, ref, 2e-2)
+    rf = ref.double()  # the slab holds the statistics of the fp32 outputs (the accumulators)
+    torch.testing.assert_close(part[:, :cout].double().sum(0), rf.sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(part[:, cout:].double().sum(0), rf.square().sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+    assert part.shape[0] <= 256
+    y1, p1 = torch.ops.rtseg.conv_wres(x, wk, [1, 1], [1, 1], [1, 1], True)
+    assert torch.equal(p1, part) and torch.equal(y1, y)  # deterministic
+    y2, p2 = torch.ops.rtseg.conv_wres(x, wk, [1, 1], [1, 1], [1, 1], False)
+    assert torch.equal(y2, y) and p2.numel() == 0
+
+
+@pytest.mark.parametrize("geom", DGRAD)
+@pytest.mark.parametrize("with_addend", [False, True])
+def test_wres_dgrad(geom, with_addend):
+    n, h, w, cin = geom
+    g = torch.Generator().manual_seed(2)
+    cl = dict(memory_format=torch.channels_last)
+    wt = _t((64, cin, 3, 3), g, 1 / 24)
+    dy = _t((n, 64, h, w), g).contiguous(**cl)
+    add = _t((n, cin, h, w), g).contiguous(**cl)
+    dx = torch.ops.rtseg.conv_wres_dgrad(dy, wt.permute(1, 2, 3, 0).contiguous(), [n, cin, h, w], [1, 1], [1, 1],
+                                         [1, 1], add if with_addend else None)
+    ref = torch.nn.grad.conv2d_input((n, cin, h, w), wt.float(), dy.float(), 1, 1, 1)
+    _close(dx, ref + add.float() if with_addend else ref, 2e-2)
+
+
+def test_wres_rejects_other_shapes():
+    g = torch.Generator().manual_seed(1)
+    x = _t((1, 128, 8, 32), g).contiguous(memory_format=torch.channels_last)
+    wk = _t((64, 3, 3, 128), g)
+    with pytest.raises(RuntimeError, match="conv_wres"):
+        torch.ops.rtseg.conv_wres(x, wk, [1, 1], [1, 1], [1, 1], False)
+    x = _t((1, 64, 8, 32), g).contiguous(memory_format=torch.channels_last)
+    with pytest.raises(RuntimeError, match="conv_wres"):  # stride 2
+        torch.ops.rtseg.conv_wres(x, _t((64, 3, 3, 64), g), [2, 2], [1, 1], [1, 1], False)
+
+
+def test_wres_routed_training_step(monkeypatch):
+    """DDRNet RB chain (64 channels) with conv_wres forced first vs the gather kernel: outputs and
+    gradients agree up to bf16 rounding, and the routing really called the new kernels."""
+    from realtime_semantic_segmentation_pytorch_amd.models.ddrnet import RB
+    from realtime_semantic_segmentation_pytorch_amd.ops import conv as conv_mod
+
+    torch.manual_seed(0)
+    net = ops.convert_batchnorm(torch.nn.Sequential(RB(64, 64), RB(64, 64))).to(DEV)
+    net = net.to(memory_format=torch.channels_last).train()
+    x0 = torch.randn(2, 64, 24, 72, device=DEV).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(2, 64, 24, 72, device=DEV)
+    calls = []
+
+    class _Spy:  # records which rtseg ops the conv routing calls
+        def __getattr__(self, name):
+            calls[-1].add(name)
+            return getattr(torch.ops.rtseg, name)
+
+    spy = _Spy()
+    monkeypatch.setattr(conv_mod, "ops", lambda: spy)
+    res = []
+    for env in ({"RTSEG_CONV_MFMA": "1", "RTSEG_CONV_WRES": "1"}, {"RTSEG_CONV_MFMA": "1", "RTSEG_CONV_WRES": "0"}):
+        for k in ("RTSEG_CONV_MFMA", "RTSEG_CONV_HALO", "RTSEG_CONV_WRES", "RTSEG_DISABLE_HIP"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        calls.append(set())
+        net.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = net(x)
+        (y.float() * gy).sum().backward()
+        res.append((y.float().detach(), x.grad.float().clone(),
+                    {n: p.grad.float().clone() for n, p in net.named_parameters()}))
+    (y0, gx0, gp0), (y1, gx1, gp1) = res
+
+    def rel(a, b):
+        return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+    assert rel(y0, y1) < 1e-2
+    assert rel(gx0, gx1) < 2e-2
+    for n, g in gp1.items():
+        assert rel(gp0[n], g) < 3e-2, n
+    assert {"conv_wres", "conv_wres_dgrad"} <= calls[0], calls[0]
+    assert not {"conv_wres", "conv_wres_dgrad"} & calls[1], calls[1]

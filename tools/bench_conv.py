@@ -5,7 +5,8 @@ Run on the GPU box:  python tools/bench_conv.py [--batch 32] [--iters 20] [--onl
 One line per shape and pass: relative max error vs MIOpen, time (us) of MIOpen and of ours,
 TFLOP/s of both.  Ours: ``conv_igemm`` (+ its BN-statistics epilogue, ``fwd+st``),
 ``conv_igemm_dgrad``, ``conv_igemm_wgrad``, and for stride-1 3x3 shapes the halo-tiled
-``conv_halo`` (``halo``, ``halo+st``) / ``conv_halo_dgrad`` (``halo_dg``); MIOpen: ``F.conv2d`` / ``aten.convolution_backward``
+``conv_halo`` (``halo``, ``halo+st``) / ``conv_halo_dgrad`` (``halo_dg``), and where the conv sums
+over 64 channels the weights-resident ``conv_wres`` (``wres``, ``wres+st``, ``wres_dg``); MIOpen: ``F.conv2d`` / ``aten.convolution_backward``
 (MIOpen find mode, i.e. its best solver per shape).
 """
 import argparse
@@ -84,6 +85,7 @@ def main():
         dy = torch.randn_like(y_ref).contiguous(memory_format=torch.channels_last)
         tag = f"{n}x{cin}x{h}x{w}->{cout} k{k}s{s}"
         halo = s == 1 and k == 3 and cin % 64 == 0 and cout % 64 == 0 and os.environ.get("RTSEG_CONV_HALO") != "0"
+        wres = s == 1 and k == 3 and os.environ.get("RTSEG_CONV_WRES") != "0"
         rows = []
         for cfg in cfgs:
             sfx = "" if cfg is None else f"@{cfg}"
@@ -107,6 +109,12 @@ def main():
                         t_hs = timeit(lambda: torch.ops.rtseg.conv_halo(x, wk, [s, s], [p, p], [1, 1], True, None,
                                                                         None, 0), a.iters)
                         rows.append(("halo+st", 0.0, t_m, t_hs))
+                    if wres and cin == 64:  # the weights-resident halo kernel (conv_wres.hip)
+                        yw, _ = torch.ops.rtseg.conv_wres(x, wk, [s, s], [p, p], [1, 1], False)
+                        t_w = timeit(lambda: torch.ops.rtseg.conv_wres(x, wk, [s, s], [p, p], [1, 1], False), a.iters)
+                        rows.append(("wres", relerr(yw, y_ref), t_m, t_w))
+                        t_ws = timeit(lambda: torch.ops.rtseg.conv_wres(x, wk, [s, s], [p, p], [1, 1], True), a.iters)
+                        rows.append(("wres+st", 0.0, t_m, t_ws))
             if "dgrad" in passes:
                 dx_ref = conv_bw(dy, x, wcl, None, [s, s], [p, p], [1, 1], False, [0, 0], 1, [True, False, False])[0]
                 dx = torch.ops.rtseg.conv_igemm_dgrad(dy, wtr, list(x.shape), [s, s], [p, p], [1, 1])
@@ -120,6 +128,11 @@ def main():
                     t_h = timeit(lambda: torch.ops.rtseg.conv_halo_dgrad(dy, wtr, list(x.shape), [s, s], [p, p],
                                                                          [1, 1]), a.iters)
                     rows.append(("halo_dg", relerr(dxh, dx_ref), t_m, t_h))
+                if wres and cout == 64 and cfg is None:
+                    dxw = torch.ops.rtseg.conv_wres_dgrad(dy, wtr, list(x.shape), [s, s], [p, p], [1, 1])
+                    t_w = timeit(lambda: torch.ops.rtseg.conv_wres_dgrad(dy, wtr, list(x.shape), [s, s], [p, p],
+                                                                         [1, 1]), a.iters)
+                    rows.append(("wres_dg", relerr(dxw, dx_ref), t_m, t_w))
         os.environ.pop("RTSEG_IGEMM_CFG", None)
         if "wgrad" in passes:
             dw_ref = conv_bw(dy, x, wcl, None, [s, s], [p, p], [1, 1], False, [0, 0], 1, [False, True, False])[1]

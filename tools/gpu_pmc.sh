@@ -19,4 +19,7 @@ for spec in "$@"; do
     timeout -s KILL 90 rocprofv3 --pmc $P -d $OUT/${tag}_p$i -o run -- python3 $R/tools/conv_probe.py --kind $kind --shape $shape --iters 10 $extra > $OUT/${tag}_p$i.log 2>&1 || { echo "FAIL $spec pass $i"; tail -5 $OUT/${tag}_p$i.log; exit 1; }
   done
 done
-python3 $R/tools/pmc_summary.py $OUT/*_p? > $OUT/summary.txt && echo ok
+python3 $R/tools/pmc_summary.py $OUT/*_p? > $OUT/summary.txt || exit 1
+# raw rocprofv3 databases are large (gpurun copies back <= 64 MiB): keep the summary only
+rm -rf $OUT/*_p?
+echo ok
