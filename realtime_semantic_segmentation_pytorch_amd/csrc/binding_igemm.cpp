@@ -202,6 +202,25 @@ at::Tensor conv_igemm_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t k
   return dw;
 }
 
+// halo-tiled weight gradient (conv_whalo.hip): 3 x 3 / stride 1 / pad 1, Cin and Cout % 64 == 0
+at::Tensor conv_whalo_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t kh, int64_t kw, at::IntArrayRef stride,
+                            at::IntArrayRef padding, at::IntArrayRef dilation, bool channels_last) {
+  check_act(x, "input");
+  check_act(dy, "grad_output");
+  ConvGeom g = geom(x.size(0), x.size(1), x.size(2), x.size(3), dy.size(1), kh, kw, stride, padding, dilation);
+  TORCH_CHECK(g.ho == dy.size(2) && g.wo == dy.size(3) && g.n == dy.size(0),
+              "rtseg.conv_whalo_wgrad: grad_output does not match the geometry");
+  TORCH_CHECK(conv_whalo_supported(g), "rtseg.conv_whalo_wgrad: needs 3 x 3 / stride 1 / pad 1, Cin and Cout % 64 == 0");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  g.x = x.data_ptr(); g.y = dy.data_ptr();
+  at::Tensor ws = at::empty({conv_whalo_ws_elems(g)}, x.options().dtype(at::kFloat));
+  at::Tensor dw = at::empty({g.cout, g.cin, g.kh, g.kw},
+                            x.options().dtype(at::kFloat).memory_format(channels_last ? at::MemoryFormat::ChannelsLast
+                                                                                      : at::MemoryFormat::Contiguous));
+  launch_conv_whalo_wgrad(g, ws.data_ptr<float>(), dw.data_ptr<float>(), channels_last, cur_stream());
+  return dw;
+}
+
 }  // namespace
 }  // namespace rtseg
 
@@ -217,6 +236,8 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
   m.def("conv_wres(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats) -> (Tensor, Tensor)");
   m.def("conv_wres_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
         "Tensor? addend=None) -> Tensor");
+  m.def("conv_whalo_wgrad(Tensor x, Tensor dy, int kh, int kw, int[] stride, int[] padding, int[] dilation, "
+        "bool channels_last=False) -> Tensor");
   m.def("conv_igemm_wgrad(Tensor x, Tensor dy, int kh, int kw, int[] stride, int[] padding, int[] dilation, "
         "bool channels_last=False) -> Tensor");
 }
@@ -229,4 +250,5 @@ TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
   m.impl("conv_wres", &rtseg::conv_wres);
   m.impl("conv_wres_dgrad", &rtseg::conv_wres_dgrad);
   m.impl("conv_igemm_wgrad", &rtseg::conv_igemm_wgrad);
+  m.impl("conv_whalo_wgrad", &rtseg::conv_whalo_wgrad);
 }

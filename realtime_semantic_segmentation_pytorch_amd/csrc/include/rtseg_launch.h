@@ -177,6 +177,9 @@ void launch_conv_igemm_dgrad(const ConvGeom& g, hipStream_t st);
 // dw fp32 [Cout][Cin][KH][KW]
 int64_t conv_igemm_wgrad_ws_elems(const ConvGeom& g);
 void launch_conv_igemm_wgrad(const ConvGeom& g, float* ws, float* dw, bool krsc, hipStream_t st);
+// split-K slab [splits][cout][kt * cin] -> dw (NCHW or, krsc, [Cout][KH][KW][Cin] order)
+void launch_wgrad_slab_reduce(float* ws, int splits, int cout, int cin, int kt, float* dw, bool krsc,
+                              hipStream_t st);
 
 // ---- conv_halo.hip ------------------------------------------------------------
 // Halo-tiled stride-1 conv (taps within a 3 x 3 footprint, Cin % 64 == 0, Cout % 64 == 0):
@@ -195,6 +198,13 @@ bool conv_wres_supported(const ConvGeom& g, int mode);
 int conv_wres_slabs(const ConvGeom& g);
 void launch_conv_wres_fwd(const ConvGeom& g, hipStream_t st);
 void launch_conv_wres_dgrad(const ConvGeom& g, hipStream_t st);
+
+// ---- conv_whalo.hip -----------------------------------------------------------
+// Halo-tiled weight gradient of 3 x 3 / stride 1 / pad 1 / dilation 1 convs (Cin, Cout % 64 == 0):
+// g.x = x, g.y = dy; ws of conv_whalo_ws_elems(g) floats; dw fp32 as launch_conv_igemm_wgrad.
+bool conv_whalo_supported(const ConvGeom& g);
+int64_t conv_whalo_ws_elems(const ConvGeom& g);
+void launch_conv_whalo_wgrad(const ConvGeom& g, float* ws, float* dw, bool krsc, hipStream_t st);
 
 // ---- gate.hip -----------------------------------------------------------------
 // out = x * s (mul), x * (1 + s) (residual), x * s + y * (1 - s) (blend); s = att or

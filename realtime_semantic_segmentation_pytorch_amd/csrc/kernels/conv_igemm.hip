@@ -954,11 +954,18 @@ void launch_conv_igemm_wgrad(const ConvGeom& g, float* ws, float* dw, bool krsc,
     case 5: igemm_wgrad_kernel<2, 6, 2, 4, 2><<<grid, 512, 0, st>>>(k); break;
     default: igemm_wgrad_kernel<2, 4, 2, 4, 3><<<grid, 512, 0, st>>>(k); break;
   }
-  const int64_t plane = static_cast<int64_t>(g.cout) * k.kp;
+  launch_wgrad_slab_reduce(ws, p.splits, g.cout, g.cin, g.kh * g.kw, dw, krsc, st);
+}
+
+// ws [splits][cout][kt * cin] fp32 partial weight gradients (+ ceil(splits / 16) planes of room
+// after them when splits > 16) -> dw, deterministic
+void launch_wgrad_slab_reduce(float* ws, int splits, int cout, int cin, int kt, float* dw, bool krsc,
+                              hipStream_t st) {
+  const int64_t plane = static_cast<int64_t>(cout) * kt * cin;
   const float* src = ws;
-  int rows = p.splits;
+  int rows = splits;
   if (rows > 16) {  // plane % 4 == 0: Cout % 64 == 0
-    float* mid = ws + plane * p.splits;
+    float* mid = ws + plane * splits;
     const int64_t plane4 = plane / 4;
     const dim3 g1(static_cast<unsigned>((plane4 + 255) / 256), static_cast<unsigned>((rows + 15) / 16));
     igemm_wgrad_reduce16<<<g1, 256, 0, st>>>(reinterpret_cast<const float4*>(ws), reinterpret_cast<float4*>(mid),
@@ -967,8 +974,8 @@ void launch_conv_igemm_wgrad(const ConvGeom& g, float* ws, float* dw, bool krsc,
     rows = (rows + 15) / 16;
   }
   const int rg = static_cast<int>(std::min<int64_t>((plane + 255) / 256, 4096));
-  if (krsc) igemm_wgrad_reduce<true><<<rg, 256, 0, st>>>(src, dw, rows, g.cout, g.cin, g.kh * g.kw);
-  else igemm_wgrad_reduce<false><<<rg, 256, 0, st>>>(src, dw, rows, g.cout, g.cin, g.kh * g.kw);
+  if (krsc) igemm_wgrad_reduce<true><<<rg, 256, 0, st>>>(src, dw, rows, cout, cin, kt);
+  else igemm_wgrad_reduce<false><<<rg, 256, 0, st>>>(src, dw, rows, cout, cin, kt);
 }
 
 }  // namespace rtseg

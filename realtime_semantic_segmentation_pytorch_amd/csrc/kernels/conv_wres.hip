@@ -29,6 +29,7 @@
 #include "rtseg_mfma_dev.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace rtseg {
 
@@ -43,7 +44,6 @@ constexpr int kHInstr = (kHRows + 7) / 8;             // 43 DMA instructions (8 
 constexpr int kHStage = kHInstr * 8 * 8;              // 16-byte chunks per halo buffer (344 rows)
 constexpr int kWRows = 9 * 64;                        // weight rows [tap][co]
 constexpr int kWStage = kWRows * 8;                   // 16-byte chunks of the weight slice
-constexpr int kNW = 8;                                // waves
 static_assert((kWStage + 2 * kHStage) * 16 <= 160 * 1024, "LDS budget");
 
 struct WresArgs {
@@ -75,8 +75,13 @@ __device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t r, uint32_t voff, 
       : "memory");
 }
 
-template <int STATS, int FLIP>
-__global__ void __launch_bounds__(kNW * 64) wres_conv_kernel(const WresArgs a) {
+// NW waves; wave w owns TJ = kTH / NW consecutive output rows of the tile (32 pixels each) x all
+// 64 channels (TI = 2 channel tiles); PD = fragment prefetch distance in (tap, K sub-step) steps
+template <int STATS, int FLIP, int NW, int PD>
+__global__ void __launch_bounds__(NW * 64) wres_conv_kernel(const WresArgs a) {
+  constexpr int TJ = kTH / NW;
+  static_assert(TJ * NW == kTH && PD >= 1 && PD <= 4, "wave tiling / prefetch");
+  constexpr int NSTEP = 36;  // 9 taps x 4 sixteen-channel sub-steps
   __shared__ uint4 lds[kWStage + 2 * kHStage];
   uint4* const wl = lds;
   uint4* const hl = lds + kWStage;
@@ -93,7 +98,7 @@ __global__ void __launch_bounds__(kNW * 64) wres_conv_kernel(const WresArgs a) {
   const int lr8 = lane >> 3, lch = lane & 7;
 
   // ---- weights of this block's 64 output channels, once: LDS row tap * 64 + co
-  for (int e = wid; e < kWRows / 8; e += kNW) {
+  for (int e = wid; e < kWRows / 8; e += NW) {
     const int row = e * 8 + lr8;
     const int tap = row >> 6, co = row & 63;
     const int lc = lch ^ ((row >> 1) & 7);
@@ -115,7 +120,7 @@ __global__ void __launch_bounds__(kNW * 64) wres_conv_kernel(const WresArgs a) {
     int n, oy0, ox0;
     tile_xyz(mt, n, oy0, ox0);
     const uint32_t base = lds_addr(hl + hb * kHStage);
-    for (int e = wid; e < kHInstr; e += kNW) {
+    for (int e = wid; e < kHInstr; e += NW) {
       const int r = e * 8 + lr8;
       const int hy = r / kHW, hx = r - hy * kHW;
       const int ih = oy0 + a.dh0 + hy, iw = ox0 + a.dw0 + hx;
@@ -128,15 +133,19 @@ __global__ void __launch_bounds__(kNW * 64) wres_conv_kernel(const WresArgs a) {
     }
   };
 
-  // ---- fragment geometry: lane -> pixel frow of the wave's tile row, K half fhi
+  // ---- fragment geometry: lane -> pixel frow of each of the wave's tile rows, K half fhi
   const int frow = lane & 31, fhi = lane >> 5;
-  const int hrow0 = wid * kHW + frow;  // halo row of this lane's pixel at tap offset (0, 0)
+  int hrow0[TJ];  // halo row of this lane's pixel (row tj) at tap offset (0, 0)
+#pragma unroll
+  for (int tj = 0; tj < TJ; ++tj) hrow0[tj] = (wid * TJ + tj) * kHW + frow;
 
-  f32x16_t acc[2];
+  f32x16_t acc[2][TJ];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   float pst[STATS ? 32 : 1];
 #pragma unroll
@@ -146,39 +155,51 @@ __global__ void __launch_bounds__(kNW * 64) wres_conv_kernel(const WresArgs a) {
   auto epilogue = [&](int mt) __attribute__((always_inline)) {
     int n, oy0, ox0;
     tile_xyz(mt, n, oy0, ox0);
-    const int oy = oy0 + wid, ox = ox0 + frow;
-    const bool ok = oy < a.Ho && ox < a.Wo;
-    const int64_t off = ((static_cast<int64_t>(n) * a.Ho + (ok ? oy : 0)) * a.Wo + (ok ? ox : 0)) * a.cout;
     float ts[STATS ? 2 : 1][16], tq[STATS ? 2 : 1][16];
+    if constexpr (STATS) {
 #pragma unroll
-    for (int ti = 0; ti < 2; ++ti) {
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int co = co_lane + ti * 32 + 8 * g;
-        float v[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = acc[ti][4 * g + q];
-        if (a.addend != nullptr && ok) {
-          float r[4];
-          bf16x4_unpack(*reinterpret_cast<const uint2*>(a.addend + off + co), r);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] += r[q];
+        for (int r = 0; r < 16; ++r) {
+          ts[i][r] = 0.f;
+          tq[i][r] = 0.f;
         }
-        uint2 pk;
-        pk.x = pack2(v[0], v[1]);
-        pk.y = pack2(v[2], v[3]);
-        if (ok) *reinterpret_cast<uint2*>(a.y + off + co) = pk;
-        if constexpr (STATS) {  // statistics of the fp32 outputs; pixels past the image do not count
+    }
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float u = ok ? v[q] : 0.f;
-            ts[ti][4 * g + q] = u;
-            tq[ti][4 * g + q] = u * u;
+    for (int tj = 0; tj < TJ; ++tj) {
+      const int oy = oy0 + wid * TJ + tj, ox = ox0 + frow;
+      const bool ok = oy < a.Ho && ox < a.Wo;
+      const int64_t off = ((static_cast<int64_t>(n) * a.Ho + (ok ? oy : 0)) * a.Wo + (ok ? ox : 0)) * a.cout;
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int co = co_lane + ti * 32 + 8 * g;
+          float v[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = acc[ti][tj][4 * g + q];
+          if (a.addend != nullptr && ok) {
+            float r[4];
+            bf16x4_unpack(*reinterpret_cast<const uint2*>(a.addend + off + co), r);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] += r[q];
+          }
+          uint2 pk;
+          pk.x = pack2(v[0], v[1]);
+          pk.y = pack2(v[2], v[3]);
+          if (ok) *reinterpret_cast<uint2*>(a.y + off + co) = pk;
+          if constexpr (STATS) {  // statistics of the fp32 outputs; pixels past the image do not count
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float u = ok ? v[q] : 0.f;
+              ts[ti][4 * g + q] += u;
+              tq[ti][4 * g + q] = fmaf(u, u, tq[ti][4 * g + q]);
+            }
           }
         }
-      }
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[ti][r] = 0.f;
+        for (int r = 0; r < 16; ++r) acc[ti][tj][r] = 0.f;
+      }
     }
     if constexpr (STATS) {
       float y1[32];
@@ -199,44 +220,51 @@ __global__ void __launch_bounds__(kNW * 64) wres_conv_kernel(const WresArgs a) {
     if (t + 1 < my_tiles) halo_dma(mfirst + (t + 1) * mstep, (t + 1) & 1);
 
     const uint4* hb = hl + (t & 1) * kHStage;
-    // fragment reads one step ahead of the MFMAs (two register slots)
-    bf16x8_t af[2][2], bfg[2];
+    // fragment reads PD steps ahead of the MFMAs (PD + 1 register slots)
+    bf16x8_t af[PD + 1][2], bfg[PD + 1][TJ];
     auto load = [&](int s, int slot) {
       const int tap = s >> 2, ks = s & 3;
       const int i = tap / 3, j = tap - 3 * (tap / 3);
       const int sh = FLIP ? (2 - i) * kHW + (2 - j) : i * kHW + j;
-      const int hr = hrow0 + sh;
       const int ch = 2 * ks + fhi;
-      bfg[slot] = as_frag(hb[hr * 8 + (ch ^ ((hr >> 1) & 7))]);
+#pragma unroll
+      for (int tj = 0; tj < TJ; ++tj) {
+        const int hr = hrow0[tj] + sh;
+        bfg[slot][tj] = as_frag(hb[hr * 8 + (ch ^ ((hr >> 1) & 7))]);
+      }
 #pragma unroll
       for (int ti = 0; ti < 2; ++ti) {
         const int wr = tap * 64 + ti * 32 + frow;
         af[slot][ti] = as_frag(wl[wr * 8 + (ch ^ ((wr >> 1) & 7))]);
       }
     };
-    load(0, 0);
 #pragma unroll
-    for (int s = 0; s < 36; ++s) {
-      if (s + 1 < 36) load(s + 1, (s + 1) & 1);
+    for (int p = 0; p < PD; ++p) load(p, p);
+#pragma unroll
+    for (int s = 0; s < NSTEP; ++s) {
+      if (s + PD < NSTEP) load(s + PD, (s + PD) % (PD + 1));
+      const int sl = s % (PD + 1);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int ti = 0; ti < 2; ++ti)
-        acc[ti] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s & 1][ti], bfg[s & 1], acc[ti], 0, 0, 0);
+#pragma unroll
+        for (int tj = 0; tj < TJ; ++tj)
+          acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[sl][ti], bfg[sl][tj], acc[ti][tj], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
   }
   if (my_tiles > 0) epilogue(mfirst + (my_tiles - 1) * mstep);
 
   if constexpr (STATS) {
-    // one slab row per block: the 8 pixel waves' per-channel sums through LDS in a fixed order
+    // one slab row per block: the pixel waves' per-channel sums through LDS in a fixed order
     __syncthreads();  // all fragment reads done, no DMA in flight
-    float* red = reinterpret_cast<float*>(lds);  // [8][2][64]
+    float* red = reinterpret_cast<float*>(lds);  // [NW][2][64]
     stats_stage2<2>(pst, lane, [&](int, int sq, int dc, float v) { red[(wid * 2 + sq) * 64 + 4 * fhi + dc] = v; });
     __syncthreads();
-    for (int e = tid; e < 128; e += kNW * 64) {
+    for (int e = tid; e < 128; e += NW * 64) {
       float s = 0.f;
 #pragma unroll
-      for (int w = 0; w < kNW; ++w) s += red[w * 128 + e];
+      for (int w = 0; w < NW; ++w) s += red[w * 128 + e];
       const int sq = e >= 64, c = co0 + (sq ? e - 64 : e);
       a.part[static_cast<int64_t>(mfirst) * 2 * a.cout + (sq ? a.cout : 0) + c] = s;
     }
@@ -274,6 +302,23 @@ bool wres_fill(WresArgs& k, const ConvGeom& g, bool dgrad) {
   return true;
 }
 
+// RTSEG_WRES_CFG=<n> (A/B sweeps): 0 = 8 waves x 1 row, prefetch 1; 1 = 8 x 1, prefetch 2;
+// 2 = 4 waves x 2 rows, prefetch 2 (default); 3 = 4 x 2, prefetch 3
+int wres_cfg() {
+  static const int c = std::getenv("RTSEG_WRES_CFG") ? std::atoi(std::getenv("RTSEG_WRES_CFG")) : 2;
+  return c;
+}
+
+template <int STATS, int FLIP>
+void wres_launch(const WresArgs& k, int grid, hipStream_t st) {
+  switch (wres_cfg()) {
+    case 0: wres_conv_kernel<STATS, FLIP, 8, 1><<<grid, 512, 0, st>>>(k); break;
+    case 1: wres_conv_kernel<STATS, FLIP, 8, 2><<<grid, 512, 0, st>>>(k); break;
+    case 3: wres_conv_kernel<STATS, FLIP, 4, 3><<<grid, 256, 0, st>>>(k); break;
+    default: wres_conv_kernel<STATS, FLIP, 4, 2><<<grid, 256, 0, st>>>(k); break;
+  }
+}
+
 }  // namespace
 
 bool conv_wres_supported(const ConvGeom& g, int mode) {
@@ -298,8 +343,8 @@ void launch_conv_wres_fwd(const ConvGeom& g, hipStream_t st) {
   k.addend = nullptr;
   const int grid = wres_grid(k.mtiles, k.ntiles);
   if (grid <= 0) return;
-  if (k.part != nullptr) wres_conv_kernel<1, 0><<<grid, kNW * 64, 0, st>>>(k);
-  else wres_conv_kernel<0, 0><<<grid, kNW * 64, 0, st>>>(k);
+  if (k.part != nullptr) wres_launch<1, 0>(k, grid, st);
+  else wres_launch<0, 0>(k, grid, st);
 }
 
 // data gradient: g = forward geometry; g.x = dy, g.w = wt [Cin][3][3][64], g.y = dx, g.res = addend
@@ -313,7 +358,7 @@ void launch_conv_wres_dgrad(const ConvGeom& g, hipStream_t st) {
   k.addend = static_cast<const uint16_t*>(g.res);
   const int grid = wres_grid(k.mtiles, k.ntiles);
   if (grid <= 0) return;
-  wres_conv_kernel<0, 1><<<grid, kNW * 64, 0, st>>>(k);
+  wres_launch<0, 1>(k, grid, st);
 }
 
 }  // namespace rtseg

@@ -133,6 +133,15 @@ def wres_ok(conv, reduce_c: int, out_c: int) -> bool:
             and tuple(conv.dilation) == (1, 1) and reduce_c == 64 and out_c % 64 == 0)
 
 
+def whalo_ok(conv, cin: int, cout: int) -> bool:
+    """Weight gradients ``conv_whalo_wgrad`` takes (``csrc/kernels/conv_whalo.hip``): 3 x 3,
+    stride 1, pad 1, dilation 1, 64-channel multiples on both sides."""
+    if os.environ.get("RTSEG_CONV_WHALO", "auto") == "0":
+        return False
+    return (tuple(conv.kernel_size) == (3, 3) and tuple(conv.stride) == (1, 1) and tuple(conv.padding) == (1, 1)
+            and tuple(conv.dilation) == (1, 1) and cin % 64 == 0 and cout % 64 == 0)
+
+
 def _order(cands):
     """``RTSEG_CONV_HALO=1`` / ``RTSEG_CONV_WRES=1``: that candidate first (what
     ``RTSEG_CONV_MFMA=1`` forces)."""
@@ -140,6 +149,8 @@ def _order(cands):
         cands.sort(key=lambda c: c[0] != "halo" and not c[0].startswith("halo"))
     if os.environ.get("RTSEG_CONV_WRES") == "1":
         cands.sort(key=lambda c: c[0] != "wres")
+    if os.environ.get("RTSEG_CONV_WHALO") == "1":
+        cands.sort(key=lambda c: c[0] != "whalo")
     return cands
 
 
@@ -429,12 +440,18 @@ def _wgrad(x, dy, wk, conv, key, stride, padding, dilation):
     def ours():
         return ops().conv_igemm_wgrad(x, dy, kh, kw, stride, padding, dilation, cl or (kh == 1 and kw == 1))
 
+    def whalo():
+        return ops().conv_whalo_wgrad(x, dy, kh, kw, stride, padding, dilation, cl or (kh == 1 and kw == 1))
+
     def miopen():
         return torch.ops.aten.convolution_backward(dy, x, wk.permute(0, 3, 1, 2), None, stride, padding, dilation,
                                                    False, [0, 0], 1, [False, True, False])[1]
 
     cands = [("igemm", ours)] if cin % 64 == 0 and cout % 64 == 0 else []
+    if whalo_ok(conv, cin, cout):
+        cands.append(("whalo", whalo))
     cands.append(("miopen", miopen))
+    cands = _order(cands)
     dw = cands[_choose(("wgrad",) + key, cands)][1]()
     return like_param(dw, w)
 
@@ -452,8 +469,14 @@ def conv_bn_stats(x: torch.Tensor, conv: nn.Conv2d):
 
 
 def conv_bn_act_eval(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, act_code: int, residual=None):
-    """Inference: act(BN_running(conv(x)) + residual) in one kernel, or None -> caller's path."""
+    """Inference: act(BN_running(conv(x)) + residual) in one kernel, or None -> caller's path.
+    The kernel output has no autograd graph, so a frozen (eval-mode) BN inside a TRAINING step
+    -- gradients wanted for x, the conv weight or the residual -- takes the caller's
+    differentiable path instead."""
     if bn.training or not bn.track_running_stats or bn.running_mean is None or act_code not in (0, 1, 2):
+        return None
+    if torch.is_grad_enabled() and (x.requires_grad or conv.weight.requires_grad
+                                    or (residual is not None and residual.requires_grad)):
         return None
     if residual is not None and not (residual.is_contiguous(memory_format=torch.channels_last)
                                      and residual.dim() == 4):

@@ -1,4 +1,5 @@
-"""Weights-resident halo conv (csrc/kernels/conv_wres.hip) vs fp32 PyTorch: forward (+ BN-statistics
+"""Weights-resident halo conv (csrc/kernels/conv_wres.hip) and halo-tiled weight gradient
+(csrc/kernels/conv_whalo.hip) vs fp32 PyTorch: forward (+ BN-statistics
 slab) of 3x3 / stride-1 / pad-1 convs with Cin = 64 and the data gradient (+ residual-gradient
 addend) of such convs with Cout = 64 -- partial tiles (H % 8, W % 32), several 64-channel output
 slices, fewer tiles than blocks, and many tiles per block (statistics summed over a block's tiles
@@ -49,7 +50,7 @@ def test_wres_forward_and_stats(geom):
     y1, p1 = torch.ops.rtseg.conv_wres(x, wk, [1, 1], [1, 1], [1, 1], True)
     assert torch.equal(p1, part) and torch.equal(y1, y)  # deterministic
     y2, p2 = torch.ops.rtseg.conv_wres(x, wk, [1, 1], [1, 1], [1, 1], False)
-    assert torch.equal(y2, y) and p2.numel() == 0
+    assert torch.equal(y2, y) and (p2 is None or p2.numel() == 0)
 
 
 @pytest.mark.parametrize("geom", DGRAD)
@@ -123,3 +124,26 @@ def test_wres_routed_training_step(monkeypatch):
         assert rel(gp0[n], g) < 3e-2, n
     assert {"conv_wres", "conv_wres_dgrad"} <= calls[0], calls[0]
     assert not {"conv_wres", "conv_wres_dgrad"} & calls[1], calls[1]
+
+
+# weight-gradient geometries (n, cin, h, w, cout) of 3x3 / stride-1 / pad-1 convs
+WGRAD = [(2, 64, 17, 70, 64), (3, 128, 9, 40, 64), (1, 64, 6, 33, 192), (8, 64, 66, 256, 64), (2, 128, 16, 64, 128)]
+
+
+@pytest.mark.parametrize("geom", WGRAD)
+@pytest.mark.parametrize("channels_last", [False, True])
+def test_whalo_wgrad(geom, channels_last):
+    """Halo-tiled weight gradient (csrc/kernels/conv_whalo.hip) vs fp32 PyTorch on the same bf16
+    operands: partial tiles, several channel pairs, split-K over many tiles (two-stage slab
+    reduction), both parameter layouts; deterministic."""
+    n, cin, h, w, cout = geom
+    g = torch.Generator().manual_seed(4)
+    cl = dict(memory_format=torch.channels_last)
+    x = _t((n, cin, h, w), g).contiguous(**cl)
+    dy = _t((n, cout, h, w), g).contiguous(**cl)
+    dw = torch.ops.rtseg.conv_whalo_wgrad(x, dy, 3, 3, [1, 1], [1, 1], [1, 1], channels_last)
+    ref = torch.nn.grad.conv2d_weight(x.float(), (cout, cin, 3, 3), dy.float(), 1, 1, 1)
+    assert dw.shape == ref.shape and dw.dtype == torch.float32
+    assert dw.is_contiguous(memory_format=torch.channels_last) == channels_last or cin == 1
+    _close(dw, ref, 1e-3)
+    assert torch.equal(torch.ops.rtseg.conv_whalo_wgrad(x, dy, 3, 3, [1, 1], [1, 1], [1, 1], channels_last), dw)

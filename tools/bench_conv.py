@@ -145,6 +145,10 @@ def main():
                 t_o = timeit(lambda: torch.ops.rtseg.conv_igemm_wgrad(x, dy, k, k, [s, s], [p, p], [1, 1]), a.iters)
                 rows.append(("wgrad" + ("" if wc is None else f"@{wc}"), relerr(dw, dw_ref), t_m, t_o))
             os.environ.pop("RTSEG_WGRAD_CFG", None)
+            if s == 1 and k == 3 and cin % 64 == 0 and cout % 64 == 0:  # halo-tiled wgrad (conv_whalo.hip)
+                dwh = torch.ops.rtseg.conv_whalo_wgrad(x, dy, k, k, [s, s], [p, p], [1, 1])
+                t_h = timeit(lambda: torch.ops.rtseg.conv_whalo_wgrad(x, dy, k, k, [s, s], [p, p], [1, 1]), a.iters)
+                rows.append(("whalo", relerr(dwh, dw_ref), t_m, t_h))
         for name, err, t_m, t_o in rows:
             print(f"{tag:34s} {name:9s} {err:9.2e} {t_m:8.1f} {t_o:8.1f}  {flop / t_m / 1e6:5.0f}/{flop / t_o / 1e6:5.0f}"
                   f"   {t_m / t_o:5.2f}x", flush=True)
