@@ -1,6 +1,6 @@
 """Run one conv kernel variant repeatedly (for rocprofv3 --pmc passes).
 
-python tools/conv_probe.py --kind halo|igemm|halo_dg|igemm_dg --shape CIN,H,W,COUT [--batch 32] [--iters 20]
+python tools/conv_probe.py --kind halo|igemm|halo_dg|igemm_dg|wgrad|wres|wres_dg|whalo --shape CIN,H,W,COUT [--batch 32] [--iters 20]
 """
 import argparse
 import os
@@ -36,6 +36,9 @@ def main():
         "halo_dg": lambda: r.conv_halo_dgrad(dy, wtr, list(x.shape), [1, 1], [1, 1], [1, 1]),
         "igemm_dg": lambda: r.conv_igemm_dgrad(dy, wtr, list(x.shape), [1, 1], [1, 1], [1, 1]),
         "wgrad": lambda: r.conv_igemm_wgrad(x, dy, 3, 3, [1, 1], [1, 1], [1, 1]),
+        "wres": lambda: r.conv_wres(x, wk, [1, 1], [1, 1], [1, 1], a.stats),
+        "wres_dg": lambda: r.conv_wres_dgrad(dy, wtr, list(x.shape), [1, 1], [1, 1], [1, 1]),
+        "whalo": lambda: r.conv_whalo_wgrad(x, dy, 3, 3, [1, 1], [1, 1], [1, 1]),
     }
     fn = fns[a.kind]
     for _ in range(a.iters):
