@@ -42,7 +42,7 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::
                                                  at::IntArrayRef padding, at::IntArrayRef dilation, bool stats,
                                                  const std::optional<at::Tensor>& scale_shift,
                                                  const std::optional<at::Tensor>& residual, int64_t act, int kind) {
-  const bool halo = kind == 1, wres = kind == 2;
+  const bool halo = kind == 1, wres = kind == 2, hreg = kind == 3;
   check_act(x, "input");
   TORCH_CHECK(wk.is_cuda() && wk.dim() == 4 && wk.scalar_type() == at::kBFloat16 && wk.is_contiguous() &&
                   wk.size(3) == x.size(1),
@@ -56,6 +56,10 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::
   } else if (wres) {
     TORCH_CHECK(conv_wres_supported(g, 0), "rtseg.conv_wres: needs 3 x 3 / stride 1 / pad 1, Cin == 64, Cout % 64 == 0");
     TORCH_CHECK(!(scale_shift.has_value() && scale_shift->defined()), "rtseg.conv_wres: no inference BN epilogue");
+  } else if (hreg) {
+    TORCH_CHECK(conv_hreg_supported(g, 0),
+                "rtseg.conv_hreg: needs 3 x 3 / stride 1 / pad 1, Cin % 64 == 0, Cout % 128 == 0");
+    TORCH_CHECK(!(scale_shift.has_value() && scale_shift->defined()), "rtseg.conv_hreg: no inference BN epilogue");
   } else {
     TORCH_CHECK(conv_igemm_supported(g, 0), "rtseg.conv_igemm: needs Cin % 64 == 0, Cout % 8 == 0, <= 49 taps");
   }
@@ -65,7 +69,9 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::
   g.part = nullptr; g.scale_shift = nullptr; g.res = nullptr; g.act = static_cast<int>(act);
   at::Tensor part;
   if (stats) {
-    part = at::empty({halo ? conv_halo_slabs(g) : wres ? conv_wres_slabs(g) : conv_igemm_slabs(g), 2 * g.cout},
+    part = at::empty({halo ? conv_halo_slabs(g) : wres ? conv_wres_slabs(g) : hreg ? conv_hreg_slabs(g)
+                                                                                 : conv_igemm_slabs(g),
+                      2 * g.cout},
                      x.options().dtype(at::kFloat));
     g.part = part.data_ptr<float>();
   }
@@ -86,7 +92,10 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::
   }
   if (halo) launch_conv_halo_fwd(g, cur_stream());
   else if (wres) launch_conv_wres_fwd(g, cur_stream());
-  else launch_conv_igemm_fwd(g, cur_stream());
+  else if (hreg) {
+    at::Tensor wpack = at::empty({conv_hreg_pack_elems(g, 0)}, wk.options());
+    launch_conv_hreg(g, 0, wpack.data_ptr(), cur_stream());
+  } else launch_conv_igemm_fwd(g, cur_stream());
   if (stats && part.size(0) > 256) {  // fold the per-tile rows so the BN finalize stays cheap
     const int rows = static_cast<int>(part.size(0));
     const int chunk = (rows + 255) / 256;
@@ -112,6 +121,12 @@ std::tuple<at::Tensor, at::Tensor> conv_halo(const at::Tensor& x, const at::Tens
   return conv_fwd_impl(x, wk, stride, padding, dilation, stats, scale_shift, residual, act, 1);
 }
 
+// the register-weight halo kernel (conv_hreg.hip): 3 x 3 stride-1 convs, Cin % 64, Cout % 128
+std::tuple<at::Tensor, at::Tensor> conv_hreg(const at::Tensor& x, const at::Tensor& wk, at::IntArrayRef stride,
+                                             at::IntArrayRef padding, at::IntArrayRef dilation, bool stats) {
+  return conv_fwd_impl(x, wk, stride, padding, dilation, stats, std::nullopt, std::nullopt, 0, 3);
+}
+
 // the weights-resident halo kernel (conv_wres.hip): 3 x 3 stride-1 convs with Cin == 64
 std::tuple<at::Tensor, at::Tensor> conv_wres(const at::Tensor& x, const at::Tensor& wk, at::IntArrayRef stride,
                                              at::IntArrayRef padding, at::IntArrayRef dilation, bool stats) {
@@ -122,7 +137,7 @@ std::tuple<at::Tensor, at::Tensor> conv_wres(const at::Tensor& x, const at::Tens
 at::Tensor conv_dgrad_impl(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
                            at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
                            const std::optional<at::Tensor>& bias, const std::optional<at::Tensor>& addend, int kind) {
-  const bool halo = kind == 1, wres = kind == 2;
+  const bool halo = kind == 1, wres = kind == 2, hreg = kind == 3;
   check_act(dy, "grad_output");
   TORCH_CHECK(x_size.size() == 4, "rtseg.conv_igemm_dgrad: x_size must be [N, Cin, H, W]");
   TORCH_CHECK(wt.is_cuda() && wt.dim() == 4 && wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() &&
@@ -139,6 +154,10 @@ at::Tensor conv_dgrad_impl(const at::Tensor& dy, const at::Tensor& wt, at::IntAr
   } else if (wres) {
     TORCH_CHECK(conv_wres_supported(g, 1), "rtseg.conv_wres_dgrad: needs 3 x 3 / stride 1 / pad 1, Cout == 64, Cin % 64 == 0");
     TORCH_CHECK(!(bias.has_value() && bias->defined()), "rtseg.conv_wres_dgrad: no bias");
+  } else if (hreg) {
+    TORCH_CHECK(conv_hreg_supported(g, 1),
+                "rtseg.conv_hreg_dgrad: needs 3 x 3 / stride 1 / pad 1, Cout % 64 == 0, Cin % 128 == 0");
+    TORCH_CHECK(!(bias.has_value() && bias->defined()), "rtseg.conv_hreg_dgrad: no bias");
   } else {
     TORCH_CHECK(conv_igemm_supported(g, 1), "rtseg.conv_igemm_dgrad: needs Cout % 64 == 0, Cin % 8 == 0");
   }
@@ -160,7 +179,10 @@ at::Tensor conv_dgrad_impl(const at::Tensor& dy, const at::Tensor& wt, at::IntAr
   }
   if (halo) launch_conv_halo_dgrad(g, cur_stream());
   else if (wres) launch_conv_wres_dgrad(g, cur_stream());
-  else launch_conv_igemm_dgrad(g, cur_stream());
+  else if (hreg) {
+    at::Tensor wpack = at::empty({conv_hreg_pack_elems(g, 1)}, wt.options());
+    launch_conv_hreg(g, 1, wpack.data_ptr(), cur_stream());
+  } else launch_conv_igemm_dgrad(g, cur_stream());
   return dx;
 }
 
@@ -174,6 +196,12 @@ at::Tensor conv_halo_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntAr
                            at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
                            const std::optional<at::Tensor>& addend) {
   return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, std::nullopt, addend, 1);
+}
+
+at::Tensor conv_hreg_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
+                           at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
+                           const std::optional<at::Tensor>& addend) {
+  return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, std::nullopt, addend, 3);
 }
 
 at::Tensor conv_wres_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
@@ -233,6 +261,9 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
         "Tensor? scale_shift, Tensor? residual, int act) -> (Tensor, Tensor)");
   m.def("conv_halo_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
         "Tensor? addend=None) -> Tensor");
+  m.def("conv_hreg(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats) -> (Tensor, Tensor)");
+  m.def("conv_hreg_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
+        "Tensor? addend=None) -> Tensor");
   m.def("conv_wres(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats) -> (Tensor, Tensor)");
   m.def("conv_wres_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
         "Tensor? addend=None) -> Tensor");
@@ -247,6 +278,8 @@ TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
   m.impl("conv_igemm_dgrad", &rtseg::conv_igemm_dgrad);
   m.impl("conv_halo", &rtseg::conv_halo);
   m.impl("conv_halo_dgrad", &rtseg::conv_halo_dgrad);
+  m.impl("conv_hreg", &rtseg::conv_hreg);
+  m.impl("conv_hreg_dgrad", &rtseg::conv_hreg_dgrad);
   m.impl("conv_wres", &rtseg::conv_wres);
   m.impl("conv_wres_dgrad", &rtseg::conv_wres_dgrad);
   m.impl("conv_igemm_wgrad", &rtseg::conv_igemm_wgrad);

@@ -199,6 +199,16 @@ int conv_wres_slabs(const ConvGeom& g);
 void launch_conv_wres_fwd(const ConvGeom& g, hipStream_t st);
 void launch_conv_wres_dgrad(const ConvGeom& g, hipStream_t st);
 
+// ---- conv_hreg.hip ------------------------------------------------------------
+// Halo-tiled 3 x 3 / stride 1 / pad 1 conv with register-streamed weights: reduction channels
+// % 64 == 0, output channels % 128 == 0.  mode 0 forward (+ BN statistics slab of
+// conv_hreg_slabs(g) rows), 1 data gradient (g as for launch_conv_igemm_dgrad, g.res = addend);
+// wpack: scratch of conv_hreg_pack_elems(g, mode) bf16.
+bool conv_hreg_supported(const ConvGeom& g, int mode);
+int conv_hreg_slabs(const ConvGeom& g);
+int64_t conv_hreg_pack_elems(const ConvGeom& g, int mode);
+void launch_conv_hreg(const ConvGeom& g, int mode, void* wpack, hipStream_t st);
+
 // ---- conv_whalo.hip -----------------------------------------------------------
 // Halo-tiled weight gradient of 3 x 3 / stride 1 / pad 1 / dilation 1 convs (Cin, Cout % 64 == 0):
 // g.x = x, g.y = dy; ws of conv_whalo_ws_elems(g) floats; dw fp32 as launch_conv_igemm_wgrad.

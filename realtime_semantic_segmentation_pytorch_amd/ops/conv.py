@@ -133,6 +133,15 @@ def wres_ok(conv, reduce_c: int, out_c: int) -> bool:
             and tuple(conv.dilation) == (1, 1) and reduce_c == 64 and out_c % 64 == 0)
 
 
+def hreg_ok(conv, reduce_c: int, out_c: int) -> bool:
+    """Shapes ``conv_hreg`` takes (``csrc/kernels/conv_hreg.hip``): 3 x 3, stride 1, pad 1, dilation
+    1, a 64-channel multiple summed over, a 128-channel multiple produced."""
+    if os.environ.get("RTSEG_CONV_HREG", "auto") == "0":
+        return False
+    return (tuple(conv.kernel_size) == (3, 3) and tuple(conv.stride) == (1, 1) and tuple(conv.padding) == (1, 1)
+            and tuple(conv.dilation) == (1, 1) and reduce_c % 64 == 0 and out_c % 128 == 0)
+
+
 def whalo_ok(conv, cin: int, cout: int) -> bool:
     """Weight gradients ``conv_whalo_wgrad`` takes (``csrc/kernels/conv_whalo.hip``): 3 x 3,
     stride 1, pad 1, dilation 1, 64-channel multiples on both sides."""
@@ -151,6 +160,8 @@ def _order(cands):
         cands.sort(key=lambda c: c[0] != "wres")
     if os.environ.get("RTSEG_CONV_WHALO") == "1":
         cands.sort(key=lambda c: c[0] != "whalo")
+    if os.environ.get("RTSEG_CONV_HREG") == "1":
+        cands.sort(key=lambda c: c[0] != "hreg")
     return cands
 
 
@@ -280,6 +291,8 @@ class _ConvFn(torch.autograd.Function):
             y, part = ops().conv_halo(x, wk, stride, padding, dilation, stats, None, None, 0)
         elif impl == "wres":
             y, part = ops().conv_wres(x, wk, stride, padding, dilation, stats)
+        elif impl == "hreg":
+            y, part = ops().conv_hreg(x, wk, stride, padding, dilation, stats)
         elif impl == "mfma":
             y, part = ops().conv_mfma(x, wk, stride, padding, dilation, stats, None, None, 0)
         else:
@@ -334,6 +347,8 @@ def _fwd_impl(x, wk, conv, key, stats) -> str:
             cands.append(("halo", lambda: ops().conv_halo(x, wk, stride, padding, dilation, stats, None, None, 0)))
         if wres_ok(conv, cin, cout):
             cands.append(("wres", lambda: ops().conv_wres(x, wk, stride, padding, dilation, stats)))
+        if hreg_ok(conv, cin, cout):
+            cands.append(("hreg", lambda: ops().conv_hreg(x, wk, stride, padding, dilation, stats)))
     elif cin % 32 == 0 and cout % 8 == 0:
         cands.append(("mfma", lambda: ops().conv_mfma(x, wk, stride, padding, dilation, stats, None, None, 0)))
     if not cands:
@@ -376,15 +391,22 @@ def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None):
         return torch.ops.aten.convolution_backward(dy, x, wk.permute(0, 3, 1, 2), None, stride, padding, dilation, False,
                                                    [0, 0], 1, [True, False, False])[0]
 
+    def hreg():
+        if not wt:
+            wt.append(wk.permute(3, 1, 2, 0).contiguous())
+        return ops().conv_hreg_dgrad(dy, wt[0], list(x.shape), stride, padding, dilation, addend)
+
     cands = [("igemm", ours)] if cout % 64 == 0 and cin % 8 == 0 else []
     if halo_ok(conv, cout, cin):
         cands.append(("halo", halo))
     if wres_ok(conv, cout, cin):
         cands.append(("wres", wres))
+    if hreg_ok(conv, cout, cin):
+        cands.append(("hreg", hreg))
     cands.append(("miopen", miopen))
     name, fn = cands[_choose(("dgrad",) + key, _order(cands))]
     dx = fn()
-    if addend is not None and name not in ("igemm", "halo", "wres"):
+    if addend is not None and name not in ("igemm", "halo", "wres", "hreg"):
         dx = dx + addend
     return dx
 

@@ -147,3 +147,44 @@ def test_whalo_wgrad(geom, channels_last):
     assert dw.is_contiguous(memory_format=torch.channels_last) == channels_last or cin == 1
     _close(dw, ref, 1e-3)
     assert torch.equal(torch.ops.rtseg.conv_whalo_wgrad(x, dy, 3, 3, [1, 1], [1, 1], [1, 1], channels_last), dw)
+
+
+# register-weight halo conv (csrc/kernels/conv_hreg.hip): (n, cin, h, w, cout), Cin % 64, Cout % 128
+HREG = [(2, 64, 9, 70, 128), (1, 128, 17, 130, 128), (3, 192, 6, 40, 256), (8, 128, 66, 256, 128)]
+
+
+@pytest.mark.parametrize("geom", HREG)
+def test_hreg_forward_and_stats(geom):
+    n, cin, h, w, cout = geom
+    g = torch.Generator().manual_seed(6)
+    x = _t((n, cin, h, w), g).contiguous(memory_format=torch.channels_last)
+    wt = _t((cout, cin, 3, 3), g, 1 / (3 * cin ** 0.5))
+    wk = wt.permute(0, 2, 3, 1).contiguous()
+    y, part = torch.ops.rtseg.conv_hreg(x, wk, [1, 1], [1, 1], [1, 1], True)
+    ref = F.conv2d(x.float(), wt.float(), None, 1, 1)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    _close(y, ref, 2e-2)
+    rf = ref.double()
+    torch.testing.assert_close(part[:, :cout].double().sum(0), rf.sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(part[:, cout:].double().sum(0), rf.square().sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+    y1, p1 = torch.ops.rtseg.conv_hreg(x, wk, [1, 1], [1, 1], [1, 1], True)
+    assert torch.equal(y1, y) and torch.equal(p1, part)
+    y2, _ = torch.ops.rtseg.conv_hreg(x, wk, [1, 1], [1, 1], [1, 1], False)
+    assert torch.equal(y2, y)
+
+
+@pytest.mark.parametrize("geom", HREG)
+@pytest.mark.parametrize("with_addend", [False, True])
+def test_hreg_dgrad(geom, with_addend):
+    """Data gradient of the forward conv (n, cout -> cin roles swapped: the dgrad reduces over the
+    forward Cout and produces the forward Cin, so geometry (n, a, h, w, b) tests a conv b -> a)."""
+    n, cout_fwd, h, w, cin_fwd = geom
+    g = torch.Generator().manual_seed(8)
+    cl = dict(memory_format=torch.channels_last)
+    wt = _t((cout_fwd, cin_fwd, 3, 3), g, 1 / (3 * cout_fwd ** 0.5))
+    dy = _t((n, cout_fwd, h, w), g).contiguous(**cl)
+    add = _t((n, cin_fwd, h, w), g).contiguous(**cl)
+    dx = torch.ops.rtseg.conv_hreg_dgrad(dy, wt.permute(1, 2, 3, 0).contiguous(), [n, cin_fwd, h, w], [1, 1], [1, 1],
+                                         [1, 1], add if with_addend else None)
+    ref = torch.nn.grad.conv2d_input((n, cin_fwd, h, w), wt.float(), dy.float(), 1, 1, 1)
+    _close(dx, ref + add.float() if with_addend else ref, 2e-2)

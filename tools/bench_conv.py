@@ -109,6 +109,12 @@ def main():
                         t_hs = timeit(lambda: torch.ops.rtseg.conv_halo(x, wk, [s, s], [p, p], [1, 1], True, None,
                                                                         None, 0), a.iters)
                         rows.append(("halo+st", 0.0, t_m, t_hs))
+                    if wres and cin % 64 == 0 and cout % 128 == 0:  # register-weight halo kernel (conv_hreg.hip)
+                        yg, _ = torch.ops.rtseg.conv_hreg(x, wk, [s, s], [p, p], [1, 1], False)
+                        t_g = timeit(lambda: torch.ops.rtseg.conv_hreg(x, wk, [s, s], [p, p], [1, 1], False), a.iters)
+                        rows.append(("hreg", relerr(yg, y_ref), t_m, t_g))
+                        t_gs = timeit(lambda: torch.ops.rtseg.conv_hreg(x, wk, [s, s], [p, p], [1, 1], True), a.iters)
+                        rows.append(("hreg+st", 0.0, t_m, t_gs))
                     if wres and cin == 64:  # the weights-resident halo kernel (conv_wres.hip)
                         yw, _ = torch.ops.rtseg.conv_wres(x, wk, [s, s], [p, p], [1, 1], False)
                         t_w = timeit(lambda: torch.ops.rtseg.conv_wres(x, wk, [s, s], [p, p], [1, 1], False), a.iters)
@@ -128,6 +134,11 @@ def main():
                     t_h = timeit(lambda: torch.ops.rtseg.conv_halo_dgrad(dy, wtr, list(x.shape), [s, s], [p, p],
                                                                          [1, 1]), a.iters)
                     rows.append(("halo_dg", relerr(dxh, dx_ref), t_m, t_h))
+                if wres and cout % 64 == 0 and cin % 128 == 0 and cfg is None:
+                    dxg = torch.ops.rtseg.conv_hreg_dgrad(dy, wtr, list(x.shape), [s, s], [p, p], [1, 1])
+                    t_g = timeit(lambda: torch.ops.rtseg.conv_hreg_dgrad(dy, wtr, list(x.shape), [s, s], [p, p],
+                                                                         [1, 1]), a.iters)
+                    rows.append(("hreg_dg", relerr(dxg, dx_ref), t_m, t_g))
                 if wres and cout == 64 and cfg is None:
                     dxw = torch.ops.rtseg.conv_wres_dgrad(dy, wtr, list(x.shape), [s, s], [p, p], [1, 1])
                     t_w = timeit(lambda: torch.ops.rtseg.conv_wres_dgrad(dy, wtr, list(x.shape), [s, s], [p, p],

@@ -39,6 +39,8 @@ def main():
         "wres": lambda: r.conv_wres(x, wk, [1, 1], [1, 1], [1, 1], a.stats),
         "wres_dg": lambda: r.conv_wres_dgrad(dy, wtr, list(x.shape), [1, 1], [1, 1], [1, 1]),
         "whalo": lambda: r.conv_whalo_wgrad(x, dy, 3, 3, [1, 1], [1, 1], [1, 1]),
+        "hreg": lambda: r.conv_hreg(x, wk, [1, 1], [1, 1], [1, 1], a.stats),
+        "hreg_dg": lambda: r.conv_hreg_dgrad(dy, wtr, list(x.shape), [1, 1], [1, 1], [1, 1]),
     }
     fn = fns[a.kind]
     for _ in range(a.iters):
