@@ -302,20 +302,21 @@ bool wres_fill(WresArgs& k, const ConvGeom& g, bool dgrad) {
   return true;
 }
 
-// RTSEG_WRES_CFG=<n> (A/B sweeps): 0 = 8 waves x 1 row, prefetch 1; 1 = 8 x 1, prefetch 2;
-// 2 = 4 waves x 2 rows, prefetch 2 (default); 3 = 4 x 2, prefetch 3
+// RTSEG_WRES_CFG=<n> (A/B sweeps): 0 = 8 waves x 1 row, prefetch 1 (default: fastest measured,
+// profiles/r4_conv/bench_wres_cfg*.txt); 1 = 8 x 1, prefetch 2; 2 = 4 waves x 2 rows, prefetch 2;
+// 3 = 4 x 2, prefetch 3
 int wres_cfg() {
-  static const int c = std::getenv("RTSEG_WRES_CFG") ? std::atoi(std::getenv("RTSEG_WRES_CFG")) : 2;
+  static const int c = std::getenv("RTSEG_WRES_CFG") ? std::atoi(std::getenv("RTSEG_WRES_CFG")) : 0;
   return c;
 }
 
 template <int STATS, int FLIP>
 void wres_launch(const WresArgs& k, int grid, hipStream_t st) {
   switch (wres_cfg()) {
-    case 0: wres_conv_kernel<STATS, FLIP, 8, 1><<<grid, 512, 0, st>>>(k); break;
     case 1: wres_conv_kernel<STATS, FLIP, 8, 2><<<grid, 512, 0, st>>>(k); break;
     case 3: wres_conv_kernel<STATS, FLIP, 4, 3><<<grid, 256, 0, st>>>(k); break;
-    default: wres_conv_kernel<STATS, FLIP, 4, 2><<<grid, 256, 0, st>>>(k); break;
+    case 2: wres_conv_kernel<STATS, FLIP, 4, 2><<<grid, 256, 0, st>>>(k); break;
+    default: wres_conv_kernel<STATS, FLIP, 8, 1><<<grid, 512, 0, st>>>(k); break;
   }
 }
 

@@ -309,10 +309,15 @@ class _ConvFn(torch.autograd.Function):
         ctx.wdtype = weight.dtype
         if part is not None:
             ctx.mark_non_differentiable(part)
+        # the statistics slab never gets a gradient: without this autograd would allocate and
+        # zero-fill one [slabs, 2C] tensor per conv per step (~50 fill kernels per DDRNet step)
+        ctx.set_materialize_grads(False)
         return y, part
 
     @staticmethod
     def backward(ctx, dy, _dpart):
+        if dy is None:
+            return None, None, None, None
         x, wk = ctx.saved_tensors
         conv, key = ctx.conv, ctx.key
         stride, padding, dilation = _geom(conv)

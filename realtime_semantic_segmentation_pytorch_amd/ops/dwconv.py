@@ -61,10 +61,13 @@ class _DWConvFn(torch.autograd.Function):
             return y
         if part is not None:
             ctx.mark_non_differentiable(part)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics slab
         return y, part
 
     @staticmethod
     def backward(ctx, dy, _dpart=None):
+        if dy is None:
+            return None, None, None, None, None
         x, wt = ctx.saved_tensors
         cout, kh, kw, sh, sw, ph, pw, dh, dw = ctx.geom
         dy = _cl_aligned(dy.to(x.dtype))

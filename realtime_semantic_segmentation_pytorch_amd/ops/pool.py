@@ -78,10 +78,13 @@ class _MaxPoolIdxFn(torch.autograd.Function):
         ctx.geom = (x.shape[2], x.shape[3], k, s, p)
         ctx.save_for_backward(win)
         ctx.mark_non_differentiable(idx)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the index output
         return y, idx
 
     @staticmethod
     def backward(ctx, gy, _gidx):
+        if gy is None:
+            return None, None, None, None
         h, w, k, s, p = ctx.geom
         (win,) = ctx.saved_tensors
         return ops().pool2d_bwd(gy, win, h, w, k, s, p, _MAX, True), None, None, None

@@ -9,6 +9,12 @@ if ROOT not in sys.path:
 
 
 def pytest_configure(config):
+    # under pytest-xdist every worker would start one intra-op thread per CPU: share them instead
+    workers = int(os.environ.get("PYTEST_XDIST_WORKER_COUNT", "1") or 1)
+    if workers > 1:
+        import torch
+
+        torch.set_num_threads(max(1, (os.cpu_count() or 1) // workers))
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP kernels on cuda:0)")
     config.addinivalue_line("markers", "slow: long-running test")
     config.addinivalue_line("markers", "no_guard: cannot run under the guard-page allocator (graph capture)")

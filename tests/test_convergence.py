@@ -62,7 +62,6 @@ def _check(tr, history, cfg, floor):
 def test_learnable_task_converges_cpu(tmp_path, monkeypatch):
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE"):
         monkeypatch.delenv(k, raising=False)
-    torch.set_num_threads(min(8, os.cpu_count() or 1))
     cfg = _cfg(tmp_path, "cpu", model="fastscnn", synthetic_len=64, synthetic_size=(64, 128), crop_size=64,
                synthetic_cell=32, train_bs=8, val_bs=8, total_epoch=16, optimizer_type="adam",
                lr_policy="linear", amp_training=False)
