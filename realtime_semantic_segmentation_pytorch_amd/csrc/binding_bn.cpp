@@ -32,6 +32,30 @@ void check_cl(const at::Tensor& x, const char* what) {
               " must be 16-byte aligned");
 }
 
+// A channel slice [N, C, H, W] of a wider channels-last tensor (row stride ld elements): the
+// concat buffer of ops/concat.py, which the apply kernels also write and whose gradient the
+// backward kernels read in place of / on top of dy.  Full 16-byte channel vectors only.
+struct Slice {
+  void* p = nullptr;
+  int64_t ld = 0;
+};
+Slice slice_of(const std::optional<at::Tensor>& t, const at::Tensor& like, const char* what) {
+  if (!t.has_value() || !t->defined()) return {};
+  TORCH_CHECK(t->is_cuda() && t->dim() == 4 && like.dim() == 4 && t->scalar_type() == like.scalar_type(),
+              "rtseg.bn: ", what, " must be a 4-D GPU tensor of the activation's dtype");
+  TORCH_CHECK(t->sizes() == like.sizes(), "rtseg.bn: ", what, " must have the activation's shape");
+  const int64_t ld = t->stride(3), H = t->size(2), W = t->size(3);
+  TORCH_CHECK(t->stride(1) == 1 && ld >= t->size(1) && (H == 1 || t->stride(2) == ld * W) &&
+                  (t->size(0) == 1 || t->stride(0) == ld * W * H),
+              "rtseg.bn: ", what, " must be a channel slice of a channels-last tensor");
+  const int C = static_cast<int>(like.size(1));
+  const int V = bn_vec_width(dtype_code(like), C);
+  TORCH_CHECK(V * static_cast<int>(like.element_size()) == 16 && ld % V == 0 &&
+                  reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0,
+              "rtseg.bn: ", what, " needs 16-byte channel vectors and a 16-byte aligned slice");
+  return {t->data_ptr(), ld};
+}
+
 const float* fptr(const std::optional<at::Tensor>& t) {
   return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr;
 }
@@ -118,7 +142,7 @@ std::tuple<at::Tensor, at::Tensor> bn_eval_coeffs(const std::optional<at::Tensor
 }
 
 at::Tensor bn_apply(const at::Tensor& x, const at::Tensor& scale_shift,
-                    const std::optional<at::Tensor>& res, int64_t act) {
+                    const std::optional<at::Tensor>& res, int64_t act, const std::optional<at::Tensor>& out2) {
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   check_cl(x, "x");
   const void* rp = nullptr;
@@ -128,16 +152,18 @@ at::Tensor bn_apply(const at::Tensor& x, const at::Tensor& scale_shift,
                 "rtseg.bn_apply: residual mismatch");
     rp = res->data_ptr();
   }
+  const Slice o2 = slice_of(out2, x, "out2");
   at::Tensor y = at::empty_like(x);
   launch_bn_apply(x.data_ptr(), rp, scale_shift.data_ptr<float>(), y.data_ptr(), dtype_code(x),
-                  rows_of(x), static_cast<int>(x.size(1)), static_cast<int>(act), cur_stream());
+                  rows_of(x), static_cast<int>(x.size(1)), static_cast<int>(act), cur_stream(), o2.p, o2.ld);
   return y;
 }
 
 // Residual + activation forward that also returns the activation-derivative bit mask
 // (one byte per channel vector; mask mode 3 of bn_bwd_sums / bn_backward).
 std::tuple<at::Tensor, at::Tensor> bn_apply_bits(const at::Tensor& x, const at::Tensor& scale_shift,
-                                                 const std::optional<at::Tensor>& res, int64_t act) {
+                                                 const std::optional<at::Tensor>& res, int64_t act,
+                                                 const std::optional<at::Tensor>& out2) {
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   check_cl(x, "x");
   const void* rp = nullptr;
@@ -153,9 +179,10 @@ std::tuple<at::Tensor, at::Tensor> bn_apply_bits(const at::Tensor& x, const at::
   TORCH_CHECK(V > 0, "rtseg.bn_apply_bits: unsupported channel count");
   at::Tensor y = at::empty_like(x);
   at::Tensor bits = at::empty({rows_of(x) * (C / V)}, x.options().dtype(at::kByte));
+  const Slice o2 = slice_of(out2, x, "out2");
   launch_bn_apply_bits(x.data_ptr(), rp, scale_shift.data_ptr<float>(), y.data_ptr(),
                        bits.data_ptr<uint8_t>(), dtype_code(x), rows_of(x), C, static_cast<int>(act),
-                       cur_stream());
+                       cur_stream(), o2.p, o2.ld);
   return {y, bits};
 }
 
@@ -173,26 +200,38 @@ const void* opt_y(const std::optional<at::Tensor>& y, int64_t mask) {
   return yp;
 }
 
-at::Tensor bwd_slab(const at::Tensor& dy, const at::Tensor& x, const void* yp, const at::Tensor& mi,
+// dy (null: the gradient is g2's alone) + g2 (a concat-buffer slice, or null)
+const void* opt_dy(const std::optional<at::Tensor>& dy, const Slice& g2) {
+  if (dy.has_value() && dy->defined()) {
+    check_cl(*dy, "grad");
+    return dy->data_ptr();
+  }
+  TORCH_CHECK(g2.p != nullptr, "rtseg.bn_bwd: needs grad or grad2");
+  return nullptr;
+}
+
+at::Tensor bwd_slab(const void* dyp, const Slice& g2, const at::Tensor& x, const void* yp, const at::Tensor& mi,
                     const at::Tensor& ss, int64_t act, int64_t mask, int& G) {
   const int C = static_cast<int>(x.size(1));
   const int64_t M = rows_of(x);
   G = bn_partial_grid(M, C, dtype_code(x));
   at::Tensor part = at::empty({G, 2 * C}, x.options().dtype(at::kFloat));
-  launch_bn_bwd_reduce(dy.data_ptr(), x.data_ptr(), yp, mi.data_ptr<float>(), ss.data_ptr<float>(),
+  launch_bn_bwd_reduce(dyp, x.data_ptr(), yp, mi.data_ptr<float>(), ss.data_ptr<float>(),
                        dtype_code(x), M, C, static_cast<int>(act), static_cast<int>(mask),
-                       part.data_ptr<float>(), G, cur_stream());
+                       part.data_ptr<float>(), G, cur_stream(), g2.p, g2.ld);
   return part;
 }
 
 // backward, SyncBN step 1: -> bsums[2C] (to be all-reduced)
-at::Tensor bn_bwd_sums(const at::Tensor& dy, const at::Tensor& x, const std::optional<at::Tensor>& y,
-                       const at::Tensor& mi, const at::Tensor& ss, int64_t act, int64_t mask) {
+at::Tensor bn_bwd_sums(const std::optional<at::Tensor>& dy, const at::Tensor& x, const std::optional<at::Tensor>& y,
+                       const at::Tensor& mi, const at::Tensor& ss, int64_t act, int64_t mask,
+                       const std::optional<at::Tensor>& grad2) {
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   check_cl(x, "x");
-  check_cl(dy, "grad");
+  const Slice g2 = slice_of(grad2, x, "grad2");
+  const void* dyp = opt_dy(dy, g2);
   int G = 0;
-  at::Tensor part = bwd_slab(dy, x, opt_y(y, mask), mi, ss, act, mask, G);
+  at::Tensor part = bwd_slab(dyp, g2, x, opt_y(y, mask), mi, ss, act, mask, G);
   const int C = static_cast<int>(x.size(1));
   at::Tensor bsums = at::empty({2 * C}, x.options().dtype(at::kDouble));
   launch_bn_slab_to_sums(part.data_ptr<float>(), G, C, -1.0, bsums.data_ptr<double>(), cur_stream());
@@ -201,13 +240,15 @@ at::Tensor bn_bwd_sums(const at::Tensor& dy, const at::Tensor& x, const std::opt
 
 // backward: reduce (unless bsums given) + finalize + apply -> (dx, dres, dw, db)
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_backward(
-    const at::Tensor& dy, const at::Tensor& x, const std::optional<at::Tensor>& y,
+    const std::optional<at::Tensor>& dy, const at::Tensor& x, const std::optional<at::Tensor>& y,
     const std::optional<at::Tensor>& bsums, const std::optional<at::Tensor>& fwd_sums,
     const at::Tensor& mi, const at::Tensor& ss, const std::optional<at::Tensor>& w, int64_t act,
-    int64_t mask, bool want_dres, bool batch_stats, bool want_dw, const std::optional<at::Tensor>& slab) {
+    int64_t mask, bool want_dres, bool batch_stats, bool want_dw, const std::optional<at::Tensor>& slab,
+    const std::optional<at::Tensor>& grad2) {
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   check_cl(x, "x");
-  check_cl(dy, "grad");
+  const Slice g2 = slice_of(grad2, x, "grad2");
+  const void* dyp = opt_dy(dy, g2);
   const void* yp = opt_y(y, mask);
   const int C = static_cast<int>(x.size(1));
   auto f32 = x.options().dtype(at::kFloat);
@@ -223,7 +264,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_backward(
     part = *slab;
     G = static_cast<int>(part.size(0));
   } else {
-    part = bwd_slab(dy, x, yp, mi, ss, act, mask, G);
+    part = bwd_slab(dyp, g2, x, yp, mi, ss, act, mask, G);
   }
   at::Tensor k = at::empty({3 * C}, f32);
   at::Tensor dw, db;
@@ -238,10 +279,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_backward(
   at::Tensor dx = at::empty_like(x);
   at::Tensor dres;
   if (want_dres) dres = at::empty_like(x);
-  launch_bn_bwd_apply(dy.data_ptr(), x.data_ptr(), yp, mi.data_ptr<float>(), ss.data_ptr<float>(),
+  launch_bn_bwd_apply(dyp, x.data_ptr(), yp, mi.data_ptr<float>(), ss.data_ptr<float>(),
                       k.data_ptr<float>(), dx.data_ptr(), want_dres ? dres.data_ptr() : nullptr,
                       dtype_code(x), rows_of(x), C, static_cast<int>(act), static_cast<int>(mask),
-                      cur_stream());
+                      cur_stream(), g2.p, g2.ld);
   return {dx, dres, dw, db};
 }
 
@@ -257,13 +298,14 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
         "Tensor(b!)? running_var, Tensor(c!)? num_batches_tracked, float momentum, float eps) -> (Tensor, Tensor)");
   m.def("bn_eval_coeffs(Tensor? weight, Tensor? bias, Tensor running_mean, Tensor running_var, "
         "float eps) -> (Tensor, Tensor)");
-  m.def("bn_apply(Tensor x, Tensor scale_shift, Tensor? residual, int act) -> Tensor");
-  m.def("bn_apply_bits(Tensor x, Tensor scale_shift, Tensor? residual, int act) -> (Tensor, Tensor)");
-  m.def("bn_bwd_sums(Tensor grad, Tensor x, Tensor? y, Tensor mean_invstd, Tensor scale_shift, "
-        "int act, int mask) -> Tensor");
-  m.def("bn_backward(Tensor grad, Tensor x, Tensor? y, Tensor? bsums, Tensor? fwd_sums, "
+  m.def("bn_apply(Tensor x, Tensor scale_shift, Tensor? residual, int act, Tensor(a!)? out2=None) -> Tensor");
+  m.def("bn_apply_bits(Tensor x, Tensor scale_shift, Tensor? residual, int act, Tensor(a!)? out2=None) "
+        "-> (Tensor, Tensor)");
+  m.def("bn_bwd_sums(Tensor? grad, Tensor x, Tensor? y, Tensor mean_invstd, Tensor scale_shift, "
+        "int act, int mask, Tensor? grad2=None) -> Tensor");
+  m.def("bn_backward(Tensor? grad, Tensor x, Tensor? y, Tensor? bsums, Tensor? fwd_sums, "
         "Tensor mean_invstd, Tensor scale_shift, Tensor? weight, int act, int mask, bool want_dres, "
-        "bool batch_stats, bool want_dw, Tensor? slab=None) -> (Tensor, Tensor, Tensor, Tensor)");
+        "bool batch_stats, bool want_dw, Tensor? slab=None, Tensor? grad2=None) -> (Tensor, Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {

@@ -42,7 +42,7 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::
                                                  at::IntArrayRef padding, at::IntArrayRef dilation, bool stats,
                                                  const std::optional<at::Tensor>& scale_shift,
                                                  const std::optional<at::Tensor>& residual, int64_t act, int kind) {
-  const bool halo = kind == 1, wres = kind == 2, hreg = kind == 3;
+  const bool halo = kind == 1, wres = kind == 2, hreg = kind == 3 || kind == 4;
   check_act(x, "input");
   TORCH_CHECK(wk.is_cuda() && wk.dim() == 4 && wk.scalar_type() == at::kBFloat16 && wk.is_contiguous() &&
                   wk.size(3) == x.size(1),
@@ -94,7 +94,7 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::
   else if (wres) launch_conv_wres_fwd(g, cur_stream());
   else if (hreg) {
     at::Tensor wpack = at::empty({conv_hreg_pack_elems(g, 0)}, wk.options());
-    launch_conv_hreg(g, 0, wpack.data_ptr(), cur_stream());
+    launch_conv_hreg(g, 0, wpack.data_ptr(), cur_stream(), kind == 4 ? 2 : 1);
   } else launch_conv_igemm_fwd(g, cur_stream());
   if (stats && part.size(0) > 256) {  // fold the per-tile rows so the BN finalize stays cheap
     const int rows = static_cast<int>(part.size(0));
@@ -122,9 +122,13 @@ std::tuple<at::Tensor, at::Tensor> conv_halo(const at::Tensor& x, const at::Tens
 }
 
 // the register-weight halo kernel (conv_hreg.hip): 3 x 3 stride-1 convs, Cin % 64, Cout % 128
+// (rows_per_wave 1: 8 waves; 2: 4 waves with twice the accumulator tiles)
 std::tuple<at::Tensor, at::Tensor> conv_hreg(const at::Tensor& x, const at::Tensor& wk, at::IntArrayRef stride,
-                                             at::IntArrayRef padding, at::IntArrayRef dilation, bool stats) {
-  return conv_fwd_impl(x, wk, stride, padding, dilation, stats, std::nullopt, std::nullopt, 0, 3);
+                                             at::IntArrayRef padding, at::IntArrayRef dilation, bool stats,
+                                             int64_t rows_per_wave) {
+  TORCH_CHECK(rows_per_wave == 1 || rows_per_wave == 2, "rtseg.conv_hreg: rows_per_wave must be 1 or 2");
+  return conv_fwd_impl(x, wk, stride, padding, dilation, stats, std::nullopt, std::nullopt, 0,
+                       rows_per_wave == 2 ? 4 : 3);
 }
 
 // the weights-resident halo kernel (conv_wres.hip): 3 x 3 stride-1 convs with Cin == 64
@@ -137,7 +141,7 @@ std::tuple<at::Tensor, at::Tensor> conv_wres(const at::Tensor& x, const at::Tens
 at::Tensor conv_dgrad_impl(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
                            at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
                            const std::optional<at::Tensor>& bias, const std::optional<at::Tensor>& addend, int kind) {
-  const bool halo = kind == 1, wres = kind == 2, hreg = kind == 3;
+  const bool halo = kind == 1, wres = kind == 2, hreg = kind == 3 || kind == 4;
   check_act(dy, "grad_output");
   TORCH_CHECK(x_size.size() == 4, "rtseg.conv_igemm_dgrad: x_size must be [N, Cin, H, W]");
   TORCH_CHECK(wt.is_cuda() && wt.dim() == 4 && wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() &&
@@ -181,7 +185,7 @@ at::Tensor conv_dgrad_impl(const at::Tensor& dy, const at::Tensor& wt, at::IntAr
   else if (wres) launch_conv_wres_dgrad(g, cur_stream());
   else if (hreg) {
     at::Tensor wpack = at::empty({conv_hreg_pack_elems(g, 1)}, wt.options());
-    launch_conv_hreg(g, 1, wpack.data_ptr(), cur_stream());
+    launch_conv_hreg(g, 1, wpack.data_ptr(), cur_stream(), kind == 4 ? 2 : 1);
   } else launch_conv_igemm_dgrad(g, cur_stream());
   return dx;
 }
@@ -200,8 +204,10 @@ at::Tensor conv_halo_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntAr
 
 at::Tensor conv_hreg_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
                            at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
-                           const std::optional<at::Tensor>& addend) {
-  return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, std::nullopt, addend, 3);
+                           const std::optional<at::Tensor>& addend, int64_t rows_per_wave) {
+  TORCH_CHECK(rows_per_wave == 1 || rows_per_wave == 2, "rtseg.conv_hreg_dgrad: rows_per_wave must be 1 or 2");
+  return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, std::nullopt, addend,
+                         rows_per_wave == 2 ? 4 : 3);
 }
 
 at::Tensor conv_wres_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
@@ -261,9 +267,10 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
         "Tensor? scale_shift, Tensor? residual, int act) -> (Tensor, Tensor)");
   m.def("conv_halo_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
         "Tensor? addend=None) -> Tensor");
-  m.def("conv_hreg(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats) -> (Tensor, Tensor)");
+  m.def("conv_hreg(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats, "
+        "int rows_per_wave=1) -> (Tensor, Tensor)");
   m.def("conv_hreg_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
-        "Tensor? addend=None) -> Tensor");
+        "Tensor? addend=None, int rows_per_wave=1) -> Tensor");
   m.def("conv_wres(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats) -> (Tensor, Tensor)");
   m.def("conv_wres_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
         "Tensor? addend=None) -> Tensor");

@@ -74,19 +74,24 @@ void launch_bn_finalize(const double* sums, int C, const float* w, const float* 
 void launch_bn_eval_coeffs(int C, const float* w, const float* b, const float* rmean,
                            const float* rvar, float eps, float* mean_invstd, float* scale_shift,
                            hipStream_t st);
+// y2 / dy2 (channel-stationary path only, bn_flat(dtype, C) false): a channel slice of a wider
+// channels-last tensor with row stride ld2 elements -- the concat buffer (ops/concat.py).  The
+// apply kernels also store the output there; the backward kernels add it to dy (dy may be null).
 void launch_bn_apply_bits(const void* x, const void* res, const float* scale_shift, void* y,
-                          uint8_t* bits, int dtype, int64_t M, int C, int act, hipStream_t st);
+                          uint8_t* bits, int dtype, int64_t M, int C, int act, hipStream_t st,
+                          void* y2 = nullptr, int64_t ld2 = 0);
 void launch_bn_apply(const void* x, const void* res, const float* scale_shift, void* y, int dtype,
-                     int64_t M, int C, int act, hipStream_t st);
+                     int64_t M, int C, int act, hipStream_t st, void* y2 = nullptr, int64_t ld2 = 0);
 void launch_bn_bwd_reduce(const void* dy, const void* x, const void* y, const float* mean_invstd,
                           const float* scale_shift, int dtype, int64_t M, int C, int act, int mask,
-                          float* part, int G, hipStream_t st);
+                          float* part, int G, hipStream_t st, const void* dy2 = nullptr, int64_t ld2 = 0);
 void launch_bn_bwd_finalize(const float* part, int G, const double* sums, const double* count_ptr,
                             int C, const float* w, const float* mean_invstd, int batch_stats,
                             float* kcoef, float* dw, float* db, hipStream_t st);
 void launch_bn_bwd_apply(const void* dy, const void* x, const void* y, const float* mean_invstd,
                          const float* scale_shift, const float* kcoef, void* dx, void* dres,
-                         int dtype, int64_t M, int C, int act, int mask, hipStream_t st);
+                         int dtype, int64_t M, int C, int act, int mask, hipStream_t st,
+                         const void* dy2 = nullptr, int64_t ld2 = 0);
 
 
 // ---- kd_metrics.hip ---------------------------------------------------------
@@ -207,7 +212,8 @@ void launch_conv_wres_dgrad(const ConvGeom& g, hipStream_t st);
 bool conv_hreg_supported(const ConvGeom& g, int mode);
 int conv_hreg_slabs(const ConvGeom& g);
 int64_t conv_hreg_pack_elems(const ConvGeom& g, int mode);
-void launch_conv_hreg(const ConvGeom& g, int mode, void* wpack, hipStream_t st);
+// rows_per_wave: 1 = 8 waves of 2 x 2 accumulator tiles, 2 = 4 waves of 2 x 4 tiles
+void launch_conv_hreg(const ConvGeom& g, int mode, void* wpack, hipStream_t st, int rows_per_wave = 1);
 
 // ---- conv_whalo.hip -----------------------------------------------------------
 // Halo-tiled weight gradient of 3 x 3 / stride 1 / pad 1 / dilation 1 convs (Cin, Cout % 64 == 0):

@@ -281,7 +281,7 @@ __global__ void bn_eval_coeffs_kernel(int C, const float* __restrict__ w, const 
 template <typename T, int V, int ACT, bool RES, bool BITS = false>
 __device__ __forceinline__ void apply_one(const T* __restrict__ x, const T* __restrict__ res,
                                           const float* coef, T* __restrict__ y, int64_t i, int cv,
-                                          int C, uint8_t* __restrict__ bits = nullptr) {
+                                          int C, uint8_t* __restrict__ bits, T* __restrict__ y2, int64_t ld2) {
   const int c0 = static_cast<int>(i % cv) * V;
   const int64_t off = (i / cv) * C + c0;
   float f[V], r[V];
@@ -296,6 +296,7 @@ __device__ __forceinline__ void apply_one(const T* __restrict__ x, const T* __re
     if constexpr (BITS) b |= (act_grad_pre<ACT>(1.f, z) != 0.f ? 1u : 0u) << j;
   }
   VecIO<T, V>::store(y + off, f);
+  if (y2 != nullptr) VecIO<T, V>::store(y2 + (i / cv) * ld2 + c0, f);  // the concat-buffer copy
   if constexpr (BITS) bits[i] = static_cast<uint8_t>(b);  // vector i = byte i (off / V)
 }
 
@@ -308,7 +309,8 @@ __device__ __forceinline__ void apply_one(const T* __restrict__ x, const T* __re
 template <typename T, int V, int ACT, bool RES, bool BITS>
 __device__ __forceinline__ void apply_rows(const T* __restrict__ x, const T* __restrict__ res,
                                            const float* __restrict__ scale_shift, T* __restrict__ y,
-                                           int64_t M, int C, uint8_t* __restrict__ bits) {
+                                           int64_t M, int C, uint8_t* __restrict__ bits, T* __restrict__ y2,
+                                           int64_t ld2) {
   const int cv = C / V;
   const int cvi = threadIdx.x % cv;
   const int c0 = cvi * V;
@@ -330,6 +332,7 @@ __device__ __forceinline__ void apply_rows(const T* __restrict__ x, const T* __r
       if constexpr (BITS) b |= (act_grad_pre<ACT>(1.f, z) != 0.f ? 1u : 0u) << j;
     }
     VecIO<T, V>::store(y + off, f);
+    if (y2 != nullptr) VecIO<T, V>::store(y2 + row * ld2 + c0, f);
     if constexpr (BITS) bits[row * cv + cvi] = static_cast<uint8_t>(b);
   };
   int64_t row = static_cast<int64_t>(blockIdx.x) * (blockDim.x / cv) + threadIdx.x / cv;
@@ -345,9 +348,10 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x,
                                                        const T* __restrict__ res,
                                                        const float* __restrict__ scale_shift,
                                                        T* __restrict__ y, int64_t M, int C,
-                                                       uint8_t* __restrict__ bits = nullptr) {
+                                                       uint8_t* __restrict__ bits = nullptr,
+                                                       T* __restrict__ y2 = nullptr, int64_t ld2 = 0) {
   if (blockDim.x % (C / V) == 0) {  // block-uniform
-    apply_rows<T, V, ACT, RES, BITS>(x, res, scale_shift, y, M, C, bits);
+    apply_rows<T, V, ACT, RES, BITS>(x, res, scale_shift, y, M, C, bits, y2, ld2);
     return;
   }
   extern __shared__ __attribute__((aligned(16))) float coef[];  // [2][C]
@@ -358,17 +362,35 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x,
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
   for (; i + stride < total; i += 2 * stride) {  // two vectors in flight per thread
-    apply_one<T, V, ACT, RES, BITS>(x, res, coef, y, i, cv, C, bits);
-    apply_one<T, V, ACT, RES, BITS>(x, res, coef, y, i + stride, cv, C, bits);
+    apply_one<T, V, ACT, RES, BITS>(x, res, coef, y, i, cv, C, bits, y2, ld2);
+    apply_one<T, V, ACT, RES, BITS>(x, res, coef, y, i + stride, cv, C, bits, y2, ld2);
   }
-  if (i < total) apply_one<T, V, ACT, RES, BITS>(x, res, coef, y, i, cv, C, bits);
+  if (i < total) apply_one<T, V, ACT, RES, BITS>(x, res, coef, y, i, cv, C, bits, y2, ld2);
 }
 
 // ----------------------------------------------------------- backward -------
+// g = dy (+ dy2: a channel slice of a wider channels-last gradient, row stride ld2 -- the concat
+// buffer's gradient handed over by ops/concat.py; dy may then be null)
+template <typename T, int V>
+__device__ __forceinline__ void load_dy(const T* dy, const T* dy2, int64_t off, int64_t off2, float* g) {
+  if (dy != nullptr) {
+    VecIO<T, V>::load(dy + off, g);
+  } else {
+#pragma unroll
+    for (int j = 0; j < V; ++j) g[j] = 0.f;
+  }
+  if (dy2 != nullptr) {
+    float h[V];
+    VecIO<T, V>::load(dy2 + off2, h);
+#pragma unroll
+    for (int j = 0; j < V; ++j) g[j] += h[j];
+  }
+}
+
 template <typename T, int V, int ACT, int MASK>
-__device__ __forceinline__ void load_g(const T* dy, const T* x, const T* y, const float* coef, int C,
-                                       int64_t off, int c0, float* g, float* xv) {
-  VecIO<T, V>::load(dy + off, g);
+__device__ __forceinline__ void load_g(const T* dy, const T* dy2, const T* x, const T* y, const float* coef, int C,
+                                       int64_t off, int64_t off2, int c0, float* g, float* xv) {
+  load_dy<T, V>(dy, dy2, off, off2, g);
   VecIO<T, V>::load(x + off, xv);
   if constexpr (MASK == kMaskFromY) {
     float yv[V];
@@ -391,7 +413,7 @@ template <typename T, int V, int ACT, int MASK>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y,
     const float* __restrict__ mean_invstd, const float* __restrict__ scale_shift, int64_t M, int C,
-    float* __restrict__ part) {
+    float* __restrict__ part, const T* __restrict__ dy2, int64_t ld2) {
   extern __shared__ __attribute__((aligned(16))) float sm[];  // coef[2C] | mean[C] | partials
   float* coef = sm;
   float* mu = sm + 2 * C;
@@ -412,10 +434,12 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     int64_t r = r0 + g.my_r;
     for (; r + 3 * g.rpi < r1; r += 4 * g.rpi) {  // four rows (8-12 loads) in flight
       float ga[V], xa[V], gb[V], xb[V], gc[V], xc[V], gd[V], xd[V];
-      load_g<T, V, ACT, MASK>(dy, x, y, coef, C, r * C + c0, c0, ga, xa);
-      load_g<T, V, ACT, MASK>(dy, x, y, coef, C, (r + g.rpi) * C + c0, c0, gb, xb);
-      load_g<T, V, ACT, MASK>(dy, x, y, coef, C, (r + 2 * g.rpi) * C + c0, c0, gc, xc);
-      load_g<T, V, ACT, MASK>(dy, x, y, coef, C, (r + 3 * g.rpi) * C + c0, c0, gd, xd);
+      load_g<T, V, ACT, MASK>(dy, dy2, x, y, coef, C, r * C + c0, r * ld2 + c0, c0, ga, xa);
+      load_g<T, V, ACT, MASK>(dy, dy2, x, y, coef, C, (r + g.rpi) * C + c0, (r + g.rpi) * ld2 + c0, c0, gb, xb);
+      load_g<T, V, ACT, MASK>(dy, dy2, x, y, coef, C, (r + 2 * g.rpi) * C + c0, (r + 2 * g.rpi) * ld2 + c0, c0,
+                              gc, xc);
+      load_g<T, V, ACT, MASK>(dy, dy2, x, y, coef, C, (r + 3 * g.rpi) * C + c0, (r + 3 * g.rpi) * ld2 + c0, c0,
+                              gd, xd);
 #pragma unroll
       for (int j = 0; j < V; ++j) {
         s[j] += (ga[j] + gb[j]) + (gc[j] + gd[j]);
@@ -425,7 +449,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     }
     for (; r < r1; r += g.rpi) {
       float ga[V], xa[V];
-      load_g<T, V, ACT, MASK>(dy, x, y, coef, C, r * C + c0, c0, ga, xa);
+      load_g<T, V, ACT, MASK>(dy, dy2, x, y, coef, C, r * C + c0, r * ld2 + c0, c0, ga, xa);
 #pragma unroll
       for (int j = 0; j < V; ++j) { s[j] += ga[j]; q[j] += ga[j] * (xa[j] - m[j]); }
     }
@@ -471,11 +495,11 @@ __global__ void __launch_bounds__(kFinBlock) bn_bwd_finalize_kernel(
 template <typename T, int V, int ACT, int MASK, bool DRES>
 __device__ __forceinline__ void bwd_apply_one(const T* dy, const T* x, const T* y, const float* coef,
                                               const float* mu, const float* k, T* dx, T* dres,
-                                              int64_t i, int cv, int C) {
+                                              int64_t i, int cv, int C, const T* dy2, int64_t ld2) {
   const int c0 = static_cast<int>(i % cv) * V;
   const int64_t off = (i / cv) * C + c0;
   float g[V], xv[V], o[V];
-  load_g<T, V, ACT, MASK>(dy, x, y, coef, C, off, c0, g, xv);
+  load_g<T, V, ACT, MASK>(dy, dy2, x, y, coef, C, off, (i / cv) * ld2 + c0, c0, g, xv);
   if constexpr (DRES) VecIO<T, V>::store(dres + off, g);
 #pragma unroll
   for (int j = 0; j < V; ++j) {
@@ -493,7 +517,8 @@ __device__ __forceinline__ void bwd_apply_rows(const T* __restrict__ dy, const T
                                                const T* __restrict__ y, const float* __restrict__ mean_invstd,
                                                const float* __restrict__ scale_shift,
                                                const float* __restrict__ kcoef, T* __restrict__ dx,
-                                               T* __restrict__ dres, int64_t M, int C) {
+                                               T* __restrict__ dres, int64_t M, int C,
+                                               const T* __restrict__ dy2, int64_t ld2) {
   const int cv = C / V;
   const int c0 = (threadIdx.x % cv) * V;
   float cf[2 * V], k0[V], k1[V], k2[V], mu[V];  // cf: scale | shift (pre-activation mask)
@@ -511,7 +536,7 @@ __device__ __forceinline__ void bwd_apply_rows(const T* __restrict__ dy, const T
   auto one = [&](int64_t row) {
     const int64_t off = row * C + c0;
     float g[V], xv[V], o[V];
-    VecIO<T, V>::load(dy + off, g);
+    load_dy<T, V>(dy, dy2, off, row * ld2 + c0, g);
     VecIO<T, V>::load(x + off, xv);
     if constexpr (MASK == kMaskFromY) {
       float yv[V];
@@ -543,9 +568,10 @@ template <typename T, int V, int ACT, int MASK, bool DRES>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
     const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y,
     const float* __restrict__ mean_invstd, const float* __restrict__ scale_shift,
-    const float* __restrict__ kcoef, T* __restrict__ dx, T* __restrict__ dres, int64_t M, int C) {
+    const float* __restrict__ kcoef, T* __restrict__ dx, T* __restrict__ dres, int64_t M, int C,
+    const T* __restrict__ dy2, int64_t ld2) {
   if (blockDim.x % (C / V) == 0) {  // block-uniform
-    bwd_apply_rows<T, V, ACT, MASK, DRES>(dy, x, y, mean_invstd, scale_shift, kcoef, dx, dres, M, C);
+    bwd_apply_rows<T, V, ACT, MASK, DRES>(dy, x, y, mean_invstd, scale_shift, kcoef, dx, dres, M, C, dy2, ld2);
     return;
   }
   extern __shared__ __attribute__((aligned(16))) float sm[];  // coef[2C] | mu[C] | k[3C]
@@ -561,10 +587,10 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
   for (; i + stride < total; i += 2 * stride) {
-    bwd_apply_one<T, V, ACT, MASK, DRES>(dy, x, y, coef, mu, k, dx, dres, i, cv, C);
-    bwd_apply_one<T, V, ACT, MASK, DRES>(dy, x, y, coef, mu, k, dx, dres, i + stride, cv, C);
+    bwd_apply_one<T, V, ACT, MASK, DRES>(dy, x, y, coef, mu, k, dx, dres, i, cv, C, dy2, ld2);
+    bwd_apply_one<T, V, ACT, MASK, DRES>(dy, x, y, coef, mu, k, dx, dres, i + stride, cv, C, dy2, ld2);
   }
-  if (i < total) bwd_apply_one<T, V, ACT, MASK, DRES>(dy, x, y, coef, mu, k, dx, dres, i, cv, C);
+  if (i < total) bwd_apply_one<T, V, ACT, MASK, DRES>(dy, x, y, coef, mu, k, dx, dres, i, cv, C, dy2, ld2);
 }
 
 // ------------------------------------------ odd channel counts: flat chunks ---
@@ -936,47 +962,50 @@ static void apply_flat(const void* x, const void* res, const float* ss, void* y,
 
 template <typename T, int V, int ACT>
 static void apply_t(const void* x, const void* res, const float* ss, void* y, int64_t M, int C,
-                    hipStream_t st) {
+                    hipStream_t st, void* y2, int64_t ld2) {
   const int64_t work = M * (C / V);
   const size_t lds = sizeof(float) * 2 * C;
   const int grid = apply_grid(work);
   if (res)
     bn_apply_kernel<T, V, ACT, true><<<grid, 256, lds, st>>>(
-        static_cast<const T*>(x), static_cast<const T*>(res), ss, static_cast<T*>(y), M, C);
+        static_cast<const T*>(x), static_cast<const T*>(res), ss, static_cast<T*>(y), M, C, nullptr,
+        static_cast<T*>(y2), ld2);
   else
     bn_apply_kernel<T, V, ACT, false><<<grid, 256, lds, st>>>(
-        static_cast<const T*>(x), nullptr, ss, static_cast<T*>(y), M, C);
+        static_cast<const T*>(x), nullptr, ss, static_cast<T*>(y), M, C, nullptr, static_cast<T*>(y2), ld2);
 }
 
 template <typename T, int V, int ACT>
 static void apply_bits_t(const void* x, const void* res, const float* ss, void* y, uint8_t* bits,
-                         int64_t M, int C, hipStream_t st) {
+                         int64_t M, int C, hipStream_t st, void* y2, int64_t ld2) {
   const int64_t work = M * (C / V);
   if (res != nullptr)
     bn_apply_kernel<T, V, ACT, true, true><<<apply_grid(work), 256, sizeof(float) * 2 * C, st>>>(
-        static_cast<const T*>(x), static_cast<const T*>(res), ss, static_cast<T*>(y), M, C, bits);
+        static_cast<const T*>(x), static_cast<const T*>(res), ss, static_cast<T*>(y), M, C, bits,
+        static_cast<T*>(y2), ld2);
   else
     bn_apply_kernel<T, V, ACT, false, true><<<apply_grid(work), 256, sizeof(float) * 2 * C, st>>>(
-        static_cast<const T*>(x), nullptr, ss, static_cast<T*>(y), M, C, bits);
+        static_cast<const T*>(x), nullptr, ss, static_cast<T*>(y), M, C, bits, static_cast<T*>(y2), ld2);
 }
 
 // (Residual +) activation forward that also writes the derivative bit mask (kMaskBits):
 // bits holds M * C / V bytes, V = bn_vec_width(dtype, C).
 void launch_bn_apply_bits(const void* x, const void* res, const float* scale_shift, void* y,
-                          uint8_t* bits, int dtype, int64_t M, int C, int act, hipStream_t st) {
+                          uint8_t* bits, int dtype, int64_t M, int C, int act, hipStream_t st, void* y2,
+                          int64_t ld2) {
   if (bn_flat(dtype, C)) {
     if (act == kActReLU6) apply_flat<kActReLU6>(x, res, scale_shift, y, bits, M, C, dtype, st);
     else apply_flat<kActReLU>(x, res, scale_shift, y, bits, M, C, dtype, st);
     return;
   }
   with_tv(dtype, C, [&]<typename T, int V>() {
-    if (act == kActReLU6) apply_bits_t<T, V, kActReLU6>(x, res, scale_shift, y, bits, M, C, st);
-    else apply_bits_t<T, V, kActReLU>(x, res, scale_shift, y, bits, M, C, st);
+    if (act == kActReLU6) apply_bits_t<T, V, kActReLU6>(x, res, scale_shift, y, bits, M, C, st, y2, ld2);
+    else apply_bits_t<T, V, kActReLU>(x, res, scale_shift, y, bits, M, C, st, y2, ld2);
   });
 }
 
 void launch_bn_apply(const void* x, const void* res, const float* scale_shift, void* y, int dtype,
-                     int64_t M, int C, int act, hipStream_t st) {
+                     int64_t M, int C, int act, hipStream_t st, void* y2, int64_t ld2) {
   if (bn_flat(dtype, C)) {
     if (act == kActReLU) apply_flat<kActReLU>(x, res, scale_shift, y, nullptr, M, C, dtype, st);
     else if (act == kActReLU6) apply_flat<kActReLU6>(x, res, scale_shift, y, nullptr, M, C, dtype, st);
@@ -984,31 +1013,32 @@ void launch_bn_apply(const void* x, const void* res, const float* scale_shift, v
     return;
   }
   with_tv(dtype, C, [&]<typename T, int V>() {
-    if (act == kActReLU) apply_t<T, V, kActReLU>(x, res, scale_shift, y, M, C, st);
-    else if (act == kActReLU6) apply_t<T, V, kActReLU6>(x, res, scale_shift, y, M, C, st);
-    else apply_t<T, V, kActNone>(x, res, scale_shift, y, M, C, st);
+    if (act == kActReLU) apply_t<T, V, kActReLU>(x, res, scale_shift, y, M, C, st, y2, ld2);
+    else if (act == kActReLU6) apply_t<T, V, kActReLU6>(x, res, scale_shift, y, M, C, st, y2, ld2);
+    else apply_t<T, V, kActNone>(x, res, scale_shift, y, M, C, st, y2, ld2);
   });
 }
 
 template <typename T, int V, int ACT, int MASK>
 static void bwd_reduce_t(const void* dy, const void* x, const void* y, const float* mi,
-                         const float* ss, int64_t M, int C, float* part, int G, hipStream_t st) {
+                         const float* ss, int64_t M, int C, float* part, int G, hipStream_t st,
+                         const void* dy2, int64_t ld2) {
   const int rpi = 256 / (C / V);
   const size_t lds = sizeof(float) * (3 * C + 2 * rpi * C);
   bn_bwd_reduce_kernel<T, V, ACT, MASK><<<G, 256, lds, st>>>(
       static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(y), mi, ss, M, C,
-      part);
+      part, static_cast<const T*>(dy2), ld2);
 }
 
 template <typename T, int V, int ACT, int MASK, bool DRES>
 static void bwd_apply_t(const void* dy, const void* x, const void* y, const float* mi,
                         const float* ss, const float* k, void* dx, void* dres, int64_t M, int C,
-                        hipStream_t st) {
+                        hipStream_t st, const void* dy2, int64_t ld2) {
   const int64_t work = M * (C / V);
   const size_t lds = sizeof(float) * 6 * C;
   bn_bwd_apply_kernel<T, V, ACT, MASK, DRES><<<apply_grid(work), 256, lds, st>>>(
       static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(y), mi, ss, k,
-      static_cast<T*>(dx), static_cast<T*>(dres), M, C);
+      static_cast<T*>(dx), static_cast<T*>(dres), M, C, static_cast<const T*>(dy2), ld2);
 }
 
 #define RT_ACT_MASK_DISPATCH(FN, ...)                                                   \
@@ -1047,7 +1077,7 @@ static void bwd_apply_t(const void* dy, const void* x, const void* y, const floa
 
 void launch_bn_bwd_reduce(const void* dy, const void* x, const void* y, const float* mean_invstd,
                           const float* scale_shift, int dtype, int64_t M, int C, int act, int mask,
-                          float* part, int G, hipStream_t st) {
+                          float* part, int G, hipStream_t st, const void* dy2, int64_t ld2) {
   if (bn_flat(dtype, C)) {  // G (bn_partial_grid) is a multiple of C
     RT_FLAT_DISPATCH((bn_bwd_reduce_flat_kernel<T, ACT, MASK><<<G, 256, 0, st>>>(
         static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(y), mean_invstd, scale_shift,
@@ -1055,7 +1085,7 @@ void launch_bn_bwd_reduce(const void* dy, const void* x, const void* y, const fl
     return;
   }
   with_tv(dtype, C, [&]<typename T, int V>() {
-    RT_ACT_MASK_DISPATCH(bwd_reduce_t, dy, x, y, mean_invstd, scale_shift, M, C, part, G, st);
+    RT_ACT_MASK_DISPATCH(bwd_reduce_t, dy, x, y, mean_invstd, scale_shift, M, C, part, G, st, dy2, ld2);
   });
 }
 
@@ -1069,14 +1099,15 @@ void launch_bn_bwd_finalize(const float* part, int G, const double* sums, const 
 template <typename T, int V, int ACT, int MASK>
 static void bwd_apply_res(const void* dy, const void* x, const void* y, const float* mi,
                           const float* ss, const float* k, void* dx, void* dres, int64_t M, int C,
-                          hipStream_t st) {
-  if (dres) bwd_apply_t<T, V, ACT, MASK, true>(dy, x, y, mi, ss, k, dx, dres, M, C, st);
-  else bwd_apply_t<T, V, ACT, MASK, false>(dy, x, y, mi, ss, k, dx, dres, M, C, st);
+                          hipStream_t st, const void* dy2, int64_t ld2) {
+  if (dres) bwd_apply_t<T, V, ACT, MASK, true>(dy, x, y, mi, ss, k, dx, dres, M, C, st, dy2, ld2);
+  else bwd_apply_t<T, V, ACT, MASK, false>(dy, x, y, mi, ss, k, dx, dres, M, C, st, dy2, ld2);
 }
 
 void launch_bn_bwd_apply(const void* dy, const void* x, const void* y, const float* mean_invstd,
                          const float* scale_shift, const float* kcoef, void* dx, void* dres,
-                         int dtype, int64_t M, int C, int act, int mask, hipStream_t st) {
+                         int dtype, int64_t M, int C, int act, int mask, hipStream_t st,
+                         const void* dy2, int64_t ld2) {
   if (bn_flat(dtype, C)) {
     const int g = flat_grid(M, C, dtype);
     RT_FLAT_DISPATCH({
@@ -1093,7 +1124,7 @@ void launch_bn_bwd_apply(const void* dy, const void* x, const void* y, const flo
   }
   with_tv(dtype, C, [&]<typename T, int V>() {
     RT_ACT_MASK_DISPATCH(bwd_apply_res, dy, x, y, mean_invstd, scale_shift, kcoef, dx, dres, M, C,
-                         st);
+                         st, dy2, ld2);
   });
 }
 

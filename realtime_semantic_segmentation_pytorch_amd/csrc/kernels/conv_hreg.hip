@@ -37,7 +37,6 @@ constexpr int kHH = kTH + 2, kHW = kTW + 2;            // halo of one 64-channel
 constexpr int kHRows = kHH * kHW;                      // 396
 constexpr int kHInstr = (kHRows + 7) / 8;              // 50 LDS-DMA instructions of 8 rows
 constexpr int kHStage = kHInstr * 64;                  // 16-byte chunks per halo buffer (400 rows)
-constexpr int kNW = 8;
 constexpr int kBN = 128;                               // output channels per block
 constexpr int kRed = 4 * 2 * kBN;                      // BN statistics accumulator (floats)
 static_assert(2 * kHStage * 16 + kRed * 4 <= 160 * 1024, "LDS budget");
@@ -69,8 +68,12 @@ __device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t r, uint32_t voff, 
       : "memory");
 }
 
-template <int STATS, int FLIP>
-__global__ void __launch_bounds__(kNW * 64) hreg_conv_kernel(const HrArgs a) {
+// RPW = tile rows per wave: 1 -> 8 waves (2 per SIMD, 2 x 2 accumulator tiles each); 2 -> 4 waves
+// (1 per SIMD, 2 x 4 tiles in the unified 512-register file): half the per-block weight stream
+// (every wave of a channel half reads the same fragments) for twice the B-fragment reads
+template <int STATS, int FLIP, int RPW>
+__global__ void __launch_bounds__(2 * kTH / RPW * 64) hreg_conv_kernel(const HrArgs a) {
+  constexpr int kNW = 2 * kTH / RPW, TJ = 2 * RPW;
   __shared__ uint4 lds[2 * kHStage + kRed / 4];
   float* const red = reinterpret_cast<float*>(lds + 2 * kHStage);  // [4 rows][sum, sumsq][128]
 
@@ -128,13 +131,13 @@ __global__ void __launch_bounds__(kNW * 64) hreg_conv_kernel(const HrArgs a) {
 
   // B fragment geometry: lane -> pixel frow of 32-pixel half tj of the wave's tile row
   const int frow = lane & 31, fhi = lane >> 5;
-  const int hrow0 = wm * kHW + frow;  // + tj * 32 + tap shift
+  const int hrow0 = wm * RPW * kHW + frow;  // + (tj / 2) * kHW + (tj % 2) * 32 + tap shift
 
-  f32x16_t acc[2][2];
+  f32x16_t acc[2][TJ];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < TJ; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
@@ -157,8 +160,8 @@ __global__ void __launch_bounds__(kNW * 64) hreg_conv_kernel(const HrArgs a) {
         }
     }
 #pragma unroll
-    for (int tj = 0; tj < 2; ++tj) {
-      const int oy = oy0 + wm, ox = ox0 + tj * 32 + frow;
+    for (int tj = 0; tj < TJ; ++tj) {
+      const int oy = oy0 + wm * RPW + (tj >> 1), ox = ox0 + (tj & 1) * 32 + frow;
       const bool ok = oy < a.Ho && ox < a.Wo;
       const int64_t off = ((static_cast<int64_t>(n) * a.Ho + (ok ? oy : 0)) * a.Wo + (ok ? ox : 0)) * a.cout;
 #pragma unroll
@@ -229,20 +232,20 @@ __global__ void __launch_bounds__(kNW * 64) hreg_conv_kernel(const HrArgs a) {
       if (q * 9 + tap + 2 < nsteps * 9) wload(gn, wr[(tap + 2) % 3]);
       const int i = tap / 3, j = tap % 3;
       const int sh = FLIP ? (2 - i) * kHW + (2 - j) : i * kHW + j;
-      bf16x8_t bfg[2][2];
+      bf16x8_t bfg[2][TJ];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         const int ch = 2 * ks + fhi;
 #pragma unroll
-        for (int tj = 0; tj < 2; ++tj) {
-          const int hr = hrow0 + tj * 32 + sh;
+        for (int tj = 0; tj < TJ; ++tj) {
+          const int hr = hrow0 + (tj >> 1) * kHW + (tj & 1) * 32 + sh;
           bfg[ks & 1][tj] = as_frag(hb[hr * 8 + (ch ^ ((hr >> 1) & 7))]);
         }
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
-          for (int tj = 0; tj < 2; ++tj)
+          for (int tj = 0; tj < TJ; ++tj)
             acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wr[tap % 3][ti][ks], bfg[ks & 1][tj], acc[ti][tj],
                                                                   0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
@@ -332,7 +335,7 @@ int64_t conv_hreg_pack_elems(const ConvGeom& g, int mode) {  // bf16 elements of
 
 // forward (mode 0: g.x = x, g.w = wk [Cout][3][3][Cin]) or data gradient (mode 1: g.x = dy,
 // g.w = wt [Cin][3][3][Cout], g.res = addend); wpack: conv_hreg_pack_elems bf16 of scratch
-void launch_conv_hreg(const ConvGeom& g, int mode, void* wpack, hipStream_t st) {
+void launch_conv_hreg(const ConvGeom& g, int mode, void* wpack, hipStream_t st, int rows_per_wave) {
   HrArgs k{};
   const bool dgrad = mode == 1;
   if (!hreg_fill(k, g, dgrad)) return;
@@ -348,9 +351,17 @@ void launch_conv_hreg(const ConvGeom& g, int mode, void* wpack, hipStream_t st) 
   k.addend = dgrad ? static_cast<const uint16_t*>(g.res) : nullptr;
   const int grid = hreg_grid(k);
   if (grid <= 0) return;
-  if (dgrad) hreg_conv_kernel<0, 1><<<grid, kNW * 64, 0, st>>>(k);
-  else if (k.part != nullptr) hreg_conv_kernel<1, 0><<<grid, kNW * 64, 0, st>>>(k);
-  else hreg_conv_kernel<0, 0><<<grid, kNW * 64, 0, st>>>(k);
+  if (rows_per_wave == 2) {
+    constexpr int T = 2 * kTH / 2 * 64;
+    if (dgrad) hreg_conv_kernel<0, 1, 2><<<grid, T, 0, st>>>(k);
+    else if (k.part != nullptr) hreg_conv_kernel<1, 0, 2><<<grid, T, 0, st>>>(k);
+    else hreg_conv_kernel<0, 0, 2><<<grid, T, 0, st>>>(k);
+    return;
+  }
+  constexpr int T = 2 * kTH * 64;
+  if (dgrad) hreg_conv_kernel<0, 1, 1><<<grid, T, 0, st>>>(k);
+  else if (k.part != nullptr) hreg_conv_kernel<1, 0, 1><<<grid, T, 0, st>>>(k);
+  else hreg_conv_kernel<0, 0, 1><<<grid, T, 0, st>>>(k);
 }
 
 }  // namespace rtseg

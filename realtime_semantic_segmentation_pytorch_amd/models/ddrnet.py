@@ -194,6 +194,7 @@ class DAPPM(nn.Module):
     def __init__(self, in_channels, out_channels, act_type="relu"):
         super().__init__()
         hid = in_channels // 4
+        self.hid = hid
         self.conv0 = ConvBNAct(in_channels, out_channels, 1, act_type=act_type)
         self.conv1 = ConvBNAct(in_channels, hid, 1, act_type=act_type)
         for i, spec in enumerate(self.POOLS, start=2):
@@ -205,10 +206,12 @@ class DAPPM(nn.Module):
     def forward(self, x):
         hw = x.shape[2:]
         y0 = self.conv0(x)
-        prev = self.conv1(x)
+        # the five branches land in one concat buffer (ops/concat.py)
+        sink = ops.ConcatSink([self.hid] * 5)
+        prev = self.conv1(x, sink=(sink, 0))
         branches = [prev]
         for i in range(2, 6):
             pooled = getattr(self, f"pool{i}")(x)
-            prev = getattr(self, f"conv{i}")(ops.interpolate(pooled, hw, True, skip=prev))
+            prev = getattr(self, f"conv{i}")(ops.interpolate(pooled, hw, True, skip=prev), sink=(sink, i - 1))
             branches.append(prev)
-        return self.conv_last(torch.cat(branches, dim=1)) + y0
+        return self.conv_last(sink.cat(branches)) + y0

@@ -75,13 +75,14 @@ class _FusedTail:
     ``forward(x, residual=None, act=None)`` computes
     ``act(own_act(bn(conv(x))) + residual)``; with a residual the block's own
     activation must be the identity (the reference's residual blocks are built
-    that way: ``conv2`` of ``RB`` uses ``act_type='none'``).
+    that way: ``conv2`` of ``RB`` uses ``act_type='none'``).  ``sink=(ConcatSink, i)``:
+    the output is branch ``i`` of a channel concat (ops/concat.py).
     """
 
-    def forward(self, x, residual=None, act=None):
+    def forward(self, x, residual=None, act=None, sink=None):
         conv, bn, own = self[0], self[1], self[2]
         if ops.conv_ok(x, conv):
-            y = self._mfma_tail(x, conv, bn, own, residual, act)
+            y = self._mfma_tail(x, conv, bn, own, residual, act, sink)
             if y is not None:
                 return y
         elif (residual is None and isinstance(conv, ops.DepthwiseConv2d)
@@ -91,10 +92,10 @@ class _FusedTail:
             out = ops.dw_conv_bn_stats(x, conv)
             if out is not None:
                 y, part = out
-                return ops.bn_act(y, bn, own, act_module=own, part=part)
+                return ops.bn_act(y, bn, own, act_module=own, part=part, sink=sink)
         y = ops.conv_forward(x, conv)
         if residual is None:
-            return ops.bn_act(y, bn, own, act_module=own)
+            return ops.bn_act(y, bn, own, act_module=own, sink=sink)
         own_code = ops.bn_act_code(own)
         if own_code != 0:  # own activation is not identity: apply it before the add
             y = ops.bn_act(y, bn, own, act_module=own)
@@ -105,7 +106,7 @@ class _FusedTail:
                           act_module=act if isinstance(act, nn.Module) else None)
 
     @staticmethod
-    def _mfma_tail(x, conv, bn, own, residual, act):
+    def _mfma_tail(x, conv, bn, own, residual, act, sink=None):
         """conv on the MFMA kernel with the BN statistics (training) or the whole
         BN + residual + activation tail (inference) in its epilogue; None -> stock path."""
         if not isinstance(bn, (nn.BatchNorm2d, nn.SyncBatchNorm)):
@@ -127,7 +128,8 @@ class _FusedTail:
             return None
         y, part = r
         return ops.bn_act(y, bn, post, residual=residual, part=part,
-                          act_module=own if residual is None else (act if isinstance(act, nn.Module) else None))
+                          act_module=own if residual is None else (act if isinstance(act, nn.Module) else None),
+                          sink=sink)
 
 
 class ConvBNAct(_FusedTail, nn.Sequential):

@@ -90,6 +90,7 @@ class STDCModule(nn.Module):
         if stride not in (1, 2):
             raise ValueError(f"Unsupported stride: {stride}\n")
         self.stride = stride
+        self.widths = [out_channels // 2, out_channels // 4, out_channels // 8, out_channels // 8]
         self.block1 = ConvBNAct(in_channels, out_channels // 2, 1)
         self.block2 = ConvBNAct(out_channels // 2, out_channels // 4, 3, stride)
         if stride == 2:
@@ -98,12 +99,15 @@ class STDCModule(nn.Module):
         self.block4 = ConvBNAct(out_channels // 8, out_channels // 8, 3)
 
     def forward(self, x):
-        x1 = self.block1(x)
-        x2 = self.block2(x1)
+        # the four branches land in one concat buffer (ops/concat.py): their BN kernels store
+        # there too, and the cat's backward hands each BN its gradient slice in place
+        sink = ops.ConcatSink(self.widths)
+        x1 = self.block1(x, sink=(sink, 0) if self.stride == 1 else None)
+        x2 = self.block2(x1, sink=(sink, 1))
         if self.stride == 2:
             x1 = self.pool(x1)
-        x3 = self.block3(x2)
-        return torch.cat([x1, x2, x3, self.block4(x3)], dim=1)
+        x3 = self.block3(x2, sink=(sink, 2))
+        return sink.cat([x1, x2, x3, self.block4(x3, sink=(sink, 3))])
 
 
 class LaplacianConv(nn.Module):

@@ -14,6 +14,7 @@ from .bn import (bn_act, act_code as bn_act_code, fused_ok as bn_fused_ok, conve
 from .detail import detail_loss, detail_loss_reference, detail_target_reference
 from .postprocess import colorize, colorize_reference
 from .confmat import confusion_matrix, confusion_matrix_reference
+from .concat import ConcatSink
 from .dwconv import DepthwiseConv2d, convert_depthwise, depthwise_ok, dw_conv2d, dw_conv_bn_stats
 from .pool import (avg_pool2d, max_pool2d, adaptive_avg_pool2d, convert_pooling, AvgPool2d, MaxPool2d,
                    AdaptiveAvgPool2d, MaxUnpool2d, max_pool2d_with_indices, max_unpool2d, AdaptiveMaxPool2d,

@@ -62,7 +62,7 @@ def _sync_group(bn):
 
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, bn, act, use_batch_stats, pg, part=None):
+    def forward(ctx, x, weight, bias, residual, bn, act, use_batch_stats, pg, part=None, out2=None):
         if use_batch_stats:
             track = bn.track_running_stats and bn.training and bn.running_mean is not None
             rm = bn.running_mean if track else None
@@ -94,10 +94,14 @@ class _BNActFn(torch.autograd.Function):
             mask = MASK_FROM_X
         else:
             mask = MASK_BITS if _USE_BITS else MASK_FROM_Y
+        # out2: this output's channel slice of a concat buffer (ops/concat.py), stored too
         if mask == MASK_BITS:
-            y, bits = ops().bn_apply_bits(x, ss, residual, act)
+            y, bits = ops().bn_apply_bits(x, ss, residual, act, out2)
         else:
-            y, bits = ops().bn_apply(x, ss, residual, act), None
+            y, bits = ops().bn_apply(x, ss, residual, act, out2), None
+        # the concat node hands its gradient slice over here (read in place by the kernels)
+        ctx.dy2_slot = [] if out2 is not None else None
+        ctx.set_materialize_grads(False)
         ctx.act, ctx.mask, ctx.pg = act, mask, pg
         ctx.batch_stats = use_batch_stats
         ctx.has_res = residual is not None
@@ -119,17 +123,21 @@ class _BNActFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, y, mi, ss, sums, weight = ctx.saved_tensors
         mask = ctx.mask
-        dy = _aligned_cl(dy)
+        dy2 = ctx.dy2_slot.pop() if ctx.dy2_slot else None
+        if dy is None and dy2 is None:
+            return (None,) * 10
+        if dy is not None:
+            dy = _aligned_cl(dy)
         bsums = local = None
         want_dres = ctx.has_res and ctx.needs_input_grad[3]
         want_dw = ctx.has_w and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
         if ctx.pg is not None:
-            bsums = ops().bn_bwd_sums(dy, x, y, mi, ss, ctx.act, mask)
+            bsums = ops().bn_bwd_sums(dy, x, y, mi, ss, ctx.act, mask, dy2)
             if want_dw:
                 local = bsums.clone()
             dist.all_reduce(bsums, group=ctx.pg)
         dx, dres, dw, db = ops().bn_backward(dy, x, y, bsums, sums, mi, ss, weight, ctx.act,
-                                             mask, want_dres, ctx.batch_stats, want_dw, None)
+                                             mask, want_dres, ctx.batch_stats, want_dw, None, dy2)
         if local is not None:
             # parameter gradients are this rank's contribution (DDP averages them), as in torch's
             # SyncBatchNorm; only the input-gradient coefficients use the all-reduced sums
@@ -140,7 +148,7 @@ class _BNActFn(torch.autograd.Function):
             ctx.handoff.append(dres)  # the conv node adds it in its dgrad epilogue
             dres = None
         return (dx, dw if want_dw else None, db if want_dw else None,
-                dres if want_dres else None, None, None, None, None, None)
+                dres if want_dres else None, None, None, None, None, None, None)
 
 
 def eval_coeffs(bn):
@@ -195,11 +203,14 @@ def fused_ok(x: torch.Tensor, bn, act) -> bool:
 
 
 def bn_act(x: torch.Tensor, bn, act=None, residual: Optional[torch.Tensor] = None,
-           act_module: Optional[nn.Module] = None, part: Optional[torch.Tensor] = None) -> torch.Tensor:
+           act_module: Optional[nn.Module] = None, part: Optional[torch.Tensor] = None,
+           sink=None) -> torch.Tensor:
     """``act(bn(x) + residual)``; ``act`` is a fused-activation code or module/str.
 
     ``part``: BN statistics slab of ``x`` already computed by its producer (the MFMA conv
-    epilogue, ``ops.conv``); used only on the fused batch-statistics path."""
+    epilogue, ``ops.conv``); used only on the fused batch-statistics path.
+    ``sink``: ``(ConcatSink, branch index)`` -- the output is a branch of a channel concat
+    (ops/concat.py); the fused kernel also stores it into the concat buffer."""
     code = act if isinstance(act, int) else act_code(act)
     if use_hip(x, "bn") and code is not None and fused_ok(x, bn, code) and (
             residual is None or (residual.shape == x.shape
@@ -209,8 +220,12 @@ def bn_act(x: torch.Tensor, bn, act=None, residual: Optional[torch.Tensor] = Non
             residual = residual.to(x.dtype)
         use_batch = bn.training or not bn.track_running_stats or bn.running_mean is None
         pg = _sync_group(bn) if use_batch else None
-        return _BNActFn.apply(x, bn.weight, bn.bias, residual, bn, code, use_batch, pg,
-                              part if use_batch else None)
+        out2 = sink[0].slot(sink[1], x) if sink is not None and sink[0] is not None else None
+        y = _BNActFn.apply(x, bn.weight, bn.bias, residual, bn, code, use_batch, pg,
+                           part if use_batch else None, out2)
+        if out2 is not None:
+            sink[0].record(sink[1], y, y.grad_fn)
+        return y
     y = bn(x)
     if residual is not None:
         y = y + residual
@@ -255,7 +270,7 @@ class FusedBatchNorm2d(nn.BatchNorm2d):
         if use_hip(x, "bn") and fused_ok(x, self, ACT_NONE):
             use_batch = self.training or not self.track_running_stats or self.running_mean is None
             pg = _sync_group(self) if use_batch else None
-            return _BNActFn.apply(x, self.weight, self.bias, None, self, ACT_NONE, use_batch, pg)
+            return _BNActFn.apply(x, self.weight, self.bias, None, self, ACT_NONE, use_batch, pg, None, None)
         return nn.BatchNorm2d.forward(self, x)
 
 
@@ -264,7 +279,7 @@ class FusedSyncBatchNorm(nn.SyncBatchNorm):
         if use_hip(x, "bn") and fused_ok(x, self, ACT_NONE):
             use_batch = self.training or not self.track_running_stats or self.running_mean is None
             pg = _sync_group(self) if use_batch else None
-            return _BNActFn.apply(x, self.weight, self.bias, None, self, ACT_NONE, use_batch, pg)
+            return _BNActFn.apply(x, self.weight, self.bias, None, self, ACT_NONE, use_batch, pg, None, None)
         return nn.SyncBatchNorm.forward(self, x)
 
 

@@ -135,7 +135,8 @@ def wres_ok(conv, reduce_c: int, out_c: int) -> bool:
 
 def hreg_ok(conv, reduce_c: int, out_c: int) -> bool:
     """Shapes ``conv_hreg`` takes (``csrc/kernels/conv_hreg.hip``): 3 x 3, stride 1, pad 1, dilation
-    1, a 64-channel multiple summed over, a 128-channel multiple produced."""
+    1, a 64-channel multiple summed over, a 128-channel multiple produced.  Two candidates: "hreg"
+    (8 waves x 1 tile row) and "hreg2" (4 waves x 2 rows: half the weight stream)."""
     if os.environ.get("RTSEG_CONV_HREG", "auto") == "0":
         return False
     return (tuple(conv.kernel_size) == (3, 3) and tuple(conv.stride) == (1, 1) and tuple(conv.padding) == (1, 1)
@@ -162,6 +163,8 @@ def _order(cands):
         cands.sort(key=lambda c: c[0] != "whalo")
     if os.environ.get("RTSEG_CONV_HREG") == "1":
         cands.sort(key=lambda c: c[0] != "hreg")
+    if os.environ.get("RTSEG_CONV_HREG") == "2":
+        cands.sort(key=lambda c: c[0] != "hreg2")
     return cands
 
 
@@ -245,10 +248,15 @@ def _choose(key, candidates):
     if torch.cuda.is_current_stream_capturing():
         return len(candidates) - 1  # MIOpen is last
     with torch.no_grad():
-        # three interleaved rounds, best of each: one noisy round (clock ramp, a neighbour's
-        # allocation) no longer flips the pick from run to run
-        rounds = [[_time(fn, reps=4) for _, fn in candidates] for _ in range(3)]
-        times = [min(r[i] for r in rounds) for i in range(len(candidates))]
+        # one timed call each first: a candidate > 4x slower than the best is out (MIOpen's
+        # immediate-mode fallback for a shape without find-db record can be a naive direct kernel
+        # taking seconds per call -- timing it 13 times made bench.py --batch 48's first step
+        # look hung, profiles/r4_bench/README.md); then three interleaved rounds over the rest,
+        # best of each, so one noisy round (clock ramp, a neighbour's allocation) cannot flip the pick
+        first = [_time(fn, reps=1) for _, fn in candidates]
+        live = [i for i, t in enumerate(first) if t <= 4 * min(first)]
+        rounds = [{i: _time(candidates[i][1], reps=4) / 4 for i in live} for _ in range(3)]
+        times = [min(r[i] for r in rounds) if i in live else first[i] for i in range(len(candidates))]
     best = min(range(len(times)), key=times.__getitem__)
     _DECISIONS[key] = (best, candidates[best][0], [round(t, 4) for t in times])
     _db_record(key, candidates[best][0] + "@" + "+".join(sorted(names)))
@@ -291,8 +299,8 @@ class _ConvFn(torch.autograd.Function):
             y, part = ops().conv_halo(x, wk, stride, padding, dilation, stats, None, None, 0)
         elif impl == "wres":
             y, part = ops().conv_wres(x, wk, stride, padding, dilation, stats)
-        elif impl == "hreg":
-            y, part = ops().conv_hreg(x, wk, stride, padding, dilation, stats)
+        elif impl in ("hreg", "hreg2"):
+            y, part = ops().conv_hreg(x, wk, stride, padding, dilation, stats, 2 if impl == "hreg2" else 1)
         elif impl == "mfma":
             y, part = ops().conv_mfma(x, wk, stride, padding, dilation, stats, None, None, 0)
         else:
@@ -353,7 +361,8 @@ def _fwd_impl(x, wk, conv, key, stats) -> str:
         if wres_ok(conv, cin, cout):
             cands.append(("wres", lambda: ops().conv_wres(x, wk, stride, padding, dilation, stats)))
         if hreg_ok(conv, cin, cout):
-            cands.append(("hreg", lambda: ops().conv_hreg(x, wk, stride, padding, dilation, stats)))
+            cands.append(("hreg", lambda: ops().conv_hreg(x, wk, stride, padding, dilation, stats, 1)))
+            cands.append(("hreg2", lambda: ops().conv_hreg(x, wk, stride, padding, dilation, stats, 2)))
     elif cin % 32 == 0 and cout % 8 == 0:
         cands.append(("mfma", lambda: ops().conv_mfma(x, wk, stride, padding, dilation, stats, None, None, 0)))
     if not cands:
@@ -396,10 +405,10 @@ def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None):
         return torch.ops.aten.convolution_backward(dy, x, wk.permute(0, 3, 1, 2), None, stride, padding, dilation, False,
                                                    [0, 0], 1, [True, False, False])[0]
 
-    def hreg():
+    def hreg(rows_per_wave=1):
         if not wt:
             wt.append(wk.permute(3, 1, 2, 0).contiguous())
-        return ops().conv_hreg_dgrad(dy, wt[0], list(x.shape), stride, padding, dilation, addend)
+        return ops().conv_hreg_dgrad(dy, wt[0], list(x.shape), stride, padding, dilation, addend, rows_per_wave)
 
     cands = [("igemm", ours)] if cout % 64 == 0 and cin % 8 == 0 else []
     if halo_ok(conv, cout, cin):
@@ -408,10 +417,11 @@ def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None):
         cands.append(("wres", wres))
     if hreg_ok(conv, cout, cin):
         cands.append(("hreg", hreg))
+        cands.append(("hreg2", lambda: hreg(2)))
     cands.append(("miopen", miopen))
     name, fn = cands[_choose(("dgrad",) + key, _order(cands))]
     dx = fn()
-    if addend is not None and name not in ("igemm", "halo", "wres", "hreg"):
+    if addend is not None and name not in ("igemm", "halo", "wres", "hreg", "hreg2"):
         dx = dx + addend
     return dx
 

@@ -63,7 +63,7 @@ def test_wres_dgrad(geom, with_addend):
     dy = _t((n, 64, h, w), g).contiguous(**cl)
     add = _t((n, cin, h, w), g).contiguous(**cl)
     dx = torch.ops.rtseg.conv_wres_dgrad(dy, wt.permute(1, 2, 3, 0).contiguous(), [n, cin, h, w], [1, 1], [1, 1],
-                                         [1, 1], add if with_addend else None)
+                                         [1, 1], add if with_addend else None, rpw)
     ref = torch.nn.grad.conv2d_input((n, cin, h, w), wt.float(), dy.float(), 1, 1, 1)
     _close(dx, ref + add.float() if with_addend else ref, 2e-2)
 
@@ -153,29 +153,31 @@ def test_whalo_wgrad(geom, channels_last):
 HREG = [(2, 64, 9, 70, 128), (1, 128, 17, 130, 128), (3, 192, 6, 40, 256), (8, 128, 66, 256, 128)]
 
 
+@pytest.mark.parametrize("rpw", [1, 2])
 @pytest.mark.parametrize("geom", HREG)
-def test_hreg_forward_and_stats(geom):
+def test_hreg_forward_and_stats(geom, rpw):
     n, cin, h, w, cout = geom
     g = torch.Generator().manual_seed(6)
     x = _t((n, cin, h, w), g).contiguous(memory_format=torch.channels_last)
     wt = _t((cout, cin, 3, 3), g, 1 / (3 * cin ** 0.5))
     wk = wt.permute(0, 2, 3, 1).contiguous()
-    y, part = torch.ops.rtseg.conv_hreg(x, wk, [1, 1], [1, 1], [1, 1], True)
+    y, part = torch.ops.rtseg.conv_hreg(x, wk, [1, 1], [1, 1], [1, 1], True, rpw)
     ref = F.conv2d(x.float(), wt.float(), None, 1, 1)
     assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
     _close(y, ref, 2e-2)
     rf = ref.double()
     torch.testing.assert_close(part[:, :cout].double().sum(0), rf.sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
     torch.testing.assert_close(part[:, cout:].double().sum(0), rf.square().sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
-    y1, p1 = torch.ops.rtseg.conv_hreg(x, wk, [1, 1], [1, 1], [1, 1], True)
+    y1, p1 = torch.ops.rtseg.conv_hreg(x, wk, [1, 1], [1, 1], [1, 1], True, rpw)
     assert torch.equal(y1, y) and torch.equal(p1, part)
-    y2, _ = torch.ops.rtseg.conv_hreg(x, wk, [1, 1], [1, 1], [1, 1], False)
+    y2, _ = torch.ops.rtseg.conv_hreg(x, wk, [1, 1], [1, 1], [1, 1], False, rpw)
     assert torch.equal(y2, y)
 
 
+@pytest.mark.parametrize("rpw", [1, 2])
 @pytest.mark.parametrize("geom", HREG)
 @pytest.mark.parametrize("with_addend", [False, True])
-def test_hreg_dgrad(geom, with_addend):
+def test_hreg_dgrad(geom, with_addend, rpw):
     """Data gradient of the forward conv (n, cout -> cin roles swapped: the dgrad reduces over the
     forward Cout and produces the forward Cin, so geometry (n, a, h, w, b) tests a conv b -> a)."""
     n, cout_fwd, h, w, cin_fwd = geom
@@ -185,6 +187,6 @@ def test_hreg_dgrad(geom, with_addend):
     dy = _t((n, cout_fwd, h, w), g).contiguous(**cl)
     add = _t((n, cin_fwd, h, w), g).contiguous(**cl)
     dx = torch.ops.rtseg.conv_hreg_dgrad(dy, wt.permute(1, 2, 3, 0).contiguous(), [n, cin_fwd, h, w], [1, 1], [1, 1],
-                                         [1, 1], add if with_addend else None)
+                                         [1, 1], add if with_addend else None, rpw)
     ref = torch.nn.grad.conv2d_input((n, cin_fwd, h, w), wt.float(), dy.float(), 1, 1, 1)
     _close(dx, ref + add.float() if with_addend else ref, 2e-2)

@@ -72,6 +72,10 @@ def _run(rank, world, port, out, name, amp):
     c.amp_training, c.amp_dtype, c.channels_last = amp, "bf16", True
     c.base_workers, c.use_tb, c.save_ckpt, c.load_ckpt, c.use_ema = 0, False, False, False, True
     c.optimizer_type, c.lr_policy = "sgd", "cos_warmup"
+    # plain CE: OHEM keeps each rank's hardest pixels (as the reference does under DDP), which is
+    # not the hardest pixels of the concatenated batch -- only a batch-decomposable loss can be
+    # compared across the two layouts (STDC2's confident random-init heads trip OHEM's threshold)
+    c.loss_type = "ce"
     # the reference scales the SGD learning rate with the number of GPUs (utils/optimizer.py:9):
     # the one-process run gets the 2-rank run's effective rate
     c.base_lr = c.base_lr * (2 // world)

@@ -115,6 +115,11 @@ def main():
                         rows.append(("hreg", relerr(yg, y_ref), t_m, t_g))
                         t_gs = timeit(lambda: torch.ops.rtseg.conv_hreg(x, wk, [s, s], [p, p], [1, 1], True), a.iters)
                         rows.append(("hreg+st", 0.0, t_m, t_gs))
+                        yg, _ = torch.ops.rtseg.conv_hreg(x, wk, [s, s], [p, p], [1, 1], False, 2)
+                        t_g = timeit(lambda: torch.ops.rtseg.conv_hreg(x, wk, [s, s], [p, p], [1, 1], False, 2), a.iters)
+                        rows.append(("hreg2", relerr(yg, y_ref), t_m, t_g))
+                        t_gs = timeit(lambda: torch.ops.rtseg.conv_hreg(x, wk, [s, s], [p, p], [1, 1], True, 2), a.iters)
+                        rows.append(("hreg2+st", 0.0, t_m, t_gs))
                     if wres and cin == 64:  # the weights-resident halo kernel (conv_wres.hip)
                         yw, _ = torch.ops.rtseg.conv_wres(x, wk, [s, s], [p, p], [1, 1], False)
                         t_w = timeit(lambda: torch.ops.rtseg.conv_wres(x, wk, [s, s], [p, p], [1, 1], False), a.iters)
@@ -139,6 +144,10 @@ def main():
                     t_g = timeit(lambda: torch.ops.rtseg.conv_hreg_dgrad(dy, wtr, list(x.shape), [s, s], [p, p],
                                                                          [1, 1]), a.iters)
                     rows.append(("hreg_dg", relerr(dxg, dx_ref), t_m, t_g))
+                    dxg = torch.ops.rtseg.conv_hreg_dgrad(dy, wtr, list(x.shape), [s, s], [p, p], [1, 1], None, 2)
+                    t_g = timeit(lambda: torch.ops.rtseg.conv_hreg_dgrad(dy, wtr, list(x.shape), [s, s], [p, p],
+                                                                         [1, 1], None, 2), a.iters)
+                    rows.append(("hreg2_dg", relerr(dxg, dx_ref), t_m, t_g))
                 if wres and cout == 64 and cfg is None:
                     dxw = torch.ops.rtseg.conv_wres_dgrad(dy, wtr, list(x.shape), [s, s], [p, p], [1, 1])
                     t_w = timeit(lambda: torch.ops.rtseg.conv_wres_dgrad(dy, wtr, list(x.shape), [s, s], [p, p],

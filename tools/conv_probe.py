@@ -41,6 +41,8 @@ def main():
         "whalo": lambda: r.conv_whalo_wgrad(x, dy, 3, 3, [1, 1], [1, 1], [1, 1]),
         "hreg": lambda: r.conv_hreg(x, wk, [1, 1], [1, 1], [1, 1], a.stats),
         "hreg_dg": lambda: r.conv_hreg_dgrad(dy, wtr, list(x.shape), [1, 1], [1, 1], [1, 1]),
+        "hreg2": lambda: r.conv_hreg(x, wk, [1, 1], [1, 1], [1, 1], a.stats, 2),
+        "hreg2_dg": lambda: r.conv_hreg_dgrad(dy, wtr, list(x.shape), [1, 1], [1, 1], [1, 1], None, 2),
     }
     fn = fns[a.kind]
     for _ in range(a.iters):
