@@ -18,6 +18,7 @@ from typing import Sequence, Union
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from .. import ops
 
@@ -206,9 +207,19 @@ class PyramidPoolingModule(nn.Module):
         self.conv = PWConvBNAct(2 * in_channels, out_channels, act_type=act_type, bias=bias)
 
     def forward(self, x):
-        hw = x.shape[2:]
-        feats = [x] + [ops.interpolate(getattr(self, f"stage{i}")(x), hw, True) for i in range(1, 5)]
-        return self.conv(torch.cat(feats, dim=1))
+        # conv1x1(cat([x, up(s1), .., up(s4)])) == W_x x + sum_i up(W_i s_i): a 1x1 conv commutes
+        # with the bilinear resize, so the four full-size branches and their concat (the
+        # reference's torch.cat, modules.py:134-158) are never materialised -- each branch's slice
+        # of the fuse weight runs on its pooled map (1x1 .. 6x6) and is resized straight into
+        # the sum (interpolate's fused skip-add)
+        hw, c = x.shape[2:], x.shape[1]
+        conv, bn, act = self.conv[0], self.conv[1], self.conv[2]
+        y = F.conv2d(x, conv.weight[:, :c], conv.bias)
+        for i in range(1, 5):
+            s = getattr(self, f"stage{i}")(x)
+            lo = c + (i - 1) * s.shape[1]
+            y = ops.interpolate(F.conv2d(s, conv.weight[:, lo:lo + s.shape[1]]), hw, True, skip=y)
+        return ops.bn_act(y, bn, act, act_module=act)
 
 
 class SegHead(nn.Sequential):

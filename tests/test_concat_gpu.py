@@ -45,21 +45,27 @@ def test_bn_kernels_concat_slice(dtype, mask_bits):
     dbuf = torch.randn(n, total, h, w, generator=g).cuda().to(dtype).contiguous(**CL)
     d2 = dbuf[:, off:off + c]
     dy = torch.randn(n, c, h, w, generator=g).cuda().to(dtype).contiguous(**CL)
+    # reference: the dense fp32 formulation on the same (exactly representable) values -- the
+    # kernels add the slice in fp32 as well, so the parameter gradients agree to fp32 rounding
+    x32 = x.float().contiguous(**CL)
+    ysave32 = ysave
+    if mask_bits:  # the fp32 kernels' bit mask has one byte per 4 channels (bf16: per 8)
+        ysave32 = torch.ops.rtseg.bn_apply_bits(x32, ss, res.float().contiguous(**CL), 1)[1]
     for dense in (dy, None):
-        want_in = d2.float() + (dense.float() if dense is not None else 0)
-        want = torch.ops.rtseg.bn_backward(want_in.to(dtype).contiguous(**CL) if dtype == torch.float32
-                                           else want_in.to(dtype).contiguous(**CL), x, ysave, None, sums, mi, ss,
-                                           wt, 1, mask, mask_bits, True, True, None)
+        tot = (d2.float() + (dense.float() if dense is not None else 0)).contiguous(**CL)
+        want = torch.ops.rtseg.bn_backward(tot, x32, ysave32, None, sums, mi, ss, wt, 1, mask, mask_bits, True, True,
+                                           None)
         got = torch.ops.rtseg.bn_backward(dense, x, ysave, None, sums, mi, ss, wt, 1, mask, mask_bits, True, True,
                                           None, d2)
-        tol = 1e-5 if dtype == torch.float32 else 2e-2
-        for a, b_ in zip(got, want):
+        out_tol = 1e-5 if dtype == torch.float32 else 1e-2  # dx / dres are stored in the activation dtype
+        for i, (a, b_) in enumerate(zip(got, want)):
             if a is None or not a.numel():
                 continue
-            torch.testing.assert_close(a.float(), b_.float(), rtol=tol, atol=tol)
+            rel = float((a.float() - b_.float()).norm() / (b_.float().norm() + 1e-12))
+            assert rel < (out_tol if i < 2 else 1e-5), (i, rel)
         sums_got = torch.ops.rtseg.bn_bwd_sums(dense, x, ysave, mi, ss, 1, mask, d2)
-        sums_want = torch.ops.rtseg.bn_bwd_sums(want_in.to(dtype).contiguous(**CL), x, ysave, mi, ss, 1, mask)
-        torch.testing.assert_close(sums_got, sums_want, rtol=tol, atol=tol * 10)
+        sums_want = torch.ops.rtseg.bn_bwd_sums(tot, x32, ysave32, mi, ss, 1, mask)
+        torch.testing.assert_close(sums_got, sums_want, rtol=1e-5, atol=1e-4)
 
 
 def _stdc_step(mod, x, sink_on, monkeypatch):
