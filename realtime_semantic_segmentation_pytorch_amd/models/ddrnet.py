@@ -180,8 +180,12 @@ class BilateralFusion(nn.Module):
         self.act = Activation(act_type)
 
     def forward(self, x_low, x_high):
-        new_low = self.conv_high(x_high, residual=x_low, act=self.act)
-        new_high = _resize_add_act(self.conv_low(x_low), x_high.shape[2:], x_high, self.act)
+        # both branch convs first, their SyncBN statistics all-reduces in flight together (each
+        # overlaps the other branch's conv), then the two BN tails
+        h_low = self.conv_high.start(x_high)
+        h_high = self.conv_low.start(x_low)
+        new_low = self.conv_high.finish(h_low, residual=x_low, act=self.act)
+        new_high = _resize_add_act(self.conv_low.finish(h_high), x_high.shape[2:], x_high, self.act)
         return new_low, new_high
 
 

@@ -106,6 +106,33 @@ class _FusedTail:
         return ops.bn_act(y, bn, post, residual=residual,
                           act_module=act if isinstance(act, nn.Module) else None)
 
+    def start(self, x):
+        """First half of ``forward`` for a caller that interleaves independent branches: the conv
+        with its BN statistics, whose SyncBN all-reduce is issued asynchronously
+        (``ops.bn_stats_begin``); :meth:`finish` waits for it at the BN finalize.  Queued between
+        the two, the other branch's conv overlaps the collective."""
+        conv, bn = self[0], self[1]
+        if (ops.conv_ok(x, conv) and isinstance(bn, (nn.BatchNorm2d, nn.SyncBatchNorm))
+                and (bn.training or not bn.track_running_stats or bn.running_mean is None)):
+            r = ops.conv_bn_stats(x, conv)
+            if r is not None:
+                y, part = r
+                return y, part, ops.bn_stats_begin(y, bn, part)
+        return (x,)
+
+    def finish(self, h, residual=None, act=None):
+        """Second half of ``forward``: ``h`` from :meth:`start`."""
+        if len(h) == 1:
+            return self.forward(h[0], residual, act)
+        y, part, pending = h
+        bn, own = self[1], self[2]
+        own_code = ops.bn_act_code(own)
+        if residual is not None and own_code != 0:
+            raise ValueError("start/finish: a residual needs the block's own activation to be identity")
+        post = own_code if residual is None else (ops.bn_act_code(act) if act is not None else 0)
+        return ops.bn_act(y, bn, post, residual=residual, part=part, pending=pending,
+                          act_module=own if residual is None else (act if isinstance(act, nn.Module) else None))
+
     @staticmethod
     def _mfma_tail(x, conv, bn, own, residual, act, sink=None):
         """conv on the MFMA kernel with the BN statistics (training) or the whole

@@ -62,7 +62,7 @@ def _sync_group(bn):
 
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, bn, act, use_batch_stats, pg, part=None, out2=None):
+    def forward(ctx, x, weight, bias, residual, bn, act, use_batch_stats, pg, part=None, out2=None, pending=None):
         if use_batch_stats:
             track = bn.track_running_stats and bn.training and bn.running_mean is not None
             rm = bn.running_mean if track else None
@@ -76,6 +76,9 @@ class _BNActFn(torch.autograd.Function):
                 else:
                     mi, ss, sums = ops().bn_stats_finalize(x, weight, bias, rm, rv, nb,
                                                            float(bn.momentum), float(bn.eps))
+            elif pending is not None:  # SyncBN, all-reduce issued by bn_stats_begin: wait for it here
+                sums, work = pending
+                work.wait()
             else:  # SyncBN: one all-reduce of (sum, sumsq, count) in fp64 over RCCL
                 sums = ops().bn_slab_sums(part, count) if part is not None else ops().bn_stats_sums(x)
                 dist.all_reduce(sums, group=pg)
@@ -125,7 +128,7 @@ class _BNActFn(torch.autograd.Function):
         mask = ctx.mask
         dy2 = ctx.dy2_slot.pop() if ctx.dy2_slot else None
         if dy is None and dy2 is None:
-            return (None,) * 10
+            return (None,) * 11
         if dy is not None:
             dy = _aligned_cl(dy)
         bsums = local = None
@@ -148,7 +151,7 @@ class _BNActFn(torch.autograd.Function):
             ctx.handoff.append(dres)  # the conv node adds it in its dgrad epilogue
             dres = None
         return (dx, dw if want_dw else None, db if want_dw else None,
-                dres if want_dres else None, None, None, None, None, None, None)
+                dres if want_dres else None, None, None, None, None, None, None, None)
 
 
 def eval_coeffs(bn):
@@ -202,15 +205,34 @@ def fused_ok(x: torch.Tensor, bn, act) -> bool:
     return bn.affine or bn.weight is None
 
 
+def bn_stats_begin(x: torch.Tensor, bn, part: Optional[torch.Tensor] = None):
+    """Start the SyncBN batch statistics of ``x`` (the BN input) ahead of ``bn_act``: the local fp64
+    sums and their all-reduce with ``async_op=True`` -- RCCL runs it on its own stream while the
+    caller queues independent work (DDRNet's bilateral fusion: the other branch's conv) -- and
+    ``bn_act(..., pending=...)`` waits right before its finalize kernel.  None when ``bn`` is not
+    a multi-rank SyncBN on the fused path (``bn_act`` then runs as usual)."""
+    if not (use_hip(x, "bn") and fused_ok(x, bn, ACT_NONE)):
+        return None
+    if not (bn.training or not bn.track_running_stats or bn.running_mean is None):
+        return None
+    pg = _sync_group(bn)
+    if pg is None:
+        return None
+    count = float(x.numel() // x.shape[1])
+    sums = ops().bn_slab_sums(part, count) if part is not None else ops().bn_stats_sums(x)
+    return sums, dist.all_reduce(sums, group=pg, async_op=True)
+
+
 def bn_act(x: torch.Tensor, bn, act=None, residual: Optional[torch.Tensor] = None,
            act_module: Optional[nn.Module] = None, part: Optional[torch.Tensor] = None,
-           sink=None) -> torch.Tensor:
+           sink=None, pending=None) -> torch.Tensor:
     """``act(bn(x) + residual)``; ``act`` is a fused-activation code or module/str.
 
     ``part``: BN statistics slab of ``x`` already computed by its producer (the MFMA conv
     epilogue, ``ops.conv``); used only on the fused batch-statistics path.
     ``sink``: ``(ConcatSink, branch index)`` -- the output is a branch of a channel concat
-    (ops/concat.py); the fused kernel also stores it into the concat buffer."""
+    (ops/concat.py); the fused kernel also stores it into the concat buffer.
+    ``pending``: :func:`bn_stats_begin`'s in-flight SyncBN statistics of ``x``."""
     code = act if isinstance(act, int) else act_code(act)
     if use_hip(x, "bn") and code is not None and fused_ok(x, bn, code) and (
             residual is None or (residual.shape == x.shape
@@ -222,10 +244,12 @@ def bn_act(x: torch.Tensor, bn, act=None, residual: Optional[torch.Tensor] = Non
         pg = _sync_group(bn) if use_batch else None
         out2 = sink[0].slot(sink[1], x) if sink is not None and sink[0] is not None else None
         y = _BNActFn.apply(x, bn.weight, bn.bias, residual, bn, code, use_batch, pg,
-                           part if use_batch else None, out2)
+                           part if use_batch else None, out2, pending if pg is not None else None)
         if out2 is not None:
             sink[0].record(sink[1], y, y.grad_fn)
         return y
+    if pending is not None:
+        pending[1].wait()  # (stock path: the statistics are recomputed by the module)
     y = bn(x)
     if residual is not None:
         y = y + residual
@@ -270,7 +294,7 @@ class FusedBatchNorm2d(nn.BatchNorm2d):
         if use_hip(x, "bn") and fused_ok(x, self, ACT_NONE):
             use_batch = self.training or not self.track_running_stats or self.running_mean is None
             pg = _sync_group(self) if use_batch else None
-            return _BNActFn.apply(x, self.weight, self.bias, None, self, ACT_NONE, use_batch, pg, None, None)
+            return _BNActFn.apply(x, self.weight, self.bias, None, self, ACT_NONE, use_batch, pg, None, None, None)
         return nn.BatchNorm2d.forward(self, x)
 
 
@@ -279,7 +303,7 @@ class FusedSyncBatchNorm(nn.SyncBatchNorm):
         if use_hip(x, "bn") and fused_ok(x, self, ACT_NONE):
             use_batch = self.training or not self.track_running_stats or self.running_mean is None
             pg = _sync_group(self) if use_batch else None
-            return _BNActFn.apply(x, self.weight, self.bias, None, self, ACT_NONE, use_batch, pg, None, None)
+            return _BNActFn.apply(x, self.weight, self.bias, None, self, ACT_NONE, use_batch, pg, None, None, None)
         return nn.SyncBatchNorm.forward(self, x)
 
 

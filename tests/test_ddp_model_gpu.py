@@ -28,6 +28,8 @@ pytestmark = pytest.mark.gpu
 MODELS = {
     "stdc2_aux": {"model": "stdc", "arch_type": None, "encoder_type": "stdc2", "use_aux": True},
     "bisenetv2_aux": {"model": "bisenetv2", "arch_type": None, "use_aux": True},
+    # the bilateral fusion's asynchronous SyncBN statistics (start/finish, ops.bn_stats_begin)
+    "ddrnet23slim_aux": {"model": "ddrnet", "arch_type": "DDRNet-23-slim", "use_aux": True},
 }
 GLOBAL_BS, SIZE, STEPS = 4, (128, 256), 2
 
