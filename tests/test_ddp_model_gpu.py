@@ -8,8 +8,8 @@ against ONE process stepping the concatenated batch.
   running statistics of the 2-rank run equal the 1-process run's (SyncBN makes every BN see the
   global batch; DDP averages the per-rank mean gradients, equal halves);
 * bf16 (+ our MFMA convs): replicas stay identical, the fused step ran, no gradient-stride
-  warning, and the update direction agrees with the 1-process run (bf16 rounding at random init
-  moves individual layers, not the whole update).
+  warning, and the 2-rank update is as close to the fp32 update as the 1-process bf16 one (bf16
+  rounding at random init moves individual layers a lot; DDP must not add to it).
 
 Reference wiring: utils/parallel.py:34-43 (SyncBN conversion + DDP), core/seg_trainer.py:38-119.
 RCCL itself needs one GPU per rank and runs on the driver's 8-GPU node; gloo exercises the same
@@ -151,7 +151,7 @@ def _flat(d, keys):
 def test_ddp_two_ranks_match_one_process(tmp_path, name):
     out = str(tmp_path)
     init = _init_params(name, out)
-    res = {}
+    res, upd = {}, {}
     for amp in (False, True):
         _spawn(1, _port(), out, name, amp)
         _spawn(2, _port(), out, name, amp)
@@ -187,6 +187,7 @@ def test_ddp_two_ranks_match_one_process(tmp_path, name):
         rm = [k for k in s1["buffers"] if k.endswith("running_mean") or k.endswith("running_var")]
         bn_rel = float((_flat(s1["buffers"], rm) - _flat(t1["buffers"], rm)).norm() / _flat(s1["buffers"], rm).norm())
         res[amp] = (cos, rel, ema_rel, bn_rel, cos2)
+        upd[amp] = (g1, g2)
         worst = sorted(keys, key=lambda k: -float((one["params"][k] - r0["params"][k]).norm()))[:5]
         print(f"{name} amp={amp}: largest parameter differences " + ", ".join(
             f"{k} {float((one['params'][k] - r0['params'][k]).norm()):.2e}/"
@@ -199,4 +200,12 @@ def test_ddp_two_ranks_match_one_process(tmp_path, name):
     # (the halves' valid-pixel counts differ) vs one mean over the whole batch
     assert cos > 0.999 and rel < 5e-2 and ema_rel < 5e-2 and bn_rel < 1e-4, res[False]
     cos, rel, ema_rel, bn_rel, cos2 = res[True]
-    assert cos > 0.95 and bn_rel < 2e-2, res[True]
+    # bf16: at random init on a 4-image batch the bf16 gradient itself is noisy (per-parameter
+    # cosine to fp64 ~0.93, tests/test_train_numerics_gpu.py), so two bf16 runs need not agree
+    # closely with each other.  What DDP must not do is make it worse: the 2-rank bf16 update is
+    # as close to the fp32 update as the 1-process bf16 update is (and BN statistics agree)
+    ref = upd[False][0]
+    c_one = float(torch.dot(upd[True][0], ref) / (upd[True][0].norm() * ref.norm()))
+    c_ddp = float(torch.dot(upd[True][1], ref) / (upd[True][1].norm() * ref.norm()))
+    print(f"{name} bf16 step-1 update vs fp32: 1-process cos {c_one:.4f}, 2-rank cos {c_ddp:.4f}")
+    assert c_ddp > c_one - 0.05 and bn_rel < 2e-2, (c_one, c_ddp, res[True])
