@@ -152,6 +152,21 @@ __global__ void __launch_bounds__(kNW * 64) whalo_wgrad_kernel(const WhArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[u][r] = 0.f;
 
+  // Per-lane LDS byte offsets, so that every fragment read of the fully unrolled K loop is
+  // base + compile-time immediate (round-4 PMC: 9.4 VALU per MFMA with per-read address math):
+  //  * dy^T: rows kk * 16 + hh * 8 + q (+ 4): adding 16 or 4 rows keeps the swizzle bit
+  //    ((row >> 1) & 1), so one base + (kk * 16 [+ 4]) * 128;
+  //  * halo: rows (py + i) * 34 + px0 + hh * 8 + q + j: adding px0 (0 / 16) or 4 keeps the bit,
+  //    adding 34 flips it -- one base for even and one for odd py, each + (py * 34 + px0) * 128
+  const uint32_t offA = swz_off(hh * 8 + q, acol);
+  uint32_t offB[2][3];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int r0 = tap_i[u] * kHW + hh * 8 + q + tap_j[u];
+    offB[0][u] = swz_off(r0, bcol[u]) + kDStage * 16;
+    offB[1][u] = swz_off(r0 + kHW, bcol[u]) - kHW * 128 + kDStage * 16;
+  }
+
   const int my_tiles = split < a.mtiles ? (a.mtiles - split + a.splits - 1) / a.splits : 0;
   if (my_tiles > 0) stage(split, 0);
   for (int t = 0; t < my_tiles; ++t) {
@@ -160,22 +175,20 @@ __global__ void __launch_bounds__(kNW * 64) whalo_wgrad_kernel(const WhArgs a) {
     __builtin_amdgcn_s_barrier();  // tile t landed for every wave; the other buffer is free
     if (t + 1 < my_tiles) stage(split + (t + 1) * a.splits, (t + 1) & 1);
     const uint4* dbase = lds + (t & 1) * kStage;
-    const uint4* hbase = dbase + kDStage;
-#pragma unroll 2
+#pragma unroll
     for (int kk = 0; kk < kTP / 16; ++kk) {
       const int py = kk >> 1, px0 = (kk & 1) * 16;
       // dy^T fragment: rows = pixels kk*16 + hh*8 + q (+4), column acol
-      const int ar = kk * 16 + hh * 8 + q;
-      const i16x4_t alo = tr4(dbase, swz_off(ar, acol));
-      const i16x4_t ahi = tr4(dbase, swz_off(ar + 4, acol));
+      const i16x4_t alo = tr4(dbase, offA + kk * 16 * 128);
+      const i16x4_t ahi = tr4(dbase, offA + (kk * 16 + 4) * 128);
       const bf16x8_t af = __builtin_shufflevector(__builtin_bit_cast(bf16x4_t, alo),
                                                   __builtin_bit_cast(bf16x4_t, ahi), 0, 1, 2, 3, 4, 5, 6, 7);
       bf16x8_t bf[3];
 #pragma unroll
       for (int u = 0; u < 3; ++u) {
-        const int hr = (py + tap_i[u]) * kHW + px0 + hh * 8 + q + tap_j[u];
-        const i16x4_t blo = tr4(hbase, swz_off(hr, bcol[u]));
-        const i16x4_t bhi = tr4(hbase, swz_off(hr + 4, bcol[u]));
+        const uint32_t o = offB[py & 1][u] + (py * kHW + px0) * 128;
+        const i16x4_t blo = tr4(dbase, o);
+        const i16x4_t bhi = tr4(dbase, o + 4 * 128);
         bf[u] = __builtin_shufflevector(__builtin_bit_cast(bf16x4_t, blo), __builtin_bit_cast(bf16x4_t, bhi), 0, 1,
                                         2, 3, 4, 5, 6, 7);
       }
