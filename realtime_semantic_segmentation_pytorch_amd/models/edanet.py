@@ -36,7 +36,8 @@ class DownsamplingBlock(nn.Module):
         self.bn_act = nn.Sequential(nn.BatchNorm2d(out_channels), Activation(act_type))
 
     def forward(self, x):
-        y = torch.cat([self.conv(x), self.pool(x)], dim=1)
+        c = self.conv(x)  # (autocast: the pooled fp32 input joins in the conv's dtype, see enet.InitialBlock)
+        y = torch.cat([c, self.pool(x).to(c.dtype)], dim=1)
         return ops.bn_act(y, self.bn_act[0], self.bn_act[1], act_module=self.bn_act[1])
 
 
@@ -68,4 +69,5 @@ class EDAModule(nn.Module):
             ConvBNAct(k, k, (1, 3), dilation=d, act_type=act_type))
 
     def forward(self, x):
-        return torch.cat([self.conv(x), x], dim=1)
+        y = self.conv(x)
+        return torch.cat([y, x.to(y.dtype)], dim=1)

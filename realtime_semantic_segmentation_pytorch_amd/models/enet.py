@@ -50,7 +50,13 @@ class InitialBlock(nn.Module):
         self.pool = nn.MaxPool2d(3, 2, 1)
 
     def forward(self, x):
-        return torch.cat([self.conv(x), self.pool(x)], dim=1)
+        y, p = self.conv(x), self.pool(x)
+        # under autocast the conv branch is bf16 while max-pooling the fp32 input image stays fp32:
+        # torch.cat would promote the block -- and every activation of the 10 networks built on
+        # it (ENet, ERFNet, LEDNet, AGLNet, ESNet, FDDWNet, ...) -- to fp32, with a bf16 cast before
+        # each conv (profiles/r4_zoo_models).  Max pooling commutes with the rounding, so the cast
+        # of the pooled branch is exact w.r.t. pooling the rounded input
+        return torch.cat([y, p.to(y.dtype)], dim=1)
 
 
 class BottleNeck1(nn.Module):

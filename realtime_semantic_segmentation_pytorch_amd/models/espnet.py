@@ -41,7 +41,8 @@ class ESPNet(nn.Module):
         img = x
         y = self.l1_block(x)
         if self.reinforce:  # input reinforcement: image resized (align_corners=False) to each level
-            y = torch.cat([y, ops.interpolate(img, y.shape[2:], False)], dim=1)
+            # (autocast: the fp32 image joins in the features' dtype instead of promoting them)
+            y = torch.cat([y, ops.interpolate(img, y.shape[2:], False).to(y.dtype)], dim=1)
             y_l1 = y
             y = self.l2_block(y, img)
             y_l2 = y
@@ -66,7 +67,7 @@ class L2Block(nn.Module):
         if self.use_skip:
             y = torch.cat([y, s], dim=1)
         if self.reinforce:
-            y = torch.cat([y, ops.interpolate(x_input, y.shape[2:], False)], dim=1)
+            y = torch.cat([y, ops.interpolate(x_input, y.shape[2:], False).to(y.dtype)], dim=1)
         return y
 
 

@@ -51,13 +51,16 @@ def _batches():
     return out
 
 
-def _run(rank, world, port, out, name, amp):
-    """One rank (world > 1: under DDP) -> its state after STEPS steps, saved to ``out``."""
-    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "RTSEG_DISABLE_HIP", "RTSEG_CONV_MFMA"):
+def _run(rank, world, port, out, name, amp, rccl=False):
+    """One rank (world > 1: under DDP) -> its state after STEPS steps, saved to ``out``.
+    ``rccl``: a one-rank DDP job on the real backend (nccl = RCCL), see test_rccl_one_rank_job."""
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "RTSEG_DISABLE_HIP", "RTSEG_CONV_MFMA", "RTSEG_DIST_BACKEND"):
         os.environ.pop(k, None)  # (RTSEG_HIP_OFF passes through: tools/probe_ddp_bisect.py)
-    if world > 1:
+    if world > 1 or rccl:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), LOCAL_RANK=str(rank),
-                          WORLD_SIZE=str(world), RTSEG_DIST_BACKEND="gloo")
+                          WORLD_SIZE=str(world))
+        if not rccl:
+            os.environ["RTSEG_DIST_BACKEND"] = "gloo"
     from realtime_semantic_segmentation_pytorch_amd import ops
     from realtime_semantic_segmentation_pytorch_amd.configs import BaseConfig
     from realtime_semantic_segmentation_pytorch_amd.core import SegTrainer
@@ -107,8 +110,17 @@ def _run(rank, world, port, out, name, amp):
              "ema": {n: v.detach().float().cpu() for n, v in tr.ema_model.ema.state_dict().items()},
              "fused": fused, "ema_fused": tr.ema_fused, "losses": losses, "stride_warn": stride_warn,
              "synced_bn": sum(isinstance(m, torch.nn.SyncBatchNorm) for m in model.modules())}
-    torch.save(state, os.path.join(out, f"{name}_{int(amp)}_w{world}_r{rank}.pt"))
-    if world > 1:
+    if rccl:
+        import torch.distributed as dist
+
+        from realtime_semantic_segmentation_pytorch_amd.parallel.ddp import barrier, syncbn_group
+
+        state["backend"] = dist.get_backend()
+        state["ddp"] = type(tr.model).__name__
+        state["syncbn_group"] = syncbn_group() is not None
+        barrier()  # dist.barrier(device_ids=[...]) on RCCL
+    torch.save(state, os.path.join(out, f"{name}_{int(amp)}_w{world}_r{rank}{'_rccl' if rccl else ''}.pt"))
+    if world > 1 or rccl:
         import torch.distributed as dist
 
         dist.barrier()
@@ -129,9 +141,9 @@ def _init_params(name, out):
     return {n: p.detach().float() for n, p in get_model(c).named_parameters()}
 
 
-def _spawn(world, port, out, name, amp):
+def _spawn(world, port, out, name, amp, rccl=False):
     ctx = mp.get_context("spawn")
-    ps = [ctx.Process(target=_run, args=(r, world, port, out, name, amp)) for r in range(world)]
+    ps = [ctx.Process(target=_run, args=(r, world, port, out, name, amp, rccl)) for r in range(world)]
     for p in ps:
         p.start()
     for p in ps:
@@ -209,3 +221,24 @@ def test_ddp_two_ranks_match_one_process(tmp_path, name):
     c_ddp = float(torch.dot(upd[True][1], ref) / (upd[True][1].norm() * ref.norm()))
     print(f"{name} bf16 step-1 update vs fp32: 1-process cos {c_one:.4f}, 2-rank cos {c_ddp:.4f}")
     assert c_ddp > c_one - 0.05 and bn_rel < 2e-2, (c_one, c_ddp, res[True])
+
+
+@pytest.mark.timeout(300)
+def test_rccl_one_rank_job(tmp_path):
+    """The RCCL code paths on the one-GPU pool: a one-rank DDP job on the ``nccl`` backend (RCCL
+    on ROCm) -- init_process_group(device_id=...), the SyncBN process group, DDP's gradient
+    buckets all-reduced by RCCL, barrier(device_ids=...) -- must step exactly like the plain
+    process (a one-rank average is the identity).  Multi-rank RCCL needs one GPU per rank: the
+    driver's 8-GPU node runs it (bench.py --gpus N)."""
+    out = str(tmp_path)
+    name = "bisenetv2_aux"
+    _spawn(1, _port(), out, name, False)
+    _spawn(1, _port(), out, name, False, rccl=True)
+    plain = torch.load(os.path.join(out, f"{name}_0_w1_r0.pt"), weights_only=True)
+    job = torch.load(os.path.join(out, f"{name}_0_w1_r0_rccl.pt"), weights_only=True)
+    assert job["backend"] == "nccl" and job["ddp"] == "DistributedDataParallel" and job["syncbn_group"], job
+    assert all(job["fused"]) and job["ema_fused"] and not job["stride_warn"]
+    keys = sorted(plain["params"])
+    a, b = _flat(plain["params"], keys), _flat(job["params"], keys)
+    assert float((a - b).norm() / a.norm()) < 1e-5
+    torch.testing.assert_close(torch.tensor(job["losses"]), torch.tensor(plain["losses"]), rtol=1e-5, atol=1e-5)
