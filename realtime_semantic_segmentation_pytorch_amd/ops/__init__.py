@@ -9,7 +9,7 @@ from .interp import (interpolate, final_upsample, defer_final_upsample, Deferred
 from .seg_loss import (seg_cross_entropy, seg_cross_entropy_reference, MODE_OHEM, MODE_MEAN,
                        MODE_SUM)
 from .kd import kd_kl_div, kd_kl_div_reference
-from .bn import (bn_act, bn_stats_begin, act_code as bn_act_code, fused_ok as bn_fused_ok, convert_batchnorm,
+from .bn import (bn_act, bn_stats_begin, bias_add, act_code as bn_act_code, fused_ok as bn_fused_ok, convert_batchnorm,
                  FusedBatchNorm2d, FusedSyncBatchNorm)
 from .detail import detail_loss, detail_loss_reference, detail_target_reference
 from .postprocess import colorize, colorize_reference
@@ -43,5 +43,5 @@ __all__ = [
     "PrunedConv2d", "convert_pruned_convs", "pruned_conv2d", "has_dead_taps",
     "FusedSGD", "FusedAdam", "FusedAdamW", "conv_ok", "conv_bn_stats", "conv_bn_act_eval", "conv_bn_act", "conv_forward", "RoutedConv2d", "convert_routed_convs",
     "TransposedConv2d", "conv_transpose2d", "convert_transposed_convs", "deconv_ok", "gate", "gate_reference", "activation", "convert_activations", "channel_shuffle", "convert_pixel_shuffle", "pixel_shuffle", "pixel_unshuffle", "AugmentSpec", "augment_batch", "augment_reference", "draw_params",
-    "ConcatSink", "bn_act", "bn_stats_begin", "bn_act_code", "bn_fused_ok", "convert_batchnorm", "FusedBatchNorm2d", "FusedSyncBatchNorm",
+    "ConcatSink", "bn_act", "bn_stats_begin", "bias_add", "bn_act_code", "bn_fused_ok", "convert_batchnorm", "FusedBatchNorm2d", "FusedSyncBatchNorm",
 ]

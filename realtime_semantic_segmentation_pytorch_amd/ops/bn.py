@@ -278,6 +278,28 @@ def channel_sum(t: torch.Tensor) -> torch.Tensor:
     return t.float().sum((0, 2, 3))
 
 
+class _BiasAddFn(torch.autograd.Function):
+    """y + bias (per channel); the bias gradient is :func:`channel_sum` of dy."""
+
+    @staticmethod
+    def forward(ctx, y, bias):
+        ctx.bdtype = bias.dtype
+        return y + bias.to(y.dtype).view(1, -1, 1, 1)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return dy, channel_sum(dy).to(ctx.bdtype)
+
+
+def bias_add(y: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
+    """A conv's bias, added after the bias-free conv: PyTorch's own bias-gradient reduction over a
+    channels-last activation ran as a slow non-vectorised reduce (2.3-2.4 ms per LEDNet / ContextNet
+    training step at batch 8, profiles/r4_zoo_models); here it is the BN statistics pass."""
+    if use_hip(y, "bn") and y.dim() == 4 and bias.dim() == 1 and bias.numel() == y.shape[1]:
+        return _BiasAddFn.apply(y, bias)
+    return y + bias.view(1, -1, 1, 1)
+
+
 # --------------------------------------------------------------------------
 # Module-level routing: every BatchNorm2d of a model through the fused kernels.
 # --------------------------------------------------------------------------

@@ -99,6 +99,11 @@ class PrunedConv2d(nn.Conv2d):
     (:func:`pruned_conv2d`); identical to ``nn.Conv2d`` whenever no tap is dead, and on CPU."""
 
     def _conv_forward(self, input, weight, bias):
+        if bias is not None and input.is_cuda and input.dim() == 4 and self.groups == 1:
+            # bias-free conv + bias_add: the bias gradient on the HIP channel-sum pass
+            from .bn import bias_add
+
+            return bias_add(self._conv_forward(input, weight, None), bias)
         if (not input.is_cuda or self.padding_mode != "zeros"
                 or not has_dead_taps(input.shape[2:], self.kernel_size, self.stride, self.padding, self.dilation)):
             return super()._conv_forward(input, weight, bias)
@@ -106,8 +111,9 @@ class PrunedConv2d(nn.Conv2d):
 
 
 def prunable(conv: nn.Module) -> bool:
+    """Spatial convs (dead taps) and biased dense ones (their bias goes through ``bias_add``)."""
     return (type(conv) is nn.Conv2d and conv.padding_mode == "zeros" and not isinstance(conv.padding, str)
-            and max(conv.kernel_size) > 1)
+            and (max(conv.kernel_size) > 1 or (conv.bias is not None and conv.groups == 1)))
 
 
 def convert_pruned_convs(model: nn.Module) -> nn.Module:

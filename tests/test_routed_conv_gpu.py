@@ -5,6 +5,8 @@ bf16-rounded operands, and bf16 inference through the cached bf16 weight.
 Reference sites: ERFNet's non-bottleneck-1D tail conv (reference models/erfnet.py), STDC's
 ``conv4`` / ``conv5`` (reference models/stdc.py:13-101) -- ``nn.Conv2d`` modules outside any
 ConvBNAct."""
+import copy
+
 import pytest
 import torch
 import torch.nn as nn
@@ -73,3 +75,32 @@ def test_routed_conv_inference_uses_cached_bf16_weight(geom):
     ref = F.conv2d(x.to(torch.bfloat16).float(), conv.weight.to(torch.bfloat16).float(), None, s, p, d)
     _close(y, ref, 2e-2)
     torch.testing.assert_close(y, y2)
+
+
+@pytest.mark.parametrize("k,dil", [(1, 1), (3, 1), ((3, 1), (4, 1))])
+def test_biased_conv_bias_add_matches_conv2d(k, dil):
+    """Biased dense convs (PrunedConv2d after ops.convert_pruned_convs): bias-free conv + bias_add,
+    whose bias gradient is the HIP channel-sum pass, == F.conv2d with the bias (fp32 and bf16)."""
+    from realtime_semantic_segmentation_pytorch_amd.ops.dilated import PrunedConv2d, convert_pruned_convs
+
+    torch.manual_seed(0)
+    kk = k if isinstance(k, tuple) else (k, k)
+    pad = tuple((a - 1) // 2 * d for a, d in zip(kk, dil if isinstance(dil, tuple) else (dil, dil)))
+    conv = torch.nn.Conv2d(32, 48, kk, padding=pad, dilation=dil, bias=True).cuda()
+    ref = copy.deepcopy(conv)
+    convert_pruned_convs(conv)
+    assert type(conv) is PrunedConv2d
+    for dtype in (torch.float32, torch.bfloat16):
+        x = torch.randn(2, 32, 24, 40, device="cuda").contiguous(memory_format=torch.channels_last)
+        outs = []
+        for m in (conv, ref):
+            m.zero_grad()
+            xx = x.clone().requires_grad_(True)
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16):
+                y = m(xx)
+            g = torch.randn(y.shape, device="cuda", generator=torch.Generator("cuda").manual_seed(1))
+            (y.float() * g).sum().backward()
+            outs.append((y.float(), xx.grad.float(), m.weight.grad.float(), m.bias.grad.float()))
+        tol = 1e-4 if dtype == torch.float32 else 2e-2
+        for a, b in zip(*outs):
+            assert float((a - b).norm() / (b.norm() + 1e-12)) < tol
