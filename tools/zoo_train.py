@@ -38,6 +38,10 @@ def config(key, a):
     # bf16 autocast like bench.py (BaseConfig's default is fp32, on which the MFMA conv kernels
     # do not run: round 2's sweep measured fp32 by mistake); --fp32 for that column
     c.amp_training, c.amp_dtype = not a.fp32, "bf16"
+    # --graph-step: forward + loss + backward replayed from one captured HIP graph after the
+    # warm-up (SegTrainer.graph_step) -- the launch-bound small models (FDDWNet: 66 ms of kernels
+    # in a 139 ms eager step, profiles/r4_zoo_models)
+    c.graph_step = bool(a.graph_step)
     c.init_dependent_config()
     return c
 
@@ -57,7 +61,8 @@ def run(key, a):
         loss, _ = tr.train_step(*data.next())
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
-    return {"model": key, "images_per_s": round(a.batch / dt, 2), "ms_per_step": round(dt * 1e3, 2),
+    return {"model": key, "graph_step": bool(a.graph_step), "images_per_s": round(a.batch / dt, 2),
+            "ms_per_step": round(dt * 1e3, 2),
             "loss": round(float(loss), 4), "aux": cfg.use_aux, "dtype": "fp32" if a.fp32 else "bf16",
             "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2)}
 
@@ -71,6 +76,7 @@ def main():
     ap.add_argument("--width", type=int, default=2048)
     ap.add_argument("--models", default="")
     ap.add_argument("--fp32", action="store_true", help="no autocast (fp32 training)")
+    ap.add_argument("--graph-step", action="store_true", help="replay the step from a captured HIP graph")
     ap.add_argument("--out", default="gpurun_out/zoo_train.jsonl")
     a = ap.parse_args()
     assert torch.cuda.is_available() and ops.load()
