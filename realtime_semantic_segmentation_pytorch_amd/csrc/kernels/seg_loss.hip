@@ -670,9 +670,20 @@ static void bwd_t(const SegLossArgs& a, const LossGeo& g, const float* grad_out,
   }
   const int64_t nacc = static_cast<int64_t>(g.n) * g.c * g.h * g.w;
   hipMemsetAsync(a.acc, 0, sizeof(float) * nacc, st);
-  if (g.c == 19) bwd_tile<T, 16, 128, 19>(a, g, grad_out, st);
-  else if (g.c <= 32) bwd_tile<T, 16, 128, 0>(a, g, grad_out, st);
-  else bwd_tile<T, 4, 32, 0>(a, g, grad_out, st);
+  // x2 / x4 upsampling (ContextNet's, and other half-resolution heads): a 16 x 128 tile stages
+  // 10 x 66 logit cells + a 19 x 16 x 67 row buffer (131 KB of LDS, one block per CU: the x2
+  // head's backward ran 10x slower per pixel than DDRNet's x8, profiles/r4_zoo_models); 8 x 64
+  // tiles fit four blocks per CU
+  const bool fine = (g.mh.scale > 0.2f || g.mw.scale > 0.2f) && g.mh.scale <= 1.f && g.mw.scale <= 1.f;
+  if (g.c == 19) {
+    if (fine) bwd_tile<T, 8, 64, 19>(a, g, grad_out, st);
+    else bwd_tile<T, 16, 128, 19>(a, g, grad_out, st);
+  } else if (g.c <= 32) {
+    if (fine) bwd_tile<T, 8, 64, 0>(a, g, grad_out, st);
+    else bwd_tile<T, 16, 128, 0>(a, g, grad_out, st);
+  } else {
+    bwd_tile<T, 4, 32, 0>(a, g, grad_out, st);
+  }
   cast_out_kernel<G><<<stream_grid(nacc, 256), 256, 0, st>>>(a.acc, static_cast<G*>(gl.data), nacc);
 }
 

@@ -76,12 +76,13 @@ class _BNActFn(torch.autograd.Function):
                 else:
                     mi, ss, sums = ops().bn_stats_finalize(x, weight, bias, rm, rv, nb,
                                                            float(bn.momentum), float(bn.eps))
-            elif pending is not None:  # SyncBN, all-reduce issued by bn_stats_begin: wait for it here
-                sums, work = pending
-                work.wait()
             else:  # SyncBN: one all-reduce of (sum, sumsq, count) in fp64 over RCCL
-                sums = ops().bn_slab_sums(part, count) if part is not None else ops().bn_stats_sums(x)
-                dist.all_reduce(sums, group=pg)
+                if pending is not None:  # issued by bn_stats_begin (async): wait for it here
+                    sums, work = pending
+                    work.wait()
+                else:
+                    sums = ops().bn_slab_sums(part, count) if part is not None else ops().bn_stats_sums(x)
+                    dist.all_reduce(sums, group=pg)
                 mi, ss = ops().bn_finalize(sums, weight, bias, rm, rv, nb, float(bn.momentum),
                                            float(bn.eps))
             if rm is not None:

@@ -78,7 +78,8 @@ def _labels(n, h, w, c, ignore_frac=0.1, seed=0):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("scale_logits", [0.1, 3.0])  # small logits -> top-k branch; large -> threshold
-@pytest.mark.parametrize("hw,lhw", [((16, 32), (128, 256)), ((32, 64), (32, 64)), ((9, 13), (70, 100))])
+@pytest.mark.parametrize("hw,lhw", [((16, 32), (128, 256)), ((32, 64), (32, 64)), ((9, 13), (70, 100)),
+                                    ((64, 128), (128, 256)), ((32, 64), (128, 256)), ((37, 51), (70, 100))])
 def test_ohem_loss_fused(dtype, scale_logits, hw, lhw):
     _lib_loaded()
     torch.manual_seed(2)
