@@ -108,7 +108,10 @@ void launch_confmat(const Tensor4& x, const int64_t* target, int ignore, unsigne
 // ---- optim.hip --------------------------------------------------------------
 // Tensor table row: {param f32*, grad*, state1 f32*, state2 f32*, ema f32*, numel, grad_is_bf16,
 // first_step}; followed by a [nblocks, 2] (tensor, chunk-start) map.
-constexpr int kOptMetaFields = 8;
+// per tensor: param, grad, state1, state2, ema, numel, grad_bf16, first_step, then the optional bf16
+// conv-weight shadows written with the updated parameter (ops/conv.py weight_shadow): krsc
+// [Cout][KH][KW][Cin], crsk [Cin][KH][KW][Cout], Cout, Cin, KH * 256 + KW, parameter channels-last
+constexpr int kOptMetaFields = 14;
 constexpr int64_t kOptChunk = 16384;
 enum OptMode : int { kOptSGD = 0, kOptAdam = 1, kOptAdamW = 2 };
 struct OptHyper {

@@ -48,6 +48,14 @@ __global__ void __launch_bounds__(kOptBlock) fused_opt_kernel(const int64_t* met
   const int64_t n = tm[5];
   const bool g_bf16 = tm[6] != 0;
   const bool first = tm[7] != 0;
+  // bf16 conv-weight shadows: the layouts the MFMA conv kernels read (forward B operand, data-
+  // gradient B operand), rewritten here with the parameter instead of a cast + a transpose
+  // kernel per conv per step
+  uint16_t* sh_krsc = reinterpret_cast<uint16_t*>(tm[8]);
+  uint16_t* sh_crsk = reinterpret_cast<uint16_t*>(tm[9]);
+  const int cout = static_cast<int>(tm[10]), cin = static_cast<int>(tm[11]);
+  const int kh = static_cast<int>(tm[12] >> 8), kw = static_cast<int>(tm[12] & 255);
+  const bool wcl = tm[13] != 0;
   int64_t end = start + kOptChunk;
   if (end > n) end = n;
 
@@ -89,6 +97,28 @@ __global__ void __launch_bounds__(kOptBlock) fused_opt_kernel(const int64_t* met
         pp -= hp.step_size * m / denom;
       }
       p[i] = pp;
+      if (sh_krsc != nullptr) {
+        const int ii = static_cast<int>(i);  // weights have < 2^31 elements
+        int co, ci, r, q;
+        if (wcl) {  // memory order [Cout][KH][KW][Cin]
+          ci = ii % cin;
+          int t = ii / cin;
+          q = t % kw;
+          t /= kw;
+          r = t % kh;
+          co = t / kh;
+        } else {  // [Cout][Cin][KH][KW]
+          q = ii % kw;
+          int t = ii / kw;
+          r = t % kh;
+          t /= kh;
+          ci = t % cin;
+          co = t / cin;
+        }
+        const uint16_t b = f32_to_bf16(pp);
+        sh_krsc[((co * kh + r) * kw + q) * cin + ci] = b;
+        if (sh_crsk != nullptr) sh_crsk[((ci * kh + r) * kw + q) * cout + co] = b;
+      }
       if (ema != nullptr) {
         ema[i] = lerp_like_torch(ema[i], pp, hp.ema_w);
       }

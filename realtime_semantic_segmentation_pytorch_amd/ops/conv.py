@@ -35,6 +35,7 @@ likewise for ``conv_wres``.
 from __future__ import annotations
 
 import os
+import weakref
 
 import torch
 import torch.nn as nn
@@ -213,9 +214,86 @@ def _cached(conv, attr, make):
     return t
 
 
+class _Shadow:
+    """bf16 copies of a trained conv weight in the two layouts the kernels read -- krsc [Cout, KH,
+    KW, Cin] (forward) and crsk [Cin, KH, KW, Cout] (data gradient) -- rewritten by the fused
+    optimizer step itself (ops/optim.py passes them to optim.hip), so a training step has no
+    per-conv cast and transpose kernels (~100 launches per DDRNet-23 step).  Valid while the
+    weight is what the last fused step (or the last refresh) left: same storage, same version
+    counter (any other in-place write bumps it) and the same optimizer generation."""
+
+    __slots__ = ("krsc", "crsk", "gen", "crsk_gen", "version", "ptr")
+
+    def __init__(self, w):
+        cout, cin, kh, kw = w.shape
+        self.krsc = torch.empty((cout, kh, kw, cin), dtype=torch.bfloat16, device=w.device)
+        self.crsk = torch.empty((cin, kh, kw, cout), dtype=torch.bfloat16, device=w.device)
+        self.gen = self.crsk_gen = -1
+        self.version = self.ptr = None
+
+
+_SHADOWS = weakref.WeakKeyDictionary()  # conv weight Parameter -> _Shadow
+_OPT_GEN = [0]  # fused optimizer steps that rewrote the shadows
+_SHADOW_ON = os.environ.get("RTSEG_WEIGHT_SHADOW", "1") != "0"  # A/B: per-step cast + transpose
+
+
+def _shadow_current(w, sh, crsk=False) -> bool:
+    return ((sh.crsk_gen if crsk else sh.gen) == _OPT_GEN[0] and sh.version == w._version
+            and sh.ptr == w.data_ptr())
+
+
+def weight_shadows(params):
+    """{param: (krsc, crsk)} of the shadowed conv weights among ``params`` (for the fused step)."""
+    return {p: (sh.krsc, sh.crsk) for p in params if (sh := _SHADOWS.get(p)) is not None}
+
+
+def shadows_written(params) -> None:
+    """The fused step just rewrote these parameters' shadows (ops/optim.py, after its launch)."""
+    _OPT_GEN[0] += 1
+    for p in params:
+        sh = _SHADOWS.get(p)
+        if sh is not None:
+            sh.gen = sh.crsk_gen = _OPT_GEN[0]
+            sh.version, sh.ptr = p._version, p.data_ptr()
+
+
+def _train_shadow(conv, crsk=False) -> torch.Tensor:
+    w = conv.weight
+    sh = _SHADOWS.get(w)
+    if sh is None:
+        sh = _SHADOWS[w] = _Shadow(w)
+    if not _shadow_current(w, sh, crsk):
+        if (sh.version, sh.ptr) != (w._version, w.data_ptr()) or sh.gen != _OPT_GEN[0]:
+            sh.gen = sh.crsk_gen = -1  # a write the optimizer did not make: both layouts are stale
+        with torch.no_grad():
+            if crsk:
+                sh.crsk.copy_(w.detach().permute(1, 2, 3, 0))
+            else:
+                sh.krsc.copy_(w.detach().permute(0, 2, 3, 1))
+        if crsk:
+            sh.crsk_gen = _OPT_GEN[0]
+        else:
+            sh.gen = _OPT_GEN[0]
+        sh.version, sh.ptr = w._version, w.data_ptr()
+    return sh.crsk if crsk else sh.krsc
+
+
 def weight_krsc(conv: nn.Conv2d) -> torch.Tensor:
-    """[Cout, KH, KW, Cin] bf16 (forward B operand)."""
+    """[Cout, KH, KW, Cin] bf16 (forward B operand).  Training: the fused optimizer's shadow."""
+    w = conv.weight
+    if (_SHADOW_ON and conv.training and torch.is_grad_enabled() and w.is_cuda and w.dtype == torch.float32
+            and w.requires_grad):
+        return _train_shadow(conv)
     return _cached(conv, "_rtseg_wk", lambda w: w.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous())
+
+
+def weight_crsk(conv: nn.Conv2d, wk: torch.Tensor) -> torch.Tensor:
+    """[Cin, KH, KW, Cout] bf16 (data-gradient B operand) for the ``wk`` this conv's forward used."""
+    w = conv.weight
+    sh = _SHADOWS.get(w)
+    if sh is not None and wk is sh.krsc:
+        return _train_shadow(conv, crsk=True)
+    return wk.permute(3, 1, 2, 0).contiguous()
 
 
 def _time(fn, reps=8):
@@ -388,17 +466,17 @@ def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None):
 
     def ours():
         if not wt:  # [Cin, KH, KW, Cout] bf16, the dgrad B operand
-            wt.append(wk.permute(3, 1, 2, 0).contiguous())
+            wt.append(weight_crsk(conv, wk))
         return ops().conv_igemm_dgrad(dy, wt[0], list(x.shape), stride, padding, dilation, None, addend)
 
     def halo():
         if not wt:
-            wt.append(wk.permute(3, 1, 2, 0).contiguous())
+            wt.append(weight_crsk(conv, wk))
         return ops().conv_halo_dgrad(dy, wt[0], list(x.shape), stride, padding, dilation, addend)
 
     def wres():
         if not wt:
-            wt.append(wk.permute(3, 1, 2, 0).contiguous())
+            wt.append(weight_crsk(conv, wk))
         return ops().conv_wres_dgrad(dy, wt[0], list(x.shape), stride, padding, dilation, addend)
 
     def miopen():
@@ -407,7 +485,7 @@ def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None):
 
     def hreg(rows_per_wave=1):
         if not wt:
-            wt.append(wk.permute(3, 1, 2, 0).contiguous())
+            wt.append(weight_crsk(conv, wk))
         return ops().conv_hreg_dgrad(dy, wt[0], list(x.shape), stride, padding, dilation, addend, rows_per_wave)
 
     cands = [("igemm", ours)] if cout % 64 == 0 and cin % 8 == 0 else []

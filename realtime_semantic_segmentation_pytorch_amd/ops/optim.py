@@ -19,20 +19,34 @@ import torch
 from torch.optim import SGD, Adam, AdamW
 
 from ._ext import bump_write_generation, ops, use_hip
+from .conv import shadows_written, weight_shadows
 
 MODE_SGD, MODE_ADAM, MODE_ADAMW = 0, 1, 2
-META_FIELDS = 8
+META_FIELDS = 14
 CHUNK = 16384
 
 
+def _shadow_fields(p, sh):
+    """Meta fields of a conv weight's bf16 shadows (ops/conv.py weight_shadow) or zeros."""
+    if sh is None:
+        return [0, 0, 0, 0, 0, 0]
+    krsc, crsk = sh
+    cout, cin, kh, kw = p.shape
+    cl = p.dim() == 4 and not p.is_contiguous() and p.is_contiguous(memory_format=torch.channels_last)
+    return [krsc.data_ptr(), crsk.data_ptr() if crsk is not None else 0, cout, cin, kh * 256 + kw, 1 if cl else 0]
+
+
 def build_table(rows, device):
-    """rows: [(param, grad, state1|None, state2|None, ema|None, first_step)] -> (meta, ntensor, nblocks)."""
+    """rows: [(param, grad, state1|None, state2|None, ema|None, first_step[, (krsc, crsk)|None])]
+    -> (meta, ntensor, nblocks)."""
     meta, bmap = [], []
-    for ti, (p, g, s1, s2, e, first) in enumerate(rows):
+    for ti, row in enumerate(rows):
+        p, g, s1, s2, e, first = row[:6]
         n = p.numel()
         meta += [p.data_ptr(), g.data_ptr(), s1.data_ptr() if s1 is not None else 0,
                  s2.data_ptr() if s2 is not None else 0, e.data_ptr() if e is not None else 0, n,
                  1 if g.dtype == torch.bfloat16 else 0, 1 if first else 0]
+        meta += _shadow_fields(p, row[6] if len(row) > 6 else None)
         for start in range(0, n, CHUNK):
             bmap += [ti, start]
     t = torch.tensor(meta + bmap, dtype=torch.int64)
@@ -108,7 +122,8 @@ class _FusedMixin:
         slot and a replaced state buffer can never leave a stale pointer behind."""
         key = tuple((r[0].data_ptr(), r[1].data_ptr(), r[2].data_ptr() if r[2] is not None else 0,
                      r[3].data_ptr() if r[3] is not None else 0, r[4].data_ptr() if r[4] is not None else 0,
-                     r[5], r[0].numel(), r[1].dtype) for r in rows)
+                     r[5], r[0].numel(), r[1].dtype,
+                     tuple(t.data_ptr() for t in r[6]) if len(r) > 6 and r[6] is not None else ()) for r in rows)
         cache = self._tables
         if cache.get(slot, (None,))[0] != key:
             cache[slot] = (key, build_table(rows, rows[0][0].device))
@@ -134,6 +149,7 @@ class FusedSGD(_FusedMixin, SGD):
             with torch.enable_grad():
                 loss = closure()
         ema_w = self.ema_weight
+        shadows = weight_shadows([p for g in self.param_groups for p in g["params"] if p.grad is not None])
         for gi, group in enumerate(self.param_groups):
             mom = float(group["momentum"])
             rows = []
@@ -150,13 +166,15 @@ class FusedSGD(_FusedMixin, SGD):
                         first = True
                     elif not same_layout(buf, p):  # e.g. loaded from a checkpoint in another layout
                         buf = st["momentum_buffer"] = torch.empty_like(p).copy_(buf)
-                rows.append((p, p.grad, buf, None, self._ema_of.get(p) if ema_w is not None else None, first))
+                rows.append((p, p.grad, buf, None, self._ema_of.get(p) if ema_w is not None else None, first,
+                             shadows.get(p)))
             if not rows:
                 continue
             lr = float(group["lr"])
             hp = (lr, mom, float(group["dampening"]), float(group["weight_decay"]), bool(group["nesterov"]),
                   0.0, 0.0, 0.0, 0.0, 0.0, 1.0, float(ema_w) if ema_w is not None else 0.0)
             self._launch(gi, rows, hp)
+        shadows_written(shadows)
         self.last_step_fused = ema_w is not None and bool(self._ema_of)
         self.fused_steps += 1
         return loss
@@ -173,6 +191,7 @@ class _FusedAdamBase(_FusedMixin):
             with torch.enable_grad():
                 loss = closure()
         ema_w = self.ema_weight
+        shadows = weight_shadows([p for g in self.param_groups for p in g["params"] if p.grad is not None])
         for gi, group in enumerate(self.param_groups):
             beta1, beta2 = (float(b) for b in group["betas"])
             by_step = {}
@@ -190,7 +209,7 @@ class _FusedAdamBase(_FusedMixin):
                 st["step"] += 1
                 by_step.setdefault(float(st["step"]), []).append(
                     (p, p.grad, st["exp_avg"], st["exp_avg_sq"],
-                     self._ema_of.get(p) if ema_w is not None else None, False))
+                     self._ema_of.get(p) if ema_w is not None else None, False, shadows.get(p)))
             lr = float(group["lr"])
             # normally one bucket; several only after loading a hand-assembled state
             for bi, (steps, rows) in enumerate(sorted(by_step.items())):
@@ -199,6 +218,7 @@ class _FusedAdamBase(_FusedMixin):
                 hp = (lr, 0.0, 0.0, float(group["weight_decay"]), False, beta1, beta2, float(group["eps"]),
                       lr / bc1, 1.0 / math.sqrt(bc2), 1.0, float(ema_w) if ema_w is not None else 0.0)
                 self._launch((gi, bi), rows, hp)
+        shadows_written(shadows)
         self.last_step_fused = ema_w is not None and bool(self._ema_of)
         self.fused_steps += 1
         return loss

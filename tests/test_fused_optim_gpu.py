@@ -157,3 +157,48 @@ def test_ema_validation_sees_new_weights_after_training(tmp_path):
     fresh = infer(copy.deepcopy(tr.ema_model.ema))
     assert not torch.equal(first, second), "EMA model output did not change after training"
     torch.testing.assert_close(second, fresh, rtol=0, atol=0)
+
+
+def _shadow_run(shadow_on, monkeypatch, steps=3):
+    from realtime_semantic_segmentation_pytorch_amd.models.modules import ConvBNAct
+    from realtime_semantic_segmentation_pytorch_amd.ops import conv as conv_mod
+    from realtime_semantic_segmentation_pytorch_amd.ops.optim import FusedSGD
+
+    monkeypatch.setattr(conv_mod, "_SHADOW_ON", shadow_on)
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(ConvBNAct(64, 64, 3), ConvBNAct(64, 128, 3), ConvBNAct(128, 128, 1))
+    m = m.cuda().to(memory_format=torch.channels_last).train()
+    ops.convert_batchnorm(m)
+    opt = FusedSGD(m.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    for _ in range(steps):
+        x = torch.randn(4, 64, 32, 48, device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = m(x)
+        (y.float() ** 2).mean().backward()
+        opt.step()
+        assert opt.fused_steps > 0
+    torch.cuda.synchronize()
+    shadows = {n: conv_mod._SHADOWS.get(p) for n, p in m.named_parameters()}
+    return {n: p.detach().clone() for n, p in m.named_parameters()}, shadows, m
+
+
+def test_weight_shadows_written_by_the_fused_step(monkeypatch):
+    """The fused step rewrites the bf16 krsc / crsk copies of every routed conv weight
+    (ops/conv.py _Shadow): training with them is bitwise the training with the per-step cast +
+    transpose, and after the step they equal the bf16 casts of the updated weights."""
+    ref, _, _ = _shadow_run(False, monkeypatch)
+    got, shadows, m = _shadow_run(True, monkeypatch)
+    for n in ref:
+        torch.testing.assert_close(got[n], ref[n], rtol=0, atol=0, msg=n)
+    seen = 0
+    for n, p in m.named_parameters():
+        sh = shadows[n]
+        if sh is None:
+            continue
+        seen += 1
+        w16 = p.detach().to(torch.bfloat16)
+        assert torch.equal(sh.krsc, w16.permute(0, 2, 3, 1).contiguous()), n
+        assert torch.equal(sh.crsk, w16.permute(1, 2, 3, 0).contiguous()), n
+    assert seen >= 2
