@@ -47,7 +47,11 @@ class InferenceEngine:
         if channels_last:
             self.model = self.model.to(memory_format=torch.channels_last)
         fmt = torch.channels_last if channels_last else torch.contiguous_format
-        self.static_in = torch.zeros(*input_shape, device=self.device).contiguous(memory_format=fmt)
+        # a reduced-precision engine takes its input in that dtype: the copy into the static buffer
+        # casts, and image-side ops (input pyramids, pooled image shortcuts, resized inputs) run in
+        # bf16 instead of leaving fp32 islands that every consumer conv casts again
+        self.static_in = torch.zeros(*input_shape, device=self.device,
+                                     dtype=dtype if self.autocast else torch.float32).contiguous(memory_format=fmt)
         self.graph = None
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
