@@ -281,8 +281,9 @@ def _train_shadow(conv, crsk=False) -> torch.Tensor:
 def weight_krsc(conv: nn.Conv2d) -> torch.Tensor:
     """[Cout, KH, KW, Cin] bf16 (forward B operand).  Training: the fused optimizer's shadow."""
     w = conv.weight
-    if (_SHADOW_ON and conv.training and torch.is_grad_enabled() and w.is_cuda and w.dtype == torch.float32
-            and w.requires_grad):
+    # (called inside _ConvFn.forward, where autograd is off: a trainable weight of a module in
+    # training mode is the test)
+    if _SHADOW_ON and conv.training and w.requires_grad and w.is_cuda and w.dtype == torch.float32:
         return _train_shadow(conv)
     return _cached(conv, "_rtseg_wk", lambda w: w.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous())
 
