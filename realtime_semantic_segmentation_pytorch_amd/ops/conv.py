@@ -35,7 +35,6 @@ likewise for ``conv_wres``.
 from __future__ import annotations
 
 import os
-import weakref
 
 import torch
 import torch.nn as nn
@@ -232,7 +231,6 @@ class _Shadow:
         self.version = self.ptr = None
 
 
-_SHADOWS = weakref.WeakKeyDictionary()  # conv weight Parameter -> _Shadow
 _OPT_GEN = [0]  # fused optimizer steps that rewrote the shadows
 _SHADOW_ON = os.environ.get("RTSEG_WEIGHT_SHADOW", "1") != "0"  # A/B: per-step cast + transpose
 
@@ -242,16 +240,22 @@ def _shadow_current(w, sh, crsk=False) -> bool:
             and sh.ptr == w.data_ptr())
 
 
+def shadow_of(w):
+    """The :class:`_Shadow` of a conv weight (an attribute of the Parameter: a tensor cannot key a
+    weak dict -- its ``==`` is elementwise), or None."""
+    return getattr(w, "_rtseg_shadow", None)
+
+
 def weight_shadows(params):
     """{param: (krsc, crsk)} of the shadowed conv weights among ``params`` (for the fused step)."""
-    return {p: (sh.krsc, sh.crsk) for p in params if (sh := _SHADOWS.get(p)) is not None}
+    return {p: (sh.krsc, sh.crsk) for p in params if (sh := shadow_of(p)) is not None}
 
 
 def shadows_written(params) -> None:
     """The fused step just rewrote these parameters' shadows (ops/optim.py, after its launch)."""
     _OPT_GEN[0] += 1
     for p in params:
-        sh = _SHADOWS.get(p)
+        sh = shadow_of(p)
         if sh is not None:
             sh.gen = sh.crsk_gen = _OPT_GEN[0]
             sh.version, sh.ptr = p._version, p.data_ptr()
@@ -259,9 +263,9 @@ def shadows_written(params) -> None:
 
 def _train_shadow(conv, crsk=False) -> torch.Tensor:
     w = conv.weight
-    sh = _SHADOWS.get(w)
-    if sh is None:
-        sh = _SHADOWS[w] = _Shadow(w)
+    sh = shadow_of(w)
+    if sh is None or sh.krsc.shape != (w.shape[0], w.shape[2], w.shape[3], w.shape[1]) or sh.krsc.device != w.device:
+        sh = w._rtseg_shadow = _Shadow(w)
     if not _shadow_current(w, sh, crsk):
         if (sh.version, sh.ptr) != (w._version, w.data_ptr()) or sh.gen != _OPT_GEN[0]:
             sh.gen = sh.crsk_gen = -1  # a write the optimizer did not make: both layouts are stale
@@ -290,8 +294,7 @@ def weight_krsc(conv: nn.Conv2d) -> torch.Tensor:
 
 def weight_crsk(conv: nn.Conv2d, wk: torch.Tensor) -> torch.Tensor:
     """[Cin, KH, KW, Cout] bf16 (data-gradient B operand) for the ``wk`` this conv's forward used."""
-    w = conv.weight
-    sh = _SHADOWS.get(w)
+    sh = shadow_of(conv.weight)
     if sh is not None and wk is sh.krsc:
         return _train_shadow(conv, crsk=True)
     return wk.permute(3, 1, 2, 0).contiguous()

@@ -180,7 +180,7 @@ def _shadow_run(shadow_on, monkeypatch, steps=3):
         opt.step()
         assert opt.fused_steps > 0
     torch.cuda.synchronize()
-    shadows = {n: conv_mod._SHADOWS.get(p) for n, p in m.named_parameters()}
+    shadows = {n: conv_mod.shadow_of(p) for n, p in m.named_parameters()}
     return {n: p.detach().clone() for n, p in m.named_parameters()}, shadows, m
 
 
