@@ -124,32 +124,45 @@ def halo_ok(conv, reduce_c: int, out_c: int) -> bool:
     return reduce_c % 64 == 0 and out_c % 64 == 0 and max(reduce_c, out_c) <= 8192
 
 
-def wres_ok(conv, reduce_c: int, out_c: int) -> bool:
+def _npix(x: torch.Tensor) -> int:
+    return x.shape[0] * x.shape[2] * x.shape[3]
+
+
+def _fits32(npix: int, c: int) -> bool:
+    """The halo-staging kernels address the summed-over tensor with 32-bit buffer offsets."""
+    return npix * c * 2 < (1 << 31)
+
+
+def wres_ok(conv, reduce_c: int, out_c: int, npix: int) -> bool:
     """Shapes ``conv_wres`` takes (``csrc/kernels/conv_wres.hip``): 3 x 3, stride 1, pad 1,
-    dilation 1, exactly 64 channels summed over, a multiple of 64 produced."""
+    dilation 1, exactly 64 channels summed over, a multiple of 64 produced, < 2 GB summed over
+    (``npix`` = N * H * W)."""
     if os.environ.get("RTSEG_CONV_WRES", "auto") == "0":
         return False
     return (tuple(conv.kernel_size) == (3, 3) and tuple(conv.stride) == (1, 1) and tuple(conv.padding) == (1, 1)
-            and tuple(conv.dilation) == (1, 1) and reduce_c == 64 and out_c % 64 == 0)
+            and tuple(conv.dilation) == (1, 1) and reduce_c == 64 and out_c % 64 == 0
+            and _fits32(npix, reduce_c))
 
 
-def hreg_ok(conv, reduce_c: int, out_c: int) -> bool:
+def hreg_ok(conv, reduce_c: int, out_c: int, npix: int) -> bool:
     """Shapes ``conv_hreg`` takes (``csrc/kernels/conv_hreg.hip``): 3 x 3, stride 1, pad 1, dilation
     1, a 64-channel multiple summed over, a 128-channel multiple produced.  Two candidates: "hreg"
     (8 waves x 1 tile row) and "hreg2" (4 waves x 2 rows: half the weight stream)."""
     if os.environ.get("RTSEG_CONV_HREG", "auto") == "0":
         return False
     return (tuple(conv.kernel_size) == (3, 3) and tuple(conv.stride) == (1, 1) and tuple(conv.padding) == (1, 1)
-            and tuple(conv.dilation) == (1, 1) and reduce_c % 64 == 0 and out_c % 128 == 0)
+            and tuple(conv.dilation) == (1, 1) and reduce_c % 64 == 0 and out_c % 128 == 0
+            and _fits32(npix, reduce_c))
 
 
-def whalo_ok(conv, cin: int, cout: int) -> bool:
+def whalo_ok(conv, cin: int, cout: int, npix: int) -> bool:
     """Weight gradients ``conv_whalo_wgrad`` takes (``csrc/kernels/conv_whalo.hip``): 3 x 3,
     stride 1, pad 1, dilation 1, 64-channel multiples on both sides."""
     if os.environ.get("RTSEG_CONV_WHALO", "auto") == "0":
         return False
     return (tuple(conv.kernel_size) == (3, 3) and tuple(conv.stride) == (1, 1) and tuple(conv.padding) == (1, 1)
-            and tuple(conv.dilation) == (1, 1) and cin % 64 == 0 and cout % 64 == 0)
+            and tuple(conv.dilation) == (1, 1) and cin % 64 == 0 and cout % 64 == 0
+            and _fits32(npix, max(cin, cout)))
 
 
 def _order(cands):
@@ -440,9 +453,9 @@ def _fwd_impl(x, wk, conv, key, stats) -> str:
             cands.append(("igemm_nostats", nostats))
         if halo_ok(conv, cin, cout):
             cands.append(("halo", lambda: ops().conv_halo(x, wk, stride, padding, dilation, stats, None, None, 0)))
-        if wres_ok(conv, cin, cout):
+        if wres_ok(conv, cin, cout, _npix(x)):
             cands.append(("wres", lambda: ops().conv_wres(x, wk, stride, padding, dilation, stats)))
-        if hreg_ok(conv, cin, cout):
+        if hreg_ok(conv, cin, cout, _npix(x)):
             cands.append(("hreg", lambda: ops().conv_hreg(x, wk, stride, padding, dilation, stats, 1)))
             cands.append(("hreg2", lambda: ops().conv_hreg(x, wk, stride, padding, dilation, stats, 2)))
     elif cin % 32 == 0 and cout % 8 == 0:
@@ -495,9 +508,9 @@ def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None):
     cands = [("igemm", ours)] if cout % 64 == 0 and cin % 8 == 0 else []
     if halo_ok(conv, cout, cin):
         cands.append(("halo", halo))
-    if wres_ok(conv, cout, cin):
+    if wres_ok(conv, cout, cin, _npix(x)):
         cands.append(("wres", wres))
-    if hreg_ok(conv, cout, cin):
+    if hreg_ok(conv, cout, cin, _npix(x)):
         cands.append(("hreg", hreg))
         cands.append(("hreg2", lambda: hreg(2)))
     cands.append(("miopen", miopen))
@@ -567,7 +580,7 @@ def _wgrad(x, dy, wk, conv, key, stride, padding, dilation):
                                                    False, [0, 0], 1, [False, True, False])[1]
 
     cands = [("igemm", ours)] if cin % 64 == 0 and cout % 64 == 0 else []
-    if whalo_ok(conv, cin, cout):
+    if whalo_ok(conv, cin, cout, _npix(x)):
         cands.append(("whalo", whalo))
     cands.append(("miopen", miopen))
     cands = _order(cands)

@@ -36,6 +36,13 @@ def _cl_aligned(t: torch.Tensor) -> torch.Tensor:
     return t
 
 
+def _channels_inner(x: torch.Tensor) -> bool:
+    """Channels-last, or a channel slice of a channels-last tensor (FPENet's ``h[:, a:b]`` branch
+    inputs, reference models/fpenet.py:78-84): the kernels take the slice as one dense copy
+    rather than MIOpen's grouped-conv path (~120 ms per weight gradient at FPENet's shapes)."""
+    return x.is_contiguous(memory_format=torch.channels_last) or (x.stride(1) == 1 and x.stride(2) == x.stride(3) * x.shape[3])
+
+
 class _DWConvFn(torch.autograd.Function):
     """y = depth-wise conv(x); with ``stats`` also the BN-statistics slab of y (fp32 [rows, 2C],
     produced in the forward kernel's epilogue; ``ops.bn_act(..., part=slab)`` consumes it)."""
@@ -90,8 +97,7 @@ def depthwise_ok(conv: nn.Conv2d) -> bool:
 def dw_conv2d(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
     """``conv(x)`` for a depth-wise ``conv``; HIP kernels for channels-last GPU inputs
     (``RTSEG_DWCONV=0`` keeps MIOpen, for A/B comparisons)."""
-    if (x.dim() == 4 and use_hip(x, "dw") and x.is_contiguous(memory_format=torch.channels_last)
-            and os.environ.get("RTSEG_DWCONV", "1") != "0"):
+    if x.dim() == 4 and use_hip(x, "dw") and _channels_inner(x) and os.environ.get("RTSEG_DWCONV", "1") != "0":
         dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
         if dt in _DTYPES and conv.weight.dtype in _DTYPES:
             kh, kw = conv.kernel_size
@@ -105,7 +111,7 @@ def dw_conv_bn_stats(x: torch.Tensor, conv: nn.Conv2d):
     """Training forward of a depth-wise conv followed by a batch-statistics BN: (y, slab | None),
     the slab holding the BN statistics of y from the conv kernel's epilogue; None -> the caller's
     stock path (``conv(x)`` + ``ops.bn_act``)."""
-    if not (x.dim() == 4 and use_hip(x, "dw") and x.is_contiguous(memory_format=torch.channels_last)
+    if not (x.dim() == 4 and use_hip(x, "dw") and _channels_inner(x)
             and os.environ.get("RTSEG_DWCONV", "1") != "0" and conv.bias is None and depthwise_ok(conv)):
         return None
     dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
