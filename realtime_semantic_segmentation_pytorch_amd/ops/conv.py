@@ -298,6 +298,8 @@ def _train_shadow(conv, crsk=False) -> torch.Tensor:
 def weight_krsc(conv: nn.Conv2d) -> torch.Tensor:
     """[Cout, KH, KW, Cin] bf16 (forward B operand).  Training: the fused optimizer's shadow."""
     w = conv.weight
+    if getattr(conv, "_rtseg_dense_view", False):  # a per-call block-diagonal weight: never cached
+        return w.detach().to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()
     # (called inside _ConvFn.forward, where autograd is off: a trainable weight of a module in
     # training mode is the test)
     if _SHADOW_ON and conv.training and w.requires_grad and w.is_cuda and w.dtype == torch.float32:
@@ -658,7 +660,71 @@ def conv_forward(x: torch.Tensor, conv: nn.Module) -> torch.Tensor:
     if conv_ok(x, conv) and torch.is_grad_enabled() and conv.weight.requires_grad:
         y, _ = _ConvFn.apply(x.to(torch.bfloat16), conv.weight, conv, False)
         return y
+    if grouped_dense_ok(x, conv):
+        return grouped_as_dense(x, conv)
     return conv(x)
+
+
+# ----------------------------------------------------------------------------- grouped convs
+def grouped_dense_ok(x: torch.Tensor, conv: nn.Module) -> bool:
+    """Training-time grouped (not depth-wise) convs, e.g. RegSeg's D-block 3 x 3s of group width 16
+    (reference models/regseg.py:62-110).  MIOpen's grouped weight gradient in channels-last bf16
+    is pathological at these shapes (tools/probe_grouped_conv.py), so such a conv runs as the
+    dense conv of its block-diagonal weight: ``groups`` x the FLOPs of a conv that is tiny either
+    way, on the routed kernels.  ``RTSEG_GROUPED_DENSE=0`` keeps MIOpen."""
+    return (type(conv) in _ROUTED and 1 < conv.groups <= 32 and conv.groups != conv.in_channels
+            and conv.padding_mode == "zeros" and not isinstance(conv.padding, str) and x.dim() == 4
+            and x.is_cuda and torch.is_grad_enabled() and conv.weight.requires_grad
+            and os.environ.get("RTSEG_GROUPED_DENSE", "1") != "0")
+
+
+_BLOCK_MASKS: dict = {}
+
+
+def block_diagonal(w: torch.Tensor, groups: int) -> torch.Tensor:
+    """[Cout, Cin/groups, KH, KW] grouped weight -> [Cout, Cin, KH, KW] dense (zeros off the
+    diagonal blocks); its autograd backward sums the dense gradient's diagonal blocks back."""
+    cout, cg = w.shape[0], w.shape[1]
+    key = (cout, cg, groups, w.device, w.dtype)
+    mask = _BLOCK_MASKS.get(key)
+    if mask is None:
+        og = cout // groups
+        rows = torch.arange(cout, device=w.device)[:, None] // og
+        cols = torch.arange(cg * groups, device=w.device)[None, :] // cg
+        mask = _BLOCK_MASKS[key] = (rows == cols).to(w.dtype)[:, :, None, None]
+    return w.repeat(1, groups, 1, 1) * mask
+
+
+class _DenseView:
+    """A grouped conv seen as the dense conv of its block-diagonal ``weight`` (for :class:`_ConvFn`,
+    which reads geometry and the weight from the module it is given)."""
+
+    _rtseg_dense_view = True
+    groups = 1
+    bias = None
+    padding_mode = "zeros"
+
+    def __init__(self, conv: nn.Conv2d, weight: torch.Tensor):
+        self.weight = weight
+        self.stride, self.padding, self.dilation = conv.stride, conv.padding, conv.dilation
+        self.kernel_size = conv.kernel_size
+        self.in_channels, self.out_channels = conv.in_channels, conv.out_channels
+        self.training = conv.training
+
+
+def grouped_as_dense(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
+    from .bn import bias_add
+
+    wd = block_diagonal(conv.weight, conv.groups)
+    if (use_hip(x, "conv") and _mode() != "0" and _autocast_bf16(x) and x.stride(1) == 1
+            and conv.kernel_size[0] * conv.kernel_size[1] <= 49):
+        # channels-last, or a channel slice of it (RegSeg's split halves): one dense bf16 copy
+        x = x.to(torch.bfloat16)
+        if not x.is_contiguous(memory_format=torch.channels_last) or x.data_ptr() % 16:
+            x = x.clone(memory_format=torch.channels_last)
+        y, _ = _ConvFn.apply(x, wd, _DenseView(conv, wd), False)
+        return bias_add(y, conv.bias) if conv.bias is not None else y
+    return F.conv2d(x, wd, conv.bias, conv.stride, conv.padding, conv.dilation, 1)
 
 
 def conv_bn_act(x: torch.Tensor, conv: nn.Module, bn: nn.Module, act="none", residual=None, act_module=None):

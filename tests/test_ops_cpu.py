@@ -301,3 +301,22 @@ def test_conv_tuning_db_roundtrip(tmp_path, monkeypatch):
     monkeypatch.setattr(C, "_DB", None)
     assert C._tune_db() == {}
     monkeypatch.setattr(C, "_DB", None)
+
+
+@pytest.mark.parametrize("groups,cout,cg,k", [(8, 128, 16, 3), (3, 48, 16, 3), (4, 8, 2, 1)])
+def test_block_diagonal_grouped_conv_identity(groups, cout, cg, k):
+    """The grouped-conv route (ops/conv.py grouped_as_dense): a dense conv of the block-diagonal
+    weight is the grouped conv, and the weight gradient flows back to the grouped weight."""
+    from realtime_semantic_segmentation_pytorch_amd.ops.conv import block_diagonal
+
+    torch.manual_seed(0)
+    x = torch.randn(2, cg * groups, 9, 11, dtype=torch.float64)
+    w = torch.randn(cout, cg, k, k, dtype=torch.float64, requires_grad=True)
+    w2 = w.detach().clone().requires_grad_(True)
+    y = F.conv2d(x, block_diagonal(w, groups), None, 1, k // 2, 1, 1)
+    ref = F.conv2d(x, w2, None, 1, k // 2, 1, groups)
+    torch.testing.assert_close(y, ref)
+    g = torch.randn_like(y)
+    y.backward(g)
+    ref.backward(g)
+    torch.testing.assert_close(w.grad, w2.grad)

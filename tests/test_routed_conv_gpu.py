@@ -104,3 +104,35 @@ def test_biased_conv_bias_add_matches_conv2d(k, dil):
         tol = 1e-4 if dtype == torch.float32 else 2e-2
         for a, b in zip(*outs):
             assert float((a - b).norm() / (b.norm() + 1e-12)) < tol
+
+
+# (n, c, h, w, groups, stride, dilation, split): RegSeg D-block grouped 3x3s (group width 16),
+# ``split``: the input is the second channel half of a channels-last tensor (conv_right)
+GROUPED = [(2, 128, 16, 24, 8, 1, 2, True), (2, 64, 17, 20, 4, 2, 1, False), (1, 48, 12, 16, 3, 2, 1, False),
+           (2, 128, 10, 12, 8, 1, 11, False)]
+
+
+@pytest.mark.parametrize("geom", GROUPED)
+def test_grouped_conv_block_diagonal_route(geom):
+    """Training grouped conv through the block-diagonal dense route vs fp32 grouped F.conv2d."""
+    n, c, h, w, groups, s, d, split = geom
+    torch.manual_seed(0)
+    conv = nn.Conv2d(c, c, 3, s, d, d, groups=groups, bias=False).to(DEV).to(memory_format=torch.channels_last)
+    src = torch.randn(n, 2 * c if split else c, h, w, device=DEV).to(torch.bfloat16)
+    src = src.contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    x = src[:, c:] if split else src
+    assert ops.conv.grouped_dense_ok(x, conv)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = ops.conv_forward(x, conv)
+    if c % 64 == 0:
+        assert "ConvFn" in type(y.grad_fn).__name__, type(y.grad_fn).__name__
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr = x.detach().float().requires_grad_(True)
+    wr = conv.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+    ref = F.conv2d(xr, wr, None, s, d, d, groups)
+    ref.backward(g.float())
+    _close(y, ref.detach(), 2e-2)
+    gx = src.grad[:, c:] if split else src.grad
+    _close(gx, xr.grad, 3e-2)
+    _close(conv.weight.grad, wr.grad, 3e-2)

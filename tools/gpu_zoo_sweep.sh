@@ -6,7 +6,7 @@
 TAG=$1; TRAIN=$2; FPS=${3:--}
 mkdir -p gpurun_out/zoo
 if [ "$TRAIN" != "-" ]; then
-  timeout -k 10 560 python -u tools/zoo_train.py --batch 8 --steps 5 --warmup 3 --models $TRAIN --out gpurun_out/zoo/train_$TAG.jsonl > gpurun_out/zoo/train_$TAG.log 2>&1
+  timeout -k 10 ${TRAIN_TIMEOUT:-560} python -u tools/zoo_train.py --batch 8 --steps 5 --warmup 3 --models $TRAIN --out gpurun_out/zoo/train_$TAG.jsonl > gpurun_out/zoo/train_$TAG.log 2>&1
   rc=$?; echo "train rc=$rc"; if [ $rc -gt 1 ]; then exit $rc; fi
 fi
 if [ "$FPS" != "-" ]; then

@@ -53,9 +53,11 @@ def run(key, a):
     data = DeviceBatches(a.batch, (a.height, a.width), cfg.num_class, cfg.ignore_index, device=tr.device,
                          pool=2, channels_last=cfg.channels_last, seed=7)
     torch.cuda.reset_peak_memory_stats()
-    for _ in range(a.warmup):
+    for i in range(a.warmup):
+        t = time.perf_counter()
         tr.train_step(*data.next())
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        print(f"[zoo_train] {key} warm-up step {i}: {time.perf_counter() - t:.2f} s", flush=True)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         loss, _ = tr.train_step(*data.next())
@@ -82,10 +84,16 @@ def main():
     assert torch.cuda.is_available() and ops.load()
     import threading
 
-    def beat():  # keeps a long autotune visible to the runner
+    main_id = threading.get_ident()
+
+    def beat():  # keeps a long autotune visible to the runner, with where the main thread is
         while True:
             time.sleep(60)
-            print("[zoo_train] alive", flush=True)
+            fr, where = sys._current_frames().get(main_id), []
+            while fr is not None and len(where) < 6:
+                where.append(f"{os.path.basename(fr.f_code.co_filename)}:{fr.f_lineno}:{fr.f_code.co_name}")
+                fr = fr.f_back
+            print("[zoo_train] alive: " + " <- ".join(where), flush=True)
 
     threading.Thread(target=beat, daemon=True).start()
     keys = [k for k in a.models.split(",") if k] or sorted(MODEL_HUB)
