@@ -599,7 +599,7 @@ def conv_bn_stats(x: torch.Tensor, conv: nn.Conv2d):
         x = x.to(torch.bfloat16)
     if x.data_ptr() % 16:
         x = x.clone(memory_format=torch.channels_last)
-    return _ConvFn.apply(x, conv.weight, conv, True)
+    return _apply(x, conv, True)
 
 
 def conv_bn_act_eval(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, act_code: int, residual=None):
@@ -658,7 +658,7 @@ def conv_forward(x: torch.Tensor, conv: nn.Module) -> torch.Tensor:
         with torch.autocast("cuda", enabled=False):
             return conv._conv_forward(x.to(torch.bfloat16), hit[1], hit[2])
     if conv_ok(x, conv) and torch.is_grad_enabled() and conv.weight.requires_grad:
-        y, _ = _ConvFn.apply(x.to(torch.bfloat16), conv.weight, conv, False)
+        y, _ = _apply(x.to(torch.bfloat16), conv, False)
         return y
     if grouped_dense_ok(x, conv):
         return grouped_as_dense(x, conv)
@@ -672,7 +672,7 @@ def grouped_dense_ok(x: torch.Tensor, conv: nn.Module) -> bool:
     is pathological at these shapes (tools/probe_grouped_conv.py), so such a conv runs as the
     dense conv of its block-diagonal weight: ``groups`` x the FLOPs of a conv that is tiny either
     way, on the routed kernels.  ``RTSEG_GROUPED_DENSE=0`` keeps MIOpen."""
-    return (type(conv) in _ROUTED and 1 < conv.groups <= 32 and conv.groups != conv.in_channels
+    return (isinstance(conv, nn.Conv2d) and 1 < conv.groups <= 32 and conv.groups != conv.in_channels
             and conv.padding_mode == "zeros" and not isinstance(conv.padding, str) and x.dim() == 4
             and x.is_cuda and torch.is_grad_enabled() and conv.weight.requires_grad
             and os.environ.get("RTSEG_GROUPED_DENSE", "1") != "0")
@@ -696,8 +696,9 @@ def block_diagonal(w: torch.Tensor, groups: int) -> torch.Tensor:
 
 
 class _DenseView:
-    """A grouped conv seen as the dense conv of its block-diagonal ``weight`` (for :class:`_ConvFn`,
-    which reads geometry and the weight from the module it is given)."""
+    """A conv seen as the dense conv of a derived ``weight`` -- a grouped conv's block-diagonal
+    weight, or a zero-padded one (:func:`_apply`) -- for :class:`_ConvFn`, which reads geometry
+    and the weight from the module it is given."""
 
     _rtseg_dense_view = True
     groups = 1
@@ -708,8 +709,29 @@ class _DenseView:
         self.weight = weight
         self.stride, self.padding, self.dilation = conv.stride, conv.padding, conv.dilation
         self.kernel_size = conv.kernel_size
-        self.in_channels, self.out_channels = conv.in_channels, conv.out_channels
+        self.out_channels, self.in_channels = weight.shape[0], weight.shape[1]
         self.training = conv.training
+
+
+def padded_ok(conv: nn.Module) -> bool:
+    """A spatial conv whose output channel count our kernels cannot store (Cout % 8 != 0, e.g.
+    SegNet's 3 x 3 19-class classifier at full resolution, reference models/segnet.py) over a
+    64-multiple input.  MIOpen's immediate-mode pick for its NHWC bf16 weight gradient ran for
+    minutes (``profiles/r4_zoo/train_H_segnet_stall.txt``, ``tools/probe_conv_shapes.py``)."""
+    return (conv.out_channels % 8 != 0 and conv.in_channels % 64 == 0 and max(conv.kernel_size) > 1
+            and conv.groups == 1 and os.environ.get("RTSEG_PAD_COUT", "1") != "0")
+
+
+def _apply(x: torch.Tensor, conv: nn.Module, stats: bool):
+    """:class:`_ConvFn` on ``conv``'s weight -> (y, statistics slab | None).  A :func:`padded_ok`
+    conv runs on its weight zero-padded to the next 64 output channels (all three passes then
+    fit the MFMA kernels) and returns the real channels as a dense channels-last tensor."""
+    if not padded_ok(conv):
+        return _ConvFn.apply(x, conv.weight, conv, stats)
+    cp = -(-conv.out_channels // 64) * 64
+    wp = F.pad(conv.weight, (0, 0, 0, 0, 0, 0, 0, cp - conv.out_channels))
+    y, _ = _ConvFn.apply(x, wp, _DenseView(conv, wp), False)
+    return y[:, :conv.out_channels].contiguous(memory_format=torch.channels_last), None
 
 
 def grouped_as_dense(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
@@ -756,15 +778,28 @@ class RoutedConv2d(PrunedConv2d):
     (dead taps dropped, :class:`PrunedConv2d`).  Same parameters and state-dict keys."""
 
     def forward(self, x):
-        if (x.is_cuda and self.in_channels % 32 == 0 and self.out_channels % 8 == 0 and torch.is_grad_enabled()
+        if (x.is_cuda and self.in_channels % 32 == 0 and (self.out_channels % 8 == 0 or padded_ok(self))
+                and torch.is_grad_enabled()
                 and self.weight.requires_grad and conv_ok(x, self)):
             x = x.to(torch.bfloat16)
             if x.data_ptr() % 16:  # the kernels' 16-byte operand loads
                 x = x.clone(memory_format=torch.channels_last)
-            return _ConvFn.apply(x, self.weight, self, False)[0]
+            return _apply(x, self, False)[0]
         if (x.is_cuda and not self.training and not torch.is_grad_enabled() and torch.is_autocast_enabled("cuda")
                 and torch.get_autocast_dtype("cuda") == torch.bfloat16):
             return conv_forward(x, self)  # its cached-weight branch (never falls through to self(x))
+        return super().forward(x)
+
+
+class GroupedConv2d(PrunedConv2d):
+    """A grouped (not depth-wise) ``nn.Conv2d`` a model calls as a plain module -- ESPNetv2's EESP
+    ``conv_init`` / ``conv_last`` (groups = 4, reference models/espnetv2.py): in bf16 training the
+    block-diagonal dense route (:func:`grouped_as_dense`), otherwise the stock forward.  Same
+    parameters and state-dict keys."""
+
+    def forward(self, x):
+        if grouped_dense_ok(x, self):
+            return grouped_as_dense(x, self)
         return super().forward(x)
 
 
@@ -774,15 +809,19 @@ def routable(conv: nn.Module) -> bool:
 
 
 def convert_routed_convs(model: nn.Module) -> nn.Module:
-    """Swap every remaining plain dense bias-free conv to :class:`RoutedConv2d` (in place, run
-    after the other converters; parameters and checkpoint keys unchanged)."""
+    """Swap every remaining plain dense bias-free conv to :class:`RoutedConv2d` and every plain
+    grouped one to :class:`GroupedConv2d` (in place, run after the other converters; parameters
+    and checkpoint keys unchanged)."""
     for m in model.modules():
         if routable(m):
             m.__class__ = RoutedConv2d
+        elif (type(m) in (nn.Conv2d, PrunedConv2d) and 1 < m.groups != m.in_channels
+              and m.padding_mode == "zeros" and not isinstance(m.padding, str)):
+            m.__class__ = GroupedConv2d
     return model
 
 
-_ROUTED = (nn.Conv2d, PrunedConv2d, RoutedConv2d)
+_ROUTED = (nn.Conv2d, PrunedConv2d, RoutedConv2d, GroupedConv2d)
 
 
 def decisions() -> dict:

@@ -185,6 +185,10 @@ class DilatedGroupConv2d(nn.Conv2d):
 
         if not x.is_cuda or not use_hip(x, "dilated"):  # RTSEG_DISABLE_HIP=1: the stock conv, for A/B runs
             return super().forward(x)
+        from .conv import grouped_as_dense, grouped_dense_ok
+
+        if grouped_dense_ok(x, self):  # training: the block-diagonal dense route (ops/conv.py)
+            return grouped_as_dense(x, self)
         return dilated_group_pruned(x, self.weight, self.bias, tuple(self.dilation), self.groups)
 
 

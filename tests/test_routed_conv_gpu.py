@@ -136,3 +136,59 @@ def test_grouped_conv_block_diagonal_route(geom):
     gx = src.grad[:, c:] if split else src.grad
     _close(gx, xr.grad, 3e-2)
     _close(conv.weight.grad, wr.grad, 3e-2)
+
+
+def _ref_grads(x, w, g, fn):
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().to(torch.bfloat16).float().requires_grad_(True)
+    ref = fn(xr, wr)
+    ref.backward(g.float())
+    return ref.detach(), xr.grad, wr.grad
+
+
+@pytest.mark.parametrize("raw", [False, True])
+def test_padded_cout_route(raw):
+    """SegNet's 3x3 19-class classifier: Cout % 8 != 0 runs on the weight zero-padded to 64 output
+    channels (ops/conv.py padded_ok / _apply) -- through the ConvBNAct statistics path and as a
+    plain RoutedConv2d."""
+    torch.manual_seed(0)
+    conv = nn.Conv2d(64, 19, 3, 1, 1, bias=False)
+    if raw:
+        ops.convert_routed_convs(nn.Sequential(conv))
+    conv = conv.to(DEV).to(memory_format=torch.channels_last).train()
+    assert ops.conv.padded_ok(conv)
+    x = torch.randn(2, 64, 20, 36, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = conv(x) if raw else ops.conv_bn_stats(x, conv)[0]
+    assert y.shape == (2, 19, 20, 36) and y.is_contiguous(memory_format=torch.channels_last)
+    g = torch.randn_like(y)
+    y.backward(g)
+    ref, gx, gw = _ref_grads(x, conv.weight, g, lambda a, b: F.conv2d(a, b, None, 1, 1))
+    _close(y, ref, 2e-2)
+    _close(x.grad, gx, 3e-2)
+    _close(conv.weight.grad, gw, 3e-2)
+
+
+@pytest.mark.parametrize("geom", [(64, 16, 1, 4, 1), (256, 64, 1, 4, 1), (128, 128, 3, 8, 4)])
+def test_grouped_module_routes(geom):
+    """Grouped convs called as plain modules: ESPNetv2's EESP 1x1 (groups 4) -> GroupedConv2d,
+    RegSeg's dilated D-block conv -> DilatedGroupConv2d; both train on the block-diagonal route."""
+    cin, cout, k, groups, dil = geom
+    torch.manual_seed(0)
+    conv = nn.Conv2d(cin, cout, k, 1, dil * (k // 2), dil, groups=groups, bias=False)
+    ops.convert_dilated_group_convs(nn.Sequential(conv))
+    ops.convert_routed_convs(nn.Sequential(conv))
+    assert type(conv) is (ops.DilatedGroupConv2d if dil > 1 else ops.GroupedConv2d), type(conv)
+    conv = conv.to(DEV).to(memory_format=torch.channels_last).train()
+    x = torch.randn(2, cin, 24, 40, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = conv(x)
+    assert "ConvFn" in type(y.grad_fn).__name__, type(y.grad_fn).__name__
+    g = torch.randn_like(y)
+    y.backward(g)
+    ref, gx, gw = _ref_grads(x, conv.weight, g, lambda a, b: F.conv2d(a, b, None, 1, dil * (k // 2), dil, groups))
+    _close(y, ref, 2e-2)
+    _close(x.grad, gx, 3e-2)
+    _close(conv.weight.grad, gw, 3e-2)
