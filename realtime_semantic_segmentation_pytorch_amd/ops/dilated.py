@@ -16,6 +16,8 @@ and checkpoint keys unchanged); CPU tensors keep ``F.conv2d``.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -99,7 +101,8 @@ class PrunedConv2d(nn.Conv2d):
     (:func:`pruned_conv2d`); identical to ``nn.Conv2d`` whenever no tap is dead, and on CPU."""
 
     def _conv_forward(self, input, weight, bias):
-        if bias is not None and input.is_cuda and input.dim() == 4 and self.groups == 1:
+        if (bias is not None and input.is_cuda and input.dim() == 4 and self.groups == 1
+                and os.environ.get("RTSEG_BIAS_ADD", "1") != "0"):
             # bias-free conv + bias_add: the bias gradient on the HIP channel-sum pass
             from .bn import bias_add
 
