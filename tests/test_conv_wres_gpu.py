@@ -63,7 +63,7 @@ def test_wres_dgrad(geom, with_addend):
     dy = _t((n, 64, h, w), g).contiguous(**cl)
     add = _t((n, cin, h, w), g).contiguous(**cl)
     dx = torch.ops.rtseg.conv_wres_dgrad(dy, wt.permute(1, 2, 3, 0).contiguous(), [n, cin, h, w], [1, 1], [1, 1],
-                                         [1, 1], add if with_addend else None, rpw)
+                                         [1, 1], add if with_addend else None)
     ref = torch.nn.grad.conv2d_input((n, cin, h, w), wt.float(), dy.float(), 1, 1, 1)
     _close(dx, ref + add.float() if with_addend else ref, 2e-2)
 

@@ -1,10 +1,10 @@
 #!/bin/bash
-# round 4 final headline: bench on a fresh tuning DB (written for commit), a second process on it,
+# headline run: bench on a fresh tuning DB (written for commit), a second process on it,
 # the steady-state profile, one batch-48 run (the round-2 "hang", now bounded autotune)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export PYTHONUNBUFFERED=1
-OUT=gpurun_out/r4_c16
+OUT=gpurun_out/${HEADLINE_OUT:-headline}
 mkdir -p $OUT
 RTSEG_TUNE_DB=none RTSEG_TUNE_DB_OUT=$OUT/rtseg_conv_decisions.json RTSEG_DECISIONS_OUT=$OUT/decisions.txt \
   timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
