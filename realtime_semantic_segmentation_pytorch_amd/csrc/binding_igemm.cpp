@@ -42,7 +42,7 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::
                                                  at::IntArrayRef padding, at::IntArrayRef dilation, bool stats,
                                                  const std::optional<at::Tensor>& scale_shift,
                                                  const std::optional<at::Tensor>& residual, int64_t act, int kind) {
-  const bool halo = kind == 1, wres = kind == 2, hreg = kind == 3 || kind == 4;
+  const bool halo = kind == 1, wres = kind == 2, hreg = kind == 3 || kind == 4, stem = kind == 5;
   check_act(x, "input");
   TORCH_CHECK(wk.is_cuda() && wk.dim() == 4 && wk.scalar_type() == at::kBFloat16 && wk.is_contiguous() &&
                   wk.size(3) == x.size(1),
@@ -50,7 +50,11 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::
   TORCH_CHECK(act >= 0 && act <= 2, "rtseg.conv_igemm: bad activation");
   ConvGeom g = geom(x.size(0), x.size(1), x.size(2), x.size(3), wk.size(0), wk.size(1), wk.size(2), stride, padding,
                     dilation);
-  if (halo) {
+  if (stem) {
+    TORCH_CHECK(conv_stem_supported(g),
+                "rtseg.conv_stem: needs Cin == 3, 3 x 3 / pad 1 / stride 1 or 2, Cout % 16 == 0 and <= 64, even W");
+    TORCH_CHECK(!(scale_shift.has_value() && scale_shift->defined()), "rtseg.conv_stem: no inference BN epilogue");
+  } else if (halo) {
     TORCH_CHECK(conv_halo_supported(g, 0),
                 "rtseg.conv_halo: needs stride 1, taps within 3 x 3, Cin % 64 == 0, Cout % 64 == 0");
   } else if (wres) {
@@ -69,7 +73,7 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::
   g.part = nullptr; g.scale_shift = nullptr; g.res = nullptr; g.act = static_cast<int>(act);
   at::Tensor part;
   if (stats) {
-    part = at::empty({halo ? conv_halo_slabs(g) : wres ? conv_wres_slabs(g) : hreg ? conv_hreg_slabs(g)
+    part = at::empty({stem ? conv_stem_slabs(g) : halo ? conv_halo_slabs(g) : wres ? conv_wres_slabs(g) : hreg ? conv_hreg_slabs(g)
                                                                                  : conv_igemm_slabs(g),
                       2 * g.cout},
                      x.options().dtype(at::kFloat));
@@ -90,7 +94,8 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::
     TORCH_CHECK(!(residual.has_value() && residual->defined()) && act == 0,
                 "rtseg.conv_igemm: residual / activation need the BN epilogue (scale_shift)");
   }
-  if (halo) launch_conv_halo_fwd(g, cur_stream());
+  if (stem) launch_conv_stem_fwd(g, cur_stream());
+  else if (halo) launch_conv_halo_fwd(g, cur_stream());
   else if (wres) launch_conv_wres_fwd(g, cur_stream());
   else if (hreg) {
     at::Tensor wpack = at::empty({conv_hreg_pack_elems(g, 0)}, wk.options());
@@ -135,6 +140,12 @@ std::tuple<at::Tensor, at::Tensor> conv_hreg(const at::Tensor& x, const at::Tens
 std::tuple<at::Tensor, at::Tensor> conv_wres(const at::Tensor& x, const at::Tensor& wk, at::IntArrayRef stride,
                                              at::IntArrayRef padding, at::IntArrayRef dilation, bool stats) {
   return conv_fwd_impl(x, wk, stride, padding, dilation, stats, std::nullopt, std::nullopt, 0, 2);
+}
+
+// the 3-channel stem kernel (conv_stem.hip): 3 x 3 / pad 1 / stride 1 or 2, Cout % 16 <= 64
+std::tuple<at::Tensor, at::Tensor> conv_stem(const at::Tensor& x, const at::Tensor& wk, at::IntArrayRef stride,
+                                             at::IntArrayRef padding, at::IntArrayRef dilation, bool stats) {
+  return conv_fwd_impl(x, wk, stride, padding, dilation, stats, std::nullopt, std::nullopt, 0, 5);
 }
 
 // dy [N,Cout,Ho,Wo] CL bf16, wt [Cin,KH,KW,Cout] bf16 -> dx [N,Cin,H,W] CL bf16
@@ -255,6 +266,26 @@ at::Tensor conv_whalo_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t k
   return dw;
 }
 
+// stem weight gradient (conv_stem.hip): x [N,3,H,W], dy [N,Cout,Ho,Wo] CL bf16 -> dw fp32
+at::Tensor conv_stem_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t kh, int64_t kw, at::IntArrayRef stride,
+                           at::IntArrayRef padding, at::IntArrayRef dilation, bool channels_last) {
+  check_act(x, "input");
+  check_act(dy, "grad_output");
+  ConvGeom g = geom(x.size(0), x.size(1), x.size(2), x.size(3), dy.size(1), kh, kw, stride, padding, dilation);
+  TORCH_CHECK(g.ho == dy.size(2) && g.wo == dy.size(3) && g.n == dy.size(0),
+              "rtseg.conv_stem_wgrad: grad_output does not match the geometry");
+  TORCH_CHECK(conv_stem_supported(g),
+              "rtseg.conv_stem_wgrad: needs Cin == 3, 3 x 3 / pad 1 / stride 1 or 2, Cout % 16 == 0 and <= 64, even W");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  g.x = x.data_ptr(); g.y = dy.data_ptr();
+  at::Tensor ws = at::empty({conv_stem_wgrad_ws_elems(g)}, x.options().dtype(at::kFloat));
+  at::Tensor dw = at::empty({g.cout, g.cin, g.kh, g.kw},
+                            x.options().dtype(at::kFloat).memory_format(channels_last ? at::MemoryFormat::ChannelsLast
+                                                                                      : at::MemoryFormat::Contiguous));
+  launch_conv_stem_wgrad(g, ws.data_ptr<float>(), dw.data_ptr<float>(), channels_last, cur_stream());
+  return dw;
+}
+
 }  // namespace
 }  // namespace rtseg
 
@@ -274,6 +305,9 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
   m.def("conv_wres(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats) -> (Tensor, Tensor)");
   m.def("conv_wres_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
         "Tensor? addend=None) -> Tensor");
+  m.def("conv_stem(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats) -> (Tensor, Tensor)");
+  m.def("conv_stem_wgrad(Tensor x, Tensor dy, int kh, int kw, int[] stride, int[] padding, int[] dilation, "
+        "bool channels_last=False) -> Tensor");
   m.def("conv_whalo_wgrad(Tensor x, Tensor dy, int kh, int kw, int[] stride, int[] padding, int[] dilation, "
         "bool channels_last=False) -> Tensor");
   m.def("conv_igemm_wgrad(Tensor x, Tensor dy, int kh, int kw, int[] stride, int[] padding, int[] dilation, "
@@ -291,4 +325,6 @@ TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
   m.impl("conv_wres_dgrad", &rtseg::conv_wres_dgrad);
   m.impl("conv_igemm_wgrad", &rtseg::conv_igemm_wgrad);
   m.impl("conv_whalo_wgrad", &rtseg::conv_whalo_wgrad);
+  m.impl("conv_stem", &rtseg::conv_stem);
+  m.impl("conv_stem_wgrad", &rtseg::conv_stem_wgrad);
 }

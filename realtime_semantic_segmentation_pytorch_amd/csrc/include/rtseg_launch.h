@@ -218,6 +218,15 @@ int64_t conv_hreg_pack_elems(const ConvGeom& g, int mode);
 // rows_per_wave: 1 = 8 waves of 2 x 2 accumulator tiles, 2 = 4 waves of 2 x 4 tiles
 void launch_conv_hreg(const ConvGeom& g, int mode, void* wpack, hipStream_t st, int rows_per_wave = 1);
 
+// ---- conv_stem.hip ------------------------------------------------------------
+// 3-channel 3 x 3 stem conv (pad 1, stride 1 / 2, Cout % 16 == 0 and <= 64, even W): forward
+// (+ BN statistics slab of conv_stem_slabs(g) rows) and weight gradient (g.x = x, g.y = dy).
+bool conv_stem_supported(const ConvGeom& g);
+int conv_stem_slabs(const ConvGeom& g);
+void launch_conv_stem_fwd(const ConvGeom& g, hipStream_t st);
+int64_t conv_stem_wgrad_ws_elems(const ConvGeom& g);
+void launch_conv_stem_wgrad(const ConvGeom& g, float* ws, float* dw, bool krsc, hipStream_t st);
+
 // ---- conv_whalo.hip -----------------------------------------------------------
 // Halo-tiled weight gradient of 3 x 3 / stride 1 / pad 1 / dilation 1 convs (Cin, Cout % 64 == 0):
 // g.x = x, g.y = dy; ws of conv_whalo_ws_elems(g) floats; dw fp32 as launch_conv_igemm_wgrad.

@@ -1,0 +1,374 @@
+// Stem convolution: the 3-channel 3x3 conv (pad 1, stride 1 or 2) that opens almost every model
+// of the zoo -- DDRNet's conv1 (ddrnet.py:50; reference models/ddrnet.py:27-29), the STDC /
+// BiSeNet / ResNet-style stems -- on bf16 MFMA, channels-last, gfx950.
+//
+// Why its own kernel: with Cin = 3 the implicit-GEMM K is 27, so the conv is pure streaming --
+// DDRNet-23 at batch 32 reads a 0.4 GB image and writes a 2.1 GB output.  MIOpen/CK ran it at
+// 0.95 ms and the BN statistics needed a second 2.1 GB pass (0.42 ms; profiles/r4_final/steady.txt);
+// its weight gradient (igemm_wrw) another 0.87 ms.  Here:
+//
+//  * forward: K = 27 padded to 32 is ONE v_mfma_f32_16x16x32_bf16 per 16 pixels x 16 channels.
+//    A = weights [cout][k] (registers, loaded once), B = im2col [k][pixel] gathered from an LDS
+//    copy of the tile's input rows (dword loads; a pixel pair is 12 bytes, so every dword belongs
+//    to one pair -- border pairs read as zeros).  C's lane holds 4 consecutive channels of one
+//    pixel: 8-byte stores; BN statistics from the fp32 accumulators, one [2 x cout] slab row per
+//    block (persistent grid).
+//  * weight gradient: dW[k][cout] = sum_p im2col[p][k] dy[p][cout] with the pixels as the MFMA K
+//    dimension (32 per MFMA); the dy tile is staged through LDS (16-byte global loads, 66-element
+//    row pitch: conflict-free 16-bit column reads); per-block partials, then a column-sum kernel
+//    (deterministic, no atomics).
+#include "rtseg_common.h"
+#include "rtseg_launch.h"
+#include "rtseg_mfma_dev.h"
+
+#include <algorithm>
+
+namespace rtseg {
+
+namespace {
+
+using namespace mdev;
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef short s16x8_t __attribute__((ext_vector_type(8)));
+
+constexpr int kTW = 64;  // output tile width (4 MFMA pixel groups)
+
+struct StemArgs {
+  const uint16_t* x;   // [N][H][W][3] bf16
+  const uint16_t* w;   // forward: [cout][3][3][3] bf16 (KRSC)
+  const uint16_t* dy;  // weight gradient: [N][Ho][Wo][cout] bf16
+  uint16_t* y;         // forward output [N][Ho][Wo][cout]
+  float* part;         // forward: BN statistics slab [grid][2 * cout] or null; wgrad: [grid][32 * cout]
+  int N, H, W, Ho, Wo, cout;
+  int tilesW, tilesH, mtiles;
+};
+
+// per-lane LDS offsets of the 8 k entries 8h..8h+7 (k = ky * 9 + kx * 3 + ci) relative to the
+// pixel's (row 0, tap 0) element; -1 for the zero padding k >= 27
+template <int PX>
+__device__ __forceinline__ void k_offsets(int h, int (&ko)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 8 * h + j;
+    const int ky = k / 9, r = k - 9 * ky;
+    ko[j] = k < 27 ? ky * PX * 3 + r : -1;
+  }
+}
+
+// input rows of an output tile [TH x kTW] into LDS: R rows x PX pixels (3 bf16 each) starting at
+// input column ox0 * S - 2 (even, so dword-aligned); row r = input row oy0 * S - 1 + r
+template <int S, int TH>
+struct StemTile {
+  static constexpr int R = (TH - 1) * S + 3;
+  static constexpr int PX = (((kTW - 1) * S + 4) + 1) & ~1;
+  static constexpr int DW = PX * 3 / 2;  // dwords per LDS row
+};
+
+template <int S, int TH>
+__device__ __forceinline__ void stage_input(const StemArgs& a, uint32_t* l32, int n, int oy0, int ox0, int tid,
+                                            int nthr) {
+  using T = StemTile<S, TH>;
+  const int iw0 = ox0 * S - 2;
+  const uint32_t* x32 = reinterpret_cast<const uint32_t*>(a.x);
+  for (int d = tid; d < T::R * T::DW; d += nthr) {
+    const int r = d / T::DW, dd = d - r * T::DW;
+    const int ih = oy0 * S - 1 + r;
+    const int iwp = iw0 + 2 * (dd / 3);
+    uint32_t v = 0;
+    if (static_cast<unsigned>(ih) < static_cast<unsigned>(a.H) && iwp >= 0 && iwp < a.W)
+      v = x32[((static_cast<int64_t>(n) * a.H + ih) * a.W + iw0) * 3 / 2 + dd];
+    l32[d] = v;
+  }
+}
+
+template <int S, int NT, int STATS>
+__global__ void __launch_bounds__(256) stem_fwd_kernel(const StemArgs a) {
+  constexpr int TH = 8;  // 4 waves x 2 rows
+  using T = StemTile<S, TH>;
+  __shared__ uint32_t l32[T::R * T::DW];
+  __shared__ float red[4][2][64];
+  const uint16_t* l16 = reinterpret_cast<const uint16_t*>(l32);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int h = lane >> 4, px = lane & 15;
+  const int G = gridDim.x;
+  const int lb = xcd_logical(blockIdx.x, G);
+
+  // A fragments: weights [cout 16t + px][k 8h + j]
+  bf16x8_t wf[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    s16x8_t v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * h + j;
+      v[j] = k < 27 ? static_cast<short>(a.w[(16 * t + px) * 27 + k]) : short(0);
+    }
+    wf[t] = __builtin_bit_cast(bf16x8_t, v);
+  }
+  int ko[8];
+  k_offsets<T::PX>(h, ko);
+
+  float ts[NT][4], tq[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ts[t][r] = tq[t][r] = 0.f;
+
+  for (int mt = lb; mt < a.mtiles; mt += G) {
+    const int tx = mt % a.tilesW, t2 = mt / a.tilesW;
+    const int n = t2 / a.tilesH, oy0 = (t2 % a.tilesH) * TH, ox0 = tx * kTW;
+    __syncthreads();  // the previous tile's fragment reads are done
+    stage_input<S, TH>(a, l32, n, oy0, ox0, tid, 256);
+    __syncthreads();
+#pragma unroll 2
+    for (int g = 0; g < 8; ++g) {
+      const int oyl = 2 * wid + (g >> 2), oxl = (g & 3) * 16 + px;
+      const int base = oyl * S * T::PX * 3 + (oxl * S + 1) * 3;
+      s16x8_t b;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) b[j] = ko[j] >= 0 ? static_cast<short>(l16[base + ko[j]]) : short(0);
+      const bf16x8_t bf = __builtin_bit_cast(bf16x8_t, b);
+      const int oy = oy0 + oyl, ox = ox0 + oxl;
+      const bool ok = oy < a.Ho && ox < a.Wo;
+      uint16_t* yp = a.y + ((static_cast<int64_t>(n) * a.Ho + (ok ? oy : 0)) * a.Wo + (ok ? ox : 0)) * a.cout + 4 * h;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        f32x4_t c = {0.f, 0.f, 0.f, 0.f};
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t], bf, c, 0, 0, 0);
+        uint2 pk;
+        pk.x = pack2(c[0], c[1]);
+        pk.y = pack2(c[2], c[3]);
+        if (ok) *reinterpret_cast<uint2*>(yp + 16 * t) = pk;
+        if constexpr (STATS) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float u = ok ? c[r] : 0.f;
+            ts[t][r] += u;
+            tq[t][r] = fmaf(u, u, tq[t][r]);
+          }
+        }
+      }
+    }
+  }
+
+  if constexpr (STATS) {
+    // sum over the 16 pixel lanes of each row (DPP row_ror 8 / 4 / 2 / 1), then over the waves
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float s = ts[t][r], q = tq[t][r];
+        s += dpp_f<0x128, 0xF>(s); q += dpp_f<0x128, 0xF>(q);
+        s += dpp_f<0x124, 0xF>(s); q += dpp_f<0x124, 0xF>(q);
+        s += dpp_f<0x122, 0xF>(s); q += dpp_f<0x122, 0xF>(q);
+        s += dpp_f<0x121, 0xF>(s); q += dpp_f<0x121, 0xF>(q);
+        if (px == 0) {
+          red[wid][0][16 * t + 4 * h + r] = s;
+          red[wid][1][16 * t + 4 * h + r] = q;
+        }
+      }
+    __syncthreads();
+    if (tid < 2 * a.cout) {
+      const int sq = tid >= a.cout, c = sq ? tid - a.cout : tid;
+      const float v = red[0][sq][c] + red[1][sq][c] + red[2][sq][c] + red[3][sq][c];
+      a.part[static_cast<int64_t>(blockIdx.x) * 2 * a.cout + tid] = v;
+    }
+  }
+}
+
+// weight gradient partials: block b writes ws[b][k 32][cout] (k >= 27 rows are zero)
+template <int S, int NT>
+__global__ void __launch_bounds__(256) stem_wgrad_kernel(const StemArgs a) {
+  constexpr int TH = 4;  // 4 waves x 1 row of 64 pixels (2 MFMA K-steps of 32 pixels)
+  constexpr int CP = 16 * NT + 2;  // dy row pitch (elements)
+  using T = StemTile<S, TH>;
+  __shared__ uint32_t l32[T::R * T::DW];
+  __shared__ uint16_t dyl[TH * kTW * CP];
+  const uint16_t* l16 = reinterpret_cast<const uint16_t*>(l32);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int h = lane >> 4, c16 = lane & 15;
+  const int G = gridDim.x;
+  const int lb = xcd_logical(blockIdx.x, G);
+  constexpr int C = 16 * NT;
+
+  // A rows: k = 16 mt + c16 -> LDS offset of (ky, kx, ci) relative to the pixel's element
+  int ka[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const int k = 16 * m + c16;
+    const int ky = k / 9, r = k - 9 * ky;
+    ka[m] = k < 27 ? ky * T::PX * 3 + r : -1;
+  }
+  f32x4_t acc[2][NT];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[m][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  for (int mt = lb; mt < a.mtiles; mt += G) {
+    const int tx = mt % a.tilesW, t2 = mt / a.tilesW;
+    const int n = t2 / a.tilesH, oy0 = (t2 % a.tilesH) * TH, ox0 = tx * kTW;
+    __syncthreads();
+    stage_input<S, TH>(a, l32, n, oy0, ox0, tid, 256);
+    // dy tile [TH * 64 pixels][C] (pixels past the image read as zeros)
+    constexpr int V = C / 8;  // 16-byte vectors per pixel
+    for (int e = tid; e < TH * kTW * V; e += 256) {
+      const int p = e / V, v = e - p * V;
+      const int oy = oy0 + p / kTW, ox = ox0 + (p % kTW);
+      uint4 q = {0u, 0u, 0u, 0u};
+      if (oy < a.Ho && ox < a.Wo)
+        q = *reinterpret_cast<const uint4*>(a.dy + ((static_cast<int64_t>(n) * a.Ho + oy) * a.Wo + ox) * C + 8 * v);
+      uint32_t* d = reinterpret_cast<uint32_t*>(dyl + p * CP + 8 * v);
+      d[0] = q.x; d[1] = q.y; d[2] = q.z; d[3] = q.w;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      // K = 32 pixels: lane half h holds pixels 8h .. 8h + 7 of this step
+      const int p0 = wid * kTW + ks * 32 + 8 * h;  // tile pixel index
+      const int oxl0 = ks * 32 + 8 * h;
+      bf16x8_t af[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        s16x8_t v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int base = wid * S * T::PX * 3 + ((oxl0 + j) * S + 1) * 3;
+          v[j] = ka[m] >= 0 ? static_cast<short>(l16[base + ka[m]]) : short(0);
+        }
+        af[m] = __builtin_bit_cast(bf16x8_t, v);
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        s16x8_t v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = static_cast<short>(dyl[(p0 + j) * CP + 16 * t + c16]);
+        const bf16x8_t bfr = __builtin_bit_cast(bf16x8_t, v);
+#pragma unroll
+        for (int m = 0; m < 2; ++m) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr, acc[m][t], 0, 0, 0);
+      }
+    }
+  }
+
+  // block partial: C[k = 16 m + 4 h + r][cout = 16 t + c16], summed over the 4 waves through LDS
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(dyl);  // [4 waves][32][C] fp32 <= 32 KiB
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[(wid * 32 + 16 * m + 4 * h + r) * C + 16 * t + c16] = acc[m][t][r];
+  __syncthreads();
+  for (int e = tid; e < 32 * C; e += 256) {
+    const float v = red[e] + red[32 * C + e] + red[64 * C + e] + red[96 * C + e];
+    a.part[static_cast<int64_t>(blockIdx.x) * 32 * C + e] = v;
+  }
+}
+
+// dw[cout][ci][ky][kx] (or KRSC when channels_last) = sum over blocks of ws[b][k][cout]; block =
+// 16 row slices x 64 entries, the slices summed through LDS in a fixed order (deterministic)
+__global__ void __launch_bounds__(1024) stem_wgrad_reduce(const float* __restrict__ ws, int rows, int cout,
+                                                          float* __restrict__ dw, int krsc) {
+  __shared__ float red[16][64];
+  const int ei = threadIdx.x & 63, rs = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + ei;  // e = k * cout + co
+  const int n = 27 * cout;
+  float s = 0.f;
+  if (e < n)
+    for (int b = rs; b < rows; b += 16) s += ws[static_cast<int64_t>(b) * 32 * cout + e];
+  red[rs][ei] = s;
+  __syncthreads();
+  if (rs != 0 || e >= n) return;
+#pragma unroll
+  for (int r = 1; r < 16; ++r) s += red[r][ei];
+  const int k = e / cout, co = e - k * cout;
+  const int ky = k / 9, kx = (k / 3) % 3, ci = k % 3;
+  dw[krsc ? co * 27 + k : co * 27 + ci * 9 + ky * 3 + kx] = s;
+}
+
+bool stem_fill(StemArgs& k, const ConvGeom& g, int th) {
+  if (g.cin != 3 || g.kh != 3 || g.kw != 3 || g.ph != 1 || g.pw != 1 || g.dh != 1 || g.dw != 1) return false;
+  if (g.sh != g.sw || (g.sh != 1 && g.sh != 2)) return false;
+  if (g.cout % 16 != 0 || g.cout > 64 || g.w_in % 2 != 0) return false;
+  k.N = g.n; k.H = g.h; k.W = g.w_in; k.Ho = g.ho; k.Wo = g.wo; k.cout = g.cout;
+  k.tilesW = (g.wo + kTW - 1) / kTW;
+  k.tilesH = (g.ho + th - 1) / th;
+  k.mtiles = g.n * k.tilesW * k.tilesH;
+  return true;
+}
+
+int stem_grid(int mtiles) { return std::max(1, std::min(mtiles, 2048)); }
+
+template <int S, int NT>
+void fwd_launch(const StemArgs& k, int grid, hipStream_t st) {
+  if (k.part != nullptr) stem_fwd_kernel<S, NT, 1><<<grid, 256, 0, st>>>(k);
+  else stem_fwd_kernel<S, NT, 0><<<grid, 256, 0, st>>>(k);
+}
+
+template <int S>
+void fwd_dispatch(const StemArgs& k, int grid, hipStream_t st) {
+  switch (k.cout / 16) {
+    case 1: fwd_launch<S, 1>(k, grid, st); break;
+    case 2: fwd_launch<S, 2>(k, grid, st); break;
+    case 3: fwd_launch<S, 3>(k, grid, st); break;
+    default: fwd_launch<S, 4>(k, grid, st); break;
+  }
+}
+
+template <int S>
+void wgrad_dispatch(const StemArgs& k, int grid, hipStream_t st) {
+  switch (k.cout / 16) {
+    case 1: stem_wgrad_kernel<S, 1><<<grid, 256, 0, st>>>(k); break;
+    case 2: stem_wgrad_kernel<S, 2><<<grid, 256, 0, st>>>(k); break;
+    case 3: stem_wgrad_kernel<S, 3><<<grid, 256, 0, st>>>(k); break;
+    default: stem_wgrad_kernel<S, 4><<<grid, 256, 0, st>>>(k); break;
+  }
+}
+
+}  // namespace
+
+bool conv_stem_supported(const ConvGeom& g) {
+  StemArgs k{};
+  return stem_fill(k, g, 8);
+}
+
+int conv_stem_slabs(const ConvGeom& g) {
+  StemArgs k{};
+  if (!stem_fill(k, g, 8)) return 0;
+  return stem_grid(k.mtiles);
+}
+
+void launch_conv_stem_fwd(const ConvGeom& g, hipStream_t st) {
+  StemArgs k{};
+  if (!stem_fill(k, g, 8)) return;
+  k.x = static_cast<const uint16_t*>(g.x);
+  k.w = static_cast<const uint16_t*>(g.w);
+  k.y = static_cast<uint16_t*>(g.y);
+  k.part = g.part;
+  const int grid = stem_grid(k.mtiles);
+  if (g.sh == 2) fwd_dispatch<2>(k, grid, st);
+  else fwd_dispatch<1>(k, grid, st);
+}
+
+int64_t conv_stem_wgrad_ws_elems(const ConvGeom& g) {
+  StemArgs k{};
+  if (!stem_fill(k, g, 4)) return 0;
+  return static_cast<int64_t>(stem_grid(k.mtiles)) * 32 * g.cout;
+}
+
+// g.x = x [N,H,W,3], g.y = dy [N,Ho,Wo,Cout]; ws of conv_stem_wgrad_ws_elems(g) floats
+void launch_conv_stem_wgrad(const ConvGeom& g, float* ws, float* dw, bool krsc, hipStream_t st) {
+  StemArgs k{};
+  if (!stem_fill(k, g, 4)) return;
+  k.x = static_cast<const uint16_t*>(g.x);
+  k.dy = static_cast<const uint16_t*>(g.y);
+  k.part = ws;
+  const int grid = stem_grid(k.mtiles);
+  if (g.sh == 2) wgrad_dispatch<2>(k, grid, st);
+  else wgrad_dispatch<1>(k, grid, st);
+  const int n = 27 * g.cout;
+  stem_wgrad_reduce<<<(n + 63) / 64, 1024, 0, st>>>(ws, grid, g.cout, dw, krsc ? 1 : 0);
+}
+
+}  // namespace rtseg

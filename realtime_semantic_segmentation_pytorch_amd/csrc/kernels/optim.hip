@@ -59,17 +59,24 @@ __global__ void __launch_bounds__(kOptBlock) fused_opt_kernel(const int64_t* met
   int64_t end = start + kOptChunk;
   if (end > n) end = n;
 
+  const bool sgd = hp.mode == kOptSGD;
+  const bool use_m1 = !sgd || hp.momentum != 0.f;
+  const bool read_m1 = use_m1 && !(sgd && first);
   for (int64_t base = start + threadIdx.x; base < end; base += kOptBlock * kOptUnroll) {
-    float pv[kOptUnroll], gv[kOptUnroll];
+    // every operand of the kOptUnroll elements is loaded before any is used: one memory round
+    // trip per iteration instead of three (parameter + gradient, then state, then the EMA copy)
+    float pv[kOptUnroll], gv[kOptUnroll], av[kOptUnroll], bv[kOptUnroll], ev[kOptUnroll];
     bool ok[kOptUnroll];
 #pragma unroll
     for (int u = 0; u < kOptUnroll; ++u) {
       const int64_t i = base + u * kOptBlock;
       ok[u] = i < end;
-      pv[u] = ok[u] ? p[i] : 0.f;
-      if (!ok[u]) gv[u] = 0.f;
-      else if (g_bf16) gv[u] = bf16_to_f32(static_cast<const uint16_t*>(graw)[i]);
-      else gv[u] = static_cast<const float*>(graw)[i];
+      const int64_t j = ok[u] ? i : start;  // in-range dummy address for the tail lanes
+      pv[u] = p[j];
+      gv[u] = g_bf16 ? bf16_to_f32(static_cast<const uint16_t*>(graw)[j]) : static_cast<const float*>(graw)[j];
+      av[u] = read_m1 ? m1[j] : 0.f;
+      bv[u] = sgd ? 0.f : m2[j];
+      ev[u] = ema != nullptr ? ema[j] : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < kOptUnroll; ++u) {
@@ -77,11 +84,11 @@ __global__ void __launch_bounds__(kOptBlock) fused_opt_kernel(const int64_t* met
       const int64_t i = base + u * kOptBlock;
       float pp = pv[u];
       float g = gv[u] * hp.grad_scale;
-      if (hp.mode == kOptSGD) {
+      if (sgd) {
         if (hp.weight_decay != 0.f) g += hp.weight_decay * pp;
         float d = g;
         if (hp.momentum != 0.f) {
-          const float b = first ? g : hp.momentum * m1[i] + (1.f - hp.dampening) * g;
+          const float b = first ? g : hp.momentum * av[u] + (1.f - hp.dampening) * g;
           m1[i] = b;
           d = hp.nesterov ? g + hp.momentum * b : b;
         }
@@ -89,8 +96,8 @@ __global__ void __launch_bounds__(kOptBlock) fused_opt_kernel(const int64_t* met
       } else {
         if (hp.mode == kOptAdamW) pp *= 1.f - hp.lr * hp.weight_decay;
         else if (hp.weight_decay != 0.f) g += hp.weight_decay * pp;
-        const float m = hp.beta1 * m1[i] + (1.f - hp.beta1) * g;
-        const float v = hp.beta2 * m2[i] + (1.f - hp.beta2) * g * g;
+        const float m = hp.beta1 * av[u] + (1.f - hp.beta1) * g;
+        const float v = hp.beta2 * bv[u] + (1.f - hp.beta2) * g * g;
         m1[i] = m;
         m2[i] = v;
         const float denom = sqrtf(v) * hp.inv_sqrt_bc2 + hp.eps;
@@ -120,7 +127,7 @@ __global__ void __launch_bounds__(kOptBlock) fused_opt_kernel(const int64_t* met
         if (sh_crsk != nullptr) sh_crsk[((ci * kh + r) * kw + q) * cout + co] = b;
       }
       if (ema != nullptr) {
-        ema[i] = lerp_like_torch(ema[i], pp, hp.ema_w);
+        ema[i] = lerp_like_torch(ev[u], pp, hp.ema_w);
       }
     }
   }

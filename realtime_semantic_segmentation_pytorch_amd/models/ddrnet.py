@@ -147,6 +147,11 @@ class RB(nn.Module):
         self.act = nn.ReLU()
 
     def forward(self, x):
+        if self.downsample:
+            # conv1 and the projection shortcut read x: one autograd node, one input gradient
+            hs = self.conv1.start_twin(self.conv_down, x)
+            if hs is not None:
+                return self.conv2(self.conv1.finish(hs[0]), residual=self.conv_down.finish(hs[1]), act=self.act)
         shortcut = self.conv_down(x) if self.downsample else x
         # relu(BN(conv2(.)) + shortcut) as one fused BN/residual/activation kernel
         return self.conv2(self.conv1(x), residual=shortcut, act=self.act)
@@ -166,6 +171,11 @@ class RBB(nn.Module):
         self.act = Activation(act_type)
 
     def forward(self, x):
+        if self.downsample:
+            hs = self.conv1.start_twin(self.conv_down, x)
+            if hs is not None:
+                return self.conv3(self.conv2(self.conv1.finish(hs[0])), residual=self.conv_down.finish(hs[1]),
+                                  act=self.act)
         shortcut = self.conv_down(x) if self.downsample else x
         return self.conv3(self.conv2(self.conv1(x)), residual=shortcut, act=self.act)
 

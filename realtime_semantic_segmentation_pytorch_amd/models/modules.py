@@ -120,6 +120,24 @@ class _FusedTail:
                 return y, part, ops.bn_stats_begin(y, bn, part)
         return (x,)
 
+    def start_twin(self, other, x):
+        """:meth:`start` of this block and of ``other`` (another conv + BN block reading the same
+        ``x``, e.g. a downsampling residual block's projection shortcut) with both convs in one
+        autograd node (``ops.twin_conv_bn_stats``): the input gradient is written once, with no
+        accumulation add of the two.  None -> call :meth:`start` / ``forward`` separately."""
+        blocks = (self, other)
+        for b in blocks:
+            bn = b[1]
+            if not (isinstance(bn, (nn.BatchNorm2d, nn.SyncBatchNorm))
+                    and (bn.training or not bn.track_running_stats or bn.running_mean is None)):
+                return None
+        if not (torch.is_grad_enabled() and x.requires_grad):
+            return None  # nothing to save: the twin node only pays off in a training backward
+        r = ops.twin_conv_bn_stats(x, self[0], other[0])
+        if r is None:
+            return None
+        return tuple((y, part, ops.bn_stats_begin(y, b[1], part)) for b, (y, part) in zip(blocks, r))
+
     def finish(self, h, residual=None, act=None):
         """Second half of ``forward``: ``h`` from :meth:`start`."""
         if len(h) == 1:

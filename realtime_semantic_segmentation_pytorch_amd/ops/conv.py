@@ -165,6 +165,21 @@ def whalo_ok(conv, cin: int, cout: int, npix: int) -> bool:
             and _fits32(npix, max(cin, cout)))
 
 
+# new kernel paths stay opt-in until their GPU tests have passed on this tree
+_STEM_DEFAULT = "0"
+_TWIN_DEFAULT = "0"
+
+
+def stem_ok(conv, x: torch.Tensor) -> bool:
+    """Convs ``conv_stem`` takes (``csrc/kernels/conv_stem.hip``): 3 input channels, 3 x 3, pad 1,
+    dilation 1, stride 1 or 2, a multiple of 16 up to 64 produced, even input width."""
+    if os.environ.get("RTSEG_CONV_STEM", _STEM_DEFAULT) == "0":
+        return False
+    return (conv.in_channels == 3 and tuple(conv.kernel_size) == (3, 3) and tuple(conv.padding) == (1, 1)
+            and tuple(conv.dilation) == (1, 1) and tuple(conv.stride) in ((1, 1), (2, 2))
+            and conv.out_channels % 16 == 0 and conv.out_channels <= 64 and x.shape[3] % 2 == 0)
+
+
 def _order(cands):
     """``RTSEG_CONV_HALO=1`` / ``RTSEG_CONV_WRES=1``: that candidate first (what
     ``RTSEG_CONV_MFMA=1`` forces)."""
@@ -178,6 +193,8 @@ def _order(cands):
         cands.sort(key=lambda c: c[0] != "hreg")
     if os.environ.get("RTSEG_CONV_HREG") == "2":
         cands.sort(key=lambda c: c[0] != "hreg2")
+    if os.environ.get("RTSEG_CONV_STEM") == "1":
+        cands.sort(key=lambda c: c[0] != "stem")
     return cands
 
 
@@ -377,34 +394,42 @@ def _db_pick(entry, names):
 
 
 # ----------------------------------------------------------------------------- autograd node
+def _conv_fwd(x, weight, conv, stats):
+    """(y, BN statistics slab | None, KRSC bf16 weight, autotune key) of a routed conv."""
+    stride, padding, dilation = _geom(conv)
+    cout, cin, kh, kw = weight.shape
+    key = (tuple(x.shape), cout, kh, kw, tuple(stride), tuple(padding), tuple(dilation))
+    part = None
+    wk = weight_krsc(conv)
+    impl = _fwd_impl(x, wk, conv, key, stats)
+    if impl == "igemm":
+        y, part = ops().conv_igemm(x, wk, stride, padding, dilation, stats, None, None, 0)
+    elif impl == "igemm_nostats":  # short-K convs: the epilogue reduction costs more than a pass
+        y, part = ops().conv_igemm(x, wk, stride, padding, dilation, False, None, None, 0)
+    elif impl == "halo":
+        y, part = ops().conv_halo(x, wk, stride, padding, dilation, stats, None, None, 0)
+    elif impl == "wres":
+        y, part = ops().conv_wres(x, wk, stride, padding, dilation, stats)
+    elif impl in ("hreg", "hreg2"):
+        y, part = ops().conv_hreg(x, wk, stride, padding, dilation, stats, 2 if impl == "hreg2" else 1)
+    elif impl == "mfma":
+        y, part = ops().conv_mfma(x, wk, stride, padding, dilation, stats, None, None, 0)
+    elif impl == "stem":
+        y, part = ops().conv_stem(x, wk, stride, padding, dilation, stats)
+    else:
+        y = F.conv2d(x, wk.permute(0, 3, 1, 2), None, stride, padding, dilation)
+        y = y.contiguous(memory_format=torch.channels_last)
+    if part is not None and part.numel() == 0:
+        part = None
+    return y, part, wk, key
+
+
 class _ConvFn(torch.autograd.Function):
     """y (+ BN statistics slab) = conv(x, w); backward via our dgrad / wgrad or MIOpen."""
 
     @staticmethod
     def forward(ctx, x, weight, conv, stats):
-        stride, padding, dilation = _geom(conv)
-        cout, cin, kh, kw = weight.shape
-        key = (tuple(x.shape), cout, kh, kw, tuple(stride), tuple(padding), tuple(dilation))
-        part = None
-        wk = weight_krsc(conv)
-        impl = _fwd_impl(x, wk, conv, key, stats)
-        if impl == "igemm":
-            y, part = ops().conv_igemm(x, wk, stride, padding, dilation, stats, None, None, 0)
-        elif impl == "igemm_nostats":  # short-K convs: the epilogue reduction costs more than a pass
-            y, part = ops().conv_igemm(x, wk, stride, padding, dilation, False, None, None, 0)
-        elif impl == "halo":
-            y, part = ops().conv_halo(x, wk, stride, padding, dilation, stats, None, None, 0)
-        elif impl == "wres":
-            y, part = ops().conv_wres(x, wk, stride, padding, dilation, stats)
-        elif impl in ("hreg", "hreg2"):
-            y, part = ops().conv_hreg(x, wk, stride, padding, dilation, stats, 2 if impl == "hreg2" else 1)
-        elif impl == "mfma":
-            y, part = ops().conv_mfma(x, wk, stride, padding, dilation, stats, None, None, 0)
-        else:
-            y = F.conv2d(x, wk.permute(0, 3, 1, 2), None, stride, padding, dilation)
-            y = y.contiguous(memory_format=torch.channels_last)
-        if part is not None and part.numel() == 0:
-            part = None
+        y, part, wk, key = _conv_fwd(x, weight, conv, stats)
         ctx.save_for_backward(x, wk)
         ctx.conv, ctx.key = conv, key
         # identity of the input, so a residual-add node downstream can hand this node the
@@ -424,21 +449,81 @@ class _ConvFn(torch.autograd.Function):
         if dy is None:
             return None, None, None, None
         x, wk = ctx.saved_tensors
-        conv, key = ctx.conv, ctx.key
-        stride, padding, dilation = _geom(conv)
-        dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        if dy.data_ptr() % 16:
-            dy = dy.clone(memory_format=torch.channels_last)
-        want_dx, want_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
-        dx = dw = None
         addend = ctx.addend_slot.pop() if ctx.addend_slot else None
-        if want_dx:
-            dx = _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend)
-        if want_dw:
-            dw = _wgrad(x, dy, wk, conv, key, stride, padding, dilation)
-            if dw.dtype != ctx.wdtype:
-                dw = like_param(dw.to(ctx.wdtype), conv.weight)
+        dx, dw = _conv_bwd(x, wk, ctx.conv, ctx.key, dy, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
+                           ctx.wdtype, addend)
         return dx, dw, None, None
+
+
+def _conv_bwd(x, wk, conv, key, dy, want_dx, want_dw, wdtype, addend=None):
+    """(dx (+ addend) | None, dw | None) of a routed conv."""
+    stride, padding, dilation = _geom(conv)
+    dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    if dy.data_ptr() % 16:
+        dy = dy.clone(memory_format=torch.channels_last)
+    dx = dw = None
+    if want_dx:
+        dx = _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend)
+    elif addend is not None:
+        dx = addend
+    if want_dw:
+        dw = _wgrad(x, dy, wk, conv, key, stride, padding, dilation)
+        if dw.dtype != wdtype:
+            dw = like_param(dw.to(wdtype), conv.weight)
+    return dx, dw
+
+
+class _TwinConvFn(torch.autograd.Function):
+    """Two routed convs reading the same input -- the 3 x 3 conv and the 1 x 1 projection
+    shortcut of a downsampling residual block (DDRNet RB / RBB, reference models/ddrnet.py:168-219)
+    -- as ONE autograd node.  Its backward runs once both output gradients exist, so the second
+    data gradient takes the first as its epilogue addend: the input gradient is written once,
+    with no separate accumulation add of two full-size gradients (autograd's, otherwise)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, w2, conv1, conv2):
+        y1, p1, wk1, key1 = _conv_fwd(x, w1, conv1, True)
+        y2, p2, wk2, key2 = _conv_fwd(x, w2, conv2, True)
+        ctx.save_for_backward(x, wk1, wk2)
+        ctx.convs, ctx.keys, ctx.wdtypes = (conv1, conv2), (key1, key2), (w1.dtype, w2.dtype)
+        ctx.in_key = (x.data_ptr(), tuple(x.shape), x.dtype)  # residual hand-off target (ops.bn)
+        ctx.addend_slot = None
+        for p in (p1, p2):
+            if p is not None:
+                ctx.mark_non_differentiable(p)
+        ctx.set_materialize_grads(False)
+        return y1, p1, y2, p2
+
+    @staticmethod
+    def backward(ctx, dy1, _dp1, dy2, _dp2):
+        x, wk1, wk2 = ctx.saved_tensors
+        want_dx = ctx.needs_input_grad[0]
+        dx = ctx.addend_slot.pop() if ctx.addend_slot else None
+        dws = []
+        for i, (dy, wk) in enumerate(((dy1, wk1), (dy2, wk2))):
+            if dy is None:
+                dws.append(None)
+                continue
+            dx, dw = _conv_bwd(x, wk, ctx.convs[i], ctx.keys[i], dy, want_dx, ctx.needs_input_grad[1 + i],
+                               ctx.wdtypes[i], dx)
+            dws.append(dw)
+        return dx if want_dx else None, dws[0], dws[1], None, None
+
+
+def twin_conv_bn_stats(x: torch.Tensor, conv1: nn.Module, conv2: nn.Module):
+    """Training forward of two batch-statistics conv + BN blocks on the same input x (see
+    :class:`_TwinConvFn`): ((y1, slab1 | None), (y2, slab2 | None)), or None -> the caller's
+    per-conv path (``RTSEG_TWIN_CONV=0``: always)."""
+    if os.environ.get("RTSEG_TWIN_CONV", _TWIN_DEFAULT) == "0":
+        return None
+    if not (conv_ok(x, conv1) and conv_ok(x, conv2)) or padded_ok(conv1) or padded_ok(conv2):
+        return None
+    if x.dtype != torch.bfloat16:
+        x = x.to(torch.bfloat16)
+    if x.data_ptr() % 16:
+        x = x.clone(memory_format=torch.channels_last)
+    y1, p1, y2, p2 = _TwinConvFn.apply(x, conv1.weight, conv2.weight, conv1, conv2)
+    return (y1, p1), (y2, p2)
 
 
 def _fwd_impl(x, wk, conv, key, stats) -> str:
@@ -462,6 +547,8 @@ def _fwd_impl(x, wk, conv, key, stats) -> str:
             cands.append(("hreg2", lambda: ops().conv_hreg(x, wk, stride, padding, dilation, stats, 2)))
     elif cin % 32 == 0 and cout % 8 == 0:
         cands.append(("mfma", lambda: ops().conv_mfma(x, wk, stride, padding, dilation, stats, None, None, 0)))
+    elif stem_ok(conv, x):
+        cands.append(("stem", lambda: ops().conv_stem(x, wk, stride, padding, dilation, stats)))
     if not cands:
         return "miopen"
 
@@ -581,9 +668,14 @@ def _wgrad(x, dy, wk, conv, key, stride, padding, dilation):
         return torch.ops.aten.convolution_backward(dy, x, wk.permute(0, 3, 1, 2), None, stride, padding, dilation,
                                                    False, [0, 0], 1, [False, True, False])[1]
 
+    def stem():
+        return ops().conv_stem_wgrad(x, dy, kh, kw, stride, padding, dilation, cl)
+
     cands = [("igemm", ours)] if cin % 64 == 0 and cout % 64 == 0 else []
     if whalo_ok(conv, cin, cout, _npix(x)):
         cands.append(("whalo", whalo))
+    if stem_ok(conv, x):
+        cands.append(("stem", stem))
     cands.append(("miopen", miopen))
     cands = _order(cands)
     dw = cands[_choose(("wgrad",) + key, cands)][1]()

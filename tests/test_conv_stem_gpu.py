@@ -1,0 +1,173 @@
+"""3-channel stem conv (csrc/kernels/conv_stem.hip) vs fp32 PyTorch on the same bf16 operands:
+forward (+ BN-statistics slab) and weight gradient of 3x3 / pad-1 convs with Cin = 3, stride 1
+and 2, Cout 16 / 32 / 48 / 64 -- partial tiles (Ho % 8, Wo % 64), fewer tiles than blocks and
+many tiles per block, both parameter layouts; deterministic.  Reference layer: DDRNet's conv1
+(reference models/ddrnet.py:27-29), the stems of the STDC / BiSeNet / ResNet families."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from realtime_semantic_segmentation_pytorch_amd import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+# (n, h, w, cout, stride); w even
+GEOMS = [(2, 17, 70, 64, 2), (1, 9, 130, 32, 1), (3, 33, 66, 16, 2), (2, 20, 128, 48, 1),
+         (8, 256, 512, 64, 2), (1, 5, 6, 64, 2)]
+
+
+@pytest.fixture(autouse=True)
+def _lib():
+    assert ops.load(), "HIP extension must load on the GPU box"
+
+
+def _t(shape, g, scale=1.0):
+    return (torch.randn(shape, generator=g) * scale).to(DEV, torch.bfloat16)
+
+
+def _close(got, ref, tol):
+    torch.testing.assert_close(got.float(), ref, atol=tol * ref.abs().max().item() + 1e-6, rtol=tol)
+
+
+@pytest.mark.parametrize("geom", GEOMS)
+def test_stem_forward_and_stats(geom):
+    n, h, w, cout, s = geom
+    g = torch.Generator().manual_seed(0)
+    x = _t((n, 3, h, w), g).contiguous(memory_format=torch.channels_last)
+    wt = _t((cout, 3, 3, 3), g, 0.2)
+    wk = wt.permute(0, 2, 3, 1).contiguous()
+    y, part = torch.ops.rtseg.conv_stem(x, wk, [s, s], [1, 1], [1, 1], True)
+    ref = F.conv2d(x.float(), wt.float(), None, s, 1)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    _close(y, ref, 1e-2)
+    rf = ref.double()  # statistics of the fp32 accumulators
+    torch.testing.assert_close(part[:, :cout].double().sum(0), rf.sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(part[:, cout:].double().sum(0), rf.square().sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+    y1, p1 = torch.ops.rtseg.conv_stem(x, wk, [s, s], [1, 1], [1, 1], True)
+    assert torch.equal(y1, y) and torch.equal(p1, part)
+    y2, p2 = torch.ops.rtseg.conv_stem(x, wk, [s, s], [1, 1], [1, 1], False)
+    assert torch.equal(y2, y) and (p2 is None or p2.numel() == 0)
+
+
+@pytest.mark.parametrize("geom", GEOMS)
+@pytest.mark.parametrize("channels_last", [False, True])
+def test_stem_wgrad(geom, channels_last):
+    n, h, w, cout, s = geom
+    g = torch.Generator().manual_seed(3)
+    cl = dict(memory_format=torch.channels_last)
+    x = _t((n, 3, h, w), g).contiguous(**cl)
+    ho, wo = (h - 1) // s + 1, (w - 1) // s + 1
+    dy = _t((n, cout, ho, wo), g).contiguous(**cl)
+    dw = torch.ops.rtseg.conv_stem_wgrad(x, dy, 3, 3, [s, s], [1, 1], [1, 1], channels_last)
+    ref = torch.nn.grad.conv2d_weight(x.float(), (cout, 3, 3, 3), dy.float(), s, 1, 1)
+    assert dw.shape == ref.shape and dw.dtype == torch.float32
+    assert dw.is_contiguous(memory_format=torch.channels_last) == channels_last
+    _close(dw, ref, 1e-3)
+    assert torch.equal(torch.ops.rtseg.conv_stem_wgrad(x, dy, 3, 3, [s, s], [1, 1], [1, 1], channels_last), dw)
+
+
+def test_stem_rejects_other_shapes():
+    g = torch.Generator().manual_seed(1)
+    x = _t((1, 3, 8, 33), g).contiguous(memory_format=torch.channels_last)  # odd width
+    with pytest.raises(RuntimeError, match="conv_stem"):
+        torch.ops.rtseg.conv_stem(x, _t((64, 3, 3, 3), g), [2, 2], [1, 1], [1, 1], False)
+    x = _t((1, 3, 8, 32), g).contiguous(memory_format=torch.channels_last)
+    with pytest.raises(RuntimeError, match="conv_stem"):  # Cout not a multiple of 16
+        torch.ops.rtseg.conv_stem(x, _t((24, 3, 3, 3), g), [2, 2], [1, 1], [1, 1], False)
+
+
+def test_stem_routed_training_step(monkeypatch):
+    """DDRNet's conv1 (ConvBNAct 3 -> 64, stride 2) with conv_stem forced vs MIOpen: outputs, BN
+    statistics and weight gradients agree up to bf16 rounding, and the routing called the kernels."""
+    from realtime_semantic_segmentation_pytorch_amd.models.modules import ConvBNAct
+    from realtime_semantic_segmentation_pytorch_amd.ops import conv as conv_mod
+
+    torch.manual_seed(0)
+    net = ops.convert_batchnorm(ConvBNAct(3, 64, 3, 2)).to(DEV).to(memory_format=torch.channels_last).train()
+    x = torch.randn(2, 3, 48, 132, device=DEV).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(2, 64, 24, 66, device=DEV)
+    calls = []
+
+    class _Spy:
+        def __getattr__(self, name):
+            calls[-1].add(name)
+            return getattr(torch.ops.rtseg, name)
+
+    monkeypatch.setattr(conv_mod, "ops", lambda: spy)
+    spy = _Spy()
+    res = []
+    for mode in ("1", "0"):
+        monkeypatch.setenv("RTSEG_CONV_STEM", mode)
+        if mode == "1":  # the first candidate, no timing
+            monkeypatch.setenv("RTSEG_CONV_MFMA", "1")
+        else:
+            monkeypatch.delenv("RTSEG_CONV_MFMA", raising=False)
+        calls.append(set())
+        net.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = net(x)
+        (y.float() * gy).sum().backward()
+        res.append((y.float().detach(), {n: p.grad.float().clone() for n, p in net.named_parameters()}))
+    (y0, gp0), (y1, gp1) = res
+
+    def rel(a, b):
+        return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+    assert rel(y0, y1) < 1e-2
+    for n, g in gp1.items():
+        assert rel(gp0[n], g) < 2e-2, n
+    assert {"conv_stem", "conv_stem_wgrad"} <= calls[0], calls[0]
+    assert not {"conv_stem", "conv_stem_wgrad"} & calls[1], calls[1]
+
+
+@pytest.mark.parametrize("block", ["RB", "RBB"])
+def test_twin_conv_downsample_block(monkeypatch, block):
+    """A downsampling DDRNet block with conv1 + projection shortcut in one autograd node
+    (ops.twin_conv_bn_stats) vs the two separate conv nodes: identical forward, input and
+    parameter gradients up to bf16 rounding; the twin path leaves no accumulation add."""
+    from realtime_semantic_segmentation_pytorch_amd.models import ddrnet
+
+    torch.manual_seed(0)
+    cls = getattr(ddrnet, block)
+    net = ops.convert_batchnorm(cls(64, 128, 2)).to(DEV).to(memory_format=torch.channels_last).train()
+    x0 = torch.randn(2, 64, 32, 96, device=DEV).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(2, 128, 16, 48, device=DEV)
+    res = []
+    for twin in ("1", "0"):
+        monkeypatch.setenv("RTSEG_TWIN_CONV", twin)
+        net.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = net(x)
+        (y.float() * gy).sum().backward()
+        res.append((y.float().detach(), x.grad.float().clone(),
+                    {n: p.grad.float().clone() for n, p in net.named_parameters()}))
+    (y0, gx0, gp0), (y1, gx1, gp1) = res
+
+    def rel(a, b):
+        return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+    assert rel(y0, y1) < 1e-2
+    assert rel(gx0, gx1) < 2e-2
+    for n, g in gp1.items():
+        assert rel(gp0[n], g) < 3e-2, n
+
+
+def test_twin_conv_node_in_graph():
+    """The twin node really is on the training path of a downsampling RB."""
+    from realtime_semantic_segmentation_pytorch_amd.models.ddrnet import RB
+
+    net = ops.convert_batchnorm(RB(64, 128, 2)).to(DEV).to(memory_format=torch.channels_last).train()
+    x = torch.randn(1, 64, 16, 64, device=DEV).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = net(x)
+    seen, stack, names = set(), [y.grad_fn], set()
+    while stack:
+        fn = stack.pop()
+        if fn is None or id(fn) in seen:
+            continue
+        seen.add(id(fn))
+        names.add(type(fn).__name__)
+        stack.extend(f for f, _ in fn.next_functions)
+    assert any("TwinConvFn" in n for n in names), names
