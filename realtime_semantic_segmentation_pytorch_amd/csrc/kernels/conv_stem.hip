@@ -65,20 +65,26 @@ struct StemTile {
 };
 
 template <int S, int TH>
-__device__ __forceinline__ void stage_input(const StemArgs& a, uint32_t* l32, int n, int oy0, int ox0, int tid,
-                                            int nthr) {
+__device__ __forceinline__ void stage_input(const StemArgs& a, uint32_t* l32, int n, int oy0, int ox0, int tid) {
   using T = StemTile<S, TH>;
+  constexpr int kTotal = T::R * T::DW, kPer = (kTotal + 255) / 256;
   const int iw0 = ox0 * S - 2;
   const uint32_t* x32 = reinterpret_cast<const uint32_t*>(a.x);
-  for (int d = tid; d < T::R * T::DW; d += nthr) {
+  // all of this thread's loads in flight at once (compile-time count), then the LDS stores
+  uint32_t v[kPer];
+#pragma unroll
+  for (int e = 0; e < kPer; ++e) {
+    const int d = tid + 256 * e;
     const int r = d / T::DW, dd = d - r * T::DW;
     const int ih = oy0 * S - 1 + r;
     const int iwp = iw0 + 2 * (dd / 3);
-    uint32_t v = 0;
-    if (static_cast<unsigned>(ih) < static_cast<unsigned>(a.H) && iwp >= 0 && iwp < a.W)
-      v = x32[((static_cast<int64_t>(n) * a.H + ih) * a.W + iw0) * 3 / 2 + dd];
-    l32[d] = v;
+    v[e] = 0;
+    if (d < kTotal && static_cast<unsigned>(ih) < static_cast<unsigned>(a.H) && iwp >= 0 && iwp < a.W)
+      v[e] = x32[((static_cast<int64_t>(n) * a.H + ih) * a.W + iw0) * 3 / 2 + dd];
   }
+#pragma unroll
+  for (int e = 0; e < kPer; ++e)
+    if (tid + 256 * e < kTotal) l32[tid + 256 * e] = v[e];
 }
 
 template <int S, int NT, int STATS>
@@ -118,7 +124,7 @@ __global__ void __launch_bounds__(256) stem_fwd_kernel(const StemArgs a) {
     const int tx = mt % a.tilesW, t2 = mt / a.tilesW;
     const int n = t2 / a.tilesH, oy0 = (t2 % a.tilesH) * TH, ox0 = tx * kTW;
     __syncthreads();  // the previous tile's fragment reads are done
-    stage_input<S, TH>(a, l32, n, oy0, ox0, tid, 256);
+    stage_input<S, TH>(a, l32, n, oy0, ox0, tid);
     __syncthreads();
 #pragma unroll 2
     for (int g = 0; g < 8; ++g) {
@@ -209,17 +215,27 @@ __global__ void __launch_bounds__(256) stem_wgrad_kernel(const StemArgs a) {
     const int tx = mt % a.tilesW, t2 = mt / a.tilesW;
     const int n = t2 / a.tilesH, oy0 = (t2 % a.tilesH) * TH, ox0 = tx * kTW;
     __syncthreads();
-    stage_input<S, TH>(a, l32, n, oy0, ox0, tid, 256);
-    // dy tile [TH * 64 pixels][C] (pixels past the image read as zeros)
+    stage_input<S, TH>(a, l32, n, oy0, ox0, tid);
+    // dy tile [TH * 64 pixels][C] (pixels past the image read as zeros), loads all in flight
     constexpr int V = C / 8;  // 16-byte vectors per pixel
-    for (int e = tid; e < TH * kTW * V; e += 256) {
+    constexpr int kPer = TH * kTW * V / 256;
+    static_assert(kPer * 256 == TH * kTW * V, "dy staging");
+    uint4 q[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = tid + 256 * i;
       const int p = e / V, v = e - p * V;
       const int oy = oy0 + p / kTW, ox = ox0 + (p % kTW);
-      uint4 q = {0u, 0u, 0u, 0u};
+      q[i] = uint4{0u, 0u, 0u, 0u};
       if (oy < a.Ho && ox < a.Wo)
-        q = *reinterpret_cast<const uint4*>(a.dy + ((static_cast<int64_t>(n) * a.Ho + oy) * a.Wo + ox) * C + 8 * v);
+        q[i] = *reinterpret_cast<const uint4*>(a.dy + ((static_cast<int64_t>(n) * a.Ho + oy) * a.Wo + ox) * C + 8 * v);
+    }
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = tid + 256 * i;
+      const int p = e / V, v = e - p * V;
       uint32_t* d = reinterpret_cast<uint32_t*>(dyl + p * CP + 8 * v);
-      d[0] = q.x; d[1] = q.y; d[2] = q.z; d[3] = q.w;
+      d[0] = q[i].x; d[1] = q[i].y; d[2] = q[i].z; d[3] = q[i].w;
     }
     __syncthreads();
 #pragma unroll
