@@ -154,10 +154,11 @@ def test_twin_conv_downsample_block(monkeypatch, block):
         assert rel(gp0[n], g) < 3e-2, n
 
 
-def test_twin_conv_node_in_graph():
+def test_twin_conv_node_in_graph(monkeypatch):
     """The twin node really is on the training path of a downsampling RB."""
     from realtime_semantic_segmentation_pytorch_amd.models.ddrnet import RB
 
+    monkeypatch.setenv("RTSEG_TWIN_CONV", "1")
     net = ops.convert_batchnorm(RB(64, 128, 2)).to(DEV).to(memory_format=torch.channels_last).train()
     x = torch.randn(1, 64, 16, 64, device=DEV).contiguous(memory_format=torch.channels_last).requires_grad_(True)
     with torch.autocast("cuda", dtype=torch.bfloat16):
