@@ -165,9 +165,10 @@ def whalo_ok(conv, cin: int, cout: int, npix: int) -> bool:
             and _fits32(npix, max(cin, cout)))
 
 
-# new kernel paths stay opt-in until their GPU tests have passed on this tree
-_STEM_DEFAULT = "0"
-_TWIN_DEFAULT = "0"
+# RTSEG_CONV_STEM=0 / RTSEG_TWIN_CONV=0: A/B switches (bench 486.8 -> 490.9 images/s with both on,
+# profiles/r4_stem)
+_STEM_DEFAULT = "auto"
+_TWIN_DEFAULT = "1"
 
 
 def stem_ok(conv, x: torch.Tensor) -> bool:
