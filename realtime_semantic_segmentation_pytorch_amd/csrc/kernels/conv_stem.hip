@@ -99,15 +99,18 @@ __global__ void __launch_bounds__(256) stem_fwd_kernel(const StemArgs a) {
   const int G = gridDim.x;
   const int lb = xcd_logical(blockIdx.x, G);
 
-  // A fragments: weights [cout 16t + px][k 8h + j]
+  // A fragments: weights [row m = px][k 8h + j]; row m of tile t is output channel
+  // cout_of(t, m) = 4 NT (m >> 2) + 4 t + (m & 3), so the C rows 4h .. 4h + 3 of the NT tiles are
+  // the 4 NT CONSECUTIVE channels 4 NT h .. of one pixel in a lane: 16-byte stores
   bf16x8_t wf[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     s16x8_t v;
+    const int co = 4 * NT * (px >> 2) + 4 * t + (px & 3);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int k = 8 * h + j;
-      v[j] = k < 27 ? static_cast<short>(a.w[(16 * t + px) * 27 + k]) : short(0);
+      v[j] = k < 27 ? static_cast<short>(a.w[co * 27 + k]) : short(0);
     }
     wf[t] = __builtin_bit_cast(bf16x8_t, v);
   }
@@ -136,15 +139,15 @@ __global__ void __launch_bounds__(256) stem_fwd_kernel(const StemArgs a) {
       const bf16x8_t bf = __builtin_bit_cast(bf16x8_t, b);
       const int oy = oy0 + oyl, ox = ox0 + oxl;
       const bool ok = oy < a.Ho && ox < a.Wo;
-      uint16_t* yp = a.y + ((static_cast<int64_t>(n) * a.Ho + (ok ? oy : 0)) * a.Wo + (ok ? ox : 0)) * a.cout + 4 * h;
+      uint16_t* yp =
+          a.y + ((static_cast<int64_t>(n) * a.Ho + (ok ? oy : 0)) * a.Wo + (ok ? ox : 0)) * a.cout + 4 * NT * h;
+      uint32_t pk[2 * NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         f32x4_t c = {0.f, 0.f, 0.f, 0.f};
         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t], bf, c, 0, 0, 0);
-        uint2 pk;
-        pk.x = pack2(c[0], c[1]);
-        pk.y = pack2(c[2], c[3]);
-        if (ok) *reinterpret_cast<uint2*>(yp + 16 * t) = pk;
+        pk[2 * t] = pack2(c[0], c[1]);
+        pk[2 * t + 1] = pack2(c[2], c[3]);
         if constexpr (STATS) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -152,6 +155,16 @@ __global__ void __launch_bounds__(256) stem_fwd_kernel(const StemArgs a) {
             ts[t][r] += u;
             tq[t][r] = fmaf(u, u, tq[t][r]);
           }
+        }
+      }
+      if (ok) {
+        if constexpr (NT % 2 == 0) {
+#pragma unroll
+          for (int v = 0; v < NT / 2; ++v)
+            reinterpret_cast<uint4*>(yp)[v] = uint4{pk[4 * v], pk[4 * v + 1], pk[4 * v + 2], pk[4 * v + 3]};
+        } else {
+#pragma unroll
+          for (int v = 0; v < NT; ++v) reinterpret_cast<uint2*>(yp)[v] = uint2{pk[2 * v], pk[2 * v + 1]};
         }
       }
     }
@@ -169,8 +182,8 @@ __global__ void __launch_bounds__(256) stem_fwd_kernel(const StemArgs a) {
         s += dpp_f<0x122, 0xF>(s); q += dpp_f<0x122, 0xF>(q);
         s += dpp_f<0x121, 0xF>(s); q += dpp_f<0x121, 0xF>(q);
         if (px == 0) {
-          red[wid][0][16 * t + 4 * h + r] = s;
-          red[wid][1][16 * t + 4 * h + r] = q;
+          red[wid][0][4 * NT * h + 4 * t + r] = s;
+          red[wid][1][4 * NT * h + 4 * t + r] = q;
         }
       }
     __syncthreads();

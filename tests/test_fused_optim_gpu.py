@@ -156,7 +156,13 @@ def test_ema_validation_sees_new_weights_after_training(tmp_path):
     second = infer(tr.ema_model.ema)
     fresh = infer(copy.deepcopy(tr.ema_model.ema))
     assert not torch.equal(first, second), "EMA model output did not change after training"
-    torch.testing.assert_close(second, fresh, rtol=0, atol=0)
+    # a stale cache would serve the weights of `first`: second must sit at bf16-rounding distance
+    # from the fresh copy, far closer than first does.  Not bitwise: cached-weight inference and
+    # a deep copy differ by bf16 rounding even with every cache invalidated (max |diff| ~1e-3,
+    # tools/probe_ema_determinism.py; the round-4 suite hit 1.5e-3 on half the elements)
+    d_new, d_old = (second - fresh).norm().item(), (first - fresh).norm().item()
+    assert d_new <= 0.25 * d_old, (d_new, d_old)
+    torch.testing.assert_close(second, fresh, rtol=0, atol=4e-3 * fresh.abs().max().item())
 
 
 def _shadow_run(shadow_on, monkeypatch, steps=3):
