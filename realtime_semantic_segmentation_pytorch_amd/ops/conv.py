@@ -500,14 +500,18 @@ class _TwinConvFn(torch.autograd.Function):
         x, wk1, wk2 = ctx.saved_tensors
         want_dx = ctx.needs_input_grad[0]
         dx = ctx.addend_slot.pop() if ctx.addend_slot else None
-        dws = []
-        for i, (dy, wk) in enumerate(((dy1, wk1), (dy2, wk2))):
+        dws = [None, None]
+        pairs = ((dy1, wk1), (dy2, wk2))
+        # the larger-kernel conv last: its data gradient runs on our kernels (whose epilogue adds
+        # the other's dx), while a strided 1 x 1 shortcut's often autotunes to MIOpen, where the
+        # addend would cost a separate add (profiles/r4_stem)
+        order = sorted((0, 1), key=lambda i: ctx.convs[i].kernel_size[0] * ctx.convs[i].kernel_size[1])
+        for i in order:
+            dy, wk = pairs[i]
             if dy is None:
-                dws.append(None)
                 continue
-            dx, dw = _conv_bwd(x, wk, ctx.convs[i], ctx.keys[i], dy, want_dx, ctx.needs_input_grad[1 + i],
-                               ctx.wdtypes[i], dx)
-            dws.append(dw)
+            dx, dws[i] = _conv_bwd(x, wk, ctx.convs[i], ctx.keys[i], dy, want_dx, ctx.needs_input_grad[1 + i],
+                                   ctx.wdtypes[i], dx)
         return dx if want_dx else None, dws[0], dws[1], None, None
 
 
