@@ -104,6 +104,14 @@ static void ema_lerp(const at::Tensor& meta, int64_t ntensor, int64_t nblocks, d
                   static_cast<float>(w), cur_stream());
 }
 
+static void shadow_crsk(const at::Tensor& tiles, int64_t ntiles) {
+  TORCH_CHECK(tiles.is_cuda() && tiles.scalar_type() == at::kLong && tiles.is_contiguous() &&
+                  tiles.numel() == 6 * ntiles,
+              "rtseg.shadow_crsk: malformed tile table");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(tiles.device());
+  launch_shadow_crsk(tiles.data_ptr<int64_t>(), static_cast<int>(ntiles), cur_stream());
+}
+
 // ---- STDC detail loss (detail_loss.hip) ------------------------------------------
 static void check_detail(const at::Tensor& d) {
   TORCH_CHECK(d.is_cuda() && d.dim() == 4 && d.size(1) == 1, "rtseg.detail_loss: logits must be [N, 1, h, w] on GPU");
@@ -206,6 +214,7 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
         "float dampening, float weight_decay, bool nesterov, float beta1, float beta2, float eps, "
         "float step_size, float inv_sqrt_bc2, float grad_scale, float ema_w) -> ()");
   m.def("ema_lerp(Tensor meta, int ntensor, int nblocks, float w) -> ()");
+  m.def("shadow_crsk(Tensor tiles, int ntiles) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
@@ -217,6 +226,7 @@ TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
   m.impl("confmat", &rtseg::confmat);
   m.impl("fused_opt_step", &rtseg::fused_opt_step);
   m.impl("ema_lerp", &rtseg::ema_lerp);
+  m.impl("shadow_crsk", &rtseg::shadow_crsk);
 }
 
 // ------------------------------ depth-wise conv (dwconv.hip) -------------------------

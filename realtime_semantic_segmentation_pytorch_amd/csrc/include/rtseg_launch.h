@@ -124,6 +124,8 @@ struct OptHyper {
 };
 void launch_fused_opt(const int64_t* meta, int ntensor, int nblocks, const OptHyper& hp, hipStream_t st);
 void launch_ema_lerp(const int64_t* meta, int ntensor, int nblocks, float w, hipStream_t st);
+// crsk[ci][rq][co] = krsc[co][rq][ci] for a table of 64 x 64 tiles (6 int64 each, optim.hip)
+void launch_shadow_crsk(const int64_t* tiles, int ntiles, hipStream_t st);
 
 // ---- dwconv.hip -------------------------------------------------------------
 // Depth-wise conv geometry; activations channels-last, weights tap-major fp32 [KH*KW][Cout].

@@ -149,7 +149,39 @@ __global__ void __launch_bounds__(kOptBlock) ema_lerp_kernel(const int64_t* meta
   }
 }
 
+// Data-gradient weight shadows: crsk[ci][rq][co] = krsc[co][rq][ci] (bf16), one 64 x 64 (co, ci)
+// tile of one tap per block through LDS, after the fused step wrote krsc.  Written from the
+// step itself these were 2-byte stores scattered cout elements apart (0.77 ms of a 0.91 ms step
+// on DDRNet-23, profiles/r4_stem); here both sides move whole 128-byte rows.
+// tiles: [ntiles][6] = krsc, crsk, cout | cin << 32, taps | tap << 32, co0 | ci0 << 32, 0
+__global__ void __launch_bounds__(256) shadow_crsk_kernel(const int64_t* __restrict__ tiles) {
+  __shared__ uint16_t t[64][65];
+  const int64_t* d = tiles + static_cast<int64_t>(blockIdx.x) * 6;
+  const uint16_t* krsc = reinterpret_cast<const uint16_t*>(d[0]);
+  uint16_t* crsk = reinterpret_cast<uint16_t*>(d[1]);
+  const int cout = static_cast<int>(d[2] & 0xffffffff), cin = static_cast<int>(d[2] >> 32);
+  const int rqn = static_cast<int>(d[3] & 0xffffffff), rq = static_cast<int>(d[3] >> 32);
+  const int co0 = static_cast<int>(d[4] & 0xffffffff), ci0 = static_cast<int>(d[4] >> 32);
+  const int lx = threadIdx.x & 63, ly = threadIdx.x >> 6;
+#pragma unroll 4
+  for (int r = ly; r < 64; r += 4) {  // row r = output channel co0 + r, lanes along ci
+    const int co = co0 + r, ci = ci0 + lx;
+    if (co < cout && ci < cin) t[r][lx] = krsc[(static_cast<int64_t>(co) * rqn + rq) * cin + ci];
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int r = ly; r < 64; r += 4) {  // row r = input channel ci0 + r, lanes along co
+    const int ci = ci0 + r, co = co0 + lx;
+    if (co < cout && ci < cin) crsk[(static_cast<int64_t>(ci) * rqn + rq) * cout + co] = t[lx][r];
+  }
+}
+
 }  // namespace
+
+void launch_shadow_crsk(const int64_t* tiles, int ntiles, hipStream_t st) {
+  if (ntiles <= 0) return;
+  shadow_crsk_kernel<<<ntiles, 256, 0, st>>>(tiles);
+}
 
 void launch_fused_opt(const int64_t* meta, int ntensor, int nblocks, const OptHyper& hp, hipStream_t st) {
   if (nblocks <= 0) return;

@@ -14,6 +14,7 @@ updated separately by ``ModelEmaV2``).
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 from torch.optim import SGD, Adam, AdamW
@@ -33,7 +34,33 @@ def _shadow_fields(p, sh):
     krsc, crsk = sh
     cout, cin, kh, kw = p.shape
     cl = p.dim() == 4 and not p.is_contiguous() and p.is_contiguous(memory_format=torch.channels_last)
-    return [krsc.data_ptr(), crsk.data_ptr() if crsk is not None else 0, cout, cin, kh * 256 + kw, 1 if cl else 0]
+    # the data-gradient layout is written after the step by shadow_crsk_tiles' transpose kernel
+    crsk_ptr = crsk.data_ptr() if crsk is not None and not _CRSK_TILED else 0
+    return [krsc.data_ptr(), crsk_ptr, cout, cin, kh * 256 + kw, 1 if cl else 0]
+
+
+# RTSEG_CRSK_TILED=0: the fused step writes the CRSK shadow itself (2-byte stores cout apart; A/B)
+_CRSK_TILED = os.environ.get("RTSEG_CRSK_TILED", "1") != "0"
+
+
+def shadow_crsk_tiles(shadows, device):
+    """Tile table of ``rtseg.shadow_crsk``: one row per (tap, 64 output x 64 input channels) tile
+    of every shadow pair's CRSK layout -> (table, ntiles)."""
+    rows = []
+    for p, sh in shadows.items():
+        if sh is None or sh[1] is None:
+            continue
+        krsc, crsk = sh
+        cout, cin, kh, kw = p.shape
+        for rq in range(kh * kw):
+            for co0 in range(0, cout, 64):
+                for ci0 in range(0, cin, 64):
+                    rows += [krsc.data_ptr(), crsk.data_ptr(), cout | (cin << 32), (kh * kw) | (rq << 32),
+                             co0 | (ci0 << 32), 0]
+    t = torch.tensor(rows, dtype=torch.int64)
+    if device.type == "cuda":
+        t = t.pin_memory().to(device, non_blocking=True)
+    return t, len(rows) // 6
 
 
 def build_table(rows, device):
@@ -115,6 +142,19 @@ class _FusedMixin:
         ps = [p for p in group["params"] if p.grad is not None]
         return bool(ps) and all(_dense_ok(p) for p in ps) and use_hip(ps[0])
 
+    def _crsk(self, shadows):
+        """CRSK shadows of this step's weights (after the step wrote their KRSC shadows)."""
+        if not _CRSK_TILED or not shadows:
+            return
+        key = tuple((sh[0].data_ptr(), sh[1].data_ptr()) for sh in shadows.values() if sh is not None and sh[1] is not None)
+        if not key:
+            return
+        if self._tables.get("crsk", (None,))[0] != key:
+            dev = next(iter(shadows.values()))[0].device
+            self._tables["crsk"] = (key, shadow_crsk_tiles(shadows, dev))
+        table, n = self._tables["crsk"][1]
+        ops().shadow_crsk(table, n)
+
     def _launch(self, slot, rows, hp):
         """One fused launch over ``rows``.  The device pointer table is cached per ``slot`` (a
         stable id: the param-group index and bucket ordinal, never a per-step value) and rebuilt
@@ -174,6 +214,7 @@ class FusedSGD(_FusedMixin, SGD):
             hp = (lr, mom, float(group["dampening"]), float(group["weight_decay"]), bool(group["nesterov"]),
                   0.0, 0.0, 0.0, 0.0, 0.0, 1.0, float(ema_w) if ema_w is not None else 0.0)
             self._launch(gi, rows, hp)
+        self._crsk(shadows)
         shadows_written(shadows)
         self.last_step_fused = ema_w is not None and bool(self._ema_of)
         self.fused_steps += 1
@@ -218,6 +259,7 @@ class _FusedAdamBase(_FusedMixin):
                 hp = (lr, 0.0, 0.0, float(group["weight_decay"]), False, beta1, beta2, float(group["eps"]),
                       lr / bc1, 1.0 / math.sqrt(bc2), 1.0, float(ema_w) if ema_w is not None else 0.0)
                 self._launch((gi, bi), rows, hp)
+        self._crsk(shadows)
         shadows_written(shadows)
         self.last_step_fused = ema_w is not None and bool(self._ema_of)
         self.fused_steps += 1
