@@ -2,7 +2,9 @@
 forward (+ BN-statistics slab) and weight gradient of 3x3 / pad-1 convs with Cin = 3, stride 1
 and 2, Cout 16 / 32 / 48 / 64 -- partial tiles (Ho % 8, Wo % 64), fewer tiles than blocks and
 many tiles per block, both parameter layouts; deterministic.  Reference layer: DDRNet's conv1
-(reference models/ddrnet.py:27-29), the stems of the STDC / BiSeNet / ResNet families."""
+(reference models/ddrnet.py:27-29), the stems of the STDC / BiSeNet / ResNet families.
+Also the twin conv node of downsampling residual blocks (ops/conv.py _TwinConvFn, reference
+models/ddrnet.py:168-219) against the two separate conv nodes."""
 import pytest
 import torch
 import torch.nn.functional as F
