@@ -56,9 +56,27 @@ def parse():
     p.add_argument("--no-fused-loss", action="store_true")
     p.add_argument("--nchw", action="store_true")
     p.add_argument("--profile-steps", type=int, default=0)
-    p.add_argument("--no-cudnn-benchmark", action="store_true",
-                   help="use MIOpen immediate-mode heuristics instead of find")
+    p.add_argument("--cudnn-benchmark", choices=("auto", "on", "off"), default="auto",
+                   help="MIOpen find mode for the convs left on MIOpen.  auto: on only at a recorded "
+                        "config (FIND_RECORDED: the in-tree miopen_db/ holds its find results), so a new "
+                        "batch / resolution never starts MIOpen's exhaustive solver search")
+    p.add_argument("--no-cudnn-benchmark", action="store_true", help="same as --cudnn-benchmark off")
     return p.parse_args()
+
+
+# (model, arch, batch, height, width) whose MIOpen find results are in miopen_db/ (the headline
+# config and the BASELINE configs 3-4 at their bench batches)
+FIND_RECORDED = {("ddrnet", "DDRNet-23", 32, 1024, 2048), ("bisenetv2", None, 16, 1024, 2048),
+                 ("stdc", "stdc2", 16, 1024, 2048)}
+
+
+def find_mode(a) -> bool:
+    if a.no_cudnn_benchmark or a.cudnn_benchmark == "off":
+        return False
+    if a.cudnn_benchmark == "on":
+        return True
+    arch = a.arch if a.model in ("ddrnet", "stdc", "ppliteseg") else None
+    return (a.model, arch, a.batch, a.height, a.width) in FIND_RECORDED
 
 
 def make_config(a, world):
@@ -160,7 +178,7 @@ def main():
     from realtime_semantic_segmentation_pytorch_amd.parallel import barrier, de_parallel
 
     cfg = make_config(a, world)
-    cfg.cudnn_benchmark = not a.no_cudnn_benchmark
+    cfg.cudnn_benchmark = find_mode(a)
     configure_backend(cfg.cudnn_benchmark, model=cfg.model, exclude_naive=True)
     ops.load()
     trainer = SegTrainer(cfg)
@@ -175,6 +193,7 @@ def main():
         imgs, masks = data.next()
         return trainer.train_step(imgs, masks)
 
+    t_warm = time.perf_counter()
     for i in range(a.warmup):
         t_w = time.perf_counter()
         step()
@@ -190,6 +209,7 @@ def main():
         torch.cuda.synchronize()
 
     sync_all()
+    warmup_s = time.perf_counter() - t_warm
     t0 = time.perf_counter()
     for _ in range(a.steps):
         loss, _ = step()
@@ -217,7 +237,8 @@ def main():
     extra = {"loss_last": loss_val, "per_gpu_batch": a.batch,
              "peak_mem_gb": torch.cuda.max_memory_allocated(dev) / 2 ** 30,
              "hip_ext_loaded": bool(ops.load()), "channels_last": cfg.channels_last,
-             "fused_loss": cfg.fused_loss,
+             "fused_loss": cfg.fused_loss, "miopen_find_mode": bool(cfg.cudnn_benchmark),
+             "warmup_s": round(warmup_s, 1),
              # the optimizer step (+ parameter EMA) ran as the single fused HIP launch
              "fused_optimizer_step": bool(getattr(trainer.optimizer, "last_step_fused", False))}
     from realtime_semantic_segmentation_pytorch_amd.ops.conv import decisions

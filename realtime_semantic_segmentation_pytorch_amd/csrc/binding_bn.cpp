@@ -70,7 +70,7 @@ at::Tensor stats_slab(const at::Tensor& x, int& G) {
   const int C = static_cast<int>(x.size(1));
   const int64_t M = rows_of(x);
   G = bn_partial_grid(M, C, dtype_code(x));
-  at::Tensor part = at::empty({G, 2 * C}, x.options().dtype(at::kFloat));
+  at::Tensor part = at::empty({G + 1, 2 * C}, x.options().dtype(at::kFloat));  // row G: pivots
   launch_bn_stats(x.data_ptr(), dtype_code(x), M, C, part.data_ptr<float>(), G, cur_stream());
   return part;
 }
@@ -92,7 +92,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_stats_finalize(
                               fptr(w), fptr(b), fptr_mut(rmean), fptr_mut(rvar), nbt_ptr(nbt),
                               static_cast<float>(momentum), static_cast<float>(eps),
                               mi.data_ptr<float>(), ss.data_ptr<float>(), sums.data_ptr<double>(),
-                              cur_stream());
+                              cur_stream(), part.data_ptr<float>() + static_cast<int64_t>(G) * 2 * C);
   return {mi, ss, sums};
 }
 
@@ -105,7 +105,8 @@ at::Tensor bn_stats_sums(const at::Tensor& x) {
   at::Tensor part = stats_slab(x, G);
   at::Tensor sums = at::empty({2 * C + 1}, x.options().dtype(at::kDouble));
   launch_bn_slab_to_sums(part.data_ptr<float>(), G, C, static_cast<double>(rows_of(x)),
-                         sums.data_ptr<double>(), cur_stream());
+                         sums.data_ptr<double>(), cur_stream(),
+                         part.data_ptr<float>() + static_cast<int64_t>(G) * 2 * C);
   return sums;
 }
 

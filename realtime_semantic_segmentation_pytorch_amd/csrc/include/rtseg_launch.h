@@ -58,6 +58,9 @@ void launch_seg_loss_bwd(const SegLossArgs& a, const float* grad_out, const Tens
 // ---- bn_act.hip --------------------------------------------------------------
 // x is [M, C] row-major (channels-last). Partial slabs are [G, 2C] fp32
 // (G = bn_partial_grid); sums are [2C+1] fp64 (sum, second moment, count).
+// launch_bn_stats writes a [G + 1, 2C] slab of moments shifted by a per-channel pivot
+// (row G, first C floats); the reducers take that row as ``pivot`` (nullptr: raw moments,
+// e.g. a conv-epilogue slab).
 int bn_partial_grid(int64_t M, int C, int dtype);
 // Channel-vector width used for (dtype, C); 0 = layer not supported by the fused kernels.
 int bn_vec_width(int dtype, int C);
@@ -65,9 +68,9 @@ void launch_bn_stats(const void* x, int dtype, int64_t M, int C, float* part, in
 void launch_bn_finalize_partials(const float* part, int G, int C, double count, const float* w,
                                  const float* b, float* rmean, float* rvar, int64_t* nbt,
                                  float momentum, float eps, float* mean_invstd, float* scale_shift,
-                                 double* sums_out, hipStream_t st);
+                                 double* sums_out, hipStream_t st, const float* pivot = nullptr);
 void launch_bn_slab_to_sums(const float* part, int G, int C, double count, double* sums,
-                            hipStream_t st);
+                            hipStream_t st, const float* pivot = nullptr);
 void launch_bn_finalize(const double* sums, int C, const float* w, const float* b, float* rmean,
                         float* rvar, int64_t* nbt, float momentum, float eps, float* mean_invstd,
                         float* scale_shift, hipStream_t st);

@@ -119,15 +119,27 @@ __device__ __forceinline__ void block_partials_out(const float* s, const float* 
 }
 
 // --------------------------------------------------------------- stats ------
+// Shifted one-pass moments: every partial accumulates d = x - p and d*d about a per-channel
+// pivot p = x[row 0, c] (the finalize adds the shift back in fp64, ``unshift``).  Plain
+// sum / sum-of-squares partials lose var = E[x^2] - mean^2 to cancellation when |mean| >> std --
+// BatchNorms over a few pooled values per channel (DDRNet's DAPPM global branch, BiSeNetV2's
+// context block: 2 values at batch 2) had relative variance errors of 1e-3 and more.  The pivot
+// row is stored after the G slab rows (slab [G + 1, 2C], row G = pivots) by block 0.
 template <typename T, int V>
 __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, int64_t M, int C,
                                                        float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const RowGeo g(C, V);
-  float s[V], q[V];
+  float s[V], q[V], pv[V];
 #pragma unroll
   for (int j = 0; j < V; ++j) { s[j] = 0.f; q[j] = 0.f; }
   if (g.my_r < g.rpi) {
+    VecIO<T, V>::load(x + g.my_cv * V, pv);
+    if (blockIdx.x == 0 && g.my_r == 0) {
+      float* prow = part + static_cast<int64_t>(gridDim.x) * 2 * C + g.my_cv * V;
+#pragma unroll
+      for (int j = 0; j < V; ++j) prow[j] = pv[j];
+    }
     int64_t r0, r1;
     block_rows(M, g.rpi, r0, r1);
     const T* base = x + g.my_cv * V;
@@ -140,15 +152,20 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, 
       VecIO<T, V>::load(p + 2 * step, f2); VecIO<T, V>::load(p + 3 * step, f3);
 #pragma unroll
       for (int j = 0; j < V; ++j) {
-        s[j] += (f0[j] + f1[j]) + (f2[j] + f3[j]);
-        q[j] += (f0[j] * f0[j] + f1[j] * f1[j]) + (f2[j] * f2[j] + f3[j] * f3[j]);
+        const float d0 = f0[j] - pv[j], d1 = f1[j] - pv[j], d2 = f2[j] - pv[j], d3 = f3[j] - pv[j];
+        s[j] += (d0 + d1) + (d2 + d3);
+        q[j] += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
       }
     }
     for (; r < r1; r += g.rpi) {
       float f[V];
       VecIO<T, V>::load(base + r * C, f);
 #pragma unroll
-      for (int j = 0; j < V; ++j) { s[j] += f[j]; q[j] += f[j] * f[j]; }
+      for (int j = 0; j < V; ++j) {
+        const float d = f[j] - pv[j];
+        s[j] += d;
+        q[j] += d * d;
+      }
     }
   }
   block_partials_out<V>(s, q, g, C, sm, part);
@@ -214,17 +231,28 @@ __device__ __forceinline__ void finalize_channel(int c, int C, double sum, doubl
   }
 }
 
-// Fused: slab reduce + finalize (+ sums[2C+1] for the backward's count).
+// Shifted moments (S1 = sum d, S2 = sum d^2, d = x - p) -> raw (sum x, sum x^2) in fp64: exact
+// up to fp64 rounding, so E[x^2] - mean^2 downstream cancels in fp64, not fp32.
+__device__ __forceinline__ void unshift(const float* pivot, int c, double count, double& sum, double& sumsq) {
+  if (pivot == nullptr) return;
+  const double p = pivot[c], s1 = sum;
+  sum = s1 + count * p;
+  sumsq = sumsq + 2.0 * p * s1 + count * p * p;
+}
+
+// Fused: slab reduce + finalize (+ sums[2C+1] for the backward's count).  ``pivot``: the shift
+// of a bn_stats slab (its row G), nullptr for a conv-epilogue slab (raw moments).
 __global__ void __launch_bounds__(kFinBlock) bn_finalize_partials_kernel(
     const float* __restrict__ part, int G, int C, double count, const float* __restrict__ w,
     const float* __restrict__ b, float* __restrict__ rmean, float* __restrict__ rvar,
     int64_t* __restrict__ nbt, float momentum, float eps, float* __restrict__ mean_invstd,
-    float* __restrict__ scale_shift, double* __restrict__ sums_out) {
+    float* __restrict__ scale_shift, double* __restrict__ sums_out, const float* __restrict__ pivot) {
   __shared__ double red[kFinWaves * 128];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   reduce_slab64(part, G, C, c, red);
   if (threadIdx.x < 64 && c < C) {
-    const double sum = red[threadIdx.x], sumsq = red[64 + threadIdx.x];
+    double sum = red[threadIdx.x], sumsq = red[64 + threadIdx.x];
+    unshift(pivot, c, count, sum, sumsq);
     if (sums_out) { sums_out[c] = sum; sums_out[C + c] = sumsq; }
     finalize_channel(c, C, sum, sumsq, count, w, b, rmean, rvar, momentum, eps, mean_invstd,
                      scale_shift);
@@ -238,13 +266,16 @@ __global__ void __launch_bounds__(kFinBlock) bn_finalize_partials_kernel(
 // SyncBN path, step 1: slab -> fp64 [2C+1] sums (all-reduced by the caller).
 __global__ void __launch_bounds__(kFinBlock) bn_slab_to_sums_kernel(const float* __restrict__ part, int G,
                                                               int C, double count,
-                                                              double* __restrict__ sums) {
+                                                              double* __restrict__ sums,
+                                                              const float* __restrict__ pivot) {
   __shared__ double red[kFinWaves * 128];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   reduce_slab64(part, G, C, c, red);
   if (threadIdx.x < 64 && c < C) {
-    sums[c] = red[threadIdx.x];
-    sums[C + c] = red[64 + threadIdx.x];
+    double sum = red[threadIdx.x], sumsq = red[64 + threadIdx.x];
+    unshift(pivot, c, count, sum, sumsq);
+    sums[c] = sum;
+    sums[C + c] = sumsq;
   }
   if (count >= 0 && blockIdx.x == 0 && threadIdx.x == 0) sums[2 * C] = count;
 }
@@ -648,12 +679,19 @@ __global__ void __launch_bounds__(256) bn_stats_flat_kernel(const T* __restrict_
                                                             float* __restrict__ part) {
   constexpr int E = Flat<T>::E;
   const Flat<T> fl(M, C);
-  float s[E], q[E];
+  float s[E], q[E], pv[E];  // shifted moments about pv = x[row 0, channel] (see bn_stats_kernel)
 #pragma unroll
-  for (int j = 0; j < E; ++j) { s[j] = 0.f; q[j] = 0.f; }
+  for (int j = 0; j < E; ++j) { s[j] = 0.f; q[j] = 0.f; pv[j] = to_f<T>(x[fl.ch[j]]); }
+  if (blockIdx.x == 0) {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) part[static_cast<int64_t>(gridDim.x) * 2 * C + c] = to_f<T>(x[c]);
+  }
   auto acc = [&](const float* f) {
 #pragma unroll
-    for (int j = 0; j < E; ++j) { s[j] += f[j]; q[j] = fmaf(f[j], f[j], q[j]); }
+    for (int j = 0; j < E; ++j) {
+      const float d = f[j] - pv[j];
+      s[j] += d;
+      q[j] = fmaf(d, d, q[j]);
+    }
   };
   int64_t i = fl.t;
   for (; i + fl.nthreads < fl.n_chunks; i += 2 * fl.nthreads) {
@@ -673,7 +711,7 @@ __global__ void __launch_bounds__(256) bn_stats_flat_kernel(const T* __restrict_
     for (int j = 0; j < E; ++j) {
       const int64_t e = fl.n_chunks * E + j;
       if (e < fl.n_el) {
-        const float v = to_f<T>(x[e]);
+        const float v = to_f<T>(x[e]) - pv[j];
         s[j] += v;
         q[j] = fmaf(v, v, q[j]);
       }
@@ -902,15 +940,15 @@ void launch_bn_stats(const void* x, int dtype, int64_t M, int C, float* part, in
 void launch_bn_finalize_partials(const float* part, int G, int C, double count, const float* w,
                                  const float* b, float* rmean, float* rvar, int64_t* nbt,
                                  float momentum, float eps, float* mean_invstd, float* scale_shift,
-                                 double* sums_out, hipStream_t st) {
+                                 double* sums_out, hipStream_t st, const float* pivot) {
   bn_finalize_partials_kernel<<<(C + 63) / 64, kFinBlock, 0, st>>>(part, G, C, count, w, b, rmean, rvar,
                                                              nbt, momentum, eps, mean_invstd,
-                                                             scale_shift, sums_out);
+                                                             scale_shift, sums_out, pivot);
 }
 
 void launch_bn_slab_to_sums(const float* part, int G, int C, double count, double* sums,
-                            hipStream_t st) {
-  bn_slab_to_sums_kernel<<<(C + 63) / 64, kFinBlock, 0, st>>>(part, G, C, count, sums);
+                            hipStream_t st, const float* pivot) {
+  bn_slab_to_sums_kernel<<<(C + 63) / 64, kFinBlock, 0, st>>>(part, G, C, count, sums, pivot);
 }
 
 void launch_bn_finalize(const double* sums, int C, const float* w, const float* b,

@@ -41,7 +41,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ._ext import ops, use_hip, write_generation
-from .dilated import PrunedConv2d, has_dead_taps
+from .dilated import PrunedConv2d, has_dead_taps, pruned_conv2d
 
 _DECISIONS: dict = {}
 
@@ -292,6 +292,23 @@ def shadows_written(params) -> None:
             sh.version, sh.ptr = p._version, p.data_ptr()
 
 
+def invalidate_weight_shadows(params) -> int:
+    """Mark the bf16 shadows of ``params`` stale (rebuilt from the fp32 weight on next use).  For
+    parameter writes the shadow's validity key cannot see: a write through ``p.data`` (a
+    separate version counter), a collective into the parameter storage (DDP's initial broadcast,
+    ``parallel/ddp.py`` calls this), raw-pointer writers other than the fused step.  Writes
+    through ``p`` itself under ``torch.no_grad()`` (``load_state_dict``, ``p.copy_``) bump the
+    version counter and need no call.  Returns the number of shadows invalidated."""
+    n = 0
+    for p in params:
+        sh = shadow_of(p)
+        if sh is not None:
+            sh.gen = sh.crsk_gen = -1
+            sh.version = sh.ptr = None
+            n += 1
+    return n
+
+
 def _train_shadow(conv, crsk=False) -> torch.Tensor:
     w = conv.weight
     sh = shadow_of(w)
@@ -333,10 +350,11 @@ def weight_crsk(conv: nn.Conv2d, wk: torch.Tensor) -> torch.Tensor:
     return wk.permute(3, 1, 2, 0).contiguous()
 
 
-def _time(fn, reps=8):
+def _time(fn, reps=8, warm=True):
     """GPU time of ``fn`` (eager; the candidates are >= tens of microseconds at training sizes)."""
-    fn()
-    torch.cuda.synchronize()
+    if warm:
+        fn()
+        torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     for _ in range(reps):
@@ -346,9 +364,35 @@ def _time(fn, reps=8):
     return s.elapsed_time(e)
 
 
+def _wall_ms(fn) -> float:
+    """Wall-clock milliseconds of one synchronised call (includes any host-side work: MIOpen's
+    find / kernel compilation on a shape it has no record of)."""
+    import time
+
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) * 1e3
+
+
+# A vendor candidate whose first (warm) call takes longer than this many ms AND this many times
+# the best native candidate's time is dropped without further calls (RTSEG_TUNE_BUDGET_MS).
+_VENDOR_BUDGET_MS = float(os.environ.get("RTSEG_TUNE_BUDGET_MS", "50"))
+_VENDOR_BUDGET_X = 25.0
+
+
 def _choose(key, candidates):
     """Index of the fastest candidate (timed once per key, never while a graph is captured).
-    ``candidates``: [(name, fn)] with ours first; ``RTSEG_CONV_MFMA=1`` forces index 0."""
+    ``candidates``: [(name, fn)] with ours first and MIOpen ("miopen") last; ``RTSEG_CONV_MFMA=1``
+    forces index 0.
+
+    Bounded first-step cost at a new shape: the native candidates are timed first (one warm and
+    one timed call each); MIOpen's warm call is then clocked on the wall, and if it exceeded both
+    ``_VENDOR_BUDGET_MS`` and ``_VENDOR_BUDGET_X`` x the best native time (an immediate-mode
+    fallback to a naive kernel, or a find-mode search) it is dropped with no further call.  The
+    survivors within 4x of the best get three interleaved rounds, best of each, so one noisy round
+    (clock ramp, a neighbour's allocation) cannot flip the pick."""
     if len(candidates) == 1 or _mode() == "1":
         return 0
     names = [n for n, _ in candidates]
@@ -363,14 +407,22 @@ def _choose(key, candidates):
     if torch.cuda.is_current_stream_capturing():
         return len(candidates) - 1  # MIOpen is last
     with torch.no_grad():
-        # one timed call each first: a candidate > 4x slower than the best is out (MIOpen's
-        # immediate-mode fallback for a shape without find-db record can be a naive direct kernel
-        # taking seconds per call -- timing it 13 times made bench.py --batch 48's first step
-        # look hung, profiles/r4_bench/README.md); then three interleaved rounds over the rest,
-        # best of each, so one noisy round (clock ramp, a neighbour's allocation) cannot flip the pick
-        first = [_time(fn, reps=1) for _, fn in candidates]
-        live = [i for i, t in enumerate(first) if t <= 4 * min(first)]
-        rounds = [{i: _time(candidates[i][1], reps=4) / 4 for i in live} for _ in range(3)]
+        native = [i for i, n in enumerate(names) if n != "miopen"]
+        first = {i: _time(candidates[i][1], reps=1) for i in native}
+        best_native = min(first.values()) if first else float("inf")
+        dropped = set()
+        for i in range(len(candidates)):
+            if i in first:
+                continue
+            wall = _wall_ms(candidates[i][1])
+            if native and wall > max(_VENDOR_BUDGET_MS, _VENDOR_BUDGET_X * best_native):
+                first[i] = wall
+                dropped.add(i)
+                continue
+            first[i] = _time(candidates[i][1], reps=1, warm=False)
+        lo = min(first.values())
+        live = [i for i in range(len(candidates)) if i not in dropped and first[i] <= 4 * lo]
+        rounds = [{i: _time(candidates[i][1], reps=4, warm=False) / 4 for i in live} for _ in range(3)]
         times = [min(r[i] for r in rounds) if i in live else first[i] for i in range(len(candidates))]
     best = min(range(len(times)), key=times.__getitem__)
     _DECISIONS[key] = (best, candidates[best][0], [round(t, 4) for t in times])
@@ -768,11 +820,13 @@ def grouped_dense_ok(x: torch.Tensor, conv: nn.Module) -> bool:
     (reference models/regseg.py:62-110).  MIOpen's grouped weight gradient in channels-last bf16
     is pathological at these shapes (tools/probe_grouped_conv.py), so such a conv runs as the
     dense conv of its block-diagonal weight: ``groups`` x the FLOPs of a conv that is tiny either
-    way, on the routed kernels.  ``RTSEG_GROUPED_DENSE=0`` keeps MIOpen."""
+    way, on the routed kernels.  ``RTSEG_GROUPED_DENSE=0`` keeps MIOpen; so do
+    ``RTSEG_DISABLE_HIP=1`` / ``RTSEG_HIP_OFF=conv`` (the stock yardstick runs the module's own
+    grouped conv)."""
     return (isinstance(conv, nn.Conv2d) and 1 < conv.groups <= 32 and conv.groups != conv.in_channels
             and conv.padding_mode == "zeros" and not isinstance(conv.padding, str) and x.dim() == 4
             and x.is_cuda and torch.is_grad_enabled() and conv.weight.requires_grad
-            and os.environ.get("RTSEG_GROUPED_DENSE", "1") != "0")
+            and os.environ.get("RTSEG_GROUPED_DENSE", "1") != "0" and use_hip(x, "conv"))
 
 
 _BLOCK_MASKS: dict = {}
@@ -843,7 +897,7 @@ def grouped_as_dense(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
             x = x.clone(memory_format=torch.channels_last)
         y, _ = _ConvFn.apply(x, wd, _DenseView(conv, wd), False)
         return bias_add(y, conv.bias) if conv.bias is not None else y
-    return F.conv2d(x, wd, conv.bias, conv.stride, conv.padding, conv.dilation, 1)
+    return pruned_conv2d(x, wd, conv.bias, conv.stride, conv.padding, conv.dilation, 1)
 
 
 def conv_bn_act(x: torch.Tensor, conv: nn.Module, bn: nn.Module, act="none", residual=None, act_module=None):

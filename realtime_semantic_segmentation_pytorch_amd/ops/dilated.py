@@ -97,8 +97,9 @@ def pruned_conv2d(x, weight, bias, stride, padding, dilation, groups):
 
 
 class PrunedConv2d(nn.Conv2d):
-    """``nn.Conv2d`` whose GPU forward drops dead taps for the current input size
-    (:func:`pruned_conv2d`); identical to ``nn.Conv2d`` whenever no tap is dead, and on CPU."""
+    """``nn.Conv2d`` whose forward drops dead taps for the current input size
+    (:func:`pruned_conv2d`, on every device: exact); identical to ``nn.Conv2d`` whenever no tap
+    is dead."""
 
     def _conv_forward(self, input, weight, bias):
         if (bias is not None and input.is_cuda and input.dim() == 4 and self.groups == 1
@@ -107,7 +108,7 @@ class PrunedConv2d(nn.Conv2d):
             from .bn import bias_add
 
             return bias_add(self._conv_forward(input, weight, None), bias)
-        if (not input.is_cuda or self.padding_mode != "zeros"
+        if (self.padding_mode != "zeros" or input.dim() != 4
                 or not has_dead_taps(input.shape[2:], self.kernel_size, self.stride, self.padding, self.dilation)):
             return super()._conv_forward(input, weight, bias)
         return pruned_conv2d(input, weight, bias, self.stride, self.padding, self.dilation, self.groups)
@@ -186,8 +187,10 @@ class DilatedGroupConv2d(nn.Conv2d):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         from ._ext import use_hip
 
-        if not x.is_cuda or not use_hip(x, "dilated"):  # RTSEG_DISABLE_HIP=1: the stock conv, for A/B runs
-            return super().forward(x)
+        if not x.is_cuda or not use_hip(x, "dilated"):
+            # CPU / RTSEG_DISABLE_HIP=1 (the stock yardstick): the stock conv, dead taps dropped --
+            # no fallback hands a padding-only tap to the vendor library (profiles/r5_fault)
+            return pruned_conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, self.groups)
         from .conv import grouped_as_dense, grouped_dense_ok
 
         if grouped_dense_ok(x, self):  # training: the block-diagonal dense route (ops/conv.py)

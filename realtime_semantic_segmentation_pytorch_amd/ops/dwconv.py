@@ -23,6 +23,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .bn import channel_sum
+from .dilated import pruned_conv2d
 from ._ext import ops, use_hip
 
 _DTYPES = (torch.float32, torch.bfloat16, torch.float16)
@@ -104,7 +105,9 @@ def dw_conv2d(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
             geom = (conv.out_channels, kh, kw, conv.stride[0], conv.stride[1], conv.padding[0],
                     conv.padding[1], conv.dilation[0], conv.dilation[1])
             return _DWConvFn.apply(x.to(dt), conv.weight, conv.bias, geom)
-    return F.conv2d(x, conv.weight, conv.bias, conv.stride, conv.padding, conv.dilation, conv.groups)
+    # stock fallback (CPU, RTSEG_DISABLE_HIP / RTSEG_HIP_OFF=dw): dead taps dropped first, so a
+    # dilated depth-wise conv never reaches the vendor library with padding-only taps
+    return pruned_conv2d(x, conv.weight, conv.bias, conv.stride, conv.padding, conv.dilation, conv.groups)
 
 
 def dw_conv_bn_stats(x: torch.Tensor, conv: nn.Conv2d):

@@ -24,6 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .bn import channel_sum
+from .dilated import pruned_conv2d
 from ._ext import ops, use_hip
 
 MAX_CHANNELS = 16
@@ -130,7 +131,7 @@ class TapConv2d(nn.Conv2d):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if not x.is_cuda:
-            return super().forward(x)
+            return pruned_conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, self.groups)
         axis = 0 if self.kernel_size[0] > 1 else 1
         if torch.is_autocast_enabled("cuda"):
             x = x.to(torch.get_autocast_dtype("cuda"))

@@ -144,7 +144,12 @@ def parallel_model(config, model, rank, device):
               static_graph=bool(getattr(config, "ddp_static_graph", False)))
     if device.type == "cuda":
         kw.update(device_ids=[device.index], output_device=device.index)
-    return DDP(model, **kw)
+    wrapped = DDP(model, **kw)
+    # DDP's constructor broadcast rank 0's parameters into the local ones through RCCL (raw
+    # pointers: no version bump): bf16 weight shadows made by any earlier forward are stale
+    from ..ops.conv import invalidate_weight_shadows
+    invalidate_weight_shadows(model.parameters())
+    return wrapped
 
 
 def destroy_ddp_process(config):

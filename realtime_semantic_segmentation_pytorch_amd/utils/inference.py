@@ -26,7 +26,8 @@ from .. import ops
 class InferenceEngine:
     def __init__(self, model: nn.Module, input_shape: Sequence[int], dtype: torch.dtype = torch.bfloat16,
                  channels_last: bool = True, use_graph: bool = True, warmup: int = 3,
-                 device: Optional[torch.device] = None, cast_weights: bool = True):
+                 device: Optional[torch.device] = None, cast_weights: bool = True,
+                 input_dtype: Optional[torch.dtype] = None):
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.dtype = dtype
         self.channels_last = channels_last
@@ -47,11 +48,15 @@ class InferenceEngine:
         if channels_last:
             self.model = self.model.to(memory_format=torch.channels_last)
         fmt = torch.channels_last if channels_last else torch.contiguous_format
-        # a reduced-precision engine takes its input in that dtype: the copy into the static buffer
-        # casts, and image-side ops (input pyramids, pooled image shortcuts, resized inputs) run in
-        # bf16 instead of leaving fp32 islands that every consumer conv casts again
-        self.static_in = torch.zeros(*input_shape, device=self.device,
-                                     dtype=dtype if self.autocast else torch.float32).contiguous(memory_format=fmt)
+        # by default a reduced-precision engine takes its input in that dtype: the copy into the
+        # static buffer casts, and image-side ops (input pyramids, pooled image shortcuts, resized
+        # inputs) run in bf16 instead of leaving fp32 islands that every consumer conv casts again.
+        # The image is then rounded once before the model (the first conv rounds it under
+        # autocast anyway); tests/test_misc_ops_gpu.py bounds the effect on the models with image-
+        # side ops (DFANet, ESPNet, ICNet).  ``input_dtype=torch.float32`` keeps the eager path's
+        # fp32 image exactly.
+        in_dt = input_dtype or (dtype if self.autocast else torch.float32)
+        self.static_in = torch.zeros(*input_shape, device=self.device, dtype=in_dt).contiguous(memory_format=fmt)
         self.graph = None
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))

@@ -30,6 +30,22 @@ def pytest_configure(config):
             guard.install(mode)
 
 
+def pytest_sessionstart(session):
+    import _faultlog
+
+    _faultlog.bind(session.config)
+
+
+def pytest_runtest_logstart(nodeid, location):
+    # GPU runs only: a test that aborts the process is named above the faulthandler dump
+    import torch
+
+    if torch.cuda.is_available():
+        import _faultlog
+
+        _faultlog.write(f"start {nodeid}")
+
+
 def pytest_collection_modifyitems(config, items):
     import torch
 

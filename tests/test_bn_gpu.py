@@ -217,3 +217,30 @@ def test_bn_odd_channels_flat_path(dtype, act, with_res, shape):
     if with_res:
         bad_r = ((res.grad.float().cpu() - rr.grad).abs() > gt * rr.grad.abs().max().item()).float().mean()
         assert bad_r < 2e-3
+
+
+@pytest.mark.parametrize("shape", [(2, 256, 1, 1), (2, 128, 2, 4), (2, 19, 1, 1), (4, 64, 32, 32), (2, 35, 16, 16)])
+def test_bn_stats_large_mean_vs_fp64(shape):
+    """|mean| >> std (pooled ReLU features: DDRNet's DAPPM global branch, BiSeNetV2's context
+    block -- 2 values per channel at batch 2): the shifted one-pass moments keep the batch
+    variance, the normalised output and the input gradient at fp32 accuracy against fp64.  With
+    plain sum / sum-of-squares partials the variance error was mean^2 / var x 1e-7 (here ~1e-1)."""
+    assert ops.load()
+    torch.manual_seed(0)
+    c = shape[1]
+    x64 = (50.0 + 0.05 * torch.randn(shape, dtype=torch.float64)).float().double().to(DEV)  # fp32-exact
+    dy = torch.randn(shape, dtype=torch.float64, device=DEV)
+    bn = nn.BatchNorm2d(c).to(DEV)
+    ref = copy.deepcopy(bn).double()
+    xr = x64.clone().requires_grad_(True)
+    yr = ref(xr)
+    yr.backward(dy)
+    xh = x64.float().contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    yh = ops.bn_act(xh, bn, "none")
+    yh.backward(dy.float().contiguous(memory_format=torch.channels_last))
+    rel = lambda a, b: ((a.double() - b).norm() / b.norm()).item()  # noqa: E731
+    # what remains is fp32 rounding of the folded apply (x * scale + shift: |shift| ~ 1e3 for an
+    # output ~ 1, 6e-5) and of the fp32 mean in the backward's x - mean (50 * 6e-8 / 0.05)
+    assert rel(bn.running_var, ref.running_var.double()) < 2e-4
+    assert rel(yh.detach(), yr.detach()) < 2e-4
+    assert rel(xh.grad, xr.grad) < 5e-4

@@ -209,3 +209,38 @@ def test_weight_shadows_written_by_the_fused_step(monkeypatch):
         assert torch.equal(sh.krsc, w16.permute(0, 2, 3, 1).contiguous()), n
         assert torch.equal(sh.crsk, w16.permute(1, 2, 3, 0).contiguous()), n
     assert seen >= 2
+
+
+def test_weight_shadow_follows_writes_outside_the_optimizer(monkeypatch):
+    """A parameter write the fused step did not make: ``p.copy_`` under no_grad (version bump, as
+    ``load_state_dict`` does) is seen by itself; a ``p.data`` write (its own version counter) or a
+    collective into the storage is seen after ``ops.invalidate_weight_shadows`` (what
+    ``parallel_model`` calls after DDP's initial broadcast).  The next training forward then
+    equals the forward of a fresh model holding the new weights."""
+    _, _, m = _shadow_run(True, monkeypatch, steps=1)
+    torch.manual_seed(5)
+    x = torch.randn(4, 64, 32, 48, device="cuda").contiguous(memory_format=torch.channels_last)
+
+    def fwd(mod):
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            return mod(x).float()
+
+    import copy
+
+    convs = [p for n, p in m.named_parameters() if p.dim() == 4]
+    new = [torch.randn_like(p) * p.std() for p in convs]
+    with torch.no_grad():
+        for p, v in zip(convs, new):
+            p.copy_(v)
+    fresh = copy.deepcopy(m)
+    for p in fresh.parameters():
+        p._rtseg_shadow = None
+    torch.testing.assert_close(fwd(m), fwd(fresh), rtol=0, atol=0)
+    new2 = [torch.randn_like(p) * p.std() for p in convs]
+    for p, v in zip(convs, new2):
+        p.data.copy_(v)
+    assert ops.invalidate_weight_shadows(m.parameters()) >= 2
+    fresh2 = copy.deepcopy(m)
+    for p in fresh2.parameters():
+        p._rtseg_shadow = None
+    torch.testing.assert_close(fwd(m), fwd(fresh2), rtol=0, atol=0)

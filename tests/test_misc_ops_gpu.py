@@ -198,3 +198,33 @@ def test_inference_engine_bf16_matches_eager_autocast(key):
     assert torch.isfinite(out).all()
     err = (out - ref).abs().max().item()
     assert err <= 0.05 * ref.abs().max().item() + 1e-2, err
+
+
+@pytest.mark.no_guard
+@pytest.mark.parametrize("key", ["dfanet", "espnet", "icnet"])
+def test_inference_engine_bf16_input_bounded(key):
+    """The engine's bf16 static input (utils/inference.py) rounds the image before the model; on the
+    models whose image-side ops (input pyramids, pooled / resized image shortcuts) run in fp32 under
+    eager autocast, the engine's distance to the fp32 eval output stays within 1.5x eager
+    autocast's own distance (+ a small floor), and ``input_dtype=torch.float32`` is as close as
+    eager autocast."""
+    from realtime_semantic_segmentation_pytorch_amd.configs import BaseConfig
+    from realtime_semantic_segmentation_pytorch_amd.models import get_model
+    from realtime_semantic_segmentation_pytorch_amd.utils.inference import InferenceEngine
+
+    c = BaseConfig()
+    c.model, c.num_class = key, 19
+    torch.manual_seed(0)
+    m = get_model(c).cuda().eval().to(memory_format=torch.channels_last)
+    x = torch.randn(1, 3, 256, 512, device="cuda")
+    xc = x.contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        ref = ops.materialize(m(xc)).float()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            eager = ops.materialize(m(xc)).float()
+    rel = lambda a: ((a - ref).norm() / ref.norm()).item()  # noqa: E731
+    e_eager = rel(eager)
+    e_bf16_in = rel(InferenceEngine(m, (1, 3, 256, 512), dtype=torch.bfloat16)(x).float())
+    e_fp32_in = rel(InferenceEngine(m, (1, 3, 256, 512), dtype=torch.bfloat16, input_dtype=torch.float32)(x).float())
+    assert e_bf16_in <= 1.5 * e_eager + 2e-3, (e_bf16_in, e_eager)
+    assert e_fp32_in <= 1.5 * e_eager + 1e-3, (e_fp32_in, e_eager)

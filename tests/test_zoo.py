@@ -16,6 +16,8 @@ import copy
 import pytest
 import torch
 
+import _faultlog
+
 from realtime_semantic_segmentation_pytorch_amd import ops
 from realtime_semantic_segmentation_pytorch_amd.configs import BaseConfig
 from realtime_semantic_segmentation_pytorch_amd.core.loss import SegCELoss
@@ -77,7 +79,9 @@ def test_deferred_logits_materialize_to_model_output_cpu(key):
     torch.testing.assert_close(got, ref, atol=1e-5, rtol=1e-5)
 
 
-def _run_gpu(m, x, labels, disable_hip, monkeypatch):
+def _run_gpu(m, x, labels, disable_hip, monkeypatch, phase=None):
+    if phase is not None:  # survives an abort (tests/_faultlog.py)
+        _faultlog.write(f"  phase {phase}")
     if disable_hip:
         monkeypatch.setenv("RTSEG_DISABLE_HIP", "1")
     else:
@@ -142,9 +146,11 @@ def check_zoo_hip_matches_torch_path(key, monkeypatch):
     err = lambda a, b: ((a.double().cpu() - b.double().cpu()).norm() / (b.double().cpu().norm() + 1e-30)).item()  # noqa: E731
     for frozen in (True, False):
         prep = _freeze_bn if frozen else (lambda m: m)
+        bn = "frozen-BN" if frozen else "train-BN"
         y_r, l_r, g_r = _run_gpu(prep(copy.deepcopy(cpu).train().double()), x.double(), labels, False, monkeypatch)
         y_c, l_c, g_c = _run_gpu(prep(copy.deepcopy(cpu).train()), x, labels, False, monkeypatch)
-        y_h, l_h, g_h = _run_gpu(prep(copy.deepcopy(base).train()), xg, labels.cuda(), False, monkeypatch)
+        y_h, l_h, g_h = _run_gpu(prep(copy.deepcopy(base).train()), xg, labels.cuda(), False, monkeypatch,
+                                 f"{key} {bn} HIP fp32")
         assert g_h.keys() == g_c.keys() == g_r.keys()
         cat = lambda g: torch.cat([g[n].flatten().double().cpu() for n in g_r])  # noqa: E731
         hg, cg = err(cat(g_h), cat(g_r)), err(cat(g_c), cat(g_r))
@@ -159,7 +165,7 @@ def check_zoo_hip_matches_torch_path(key, monkeypatch):
         if cg > 0.1:
             continue  # ill-conditioned at batch 2 on any path (see docstring); finiteness checked
         nchw = copy.deepcopy(cpu).cuda().train()
-        _, l_t, g_t = _run_gpu(nchw, x.cuda(), labels.cuda(), True, monkeypatch)
+        _, l_t, g_t = _run_gpu(nchw, x.cuda(), labels.cuda(), True, monkeypatch, f"{key} {bn} stock fp32 NCHW")
         tg = err(cat(g_t), cat(g_r))
         tag += f", GPU torch NCHW {tg:.2e}"
         print(tag)
@@ -177,9 +183,9 @@ def check_zoo_hip_matches_torch_path(key, monkeypatch):
         assert hg <= max(4 * min(tg, cg), 2 * tg, 5 * cg, 1e-2), tag
 
 
-def _run_gpu_bf16(m, x, labels, disable_hip, monkeypatch):
+def _run_gpu_bf16(m, x, labels, disable_hip, monkeypatch, phase=None):
     with torch.autocast("cuda", dtype=torch.bfloat16):
-        return _run_gpu(m, x, labels, disable_hip, monkeypatch)
+        return _run_gpu(m, x, labels, disable_hip, monkeypatch, phase)
 
 
 def _check_bf16_vs_fp64(key, base, xg, labels, l_r, g_r, cat, err, monkeypatch):
@@ -189,8 +195,10 @@ def _check_bf16_vs_fp64(key, base, xg, labels, l_r, g_r, cat, err, monkeypatch):
     of tests/test_train_numerics_gpu.py): the whole-model gradient error and the loss error.
     Frozen BatchNorm keeps batch-statistics amplification out, so the errors measure rounding."""
     lg = labels.cuda()
-    _, l_s, g_s = _run_gpu_bf16(_freeze_bn(copy.deepcopy(base).train()), xg, lg, True, monkeypatch)
-    _, l_b, g_b = _run_gpu_bf16(_freeze_bn(copy.deepcopy(base).train()), xg, lg, False, monkeypatch)
+    _, l_s, g_s = _run_gpu_bf16(_freeze_bn(copy.deepcopy(base).train()), xg, lg, True, monkeypatch,
+                                f"{key} frozen-BN stock bf16")
+    _, l_b, g_b = _run_gpu_bf16(_freeze_bn(copy.deepcopy(base).train()), xg, lg, False, monkeypatch,
+                                f"{key} frozen-BN HIP bf16")
     assert g_b.keys() == g_r.keys() == g_s.keys(), key
     sg, bg = err(cat(g_s), cat(g_r)), err(cat(g_b), cat(g_r))
     sl, bl = abs(l_s.item() - l_r.item()), abs(l_b.item() - l_r.item())
