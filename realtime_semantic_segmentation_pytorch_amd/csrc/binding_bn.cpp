@@ -66,12 +66,12 @@ int64_t* nbt_ptr(const std::optional<at::Tensor>& t) {
   return t.has_value() && t->defined() ? t->data_ptr<int64_t>() : nullptr;
 }
 
-at::Tensor stats_slab(const at::Tensor& x, int& G) {
+at::Tensor stats_slab(const at::Tensor& x, int& G, bool shift = true) {
   const int C = static_cast<int>(x.size(1));
   const int64_t M = rows_of(x);
   G = bn_partial_grid(M, C, dtype_code(x));
   at::Tensor part = at::empty({G + 1, 2 * C}, x.options().dtype(at::kFloat));  // row G: pivots
-  launch_bn_stats(x.data_ptr(), dtype_code(x), M, C, part.data_ptr<float>(), G, cur_stream());
+  launch_bn_stats(x.data_ptr(), dtype_code(x), M, C, part.data_ptr<float>(), G, cur_stream(), shift);
   return part;
 }
 
@@ -96,13 +96,14 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_stats_finalize(
   return {mi, ss, sums};
 }
 
-// forward, SyncBN step 1: -> sums[2C+1] (to be all-reduced)
-at::Tensor bn_stats_sums(const at::Tensor& x) {
+// forward, SyncBN step 1 (and ops.channel_sum): -> sums[2C+1] (to be all-reduced).
+// shift=false: raw moments about 0 instead of the sampled pivot (bn_act.hip)
+at::Tensor bn_stats_sums(const at::Tensor& x, bool shift) {
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   check_cl(x, "x");
   const int C = static_cast<int>(x.size(1));
   int G = 0;
-  at::Tensor part = stats_slab(x, G);
+  at::Tensor part = stats_slab(x, G, shift);
   at::Tensor sums = at::empty({2 * C + 1}, x.options().dtype(at::kDouble));
   launch_bn_slab_to_sums(part.data_ptr<float>(), G, C, static_cast<double>(rows_of(x)),
                          sums.data_ptr<double>(), cur_stream(),
@@ -294,7 +295,7 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
   m.def("bn_stats_finalize(Tensor x, Tensor? weight, Tensor? bias, Tensor(a!)? running_mean, "
         "Tensor(b!)? running_var, Tensor(c!)? num_batches_tracked, float momentum, float eps) "
         "-> (Tensor, Tensor, Tensor)");
-  m.def("bn_stats_sums(Tensor x) -> Tensor");
+  m.def("bn_stats_sums(Tensor x, bool shift=True) -> Tensor");
   m.def("bn_finalize(Tensor sums, Tensor? weight, Tensor? bias, Tensor(a!)? running_mean, "
         "Tensor(b!)? running_var, Tensor(c!)? num_batches_tracked, float momentum, float eps) -> (Tensor, Tensor)");
   m.def("bn_eval_coeffs(Tensor? weight, Tensor? bias, Tensor running_mean, Tensor running_var, "

@@ -64,7 +64,8 @@ void launch_seg_loss_bwd(const SegLossArgs& a, const float* grad_out, const Tens
 int bn_partial_grid(int64_t M, int C, int dtype);
 // Channel-vector width used for (dtype, C); 0 = layer not supported by the fused kernels.
 int bn_vec_width(int dtype, int C);
-void launch_bn_stats(const void* x, int dtype, int64_t M, int C, float* part, int G, hipStream_t st);
+void launch_bn_stats(const void* x, int dtype, int64_t M, int C, float* part, int G, hipStream_t st,
+                     bool shift = true);
 void launch_bn_finalize_partials(const float* part, int G, int C, double count, const float* w,
                                  const float* b, float* rmean, float* rvar, int64_t* nbt,
                                  float momentum, float eps, float* mean_invstd, float* scale_shift,

@@ -111,30 +111,61 @@ __device__ __forceinline__ void block_partials_out(const float* s, const float* 
   __syncthreads();
   float* out = part + static_cast<int64_t>(blockIdx.x) * 2 * C;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float a = 0.f, b = 0.f;
+    double a = 0.0, b = 0.0;  // <= 256 slots per channel: fp64 costs nothing here
     for (int r = 0; r < g.rpi; ++r) { a += ss[r * C + c]; b += qq[r * C + c]; }
-    out[c] = a;
-    out[C + c] = b;
+    out[c] = static_cast<float>(a);
+    out[C + c] = static_cast<float>(b);
   }
 }
 
+// Error-free accumulation s + x = (s', e): s' = fl(s + x), e the exact rounding error (Knuth's
+// TwoSum, branch-free; relies on IEEE add/sub without reassociation, which hipcc keeps).
+__device__ __forceinline__ void two_sum_acc(float& s, float& comp, float x) {
+  const float t = s + x;
+  const float bp = t - s;
+  comp += (s - (t - bp)) + (x - bp);
+  s = t;
+}
+
+// Per-channel pivot of the shifted moments: the mean of 8 rows spread over the tensor
+// ((2k + 1) M / 16), identical in every thread (same loads, same order).  A typical value, unlike
+// the corner pixel row 0, which on zero-padded conv outputs is the atypical one: ESPNet's
+// near-constant channels sat ~100 sigma from their row-0 value (round-5 zoo numerics).
+template <typename T, int V>
+__device__ __forceinline__ void sample_pivot(const T* __restrict__ x, int64_t M, int64_t C, int c0, float* pv) {
+  float a[8][V];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) VecIO<T, V>::load(x + ((2 * k + 1) * M / 16) * C + c0, a[k]);
+#pragma unroll
+  for (int j = 0; j < V; ++j)
+    pv[j] = (((a[0][j] + a[1][j]) + (a[2][j] + a[3][j])) + ((a[4][j] + a[5][j]) + (a[6][j] + a[7][j]))) * 0.125f;
+}
+
 // --------------------------------------------------------------- stats ------
-// Shifted one-pass moments: every partial accumulates d = x - p and d*d about a per-channel
-// pivot p = x[row 0, c] (the finalize adds the shift back in fp64, ``unshift``).  Plain
-// sum / sum-of-squares partials lose var = E[x^2] - mean^2 to cancellation when |mean| >> std --
-// BatchNorms over a few pooled values per channel (DDRNet's DAPPM global branch, BiSeNetV2's
-// context block: 2 values at batch 2) had relative variance errors of 1e-3 and more.  The pivot
-// row is stored after the G slab rows (slab [G + 1, 2C], row G = pivots) by block 0.
+// Shifted, compensated one-pass moments: every partial accumulates d = x - p and d*d about a
+// per-channel pivot p (``sample_pivot``; the finalize adds the shift back in fp64, ``unshift``),
+// and the running sum of d carries its TwoSum rounding error.  Plain sum / sum-of-squares
+// partials lose var = E[x^2] - mean^2 to cancellation when |mean| >> std (BatchNorms over a few
+// pooled values per channel: DDRNet's DAPPM global branch, BiSeNetV2's context block, 2 values
+// at batch 2), and a plain fp32 running sum loses a channel sum whose terms cancel (a
+// classifier's bias gradient: ~+1/19 on most pixels, ~-1 on the class's own; DDRNet-23's head
+// bias gradients were 3.5e-3 off fp64 that way in round 4).  The pivot row is stored after the
+// G slab rows (slab [G + 1, 2C], row G = pivots) by block 0.  shift = 0: pivot 0 (raw moments).
 template <typename T, int V>
 __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, int64_t M, int C,
-                                                       float* __restrict__ part) {
+                                                       float* __restrict__ part, int shift) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const RowGeo g(C, V);
-  float s[V], q[V], pv[V];
+  float s[V], q[V], pv[V], e[V];
 #pragma unroll
-  for (int j = 0; j < V; ++j) { s[j] = 0.f; q[j] = 0.f; }
+  for (int j = 0; j < V; ++j) { s[j] = 0.f; q[j] = 0.f; e[j] = 0.f; }
   if (g.my_r < g.rpi) {
-    VecIO<T, V>::load(x + g.my_cv * V, pv);
+    if (shift) {
+      sample_pivot<T, V>(x, M, C, g.my_cv * V, pv);
+    } else {
+#pragma unroll
+      for (int j = 0; j < V; ++j) pv[j] = 0.f;
+    }
     if (blockIdx.x == 0 && g.my_r == 0) {
       float* prow = part + static_cast<int64_t>(gridDim.x) * 2 * C + g.my_cv * V;
 #pragma unroll
@@ -153,7 +184,7 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, 
 #pragma unroll
       for (int j = 0; j < V; ++j) {
         const float d0 = f0[j] - pv[j], d1 = f1[j] - pv[j], d2 = f2[j] - pv[j], d3 = f3[j] - pv[j];
-        s[j] += (d0 + d1) + (d2 + d3);
+        two_sum_acc(s[j], e[j], (d0 + d1) + (d2 + d3));
         q[j] += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
       }
     }
@@ -163,10 +194,12 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, 
 #pragma unroll
       for (int j = 0; j < V; ++j) {
         const float d = f[j] - pv[j];
-        s[j] += d;
+        two_sum_acc(s[j], e[j], d);
         q[j] += d * d;
       }
     }
+#pragma unroll
+    for (int j = 0; j < V; ++j) s[j] += e[j];
   }
   block_partials_out<V>(s, q, g, C, sm, part);
 }
@@ -667,29 +700,37 @@ __device__ __forceinline__ void flat_partials_out(const float* s, const float* q
   const int b0 = static_cast<int>((static_cast<int64_t>(E) * blockIdx.x * blockDim.x) % C);
   const int nslot = blockDim.x * E;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float a = 0.f, b = 0.f;
+    double a = 0.0, b = 0.0;
     for (int f = ((c - b0) % C + C) % C; f < nslot; f += C) { a += red[0][f]; b += red[1][f]; }
-    part[static_cast<int64_t>(blockIdx.x) * 2 * C + c] = a;
-    part[static_cast<int64_t>(blockIdx.x) * 2 * C + C + c] = b;
+    part[static_cast<int64_t>(blockIdx.x) * 2 * C + c] = static_cast<float>(a);
+    part[static_cast<int64_t>(blockIdx.x) * 2 * C + C + c] = static_cast<float>(b);
   }
 }
 
 template <typename T>
 __global__ void __launch_bounds__(256) bn_stats_flat_kernel(const T* __restrict__ x, int64_t M, int C,
-                                                            float* __restrict__ part) {
+                                                            float* __restrict__ part, int shift) {
   constexpr int E = Flat<T>::E;
   const Flat<T> fl(M, C);
-  float s[E], q[E], pv[E];  // shifted moments about pv = x[row 0, channel] (see bn_stats_kernel)
+  // shifted, compensated moments about the sampled pivot (see bn_stats_kernel)
+  float s[E], q[E], pv[E], cmp[E];
+  auto pivot = [&](int c) {
+    float a[8];
 #pragma unroll
-  for (int j = 0; j < E; ++j) { s[j] = 0.f; q[j] = 0.f; pv[j] = to_f<T>(x[fl.ch[j]]); }
+    for (int k = 0; k < 8; ++k) a[k] = to_f<T>(x[((2 * k + 1) * M / 16) * C + c]);
+    return (((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]))) * 0.125f;
+  };
+#pragma unroll
+  for (int j = 0; j < E; ++j) { s[j] = 0.f; q[j] = 0.f; cmp[j] = 0.f; pv[j] = shift ? pivot(fl.ch[j]) : 0.f; }
   if (blockIdx.x == 0) {
-    for (int c = threadIdx.x; c < C; c += blockDim.x) part[static_cast<int64_t>(gridDim.x) * 2 * C + c] = to_f<T>(x[c]);
+    for (int c = threadIdx.x; c < C; c += blockDim.x)
+      part[static_cast<int64_t>(gridDim.x) * 2 * C + c] = shift ? pivot(c) : 0.f;
   }
   auto acc = [&](const float* f) {
 #pragma unroll
     for (int j = 0; j < E; ++j) {
       const float d = f[j] - pv[j];
-      s[j] += d;
+      two_sum_acc(s[j], cmp[j], d);
       q[j] = fmaf(d, d, q[j]);
     }
   };
@@ -712,11 +753,13 @@ __global__ void __launch_bounds__(256) bn_stats_flat_kernel(const T* __restrict_
       const int64_t e = fl.n_chunks * E + j;
       if (e < fl.n_el) {
         const float v = to_f<T>(x[e]) - pv[j];
-        s[j] += v;
+        two_sum_acc(s[j], cmp[j], v);
         q[j] = fmaf(v, v, q[j]);
       }
     }
   }
+#pragma unroll
+  for (int j = 0; j < E; ++j) s[j] += cmp[j];
   flat_partials_out<E>(s, q, C, part);
 }
 
@@ -924,16 +967,17 @@ static void with_tv(int dtype, int C, F&& f) {
 }
 
 void launch_bn_stats(const void* x, int dtype, int64_t M, int C, float* part, int G,
-                     hipStream_t st) {
+                     hipStream_t st, bool shift) {
+  const int sh = shift ? 1 : 0;
   if (bn_flat(dtype, C)) {  // G (bn_partial_grid) is a multiple of C
-    if (dtype == kF32) bn_stats_flat_kernel<float><<<G, 256, 0, st>>>(static_cast<const float*>(x), M, C, part);
-    else bn_stats_flat_kernel<uint16_t><<<G, 256, 0, st>>>(static_cast<const uint16_t*>(x), M, C, part);
+    if (dtype == kF32) bn_stats_flat_kernel<float><<<G, 256, 0, st>>>(static_cast<const float*>(x), M, C, part, sh);
+    else bn_stats_flat_kernel<uint16_t><<<G, 256, 0, st>>>(static_cast<const uint16_t*>(x), M, C, part, sh);
     return;
   }
   with_tv(dtype, C, [&]<typename T, int V>() {
     const int rpi = 256 / (C / V);
     const size_t lds = sizeof(float) * 2 * rpi * C;
-    bn_stats_kernel<T, V><<<G, 256, lds, st>>>(static_cast<const T*>(x), M, C, part);
+    bn_stats_kernel<T, V><<<G, 256, lds, st>>>(static_cast<const T*>(x), M, C, part, sh);
   });
 }
 

@@ -4,6 +4,11 @@ Behavioural target: SMP ``Unet`` / ``UnetPlusPlus`` (reference
 models/__init__.py:42-44): nearest x2 upsample, concat skip, two 3x3
 Conv2dReLU per block; U-Net++ builds the nested dense skip grid
 ``x_{depth}_{layer}``.  Head: 3x3 conv at full resolution.
+
+VGG encoders (``encoder_name`` starting with ``vgg``) get SMP's center block: two 3x3 Conv2dReLU
+at the deepest feature's width (``decoder.center.{0,1}.*``).  U-Net runs it on the deepest
+feature before the first decoder block; U-Net++ builds it (same state-dict keys as SMP) but, as in
+SMP, its forward never calls it -- those parameters get no gradient there.
 """
 from __future__ import annotations
 
@@ -13,6 +18,14 @@ import torch.nn.functional as F
 
 from .base import Conv2dReLU, SegmentationHead, SegmentationModel
 from .encoders import get_encoder
+
+
+class CenterBlock(nn.Sequential):
+    """SMP's center block of VGG-encoder U-Nets: Conv2dReLU x 2 at ``channels``."""
+
+    def __init__(self, in_channels, out_channels, use_batchnorm=True):
+        super().__init__(Conv2dReLU(in_channels, out_channels, 3, padding=1, use_batchnorm=use_batchnorm),
+                         Conv2dReLU(out_channels, out_channels, 3, padding=1, use_batchnorm=use_batchnorm))
 
 
 class DecoderBlock(nn.Module):
@@ -44,16 +57,14 @@ class UnetDecoder(nn.Module):
         if n_blocks != len(decoder_channels):
             raise ValueError(f"Model depth is {n_blocks}, but you provide `decoder_channels` for "
                              f"{len(decoder_channels)} blocks.")
-        if center:
-            raise NotImplementedError("center block (VGG encoders) is not supported")
-        _, ins, skips, outs = _decoder_channels(encoder_channels, decoder_channels)
-        self.center = nn.Identity()
+        enc, ins, skips, outs = _decoder_channels(encoder_channels, decoder_channels)
+        self.center = CenterBlock(enc[0], enc[0], use_batchnorm) if center else nn.Identity()
         self.blocks = nn.ModuleList([DecoderBlock(i, s, o, use_batchnorm, attention_type)
                                      for i, s, o in zip(ins, skips, outs)])
 
     def forward(self, *features):
         feats = list(features[1:])[::-1]
-        x, skips = feats[0], feats[1:]
+        x, skips = self.center(feats[0]), feats[1:]
         for i, blk in enumerate(self.blocks):
             x = blk(x, skips[i] if i < len(skips) else None)
         return x
@@ -65,7 +76,7 @@ class Unet(SegmentationModel):
         super().__init__()
         self.encoder = get_encoder(encoder_name, in_channels, encoder_depth, encoder_weights)
         self.decoder = UnetDecoder(self.encoder.out_channels, decoder_channels, encoder_depth, decoder_use_batchnorm,
-                                   decoder_attention_type)
+                                   decoder_attention_type, center=encoder_name.startswith("vgg"))
         self.segmentation_head = SegmentationHead(decoder_channels[-1], classes, kernel_size=3)
         self.initialize()
 
@@ -77,11 +88,10 @@ class UnetPlusPlusDecoder(nn.Module):
         if n_blocks != len(decoder_channels):
             raise ValueError(f"Model depth is {n_blocks}, but you provide `decoder_channels` for "
                              f"{len(decoder_channels)} blocks.")
-        if center:
-            raise NotImplementedError("center block (VGG encoders) is not supported")
-        _, self.in_channels, self.skip_channels, self.out_channels = _decoder_channels(encoder_channels,
-                                                                                        decoder_channels)
-        self.center = nn.Identity()
+        enc, self.in_channels, self.skip_channels, self.out_channels = _decoder_channels(encoder_channels,
+                                                                                          decoder_channels)
+        # built for the state-dict layout; unused by forward, as in SMP
+        self.center = CenterBlock(enc[0], enc[0], use_batchnorm) if center else nn.Identity()
         blocks = {}
         for layer in range(len(self.in_channels) - 1):
             for depth in range(layer + 1):
@@ -122,6 +132,7 @@ class UnetPlusPlus(SegmentationModel):
         super().__init__()
         self.encoder = get_encoder(encoder_name, in_channels, encoder_depth, encoder_weights)
         self.decoder = UnetPlusPlusDecoder(self.encoder.out_channels, decoder_channels, encoder_depth,
-                                           decoder_use_batchnorm, decoder_attention_type)
+                                           decoder_use_batchnorm, decoder_attention_type,
+                                           center=encoder_name.startswith("vgg"))
         self.segmentation_head = SegmentationHead(decoder_channels[-1], classes, kernel_size=3)
         self.initialize()

@@ -275,7 +275,7 @@ def channel_sum(t: torch.Tensor) -> torch.Tensor:
     if (use_hip(t, "bn") and t.dim() == 4 and t.dtype in (torch.float32, torch.bfloat16) and t.numel() > 0
             and vec_width(t.dtype, t.shape[1]) and t.is_contiguous(memory_format=torch.channels_last)
             and t.data_ptr() % 16 == 0):
-        return ops().bn_stats_sums(t)[: t.shape[1]].float()
+        return ops().bn_stats_sums(t)[: t.shape[1]].float()  # shifted, compensated sums (bn_act.hip)
     return t.float().sum((0, 2, 3))
 
 

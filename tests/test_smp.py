@@ -177,7 +177,24 @@ def test_unet_with_extra_encoder_trains(enc):
     y = m(torch.randn(2, 3, 64, 64))
     assert y.shape == (2, 19, 64, 64)
     y.float().mean().backward()
+    if enc.startswith("vgg"):  # SMP's center block for VGG encoders: deepest width, two Conv2dReLU
+        sd = m.state_dict()
+        c = m.encoder.out_channels[-1]
+        assert sd["decoder.center.0.0.weight"].shape == (c, c, 3, 3)
+        assert sd["decoder.center.1.0.weight"].shape == (c, c, 3, 3)
+        assert "decoder.center.1.1.running_var" in sd
     # EfficientNet keeps its (unused) _conv_head / _bn1 in the state dict, as SMP does
     missing = [n for n, p in m.named_parameters() if p.grad is None and "_conv_head" not in n and ".encoder._bn1" not in
                "." + n]
     assert not missing, missing[:5]
+
+
+def test_unetplusplus_vgg_center_keys_unused():
+    """SMP's U-Net++ builds the VGG center block (its state-dict keys) but its forward skips it."""
+    from realtime_semantic_segmentation_pytorch_amd.models.smp import build_smp_model
+
+    m = build_smp_model("unetpp", "vgg11_bn", None, 19).train()
+    assert "decoder.center.0.0.weight" in m.state_dict()
+    m(torch.randn(2, 3, 64, 64)).float().mean().backward()
+    assert all(p.grad is None for n, p in m.named_parameters() if n.startswith("decoder.center."))
+    assert all(p.grad is not None for n, p in m.named_parameters() if n.startswith("decoder.blocks."))

@@ -121,8 +121,8 @@ def check_zoo_hip_matches_torch_path(key, monkeypatch):
     * frozen BatchNorm (running statistics): every model's whole HIP training path -- convs,
       depth-wise convs, pooling, interpolation, gating, activations, the loss -- must be within
       10x the CPU fp32 error (floor 1e-3);
-    * batch-statistics BatchNorm at batch 2: within 4x the better of the two yardsticks, or 2x the
-      GPU torch path's error (floor 1e-2).  Where even CPU fp32 is > 0.1 off fp64 (DFANet, Lite-HRNet, MiniNetV2: BN over a
+    * batch-statistics BatchNorm at batch 2: within 4x the better of the two yardsticks, or 1.5x
+      either one (floor 1e-3).  Where even CPU fp32 is > 0.1 off fp64 (DFANet, Lite-HRNet, MiniNetV2: BN over a
       handful of values at batch 2, gradients of ~1e8), the step is only checked for finite
       gradients; the frozen pass above still pins their numerics."""
     torch.manual_seed(0)
@@ -171,16 +171,17 @@ def check_zoo_hip_matches_torch_path(key, monkeypatch):
         print(tag)
         assert abs(l_h.item() - l_r.item()) <= max(4 * min(abs(l_t.item() - l_r.item()), abs(l_c.item() - l_r.item())),
                                                    1e-3 * abs(l_r.item())), tag
-        # batch-2 statistics amplify summation order: every path is 1e-2-ish off fp64 here (MI355X,
-        # BiSeNetV2: CPU fp32 1.0e-2, GPU torch 1.9e-2 .. 3.0e-2 run to run, HIP 4.2e-2 .. 5.0e-2),
-        # so the HIP path must be within 4x the better yardstick, no more than 2x the stock GPU
-        # path's own error, OR within 5x the (deterministic) CPU fp32 error: the GPU torch
-        # yardstick is not deterministic, and round 4's suite failed BiSeNetV2 at 4.15e-2 against
-        # a 4.12e-2 bound drawn from a low sample of it.  The HIP excess is the one-pass BN
-        # variance (fp32 sum / sum-of-squares partials, fp64 finalize) on BatchNorms that see
-        # 2 .. 64 values per channel at batch 2 (BiSeNetV2's pooled context branch: 2); the
-        # frozen-BN pass above holds every kernel to 10x CPU fp32 without that effect.
-        assert hg <= max(4 * min(tg, cg), 2 * tg, 5 * cg, 1e-2), tag
+        # batch-2 statistics amplify summation order: stock paths are up to ~1e-2 off fp64 here
+        # (MI355X, BiSeNetV2: CPU fp32 1.0e-2, GPU torch 1.7e-2 .. 7.7e-2 run to run).  The HIP
+        # path must be within 4x the better yardstick, or no worse than 1.5x either stock run on
+        # its own: the deterministic CPU fp32 run (SwiftNet: GPU torch 6e-6 vs CPU 6.7e-3), or
+        # the stock GPU run, which shares the fp32 MIOpen convs with the HIP path -- their
+        # solver picks vary from process to process, and both paths move together (MiniNet:
+        # HIP = GPU torch = 8.8e-4 in one run, 8e-7 in another; PP-LiteSeg 3.3e-3 / 5.5e-3 vs
+        # 3.2e-4 / 3.7e-4).  Since round 5 the BN statistics are shifted, compensated one-pass
+        # moments (csrc/kernels/bn_act.hip): DDRNet 1.2e-5 (CPU 1.1e-5; round 4: 3.5e-3),
+        # profiles/r5_numerics.
+        assert hg <= max(4 * min(tg, cg), 1.5 * cg, 1.5 * tg, 1e-3), tag
 
 
 def _run_gpu_bf16(m, x, labels, disable_hip, monkeypatch, phase=None):
@@ -209,8 +210,10 @@ def _check_bf16_vs_fp64(key, base, xg, labels, l_r, g_r, cat, err, monkeypatch):
     assert bl <= max(ZOO_BF16_LOSS_SLACK * sl, 2e-3 * abs(l_r.item())), tag
 
 
-# HIP bf16 vs stock bf16 distance to fp64 (frozen BN, 128 x 256, batch 2)
-ZOO_BF16_GRAD_SLACK, ZOO_BF16_GRAD_FLOOR, ZOO_BF16_LOSS_SLACK = 1.5, 2e-2, 2.0
+# HIP bf16 vs stock bf16 distance to fp64 (frozen BN, 128 x 256, batch 2).  Round 5 on MI355X: HIP
+# / stock between 0.14 (SwiftNet) and 1.14 (ENet), smallest stock 4.6e-3 (FastSCNN); the floor
+# (2e-2 until round 4) only covers stock's run-to-run spread below 5e-3.
+ZOO_BF16_GRAD_SLACK, ZOO_BF16_GRAD_FLOOR, ZOO_BF16_LOSS_SLACK = 1.5, 5e-3, 2.0
 
 
 @pytest.mark.gpu
