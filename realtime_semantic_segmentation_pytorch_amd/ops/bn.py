@@ -107,6 +107,9 @@ class _BNActFn(torch.autograd.Function):
         ctx.dy2_slot = [] if out2 is not None else None
         ctx.set_materialize_grads(False)
         ctx.act, ctx.mask, ctx.pg = act, mask, pg
+        # SyncBN: the consumer conv's backward may issue this node's gradient all-reduce early,
+        # between its data and weight gradients (syncbn_bwd_early), and park it here
+        ctx.early = [] if pg is not None else None
         ctx.batch_stats = use_batch_stats
         ctx.has_res = residual is not None
         # residual add whose residual is the input of an upstream routed conv (DDRNet's RB, ResNet
@@ -136,10 +139,17 @@ class _BNActFn(torch.autograd.Function):
         want_dres = ctx.has_res and ctx.needs_input_grad[3]
         want_dw = ctx.has_w and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
         if ctx.pg is not None:
-            bsums = ops().bn_bwd_sums(dy, x, y, mi, ss, ctx.act, mask, dy2)
-            if want_dw:
-                local = bsums.clone()
-            dist.all_reduce(bsums, group=ctx.pg)
+            early = ctx.early.pop() if ctx.early else None
+            if early is not None:
+                key, e_sums, e_local, work = early
+                work.wait()
+                if dy is not None and dy2 is None and dy.data_ptr() == key:
+                    bsums, local = e_sums, e_local  # reduced while the consumer's wgrad ran
+            if bsums is None:
+                bsums = ops().bn_bwd_sums(dy, x, y, mi, ss, ctx.act, mask, dy2)
+                if want_dw:
+                    local = bsums.clone()
+                dist.all_reduce(bsums, group=ctx.pg)
         dx, dres, dw, db = ops().bn_backward(dy, x, y, bsums, sums, mi, ss, weight, ctx.act,
                                              mask, want_dres, ctx.batch_stats, want_dw, None, dy2)
         if local is not None:
@@ -153,6 +163,34 @@ class _BNActFn(torch.autograd.Function):
             dres = None
         return (dx, dw if want_dw else None, db if want_dw else None,
                 dres if want_dres else None, None, None, None, None, None, None, None)
+
+
+EARLY_ISSUED = [0]  # SyncBN backward all-reduces issued early by a consumer conv (tests)
+
+
+def syncbn_bwd_early(node, dy: torch.Tensor) -> bool:
+    """Issue SyncBN node ``node``'s backward all-reduce now, asynchronously, from the backward
+    of the conv that consumes the BN output (ops/conv.py, right after its data gradient ``dy``
+    is computed and before its weight gradient): the RCCL round trip then runs under that wgrad
+    instead of stalling the stream between ``bn_bwd_sums`` and the dx kernel of every SyncBN layer
+    (reference utils/parallel.py:34-43 runs torch's SyncBatchNorm, whose backward all-reduce is
+    synchronous).  ``_BNActFn.backward`` waits on it and uses it only if the gradient it receives
+    is exactly ``dy`` (the conv was the output's only consumer); otherwise it recomputes.  Every
+    rank takes the same decisions (same graph), so the collectives stay matched."""
+    early = getattr(node, "early", None)
+    if early is None or early or getattr(node, "dy2_slot", None) is not None or node.pg is None:
+        return False
+    x, y, mi, ss, _, _ = node.saved_tensors
+    if (dy.dtype != x.dtype or dy.shape != x.shape or dy.data_ptr() % 16
+            or not dy.is_contiguous(memory_format=torch.channels_last)):
+        return False
+    bsums = ops().bn_bwd_sums(dy, x, y, mi, ss, node.act, node.mask, None)
+    want_dw = node.has_w and (node.needs_input_grad[1] or node.needs_input_grad[2])
+    local = bsums.clone() if want_dw else None
+    work = dist.all_reduce(bsums, group=node.pg, async_op=True)
+    early.append((dy.data_ptr(), bsums, local, work))
+    EARLY_ISSUED[0] += 1
+    return True
 
 
 def eval_coeffs(bn):

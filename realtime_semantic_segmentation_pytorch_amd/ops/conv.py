@@ -490,6 +490,10 @@ class _ConvFn(torch.autograd.Function):
         ctx.in_key = (x.data_ptr(), tuple(x.shape), x.dtype)
         ctx.addend_slot = None
         ctx.wdtype = weight.dtype
+        # a multi-rank SyncBN node that produced x: its backward all-reduce is issued from this
+        # node's backward, between dgrad and wgrad (ops.bn.syncbn_bwd_early)
+        prod = x.grad_fn
+        ctx.bn_node = prod if getattr(prod, "early", None) is not None else None
         if part is not None:
             ctx.mark_non_differentiable(part)
         # the statistics slab never gets a gradient: without this autograd would allocate and
@@ -503,13 +507,21 @@ class _ConvFn(torch.autograd.Function):
             return None, None, None, None
         x, wk = ctx.saved_tensors
         addend = ctx.addend_slot.pop() if ctx.addend_slot else None
+        node, ctx.bn_node = ctx.bn_node, None
+        on_dx = None
+        if node is not None:
+            from .bn import syncbn_bwd_early
+
+            def on_dx(dx):
+                syncbn_bwd_early(node, dx)
         dx, dw = _conv_bwd(x, wk, ctx.conv, ctx.key, dy, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
-                           ctx.wdtype, addend)
+                           ctx.wdtype, addend, on_dx)
         return dx, dw, None, None
 
 
-def _conv_bwd(x, wk, conv, key, dy, want_dx, want_dw, wdtype, addend=None):
-    """(dx (+ addend) | None, dw | None) of a routed conv."""
+def _conv_bwd(x, wk, conv, key, dy, want_dx, want_dw, wdtype, addend=None, on_dx=None):
+    """(dx (+ addend) | None, dw | None) of a routed conv.  ``on_dx(dx)`` runs between the data
+    and the weight gradient (the early SyncBN all-reduce of the producer BN)."""
     stride, padding, dilation = _geom(conv)
     dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     if dy.data_ptr() % 16:
@@ -519,6 +531,8 @@ def _conv_bwd(x, wk, conv, key, dy, want_dx, want_dw, wdtype, addend=None):
         dx = _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend)
     elif addend is not None:
         dx = addend
+    if on_dx is not None and want_dx:
+        on_dx(dx)  # dx is the input's whole gradient (a handed-off residual gradient included)
     if want_dw:
         dw = _wgrad(x, dy, wk, conv, key, stride, padding, dilation)
         if dw.dtype != wdtype:
