@@ -285,7 +285,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32" if a.fp32 else "bf16",
-            "data": "synthetic (device-resident random 1024x2048 images, blocky 19-class masks, "
+            "data": f"synthetic (device-resident random {a.height}x{a.width} images, blocky 19-class masks, "
                     "random-init weights)",
             "config": {"model": a.arch if a.model == "ddrnet" else f"{a.model}-{a.arch}" if a.model in (
                            "stdc", "ppliteseg") else a.model,

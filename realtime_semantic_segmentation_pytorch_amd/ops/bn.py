@@ -109,7 +109,8 @@ class _BNActFn(torch.autograd.Function):
         ctx.act, ctx.mask, ctx.pg = act, mask, pg
         # SyncBN: the consumer conv's backward may issue this node's gradient all-reduce early,
         # between its data and weight gradients (syncbn_bwd_early), and park it here
-        ctx.early = [] if pg is not None else None
+        ctx.early = [] if pg is not None and not getattr(bn, "_rtseg_no_early", False) else None
+        ctx.bn_module = bn if pg is not None else None
         ctx.batch_stats = use_batch_stats
         ctx.has_res = residual is not None
         # residual add whose residual is the input of an upstream routed conv (DDRNet's RB, ResNet
@@ -145,6 +146,10 @@ class _BNActFn(torch.autograd.Function):
                 work.wait()
                 if dy is not None and dy2 is None and dy.data_ptr() == key:
                     bsums, local = e_sums, e_local  # reduced while the consumer's wgrad ran
+                else:
+                    # the output had another consumer (its gradient is a sum): this site never
+                    # issues early again -- every rank sees the same graph, so decides the same
+                    ctx.bn_module._rtseg_no_early = True
             if bsums is None:
                 bsums = ops().bn_bwd_sums(dy, x, y, mi, ss, ctx.act, mask, dy2)
                 if want_dw:

@@ -64,6 +64,7 @@ class _DWConvFn(torch.autograd.Function):
         ctx.geom = geom
         ctx.has_bias = bias is not None
         ctx.wdtype = weight.dtype
+        ctx.wparam = weight  # its strides: DDP's gradient bucket views want them (like_param)
         ctx.save_for_backward(x, wt)
         if not stats:
             return y
@@ -83,7 +84,9 @@ class _DWConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = ops().dw_conv_dgrad(dy, wt, x.shape[1], x.shape[2], x.shape[3], kh, kw, sh, sw, ph, pw, dh, dw)
         if ctx.needs_input_grad[1]:
-            dwt = ops().dw_conv_wgrad(dy, x, kh, kw, sh, sw, ph, pw, dh, dw).to(ctx.wdtype)
+            from .conv import like_param
+
+            dwt = like_param(ops().dw_conv_wgrad(dy, x, kh, kw, sh, sw, ph, pw, dh, dw).to(ctx.wdtype), ctx.wparam)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = channel_sum(dy)
         return dx, dwt, db, None, None

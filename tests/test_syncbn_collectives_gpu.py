@@ -5,7 +5,9 @@ Per step, for DDRNet-23-slim + aux head (reference wiring utils/parallel.py:34-4
 * exactly ONE forward SyncBN all-reduce ([2C+1] fp64 sums) and ONE backward all-reduce ([2C])
   per SyncBatchNorm layer, all on the SyncBN process group (parallel/ddp.py:syncbn_group);
 * the backward ones mostly issued early, asynchronously, from the consumer conv's backward
-  (ops.bn.syncbn_bwd_early) -- counted, and required to be > 0;
+  (ops.bn.syncbn_bwd_early) -- counted, and required to be > 0.  A site whose output turns out to
+  have a second consumer wastes its early reduction once (step 1) and never issues early again;
+
 * DDP gradient buckets: every gradient element reduced exactly once per step, in a fixed number
   of buckets no larger than the configured cap allows (counted through a DDP comm hook).
 """
@@ -19,7 +21,7 @@ import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
 
-SIZE, BS, STEPS, BUCKET_MB = (128, 256), 2, 3, 1
+SIZE, BS, STEPS, BUCKET_MB = (128, 256), 2, 4, 1
 
 
 def _port():
@@ -118,11 +120,16 @@ def test_syncbn_and_ddp_collectives_per_step(tmp_path):
     r = res[0]
     print(r)
     cap = BUCKET_MB * 2 ** 20
-    for st in r["per_step"]:
+    for i, st in enumerate(r["per_step"]):
         assert st["fwd"] == r["n_sbn"], st
-        assert st["bwd"] == r["n_sbn"], st
-        assert st["other"] == 0, st  # nothing else all-reduces through Python in a train step
         assert st["early"] > 0, st
         assert st["bucket_numel"] == r["n_grad"], st  # every gradient element exactly once
-        assert st["buckets"] <= math.ceil(r["grad_bytes"] / cap) + 2, st
-    assert len({st["buckets"] for st in r["per_step"]}) == 1
+        # the DDP allreduce hook's own dist.all_reduce calls (one per bucket): nothing else
+        # all-reduces through Python in a train step
+        assert st["other"] == st["buckets"], st
+        if i >= 1:  # after step 1's waste (see docstring): one backward all-reduce per layer
+            assert st["bwd"] == r["n_sbn"], st
+    # DDP rebuilds its buckets from the observed gradient order after the first iterations;
+    # from then on a fixed count within what the cap allows
+    late = r["per_step"][-2:]
+    assert late[0]["buckets"] == late[1]["buckets"] <= math.ceil(r["grad_bytes"] / cap) + 2, late
