@@ -25,6 +25,8 @@
 //  * Backward recomputes the softmax per pixel, weights it by the device-side
 //    selection rule, and reduces the transpose of the bilinear map through LDS
 //    (row pass, then column pass); only block-border cells use global atomics.
+#include <cstdlib>
+
 #include "rtseg_common.h"
 #include "rtseg_launch.h"
 
@@ -529,6 +531,152 @@ __global__ void __launch_bounds__(256) seg_ce_bwd_tile(
   }
 }
 
+// Upsampled geometry, class count known at compile time (Cityscapes' 19): the "run" form.
+// Every output pixel has ONE left horizontal tap x0; the ~1/scale pixels of an output row
+// that share x0 = j (a run) also share their right tap x1 and the row's two vertical taps.
+// One thread per (output row r, run j) -- the tile is sized so that TH x BW <= 256 threads:
+//   * the tile's per-pixel (weight, lse, label) are staged to LDS first, coalesced, so the
+//     run loop below issues no global loads;
+//   * the thread reads the run's 4 x C tap logits from LDS once and folds them vertically into
+//     u_c = lerp_y(L[y0][j], L[y1][j]) and d_c = lerp_y(L[y0][x1], L[y1][x1]) - u_c (registers);
+//   * per pixel of the run: z_c = u_c + lx * d_c (one FMA), G_c = w (exp(z_c - lse) - [c == y]),
+//     A0_c += (1 - lx) G_c, A1_c += lx G_c -- every pixel's softmax is computed exactly once;
+//   * stores A0 to R[c][r][j]; after a barrier adds A1 (still in registers) to R[c][r][x1]:
+//     runs of one row have distinct x1, so no two threads write one cell in either phase;
+//   * the column pass folds R onto low-res rows (global atomics only for tile-border cells).
+// The round-4 form above visits every pixel from both of its columns (2 softmaxes per pixel),
+// re-interpolates 4 taps per class per visit from LDS and loads each pixel's loss / lse /
+// label inside its serial loop: 2.05 ms per DDRNet-23 step (profiles/r5_start_prof).
+template <typename T, int TH, int TW, int NC>
+__global__ void __launch_bounds__(256) seg_ce_bwd_run(
+    const T* __restrict__ x, LossGeo g, int ignore,
+    const float* __restrict__ cw, const float* __restrict__ pix_loss,
+    const float* __restrict__ pix_lse, const double* __restrict__ stats, int mode,
+    const float* __restrict__ grad_out, float* __restrict__ gacc, int64_t asn, int64_t asc,
+    int64_t ash, int64_t asw) {
+  static_assert(NC > 0, "run form needs the class count at compile time");
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  __shared__ int tx0[TW], tx1[TW], ty0[TH], ty1[TH], jlo[TW + 4], jhi[TW + 4];  // BW <= TW + 2
+  __shared__ float tlx[TW], tly[TH];
+  __shared__ float2 pwl[TH * TW];  // per tile pixel: (gradient weight, lse)
+  __shared__ uint8_t plab[TH * TW];
+  const TileGeo t = tile_geo<TH, TW>(g);
+  const int BW = t.BW, RS = BW | 1;
+  const int nx = t.ox1 - t.ox0 + 1, ny = t.oy1 - t.oy0 + 1;
+  float* L = sm;                          // [BH][BW][CP]
+  float* R = L + t.BH * t.BW * t.CP;      // [TH][BW][NC]: classes innermost (conflict-free)
+  for (int k = threadIdx.x; k < TW; k += blockDim.x) {
+    int a0, a1; float l;
+    g.mw.map(min(t.ox0 + k, t.ox1), a0, a1, l);
+    tx0[k] = a0 - t.bx0; tx1[k] = a1 - t.bx0; tlx[k] = l;
+  }
+  for (int k = threadIdx.x; k < TH; k += blockDim.x) {
+    int a0, a1; float l;
+    g.mh.map(min(t.oy0 + k, t.oy1), a0, a1, l);
+    ty0[k] = a0 - t.by0; ty1[k] = a1 - t.by0; tly[k] = l;
+  }
+  {
+    const SelRule rule = load_rule(stats, mode);
+    const float go = *grad_out;
+    for (int p = threadIdx.x; p < TH * TW; p += blockDim.x) {
+      const int r = p / TW, k = p - (p / TW) * TW;
+      float w = 0.f, lse = 0.f;
+      int64_t y = 0;
+      if (r < ny && k < nx) {
+        const int oy = t.oy0 + r, ox = t.ox0 + k;
+        const int64_t pi = (static_cast<int64_t>(t.n) * g.oh + oy) * g.ow + ox;
+        y = label_at(g, t.n, oy, ox);
+        w = pixel_weight(rule, pix_loss[pi], y, ignore, NC, cw) * go;
+        lse = pix_lse[pi];
+      }
+      pwl[p] = make_float2(w, lse);
+      plab[p] = static_cast<uint8_t>(w != 0.f ? y : 0);  // w != 0 implies 0 <= y < NC <= 255
+    }
+  }
+  for (int j = threadIdx.x; j < TW + 4; j += blockDim.x) { jlo[j] = nx; jhi[j] = -1; }
+  stage_logits<T, TH, NC>(x, g, t, L, nullptr, false);  // syncs: tables and pixels visible too
+  // the run of each low-res column: tile columns k with x0(k) == j (x0 is monotone in k), from
+  // the run boundaries -- one thread per tile column
+  for (int k = threadIdx.x; k < nx; k += blockDim.x) {
+    const int j = tx0[k];
+    if (k == 0 || tx0[k - 1] != j) jlo[j] = k;
+    if (k == nx - 1 || tx0[k + 1] != j) jhi[j] = k;
+  }
+  __syncthreads();
+  // one item per thread (launcher: TH * BW <= blockDim)
+  const int rj = threadIdx.x;
+  const bool item = rj < TH * BW;
+  const int r = item ? rj / BW : 0, j = item ? rj - (rj / BW) * BW : 0;
+  float a0[NC], a1[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) { a0[c] = 0.f; a1[c] = 0.f; }
+  int j1 = j;
+  if (item && r < ny && jlo[j] <= jhi[j]) {
+    j1 = tx1[jlo[j]];
+    const float ly = tly[r];
+    const float* q00 = L + (ty0[r] * t.BW + j) * t.CP;
+    const float* q10 = L + (ty1[r] * t.BW + j) * t.CP;
+    const float* q01 = L + (ty0[r] * t.BW + j1) * t.CP;
+    const float* q11 = L + (ty1[r] * t.BW + j1) * t.CP;
+    float u[NC], d[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const float left = q00[c] + ly * (q10[c] - q00[c]);
+      const float right = q01[c] + ly * (q11[c] - q01[c]);
+      u[c] = left;
+      d[c] = right - left;
+    }
+    for (int k = jlo[j]; k <= jhi[j]; ++k) {
+      const float2 wl = pwl[r * TW + k];
+      if (wl.x == 0.f) continue;
+      const int y = plab[r * TW + k];
+      const float lx = tlx[k];
+      const float wa = wl.x * (1.f - lx), wb = wl.x * lx;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const float gc = __expf(fmaf(lx, d[c], u[c]) - wl.y) - (c == y ? 1.f : 0.f);
+        a0[c] = fmaf(wa, gc, a0[c]);
+        a1[c] = fmaf(wb, gc, a1[c]);
+      }
+    }
+  }
+  if (j1 == j) {  // no right column (empty run, or the clamped last low-res column)
+#pragma unroll
+    for (int c = 0; c < NC; ++c) { a0[c] += a1[c]; a1[c] = 0.f; }
+  }
+  if (item) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) R[(r * RS + j) * NC + c] = a0[c];
+  }
+  __syncthreads();
+  if (item && j1 != j) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) R[(r * RS + j1) * NC + c] += a1[c];
+  }
+  __syncthreads();
+  // column pass: fold output rows onto low-res rows, accumulate globally.  Classes fastest
+  // across lanes: a wave's atomics then cover contiguous channels-last cells (64 x 4 B runs)
+  // instead of one 4-B add per 76-B pixel row
+  for (int cj = threadIdx.x; cj < NC * BW; cj += blockDim.x) {
+    const int jj = cj / NC, c = cj - (cj / NC) * NC;
+    float* dst = gacc + t.n * asn + c * asc + t.by0 * ash + (t.bx0 + jj) * asw;
+    int ic = ty0[0];
+    float a = 0.f, b = 0.f;
+    for (int rr = 0; rr < ny; ++rr) {
+      const int i0 = ty0[rr];
+      while (ic < i0) {
+        if (a != 0.f) atomicAdd(dst + static_cast<int64_t>(ic) * ash, a);
+        a = b; b = 0.f; ++ic;
+      }
+      const float v = R[(rr * RS + jj) * NC + c];
+      if (ty1[rr] == i0) a += v;
+      else { const float l = tly[rr]; a += (1.f - l) * v; b += l * v; }
+    }
+    if (a != 0.f) atomicAdd(dst + static_cast<int64_t>(ic) * ash, a);
+    if (b != 0.f && ic + 1 < t.BH) atomicAdd(dst + static_cast<int64_t>(ic + 1) * ash, b);
+  }
+}
+
 // fp32 accumulator (same strides as the gradient tensor) -> gradient dtype
 template <typename G>
 __global__ void __launch_bounds__(256) cast_out_kernel(const float* __restrict__ acc,
@@ -643,6 +791,20 @@ void launch_seg_loss_fwd(const SegLossArgs& a, hipStream_t st) {
 }
 
 template <typename T, int TH, int TW, int NC>
+static void bwd_run(const SegLossArgs& a, const LossGeo& g, const float* grad_out, hipStream_t st) {
+  const int bh = static_cast<int>((TH - 1) * g.mh.scale) + 3;
+  const int bw = static_cast<int>((TW - 1) * g.mw.scale) + 3;
+  const size_t lds = sizeof(float) * (static_cast<size_t>(bh) * bw * (g.c | 1) +
+                                      static_cast<size_t>(g.c) * TH * (bw | 1));
+  auto k = seg_ce_bwd_run<T, TH, TW, NC>;
+  allow_lds(k, lds);
+  k<<<tiles_of<TH, TW>(g), 256, lds, st>>>(
+      static_cast<const T*>(a.logits.data), g, a.ignore_index, a.class_weight,
+      a.pix_loss, a.pix_lse, a.stats, a.mode, grad_out, a.acc, a.acc_sn, a.acc_sc, a.acc_sh,
+      a.acc_sw);
+}
+
+template <typename T, int TH, int TW, int NC>
 static void bwd_tile(const SegLossArgs& a, const LossGeo& g, const float* grad_out,
                      hipStream_t st) {
   const int bh = static_cast<int>((TH - 1) * g.mh.scale) + 3;
@@ -677,6 +839,9 @@ static void bwd_t(const SegLossArgs& a, const LossGeo& g, const float* grad_out,
   const bool fine = (g.mh.scale > 0.2f || g.mw.scale > 0.2f) && g.mh.scale <= 1.f && g.mw.scale <= 1.f;
   if (g.c == 19) {
     if (fine) bwd_tile<T, 8, 64, 19>(a, g, grad_out, st);
+    else if ((static_cast<int>(127 * g.mw.scale) + 3) * 14 <= 256 &&
+             (std::getenv("RTSEG_LOSS_BWD_RUN") == nullptr || std::getenv("RTSEG_LOSS_BWD_RUN")[0] != '0'))
+      bwd_run<T, 14, 128, 19>(a, g, grad_out, st);  // one (row, run) item per thread; =0: round-4 form
     else bwd_tile<T, 16, 128, 19>(a, g, grad_out, st);
   } else if (g.c <= 32) {
     if (fine) bwd_tile<T, 8, 64, 0>(a, g, grad_out, st);

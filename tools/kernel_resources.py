@@ -10,7 +10,7 @@ def main():
     src = sys.argv[1]
     filt = sys.argv[2] if len(sys.argv) > 2 else ""
     inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(src))), "include")
-    out = subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-I" + inc, "-c", src, "-o",
+    out = subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++20", "-I" + inc, "-c", src, "-o",
                           "/tmp/_kr.o", "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True)
     if out.returncode:
         sys.exit(out.stderr[-3000:])
