@@ -22,6 +22,8 @@
 // residual -- from a bit mask the forward wrote next to y (kMaskBits: one byte per
 // V-channel vector, bit j = activation derivative of channel c0+j is 1), which replaces
 // the 2-byte-per-element re-read of y in both backward passes by 1/8 byte.
+#include <cstdlib>
+
 #include "rtseg_common.h"
 #include "rtseg_launch.h"
 
@@ -931,6 +933,14 @@ static bool bn_flat(int dtype, int C) { return dtype != kF16 && C >= 3 && (C & 1
 
 static int64_t round_up_to(int64_t g, int m) { return (g + m - 1) / m * m; }
 
+// Grid caps of the streaming passes (RTSEG_BN_APPLY_CAP / RTSEG_BN_REDUCE_CAP: A/B of the
+// block counts, tools/bench_bn_bw.py; read once)
+static int64_t env_cap(const char* name, int64_t dflt) {
+  const char* v = std::getenv(name);
+  const long long x = v ? std::atoll(v) : 0;
+  return x > 0 ? x : dflt;
+}
+
 int bn_partial_grid(int64_t M, int C, int dtype) {
   if (bn_flat(dtype, C)) {  // ~16 chunks per thread, <= ~1024 blocks, a multiple of C blocks
     const int64_t chunks = M * C / (dtype == kF32 ? 4 : 8);
@@ -943,7 +953,10 @@ int bn_partial_grid(int64_t M, int C, int dtype) {
   int64_t g = (M + static_cast<int64_t>(rpi) * 32 - 1) / (static_cast<int64_t>(rpi) * 32);
   // 4 blocks (16 waves) per CU: with 4 rows (8 x 16-B loads) in flight per lane that keeps
   // ~64 KiB of reads outstanding per CU, what HBM3E latency x bandwidth needs
-  if (g > 1024) g = 1024;
+  // cap 2048 (8 blocks per CU): the backward reduce of the 537 MB / 268 MB / 134 MB DDRNet-23 layers
+  // 925 -> 769 / 255 -> 233 / 135 -> 127 us vs 1024 (profiles/r5_bn_caps)
+  static const int64_t cap = env_cap("RTSEG_BN_REDUCE_CAP", 2048);
+  if (g > cap) g = cap;
   if (g < 1) g = 1;
   return static_cast<int>(g);
 }
@@ -1011,7 +1024,9 @@ void launch_bn_eval_coeffs(int C, const float* w, const float* b, const float* r
 
 static int apply_grid(int64_t work) {
   int64_t g = (work + 511) / 512;  // two vectors per thread
-  const int64_t cap = 256 * 8;
+  // cap 1024 (4 blocks per CU): forward apply / backward apply of the 537 MB layer 906 -> 859 / 2209 ->
+  // 2124 us, residual + bit-mask variants 3-7 % faster than at 2048 (profiles/r5_bn_caps)
+  static const int64_t cap = env_cap("RTSEG_BN_APPLY_CAP", 1024);
   if (g > cap) g = cap;
   if (g < 1) g = 1;
   return static_cast<int>(g);

@@ -806,11 +806,50 @@ def conv_bn_act_eval(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, act_code: 
     return ours()
 
 
+def stem_infer_ok(conv: nn.Module, x: torch.Tensor) -> bool:
+    """A 3-channel 3 x 3 stem conv (pad 1, stride 1 / 2, <= 64 outputs, even W) in bf16 inference:
+    MIOpen runs these channels-last as ``naive_conv_ab_nonpacked_fwd_nhwc`` (~0.5 ms per 512 x
+    1024 image: 18-30 % of DFANet's / ESPNetv2's / FastSCNN's bf16 inference, profiles/r4_end/infer)."""
+    return (conv.in_channels == 3 and conv.groups == 1 and tuple(conv.kernel_size) == (3, 3)
+            and tuple(conv.padding) == (1, 1) and tuple(conv.dilation) == (1, 1)
+            and tuple(conv.stride) in ((1, 1), (2, 2)) and conv.out_channels <= 64 and x.dim() == 4
+            and x.shape[1] == 3 and x.shape[3] % 2 == 0 and conv.padding_mode == "zeros"
+            and os.environ.get("RTSEG_CONV_STEM", _STEM_DEFAULT) != "0")
+
+
+def _stem_infer(x: torch.Tensor, conv: nn.Module, bias) -> torch.Tensor:
+    """``conv(x)`` on ``conv_stem.hip``: the weight zero-padded to the kernel's 16-channel
+    granularity (cached, krsc bf16), the real channels sliced back out."""
+    cout = conv.out_channels
+    cp = -(-cout // 16) * 16
+
+    def make(w):
+        w = w.to(torch.bfloat16)
+        if cp != cout:
+            w = F.pad(w, (0, 0, 0, 0, 0, 0, 0, cp - cout))
+        return w.permute(0, 2, 3, 1).contiguous()
+
+    wk = _cached(conv, "_rtseg_stem_wk", make)
+    x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    if x.data_ptr() % 16:
+        x = x.clone(memory_format=torch.channels_last)
+    stride, padding, dilation = _geom(conv)
+    y, _ = ops().conv_stem(x, wk, stride, padding, dilation, False)
+    if cp != cout:
+        y = y[:, :cout].contiguous(memory_format=torch.channels_last)
+    if bias is not None:
+        y = y + bias.to(y.dtype).view(1, -1, 1, 1)
+    return y
+
+
 def conv_forward(x: torch.Tensor, conv: nn.Module) -> torch.Tensor:
     """``conv(x)``; in bf16-autocast inference the bf16 weight copy is cached on the module
-    (autocast would re-cast the fp32 weight -- one extra kernel per conv -- every forward)."""
+    (autocast would re-cast the fp32 weight -- one extra kernel per conv -- every forward), and
+    3-channel stem convs run on ``conv_stem.hip`` instead of MIOpen's naive NHWC kernel."""
     if (type(conv) in _ROUTED and not conv.training and not torch.is_grad_enabled() and x.is_cuda
             and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+        if stem_infer_ok(conv, x) and use_hip(x, "conv") and _mode() != "0":
+            return _stem_infer(x, conv, conv.bias)
         w = conv.weight
         key = (w.data_ptr(), w._version, write_generation(),
                None if conv.bias is None else (conv.bias.data_ptr(), conv.bias._version))

@@ -24,7 +24,7 @@ import torch.nn.functional as F
 
 from .bn import channel_sum
 from .dilated import pruned_conv2d
-from ._ext import ops, use_hip
+from ._ext import ops, use_hip, write_generation
 
 _DTYPES = (torch.float32, torch.bfloat16, torch.float16)
 
@@ -44,6 +44,24 @@ def _channels_inner(x: torch.Tensor) -> bool:
     return x.is_contiguous(memory_format=torch.channels_last) or (x.stride(1) == 1 and x.stride(2) == x.stride(3) * x.shape[3])
 
 
+def _dw_weight(weight: torch.Tensor, cout: int, taps: int) -> torch.Tensor:
+    """fp32 [taps, Cout] weight the kernels read, cached on the parameter while its storage,
+    version and the raw-pointer write generation (fused optimizer, BN finalize) are unchanged:
+    an inference forward (bf16 weights in the HIP-graph engine) no longer casts and transposes
+    every depth-wise weight per call (126 cast + 126 copy kernels per DFANet forward,
+    tools/probe_casts.py)."""
+    key = (weight.data_ptr(), weight._version, write_generation(), weight.dtype)
+    hit = getattr(weight, "_rtseg_dw_wt", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    wt = weight.detach().float().reshape(cout, taps).t().contiguous()
+    try:
+        weight._rtseg_dw_wt = (key, wt)
+    except (AttributeError, RuntimeError):  # a non-leaf view cannot carry attributes
+        pass
+    return wt
+
+
 class _DWConvFn(torch.autograd.Function):
     """y = depth-wise conv(x); with ``stats`` also the BN-statistics slab of y (fp32 [rows, 2C],
     produced in the forward kernel's epilogue; ``ops.bn_act(..., part=slab)`` consumes it)."""
@@ -51,7 +69,7 @@ class _DWConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, geom, stats=False):
         cout, kh, kw, sh, sw, ph, pw, dh, dw = geom
-        wt = weight.detach().float().reshape(cout, kh * kw).t().contiguous()
+        wt = _dw_weight(weight, cout, kh * kw)
         b = bias.detach().float().contiguous() if bias is not None else None
         x = _cl_aligned(x)
         part = None

@@ -174,3 +174,27 @@ def test_twin_conv_node_in_graph(monkeypatch):
         names.add(type(fn).__name__)
         stack.extend(f for f, _ in fn.next_functions)
     assert any("TwinConvFn" in n for n in names), names
+
+
+@pytest.mark.parametrize("cout,stride,bias", [(8, 2, False), (3, 1, True), (32, 2, False), (19, 1, True)])
+def test_stem_inference_path(cout, stride, bias):
+    """bf16 inference of a 3-channel stem conv (ops.conv_forward -> conv_stem.hip, weight zero-padded
+    to 16 channels and cached) == F.conv2d on the same bf16 operands in fp32, for output counts the
+    kernel does not tile natively (DFANet's 3 -> 8, ESPNetv2's 3 -> 3)."""
+    from realtime_semantic_segmentation_pytorch_amd.ops import conv as conv_mod
+
+    g = torch.Generator().manual_seed(cout)
+    conv = torch.nn.Conv2d(3, cout, 3, stride, 1, bias=bias).to(DEV).eval()
+    conv.__class__ = ops.RoutedConv2d if not bias else ops.PrunedConv2d
+    x = torch.randn(2, 3, 34, 66, generator=g).to(DEV).contiguous(memory_format=torch.channels_last)
+    assert conv_mod.stem_infer_ok(conv, x)
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        y = ops.conv_forward(x, conv)
+        y2 = ops.conv_forward(x, conv)  # the cached weight
+    xb, wb = x.to(torch.bfloat16).float(), conv.weight.to(torch.bfloat16).float()
+    ref = F.conv2d(xb, wb, None, stride, 1)
+    if bias:
+        ref = ref + conv.bias.to(torch.bfloat16).float().view(1, -1, 1, 1)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=2e-2)
+    assert torch.equal(y, y2)
