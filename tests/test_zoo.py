@@ -122,7 +122,7 @@ def check_zoo_hip_matches_torch_path(key, monkeypatch):
       depth-wise convs, pooling, interpolation, gating, activations, the loss -- must be within
       10x the CPU fp32 error (floor 1e-3);
     * batch-statistics BatchNorm at batch 2: within 4x the better of the two yardsticks, or 1.5x
-      either one (floor 1e-3).  Where even CPU fp32 is > 0.1 off fp64 (DFANet, Lite-HRNet, MiniNetV2: BN over a
+      the worse, or the flip envelope of a batch-2 BN sign flip (``TRAIN_BN_FLIP_FLOOR``).  Where even CPU fp32 is > 0.1 off fp64 (DFANet, Lite-HRNet, MiniNetV2: BN over a
       handful of values at batch 2, gradients of ~1e8), the step is only checked for finite
       gradients; the frozen pass above still pins their numerics."""
     torch.manual_seed(0)
@@ -171,17 +171,16 @@ def check_zoo_hip_matches_torch_path(key, monkeypatch):
         print(tag)
         assert abs(l_h.item() - l_r.item()) <= max(4 * min(abs(l_t.item() - l_r.item()), abs(l_c.item() - l_r.item())),
                                                    1e-3 * abs(l_r.item())), tag
-        # batch-2 statistics amplify summation order: stock paths are up to ~1e-2 off fp64 here
-        # (MI355X, BiSeNetV2: CPU fp32 1.0e-2, GPU torch 1.7e-2 .. 7.7e-2 run to run).  The HIP
-        # path must be within 4x the better yardstick, or no worse than 1.5x either stock run on
-        # its own: the deterministic CPU fp32 run (SwiftNet: GPU torch 6e-6 vs CPU 6.7e-3), or
-        # the stock GPU run, which shares the fp32 MIOpen convs with the HIP path -- their
-        # solver picks vary from process to process, and both paths move together (MiniNet:
-        # HIP = GPU torch = 8.8e-4 in one run, 8e-7 in another; PP-LiteSeg 3.3e-3 / 5.5e-3 vs
-        # 3.2e-4 / 3.7e-4).  Since round 5 the BN statistics are shifted, compensated one-pass
-        # moments (csrc/kernels/bn_act.hip): DDRNet 1.2e-5 (CPU 1.1e-5; round 4: 3.5e-3),
-        # profiles/r5_numerics.
-        assert hg <= max(4 * min(tg, cg), 1.5 * cg, 1.5 * tg, 1e-3), tag
+        # batch-2 batch statistics make this step ill-conditioned: a BN over 2 values per channel
+        # (DDRNet's DAPPM global branch, BiSeNetV2's context block) normalises to +-d/sqrt(d^2 +
+        # eps), and where d is rounding-sized the sign -- which sample passes its ReLU -- flips
+        # with the last bits of upstream sums.  Such a flip moves the whole gradient by
+        # ~3.5e-3 (DDRNet) in ANY path: on identical inputs the stock GPU path gave 1.5e-5 in one
+        # process and 3.46e-3 in the next, the HIP path 1.2e-5 or 3.47e-3, and at batch 4 even
+        # CPU fp32 shows 3.05e-3 (tools/probe_param_err.py, profiles/r5_numerics).  So the HIP
+        # path must be within 4x the better yardstick, or 1.5x the worse one, or the measured
+        # flip envelope; the frozen-BN pass above pins every kernel's precision without flips.
+        assert hg <= max(4 * min(tg, cg), 1.5 * max(tg, cg), TRAIN_BN_FLIP_FLOOR), tag
 
 
 def _run_gpu_bf16(m, x, labels, disable_hip, monkeypatch, phase=None):
@@ -209,6 +208,10 @@ def _check_bf16_vs_fp64(key, base, xg, labels, l_r, g_r, cat, err, monkeypatch):
     assert bg <= max(ZOO_BF16_GRAD_SLACK * sg, ZOO_BF16_GRAD_FLOOR), tag
     assert bl <= max(ZOO_BF16_LOSS_SLACK * sl, 2e-3 * abs(l_r.item())), tag
 
+
+# a sign flip of a batch-2 BatchNorm over 2 values (see check_zoo_hip_matches_torch_path): the
+# gradient error one flip leaves on DDRNet-23, measured on the stock GPU path too (3.46e-3)
+TRAIN_BN_FLIP_FLOOR = 4e-3
 
 # HIP bf16 vs stock bf16 distance to fp64 (frozen BN, 128 x 256, batch 2).  Round 5 on MI355X: HIP
 # / stock between 0.14 (SwiftNet) and 1.14 (ENet), smallest stock 4.6e-3 (FastSCNN); the floor
