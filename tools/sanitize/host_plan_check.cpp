@@ -89,7 +89,7 @@ static void check_bn_plans() {
         if (flat) {
           CHECK(G >= C && G % C == 0 && G < 1024 + C, "bn flat grid M=%lld C=%d G=%d", static_cast<long long>(M), C, G);
         } else {
-          CHECK(G >= 1 && G <= 1024, "bn grid M=%lld C=%d G=%d", static_cast<long long>(M), C, G);
+          CHECK(G >= 1 && G <= 2048, "bn grid M=%lld C=%d G=%d", static_cast<long long>(M), C, G);  // RTSEG_BN_REDUCE_CAP default
         }
       }
     }
