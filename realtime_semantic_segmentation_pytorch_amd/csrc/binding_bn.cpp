@@ -240,18 +240,12 @@ at::Tensor bn_bwd_sums(const std::optional<at::Tensor>& dy, const at::Tensor& x,
   return bsums;
 }
 
-// backward: reduce (unless bsums given) + finalize + apply -> (dx, dres, dw, db)
-std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_backward(
-    const std::optional<at::Tensor>& dy, const at::Tensor& x, const std::optional<at::Tensor>& y,
+// backward, first half: reduce (unless bsums / slab given) + finalize -> (kcoef[3C], dw, db)
+std::tuple<at::Tensor, at::Tensor, at::Tensor> bwd_coeffs_impl(
+    const void* dyp, const Slice& g2, const at::Tensor& x, const void* yp,
     const std::optional<at::Tensor>& bsums, const std::optional<at::Tensor>& fwd_sums,
     const at::Tensor& mi, const at::Tensor& ss, const std::optional<at::Tensor>& w, int64_t act,
-    int64_t mask, bool want_dres, bool batch_stats, bool want_dw, const std::optional<at::Tensor>& slab,
-    const std::optional<at::Tensor>& grad2) {
-  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
-  check_cl(x, "x");
-  const Slice g2 = slice_of(grad2, x, "grad2");
-  const void* dyp = opt_dy(dy, g2);
-  const void* yp = opt_y(y, mask);
+    int64_t mask, bool batch_stats, bool want_dw, const std::optional<at::Tensor>& slab) {
   const int C = static_cast<int>(x.size(1));
   auto f32 = x.options().dtype(at::kFloat);
   at::Tensor part;
@@ -278,6 +272,24 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_backward(
                          fptr(w), mi.data_ptr<float>(), batch_stats ? 1 : 0, k.data_ptr<float>(),
                          want_dw ? dw.data_ptr<float>() : nullptr,
                          want_dw ? db.data_ptr<float>() : nullptr, cur_stream());
+  return {k, dw, db};
+}
+
+// backward: reduce (unless bsums given) + finalize + apply -> (dx, dres, dw, db)
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_backward(
+    const std::optional<at::Tensor>& dy, const at::Tensor& x, const std::optional<at::Tensor>& y,
+    const std::optional<at::Tensor>& bsums, const std::optional<at::Tensor>& fwd_sums,
+    const at::Tensor& mi, const at::Tensor& ss, const std::optional<at::Tensor>& w, int64_t act,
+    int64_t mask, bool want_dres, bool batch_stats, bool want_dw, const std::optional<at::Tensor>& slab,
+    const std::optional<at::Tensor>& grad2) {
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  check_cl(x, "x");
+  const Slice g2 = slice_of(grad2, x, "grad2");
+  const void* dyp = opt_dy(dy, g2);
+  const void* yp = opt_y(y, mask);
+  const int C = static_cast<int>(x.size(1));
+  auto [k, dw, db] = bwd_coeffs_impl(dyp, g2, x, yp, bsums, fwd_sums, mi, ss, w, act, mask, batch_stats,
+                                     want_dw, slab);
   at::Tensor dx = at::empty_like(x);
   at::Tensor dres;
   if (want_dres) dres = at::empty_like(x);
@@ -286,6 +298,21 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_backward(
                       dtype_code(x), rows_of(x), C, static_cast<int>(act), static_cast<int>(mask),
                       cur_stream(), g2.p, g2.ld);
   return {dx, dres, dw, db};
+}
+
+// backward without the apply pass -> (kcoef[3C], dw, db): the dx pass is done by the consumer of
+// dx instead (the stem conv's weight gradient, conv_stem_wgrad_bn)
+std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_bwd_coeffs(
+    const at::Tensor& dy, const at::Tensor& x, const std::optional<at::Tensor>& y,
+    const std::optional<at::Tensor>& bsums, const std::optional<at::Tensor>& fwd_sums,
+    const at::Tensor& mi, const at::Tensor& ss, const std::optional<at::Tensor>& w, int64_t act,
+    int64_t mask, bool batch_stats, bool want_dw) {
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  check_cl(x, "x");
+  check_cl(dy, "grad");
+  const Slice g2{nullptr, 0};
+  return bwd_coeffs_impl(dy.data_ptr(), g2, x, opt_y(y, mask), bsums, fwd_sums, mi, ss, w, act, mask,
+                         batch_stats, want_dw, std::nullopt);
 }
 
 }  // namespace
@@ -308,6 +335,9 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
   m.def("bn_backward(Tensor? grad, Tensor x, Tensor? y, Tensor? bsums, Tensor? fwd_sums, "
         "Tensor mean_invstd, Tensor scale_shift, Tensor? weight, int act, int mask, bool want_dres, "
         "bool batch_stats, bool want_dw, Tensor? slab=None, Tensor? grad2=None) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("bn_bwd_coeffs(Tensor grad, Tensor x, Tensor? y, Tensor? bsums, Tensor? fwd_sums, "
+        "Tensor mean_invstd, Tensor scale_shift, Tensor? weight, int act, int mask, bool batch_stats, "
+        "bool want_dw) -> (Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
@@ -319,4 +349,5 @@ TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
   m.impl("bn_apply_bits", &rtseg::bn_apply_bits);
   m.impl("bn_bwd_sums", &rtseg::bn_bwd_sums);
   m.impl("bn_backward", &rtseg::bn_backward);
+  m.impl("bn_bwd_coeffs", &rtseg::bn_bwd_coeffs);
 }

@@ -286,6 +286,43 @@ at::Tensor conv_stem_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t kh
   return dw;
 }
 
+// stem weight gradient with the following BN's backward apply fused (conv_stem.hip, BNF):
+// dy = gradient of act(BN(xb)), xb = this conv's output [N,Cout,Ho,Wo] CL bf16; kcoef [3 Cout],
+// mean_invstd / scale_shift [2 Cout] fp32 from the BN (ops/bn.py); act 0 none / 1 ReLU / 2 ReLU6
+at::Tensor conv_stem_wgrad_bn(const at::Tensor& x, const at::Tensor& dy, const at::Tensor& xb,
+                              const at::Tensor& kcoef, const at::Tensor& mean_invstd,
+                              const at::Tensor& scale_shift, int64_t act, int64_t kh, int64_t kw,
+                              at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
+                              bool channels_last) {
+  check_act(x, "input");
+  check_act(dy, "grad_output");
+  check_act(xb, "bn_input");
+  ConvGeom g = geom(x.size(0), x.size(1), x.size(2), x.size(3), dy.size(1), kh, kw, stride, padding, dilation);
+  TORCH_CHECK(g.ho == dy.size(2) && g.wo == dy.size(3) && g.n == dy.size(0) && xb.sizes() == dy.sizes(),
+              "rtseg.conv_stem_wgrad_bn: grad_output / bn_input do not match the geometry");
+  TORCH_CHECK(conv_stem_supported(g) && g.cout % 16 == 0 && (g.cout / 16) != 3,
+              "rtseg.conv_stem_wgrad_bn: needs the stem geometry and Cout of 16, 32 or 64");
+  const int C = static_cast<int>(g.cout);
+  auto fchk = [&](const at::Tensor& t, int64_t n, const char* what) {
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == n,
+                "rtseg.conv_stem_wgrad_bn: ", what, " must be contiguous fp32 of ", n, " elements");
+  };
+  fchk(kcoef, 3 * C, "kcoef");
+  fchk(mean_invstd, 2 * C, "mean_invstd");
+  fchk(scale_shift, 2 * C, "scale_shift");
+  TORCH_CHECK(act >= 0 && act <= 2, "rtseg.conv_stem_wgrad_bn: act must be 0, 1 or 2");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  g.x = x.data_ptr(); g.y = dy.data_ptr();
+  at::Tensor ws = at::empty({conv_stem_wgrad_ws_elems(g)}, x.options().dtype(at::kFloat));
+  at::Tensor dw = at::empty({g.cout, g.cin, g.kh, g.kw},
+                            x.options().dtype(at::kFloat).memory_format(channels_last ? at::MemoryFormat::ChannelsLast
+                                                                                      : at::MemoryFormat::Contiguous));
+  const StemBnBwd bn{xb.data_ptr(), kcoef.data_ptr<float>(), mean_invstd.data_ptr<float>(),
+                     scale_shift.data_ptr<float>(), static_cast<int>(act)};
+  launch_conv_stem_wgrad(g, ws.data_ptr<float>(), dw.data_ptr<float>(), channels_last, cur_stream(), &bn);
+  return dw;
+}
+
 }  // namespace
 }  // namespace rtseg
 
@@ -306,6 +343,9 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
   m.def("conv_wres_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
         "Tensor? addend=None) -> Tensor");
   m.def("conv_stem(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats) -> (Tensor, Tensor)");
+  m.def("conv_stem_wgrad_bn(Tensor x, Tensor dy, Tensor bn_input, Tensor kcoef, Tensor mean_invstd, "
+        "Tensor scale_shift, int act, int kh, int kw, int[] stride, int[] padding, int[] dilation, "
+        "bool channels_last) -> Tensor");
   m.def("conv_stem_wgrad(Tensor x, Tensor dy, int kh, int kw, int[] stride, int[] padding, int[] dilation, "
         "bool channels_last=False) -> Tensor");
   m.def("conv_whalo_wgrad(Tensor x, Tensor dy, int kh, int kw, int[] stride, int[] padding, int[] dilation, "
@@ -326,5 +366,6 @@ TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
   m.impl("conv_igemm_wgrad", &rtseg::conv_igemm_wgrad);
   m.impl("conv_whalo_wgrad", &rtseg::conv_whalo_wgrad);
   m.impl("conv_stem", &rtseg::conv_stem);
+  m.impl("conv_stem_wgrad_bn", &rtseg::conv_stem_wgrad_bn);
   m.impl("conv_stem_wgrad", &rtseg::conv_stem_wgrad);
 }

@@ -231,7 +231,18 @@ bool conv_stem_supported(const ConvGeom& g);
 int conv_stem_slabs(const ConvGeom& g);
 void launch_conv_stem_fwd(const ConvGeom& g, hipStream_t st);
 int64_t conv_stem_wgrad_ws_elems(const ConvGeom& g);
-void launch_conv_stem_wgrad(const ConvGeom& g, float* ws, float* dw, bool krsc, hipStream_t st);
+// BN-fused weight gradient: g.y is the gradient of act(BN(conv output)); the BN backward's apply
+// pass (dx = k0 (g - k1 - (xb - mean) k2), g masked by act'(xb * sc + sh)) runs in the dy staging.
+// act: 0 none, 1 ReLU, 2 ReLU6.  Cout of 16, 32 or 64.
+struct StemBnBwd {
+  const void* xb;
+  const float* kcoef;
+  const float* mean_invstd;
+  const float* scale_shift;
+  int act;
+};
+void launch_conv_stem_wgrad(const ConvGeom& g, float* ws, float* dw, bool krsc, hipStream_t st,
+                            const StemBnBwd* bn = nullptr);
 
 // ---- conv_whalo.hip -----------------------------------------------------------
 // Halo-tiled weight gradient of 3 x 3 / stride 1 / pad 1 / dilation 1 convs (Cin, Cout % 64 == 0):

@@ -36,7 +36,13 @@ constexpr int kTW = 64;  // output tile width (4 MFMA pixel groups)
 struct StemArgs {
   const uint16_t* x;   // [N][H][W][3] bf16
   const uint16_t* w;   // forward: [cout][3][3][3] bf16 (KRSC)
-  const uint16_t* dy;  // weight gradient: [N][Ho][Wo][cout] bf16
+  const uint16_t* dy;  // weight gradient: [N][Ho][Wo][cout] bf16 (BN-fused: the BN OUTPUT's gradient)
+  // BN-fused weight gradient (stem conv -> BN -> act): dy of the conv is the BN backward's dx,
+  // k0 (g - k1 - (xb - mean) k2) with g = dy masked by the activation of xb * sc + sh
+  const uint16_t* xb;  // the BN input (= this conv's output) [N][Ho][Wo][cout] bf16
+  const float* kc;     // BN backward coefficients k0 | k1 | k2 [3 cout]
+  const float* mi;     // mean | invstd [2 cout]
+  const float* ss;     // scale | shift [2 cout]
   uint16_t* y;         // forward output [N][Ho][Wo][cout]
   float* part;         // forward: BN statistics slab [grid][2 * cout] or null; wgrad: [grid][32 * cout]
   int N, H, W, Ho, Wo, cout;
@@ -195,8 +201,25 @@ __global__ void __launch_bounds__(256) stem_fwd_kernel(const StemArgs a) {
   }
 }
 
+__device__ __forceinline__ float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+
+// BNF: 0 = plain dy; 1 / 2 / 3 = dy is the gradient of act(BN(conv output)) with act = none /
+// ReLU / ReLU6, turned into the conv output's gradient while staged (the BN backward apply pass,
+// fused: ops/bn.py hands its coefficients over instead of writing dx)
+template <int BNF>
+__device__ __forceinline__ float bn_dx(float g, float xv, int j, const float* k0, const float* k1, const float* k2,
+                                       const float* mu, const float* sc, const float* sh) {
+  if constexpr (BNF >= 2) {
+    const float z = fmaf(xv, sc[j], sh[j]);
+    if constexpr (BNF == 2) g = z > 0.f ? g : 0.f;
+    else g = (z > 0.f && z < 6.f) ? g : 0.f;
+  }
+  return k0[j] * (g - k1[j] - (xv - mu[j]) * k2[j]);
+}
+
 // weight gradient partials: block b writes ws[b][k 32][cout] (k >= 27 rows are zero)
-template <int S, int NT>
+template <int S, int NT, int BNF = 0>
 __global__ void __launch_bounds__(256) stem_wgrad_kernel(const StemArgs a) {
   constexpr int TH = 4;  // 4 waves x 1 row of 64 pixels (2 MFMA K-steps of 32 pixels)
   constexpr int CP = 16 * NT + 2;  // dy row pitch (elements)
@@ -223,6 +246,19 @@ __global__ void __launch_bounds__(256) stem_wgrad_kernel(const StemArgs a) {
   for (int m = 0; m < 2; ++m)
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[m][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  constexpr int V = C / 8;  // 16-byte vectors per pixel
+  // BN-fused: a thread always stages the same channel vector (V divides 256): its coefficients
+  // stay in registers
+  static_assert(BNF == 0 || 256 % V == 0, "BN-fused stem wgrad needs V | 256");
+  float k0[8], k1[8], k2[8], mu[8], sc[8], sh[8];
+  if constexpr (BNF != 0) {
+    const int c0 = 8 * (tid % V);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      k0[j] = a.kc[c0 + j]; k1[j] = a.kc[C + c0 + j]; k2[j] = a.kc[2 * C + c0 + j];
+      mu[j] = a.mi[c0 + j]; sc[j] = a.ss[c0 + j]; sh[j] = a.ss[C + c0 + j];
+    }
+  }
 
   for (int mt = lb; mt < a.mtiles; mt += G) {
     const int tx = mt % a.tilesW, t2 = mt / a.tilesW;
@@ -230,18 +266,41 @@ __global__ void __launch_bounds__(256) stem_wgrad_kernel(const StemArgs a) {
     __syncthreads();
     stage_input<S, TH>(a, l32, n, oy0, ox0, tid);
     // dy tile [TH * 64 pixels][C] (pixels past the image read as zeros), loads all in flight
-    constexpr int V = C / 8;  // 16-byte vectors per pixel
     constexpr int kPer = TH * kTW * V / 256;
     static_assert(kPer * 256 == TH * kTW * V, "dy staging");
     uint4 q[kPer];
+    uint4 xq[BNF != 0 ? kPer : 1];
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int e = tid + 256 * i;
       const int p = e / V, v = e - p * V;
       const int oy = oy0 + p / kTW, ox = ox0 + (p % kTW);
       q[i] = uint4{0u, 0u, 0u, 0u};
-      if (oy < a.Ho && ox < a.Wo)
-        q[i] = *reinterpret_cast<const uint4*>(a.dy + ((static_cast<int64_t>(n) * a.Ho + oy) * a.Wo + ox) * C + 8 * v);
+      if constexpr (BNF != 0) xq[i] = uint4{0u, 0u, 0u, 0u};
+      if (oy < a.Ho && ox < a.Wo) {
+        const int64_t off = ((static_cast<int64_t>(n) * a.Ho + oy) * a.Wo + ox) * C + 8 * v;
+        q[i] = *reinterpret_cast<const uint4*>(a.dy + off);
+        if constexpr (BNF != 0) xq[i] = *reinterpret_cast<const uint4*>(a.xb + off);
+      }
+    }
+    if constexpr (BNF != 0) {
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) {
+        const int e = tid + 256 * i;
+        const int p = e / V;
+        const int oy = oy0 + p / kTW, ox = ox0 + (p % kTW);
+        if (!(oy < a.Ho && ox < a.Wo)) continue;  // outside the tensor: stays 0
+        const uint32_t gw[4] = {q[i].x, q[i].y, q[i].z, q[i].w};
+        const uint32_t xw[4] = {xq[i].x, xq[i].y, xq[i].z, xq[i].w};
+        uint32_t ow[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float lo = bn_dx<BNF>(bf_lo(gw[u]), bf_lo(xw[u]), 2 * u, k0, k1, k2, mu, sc, sh);
+          const float hi = bn_dx<BNF>(bf_hi(gw[u]), bf_hi(xw[u]), 2 * u + 1, k0, k1, k2, mu, sc, sh);
+          ow[u] = pack2(lo, hi);
+        }
+        q[i] = uint4{ow[0], ow[1], ow[2], ow[3]};
+      }
     }
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
@@ -345,14 +404,22 @@ void fwd_dispatch(const StemArgs& k, int grid, hipStream_t st) {
   }
 }
 
-template <int S>
+template <int S, int BNF>
 void wgrad_dispatch(const StemArgs& k, int grid, hipStream_t st) {
   switch (k.cout / 16) {
-    case 1: stem_wgrad_kernel<S, 1><<<grid, 256, 0, st>>>(k); break;
-    case 2: stem_wgrad_kernel<S, 2><<<grid, 256, 0, st>>>(k); break;
-    case 3: stem_wgrad_kernel<S, 3><<<grid, 256, 0, st>>>(k); break;
-    default: stem_wgrad_kernel<S, 4><<<grid, 256, 0, st>>>(k); break;
+    case 1: stem_wgrad_kernel<S, 1, BNF><<<grid, 256, 0, st>>>(k); break;
+    case 2: stem_wgrad_kernel<S, 2, BNF><<<grid, 256, 0, st>>>(k); break;
+    case 3:
+      if constexpr (BNF == 0) stem_wgrad_kernel<S, 3, 0><<<grid, 256, 0, st>>>(k);  // (BN-fused: V = 6 does not divide 256)
+      break;
+    default: stem_wgrad_kernel<S, 4, BNF><<<grid, 256, 0, st>>>(k); break;
   }
+}
+
+template <int BNF>
+void wgrad_dispatch_s(const StemArgs& k, int grid, int s, hipStream_t st) {
+  if (s == 2) wgrad_dispatch<2, BNF>(k, grid, st);
+  else wgrad_dispatch<1, BNF>(k, grid, st);
 }
 
 }  // namespace
@@ -387,15 +454,23 @@ int64_t conv_stem_wgrad_ws_elems(const ConvGeom& g) {
 }
 
 // g.x = x [N,H,W,3], g.y = dy [N,Ho,Wo,Cout]; ws of conv_stem_wgrad_ws_elems(g) floats
-void launch_conv_stem_wgrad(const ConvGeom& g, float* ws, float* dw, bool krsc, hipStream_t st) {
+void launch_conv_stem_wgrad(const ConvGeom& g, float* ws, float* dw, bool krsc, hipStream_t st,
+                            const StemBnBwd* bn) {
   StemArgs k{};
   if (!stem_fill(k, g, 4)) return;
   k.x = static_cast<const uint16_t*>(g.x);
   k.dy = static_cast<const uint16_t*>(g.y);
   k.part = ws;
   const int grid = stem_grid(k.mtiles);
-  if (g.sh == 2) wgrad_dispatch<2>(k, grid, st);
-  else wgrad_dispatch<1>(k, grid, st);
+  if (bn == nullptr) {
+    wgrad_dispatch_s<0>(k, grid, g.sh, st);
+  } else {
+    k.xb = static_cast<const uint16_t*>(bn->xb);
+    k.kc = bn->kcoef; k.mi = bn->mean_invstd; k.ss = bn->scale_shift;
+    if (bn->act == 0) wgrad_dispatch_s<1>(k, grid, g.sh, st);
+    else if (bn->act == 1) wgrad_dispatch_s<2>(k, grid, g.sh, st);
+    else wgrad_dispatch_s<3>(k, grid, g.sh, st);
+  }
   const int n = 27 * g.cout;
   stem_wgrad_reduce<<<(n + 63) / 64, 1024, 0, st>>>(ws, grid, g.cout, dw, krsc ? 1 : 0);
 }

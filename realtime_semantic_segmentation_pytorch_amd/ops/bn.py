@@ -111,6 +111,12 @@ class _BNActFn(torch.autograd.Function):
         # between its data and weight gradients (syncbn_bwd_early), and park it here
         ctx.early = [] if pg is not None and not getattr(bn, "_rtseg_no_early", False) else None
         ctx.bn_module = bn if pg is not None else None
+        # a stem conv produced x (ops/conv.py bn_fuse_slot): this node's dx pass moves into that
+        # conv's weight gradient (conv_stem_wgrad_bn)
+        prod = x.grad_fn if use_batch_stats and residual is None and out2 is None else None
+        ctx.stem_node = (prod if getattr(prod, "bn_fuse_slot", None) is not None
+                         and mask in (MASK_NONE, MASK_FROM_X) and act in (ACT_NONE, ACT_RELU, ACT_RELU6)
+                         else None)
         ctx.batch_stats = use_batch_stats
         ctx.has_res = residual is not None
         # residual add whose residual is the input of an upstream routed conv (DDRNet's RB, ResNet
@@ -139,6 +145,9 @@ class _BNActFn(torch.autograd.Function):
         bsums = local = None
         want_dres = ctx.has_res and ctx.needs_input_grad[3]
         want_dw = ctx.has_w and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
+        stem, ctx.stem_node = ctx.stem_node, None
+        if stem is not None and dy is not None and dy2 is None and ctx.needs_input_grad[0]:
+            return _stem_handoff(ctx, stem, dy, x, y, mi, ss, sums, weight, want_dw)
         if ctx.pg is not None:
             early = ctx.early.pop() if ctx.early else None
             if early is not None:
@@ -168,6 +177,48 @@ class _BNActFn(torch.autograd.Function):
             dres = None
         return (dx, dw if want_dw else None, db if want_dw else None,
                 dres if want_dres else None, None, None, None, None, None, None, None)
+
+
+STEM_HANDOFFS = [0]  # BN backward dx passes handed to a stem conv's weight gradient (tests)
+
+
+def _stem_handoff(ctx, stem, dy, x, y, mi, ss, sums, weight, want_dw):
+    """BN backward whose dx pass runs in the producing stem conv's weight gradient: only the
+    reduction + finalize here (``bn_bwd_coeffs``), the coefficients handed to the conv node, and a
+    zero-stride placeholder returned as dx (no HBM traffic).  On the flagship this is DDRNet-23's
+    first BN, at half resolution: the largest tensor of the step (2.1 GB at batch 32)."""
+    bsums = local = None
+    if ctx.pg is not None:  # SyncBN: the reduction is all-reduced as usual (early if issued)
+        early = ctx.early.pop() if ctx.early else None
+        if early is not None:
+            key, e_sums, e_local, work = early
+            work.wait()
+            if dy.data_ptr() == key:
+                bsums, local = e_sums, e_local
+            else:
+                ctx.bn_module._rtseg_no_early = True
+        if bsums is None:
+            bsums = ops().bn_bwd_sums(dy, x, y, mi, ss, ctx.act, ctx.mask, None)
+            if want_dw:
+                local = bsums.clone()
+            dist.all_reduce(bsums, group=ctx.pg)
+    k, dw, db = ops().bn_bwd_coeffs(dy, x, y, bsums, sums, mi, ss, weight, ctx.act, ctx.mask,
+                                    ctx.batch_stats, want_dw)
+    if local is not None:
+        c = local.numel() // 2
+        dw = (local[c:] * mi[c:].double()).float()
+        db = local[:c].float()
+    dummy = x.new_zeros(()).expand(x.shape)
+    act, mask, batch = ctx.act, ctx.mask, ctx.batch_stats  # (act codes 0 / 1 / 2 = the kernel's)
+
+    def full():  # the plain dx (the conv output had another consumer)
+        return ops().bn_backward(dy, x, y, bsums, sums, mi, ss, weight, act, mask, False, batch, False,
+                                 None, None)[0]
+
+    stem.bn_fuse_slot.append((dy, x, k, mi, ss, act, dummy, full))
+    STEM_HANDOFFS[0] += 1
+    return (dummy, dw if want_dw else None, db if want_dw else None, None, None, None, None, None, None,
+            None, None)
 
 
 EARLY_ISSUED = [0]  # SyncBN backward all-reduces issued early by a consumer conv (tests)

@@ -494,6 +494,11 @@ class _ConvFn(torch.autograd.Function):
         # node's backward, between dgrad and wgrad (ops.bn.syncbn_bwd_early)
         prod = x.grad_fn
         ctx.bn_node = prod if getattr(prod, "early", None) is not None else None
+        # a 3-channel stem conv on an input that needs no gradient: a following batch-statistics
+        # BN may hand its backward over (ops.bn), and the BN's dx pass runs inside this conv's
+        # weight gradient (conv_stem_wgrad_bn) instead of writing dx to HBM
+        ctx.bn_fuse_slot = [] if (_STEM_BN_FUSE and not x.requires_grad and stem_ok(conv, x)
+                                  and conv.out_channels in (16, 32, 64)) else None
         if part is not None:
             ctx.mark_non_differentiable(part)
         # the statistics slab never gets a gradient: without this autograd would allocate and
@@ -506,6 +511,9 @@ class _ConvFn(torch.autograd.Function):
         if dy is None:
             return None, None, None, None
         x, wk = ctx.saved_tensors
+        fused = ctx.bn_fuse_slot.pop() if ctx.bn_fuse_slot else None
+        if fused is not None:
+            return None, _stem_wgrad_bn(x, ctx.conv, ctx.wdtype, dy, fused), None, None
         addend = ctx.addend_slot.pop() if ctx.addend_slot else None
         node, ctx.bn_node = ctx.bn_node, None
         on_dx = None
@@ -517,6 +525,30 @@ class _ConvFn(torch.autograd.Function):
         dx, dw = _conv_bwd(x, wk, ctx.conv, ctx.key, dy, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
                            ctx.wdtype, addend, on_dx)
         return dx, dw, None, None
+
+
+# RTSEG_STEM_BN_FUSE=0: the stem's BN backward writes dx as before (A/B, tests)
+_STEM_BN_FUSE = os.environ.get("RTSEG_STEM_BN_FUSE", "1") != "0"
+
+
+def _stem_wgrad_bn(x, conv, wdtype, dy, fused):
+    """Weight gradient of a stem conv whose output went through a batch-statistics BN that handed
+    its backward over (``fused`` = (bn output grad, bn input, kcoef, mean_invstd, scale_shift,
+    act, dummy, full)): the BN's dx is formed while the kernel stages it.  ``dy`` -- what autograd
+    passed this node -- is the BN's zero-stride placeholder when the BN was the conv output's only
+    consumer; otherwise the placeholder plus the other consumers' gradients, and then the BN's dx
+    is materialised (``full()``) and the plain kernel runs on the sum."""
+    g, xb, kc, mi, ss, act, dummy, full = fused
+    stride, padding, dilation = _geom(conv)
+    w = conv.weight
+    cl = w.dim() == 4 and w.is_contiguous(memory_format=torch.channels_last) and not w.is_contiguous()
+    if dy is dummy or (dy is not None and dy.dim() == 4 and dy.stride() == (0, 0, 0, 0)):
+        dw = ops().conv_stem_wgrad_bn(x, g, xb, kc, mi, ss, act, 3, 3, stride, padding, dilation, cl)
+    else:
+        d = full() + dy.to(g.dtype)
+        d = d.contiguous(memory_format=torch.channels_last)
+        dw = ops().conv_stem_wgrad(x, d, 3, 3, stride, padding, dilation, cl)
+    return like_param(dw.to(wdtype), w)
 
 
 def _conv_bwd(x, wk, conv, key, dy, want_dx, want_dw, wdtype, addend=None, on_dx=None):

@@ -119,8 +119,9 @@ def test_stem_routed_training_step(monkeypatch):
     assert rel(y0, y1) < 1e-2
     for n, g in gp1.items():
         assert rel(gp0[n], g) < 2e-2, n
-    assert {"conv_stem", "conv_stem_wgrad"} <= calls[0], calls[0]
-    assert not {"conv_stem", "conv_stem_wgrad"} & calls[1], calls[1]
+    # the stem's BN hands its dx pass to the stem weight gradient (conv_stem_wgrad_bn)
+    assert "conv_stem" in calls[0] and calls[0] & {"conv_stem_wgrad", "conv_stem_wgrad_bn"}, calls[0]
+    assert not {"conv_stem", "conv_stem_wgrad", "conv_stem_wgrad_bn"} & calls[1], calls[1]
 
 
 @pytest.mark.parametrize("block", ["RB", "RBB"])
@@ -198,3 +199,44 @@ def test_stem_inference_path(cout, stride, bias):
     assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
     torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=2e-2)
     assert torch.equal(y, y2)
+
+
+@pytest.mark.parametrize("act", ["relu", "none", "relu6"])
+@pytest.mark.parametrize("second_consumer", [False, True])
+@pytest.mark.parametrize("cout", [64, 32])
+def test_stem_bn_backward_fused(monkeypatch, act, second_consumer, cout):
+    """The BN after a stem conv hands its backward dx pass to the stem's weight gradient
+    (ops/bn.py _stem_handoff -> conv_stem_wgrad_bn): conv weight, BN weight / bias gradients equal
+    the unfused path (RTSEG_STEM_BN_FUSE off) up to bf16 rounding of dx; with a second consumer
+    of the conv output the fallback (materialised dx + the other gradient) is taken."""
+    from realtime_semantic_segmentation_pytorch_amd.ops import bn as bn_mod
+    from realtime_semantic_segmentation_pytorch_amd.ops import conv as conv_mod
+
+    monkeypatch.setenv("RTSEG_CONV_MFMA", "1")  # the stem kernel in the forward, no timing
+    torch.manual_seed(1)
+    conv = torch.nn.Conv2d(3, cout, 3, 2, 1, bias=False).to(DEV)
+    conv.__class__ = ops.PrunedConv2d
+    bn = ops.convert_batchnorm(torch.nn.Sequential(torch.nn.BatchNorm2d(cout)))[0].to(DEV).train()
+    x = torch.randn(2, 3, 40, 130, device=DEV).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(2, cout, 20, 65, device=DEV)
+    res = []
+    for fuse in (True, False):
+        monkeypatch.setattr(conv_mod, "_STEM_BN_FUSE", fuse)
+        for p in (conv.weight, bn.weight, bn.bias):
+            p.grad = None
+        n0 = bn_mod.STEM_HANDOFFS[0]
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y, part = ops.conv_bn_stats(x, conv)
+            out = ops.bn_act(y, bn, act, part=part)
+        loss = (out.float() * gy).sum()
+        if second_consumer:
+            loss = loss + 0.25 * (y.float() * gy.flip(0)).sum()
+        loss.backward()
+        assert (bn_mod.STEM_HANDOFFS[0] - n0) == (1 if fuse else 0)
+        res.append([t.grad.float().clone() for t in (conv.weight, bn.weight, bn.bias)])
+
+    def rel(a, b):
+        return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+    for a, b, name in zip(res[0], res[1], ("conv.weight", "bn.weight", "bn.bias")):
+        assert rel(a, b) < 1e-2, (name, rel(a, b))
