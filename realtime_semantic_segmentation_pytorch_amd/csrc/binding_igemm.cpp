@@ -249,7 +249,7 @@ at::Tensor conv_igemm_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t k
 
 // halo-tiled weight gradient (conv_whalo.hip): 3 x 3 / stride 1 / pad 1, Cin and Cout % 64 == 0
 at::Tensor conv_whalo_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t kh, int64_t kw, at::IntArrayRef stride,
-                            at::IntArrayRef padding, at::IntArrayRef dilation, bool channels_last) {
+                            at::IntArrayRef padding, at::IntArrayRef dilation, bool channels_last, int64_t variant) {
   check_act(x, "input");
   check_act(dy, "grad_output");
   ConvGeom g = geom(x.size(0), x.size(1), x.size(2), x.size(3), dy.size(1), kh, kw, stride, padding, dilation);
@@ -262,7 +262,9 @@ at::Tensor conv_whalo_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t k
   at::Tensor dw = at::empty({g.cout, g.cin, g.kh, g.kw},
                             x.options().dtype(at::kFloat).memory_format(channels_last ? at::MemoryFormat::ChannelsLast
                                                                                       : at::MemoryFormat::Contiguous));
-  launch_conv_whalo_wgrad(g, ws.data_ptr<float>(), dw.data_ptr<float>(), channels_last, cur_stream());
+  TORCH_CHECK(variant == 1 || variant == 2, "rtseg.conv_whalo_wgrad: variant must be 1 or 2");
+  launch_conv_whalo_wgrad(g, ws.data_ptr<float>(), dw.data_ptr<float>(), channels_last, cur_stream(),
+                          static_cast<int>(variant));
   return dw;
 }
 
@@ -349,7 +351,7 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
   m.def("conv_stem_wgrad(Tensor x, Tensor dy, int kh, int kw, int[] stride, int[] padding, int[] dilation, "
         "bool channels_last=False) -> Tensor");
   m.def("conv_whalo_wgrad(Tensor x, Tensor dy, int kh, int kw, int[] stride, int[] padding, int[] dilation, "
-        "bool channels_last=False) -> Tensor");
+        "bool channels_last=False, int variant=1) -> Tensor");
   m.def("conv_igemm_wgrad(Tensor x, Tensor dy, int kh, int kw, int[] stride, int[] padding, int[] dilation, "
         "bool channels_last=False) -> Tensor");
 }

@@ -249,7 +249,8 @@ void launch_conv_stem_wgrad(const ConvGeom& g, float* ws, float* dw, bool krsc, 
 // g.x = x, g.y = dy; ws of conv_whalo_ws_elems(g) floats; dw fp32 as launch_conv_igemm_wgrad.
 bool conv_whalo_supported(const ConvGeom& g);
 int64_t conv_whalo_ws_elems(const ConvGeom& g);
-void launch_conv_whalo_wgrad(const ConvGeom& g, float* ws, float* dw, bool krsc, hipStream_t st);
+// variant 1: one output tile per wave; 2: both output tiles per wave, K split across wave halves
+void launch_conv_whalo_wgrad(const ConvGeom& g, float* ws, float* dw, bool krsc, hipStream_t st, int variant = 1);
 
 // ---- gate.hip -----------------------------------------------------------------
 // out = x * s (mul), x * (1 + s) (residual), x * s + y * (1 - s) (blend); s = att or

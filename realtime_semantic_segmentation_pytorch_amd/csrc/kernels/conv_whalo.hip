@@ -82,6 +82,14 @@ __device__ __forceinline__ uint32_t swz_off(int row, int col) {  // byte offset 
   return static_cast<uint32_t>(row * 128 + ch * 16 + ((col >> 2) & 1) * 8);
 }
 
+// KS = 1: wave w owns output tile w & 1 and three (tap, input half) tiles, all 16 K sub-steps of a
+//         pixel tile (round 4): 4 fragment reads (1 dy^T + 3 x) per 3 MFMAs.
+// KS = 2: wave w owns BOTH output tiles and three (tap, input half) tiles, for half of the K
+//         sub-steps (pixel rows 0-3 or 4-7 of the tile): 5 fragment reads per 6 MFMAs -- 37.5 %
+//         fewer LDS transposed reads per MFMA (the K loop was LDS-read bound: 48 KiB of
+//         ds_read_tr per CU per sub-step against 36 MFMAs); the two K halves are summed through
+//         LDS once, after the last tile.
+template <int KS>
 __global__ void __launch_bounds__(kNW * 64) whalo_wgrad_kernel(const WhArgs a) {
   __shared__ uint4 lds[2 * kStage];
 
@@ -128,9 +136,11 @@ __global__ void __launch_bounds__(kNW * 64) whalo_wgrad_kernel(const WhArgs a) {
     }
   };
 
-  // ---- wave tiles: output-channel tile m (32 rows), three (tap, input-channel half) tiles
-  const int m = wid & 1;
-  const int nb = 3 * (wid >> 1);
+  // ---- wave tiles: output-channel tile(s) m (32 rows), three (tap, input-channel half) tiles
+  constexpr int NM = KS == 2 ? 2 : 1;           // output tiles per wave
+  const int m0 = KS == 2 ? 0 : (wid & 1);
+  const int nb = KS == 2 ? 3 * (wid % 6) : 3 * (wid >> 1);
+  const int kh = KS == 2 ? wid / 6 : 0;         // K half (KS = 2)
   int tap_i[3], tap_j[3], cit[3];
 #pragma unroll
   for (int u = 0; u < 3; ++u) {
@@ -141,16 +151,17 @@ __global__ void __launch_bounds__(kNW * 64) whalo_wgrad_kernel(const WhArgs a) {
   }
   // transposed-read geometry: row q of the 4-row block, columns 4p.., 16-column group g16, K half hh
   const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4, g16 = (lane >> 4) & 1, hh = lane >> 5;
-  const int acol = m * 32 + g16 * 16 + p4;  // dy^T: output channel within the chunk
   int bcol[3];
 #pragma unroll
   for (int u = 0; u < 3; ++u) bcol[u] = cit[u] * 32 + g16 * 16 + p4;
 
-  f32x16_t acc[3];
+  f32x16_t acc[NM][3];
 #pragma unroll
-  for (int u = 0; u < 3; ++u)
+  for (int mm = 0; mm < NM; ++mm)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[u][r] = 0.f;
+    for (int u = 0; u < 3; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mm][u][r] = 0.f;
 
   // Per-lane LDS byte offsets, so that every fragment read of the fully unrolled K loop is
   // base + compile-time immediate (round-4 PMC: 9.4 VALU per MFMA with per-read address math):
@@ -158,7 +169,9 @@ __global__ void __launch_bounds__(kNW * 64) whalo_wgrad_kernel(const WhArgs a) {
   //    ((row >> 1) & 1), so one base + (kk * 16 [+ 4]) * 128;
   //  * halo: rows (py + i) * 34 + px0 + hh * 8 + q + j: adding px0 (0 / 16) or 4 keeps the bit,
   //    adding 34 flips it -- one base for even and one for odd py, each + (py * 34 + px0) * 128
-  const uint32_t offA = swz_off(hh * 8 + q, acol);
+  uint32_t offA[NM];
+#pragma unroll
+  for (int mm = 0; mm < NM; ++mm) offA[mm] = swz_off(hh * 8 + q, (m0 + mm) * 32 + g16 * 16 + p4);  // dy^T column
   uint32_t offB[2][3];
 #pragma unroll
   for (int u = 0; u < 3; ++u) {
@@ -175,18 +188,25 @@ __global__ void __launch_bounds__(kNW * 64) whalo_wgrad_kernel(const WhArgs a) {
     __builtin_amdgcn_s_barrier();  // tile t landed for every wave; the other buffer is free
     if (t + 1 < my_tiles) stage(split + (t + 1) * a.splits, (t + 1) & 1);
     const uint4* dbase = lds + (t & 1) * kStage;
+    constexpr int KSTEPS = kTP / 16 / KS;
 #pragma unroll
-    for (int kk = 0; kk < kTP / 16; ++kk) {
-      const int py = kk >> 1, px0 = (kk & 1) * 16;
-      // dy^T fragment: rows = pixels kk*16 + hh*8 + q (+4), column acol
-      const i16x4_t alo = tr4(dbase, offA + kk * 16 * 128);
-      const i16x4_t ahi = tr4(dbase, offA + (kk * 16 + 4) * 128);
-      const bf16x8_t af = __builtin_shufflevector(__builtin_bit_cast(bf16x4_t, alo),
-                                                  __builtin_bit_cast(bf16x4_t, ahi), 0, 1, 2, 3, 4, 5, 6, 7);
+    for (int k2 = 0; k2 < KSTEPS; ++k2) {
+      const int kk = KS == 2 ? kh * KSTEPS + k2 : k2;  // (kh is wave-uniform: immediates per wave half)
+      // KSTEPS is even: the parity of the pixel row py is a compile-time function of k2
+      const int py = kk >> 1, px0 = (k2 & 1) * 16, par = (k2 >> 1) & 1;
+      // dy^T fragment(s): rows = pixels kk*16 + hh*8 + q (+4), column of output tile m0 + mm
+      bf16x8_t af[NM];
+#pragma unroll
+      for (int mm = 0; mm < NM; ++mm) {
+        const i16x4_t alo = tr4(dbase, offA[mm] + kk * 16 * 128);
+        const i16x4_t ahi = tr4(dbase, offA[mm] + (kk * 16 + 4) * 128);
+        af[mm] = __builtin_shufflevector(__builtin_bit_cast(bf16x4_t, alo), __builtin_bit_cast(bf16x4_t, ahi), 0, 1,
+                                         2, 3, 4, 5, 6, 7);
+      }
       bf16x8_t bf[3];
 #pragma unroll
       for (int u = 0; u < 3; ++u) {
-        const uint32_t o = offB[py & 1][u] + (py * kHW + px0) * 128;
+        const uint32_t o = offB[par][u] + (py * kHW + px0) * 128;
         const i16x4_t blo = tr4(dbase, o);
         const i16x4_t bhi = tr4(dbase, o + 4 * 128);
         bf[u] = __builtin_shufflevector(__builtin_bit_cast(bf16x4_t, blo), __builtin_bit_cast(bf16x4_t, bhi), 0, 1,
@@ -194,24 +214,51 @@ __global__ void __launch_bounds__(kNW * 64) whalo_wgrad_kernel(const WhArgs a) {
       }
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int u = 0; u < 3; ++u) acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf[u], acc[u], 0, 0, 0);
+      for (int mm = 0; mm < NM; ++mm)
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+          acc[mm][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mm], bf[u], acc[mm][u], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
+  }
+  if constexpr (KS == 2) {
+    // sum the two K halves: waves 6..11 park their accumulators in the (now idle) stage buffers
+    float* red = reinterpret_cast<float*>(lds);  // [6 wave groups][NM * 3 * 16][64 lanes]
+    const int wg = wid % 6;
+    __syncthreads();
+    if (kh == 1) {
+#pragma unroll
+      for (int mm = 0; mm < NM; ++mm)
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) red[((wg * NM + mm) * 3 + u) * 16 * 64 + r * 64 + lane] = acc[mm][u][r];
+    }
+    __syncthreads();
+    if (kh == 1) return;
+#pragma unroll
+    for (int mm = 0; mm < NM; ++mm)
+#pragma unroll
+      for (int u = 0; u < 3; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[mm][u][r] += red[((wg * NM + mm) * 3 + u) * 16 * 64 + r * 64 + lane];
   }
 
   // fp32 partial tile -> slab [split][cout][tap * cin + ci] (every element written by one block)
   const int64_t kp = 9 * static_cast<int64_t>(a.cin);
   float* slab = a.ws + static_cast<int64_t>(split) * a.cout * kp;
 #pragma unroll
-  for (int u = 0; u < 3; ++u) {
-    const int tap = (nb + u) >> 1;
-    const int64_t col = tap * static_cast<int64_t>(a.cin) + ci0 + cit[u] * 32 + (lane & 31);
+  for (int mm = 0; mm < NM; ++mm)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int co = co0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-      slab[co * kp + col] = acc[u][r];
+    for (int u = 0; u < 3; ++u) {
+      const int tap = (nb + u) >> 1;
+      const int64_t col = tap * static_cast<int64_t>(a.cin) + ci0 + cit[u] * 32 + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = co0 + (m0 + mm) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        slab[co * kp + col] = acc[mm][u][r];
+      }
     }
-  }
 }
 
 bool whalo_fill(WhArgs& k, const ConvGeom& g) {
@@ -248,13 +295,14 @@ int64_t conv_whalo_ws_elems(const ConvGeom& g) {
   return plane * (k.splits + (k.splits > 16 ? (k.splits + 15) / 16 : 0));
 }
 
-void launch_conv_whalo_wgrad(const ConvGeom& g, float* ws, float* dw, bool krsc, hipStream_t st) {
+void launch_conv_whalo_wgrad(const ConvGeom& g, float* ws, float* dw, bool krsc, hipStream_t st, int variant) {
   WhArgs k{};
   if (!whalo_fill(k, g)) return;
   k.x = static_cast<const uint16_t*>(g.x);
   k.dy = static_cast<const uint16_t*>(g.y);
   k.ws = ws;
-  whalo_wgrad_kernel<<<k.pairs * k.splits, kNW * 64, 0, st>>>(k);
+  if (variant == 2) whalo_wgrad_kernel<2><<<k.pairs * k.splits, kNW * 64, 0, st>>>(k);
+  else whalo_wgrad_kernel<1><<<k.pairs * k.splits, kNW * 64, 0, st>>>(k);
   launch_wgrad_slab_reduce(ws, k.splits, g.cout, g.cin, 9, dw, krsc, st);
 }
 

@@ -190,6 +190,8 @@ def _order(cands):
         cands.sort(key=lambda c: c[0] != "wres")
     if os.environ.get("RTSEG_CONV_WHALO") == "1":
         cands.sort(key=lambda c: c[0] != "whalo")
+    if os.environ.get("RTSEG_CONV_WHALO") == "2":
+        cands.sort(key=lambda c: c[0] != "whalo2")
     if os.environ.get("RTSEG_CONV_HREG") == "1":
         cands.sort(key=lambda c: c[0] != "hreg")
     if os.environ.get("RTSEG_CONV_HREG") == "2":
@@ -764,8 +766,8 @@ def _wgrad(x, dy, wk, conv, key, stride, padding, dilation):
     def ours():
         return ops().conv_igemm_wgrad(x, dy, kh, kw, stride, padding, dilation, cl or (kh == 1 and kw == 1))
 
-    def whalo():
-        return ops().conv_whalo_wgrad(x, dy, kh, kw, stride, padding, dilation, cl or (kh == 1 and kw == 1))
+    def whalo(variant=1):
+        return ops().conv_whalo_wgrad(x, dy, kh, kw, stride, padding, dilation, cl or (kh == 1 and kw == 1), variant)
 
     def miopen():
         return torch.ops.aten.convolution_backward(dy, x, wk.permute(0, 3, 1, 2), None, stride, padding, dilation,
@@ -777,6 +779,8 @@ def _wgrad(x, dy, wk, conv, key, stride, padding, dilation):
     cands = [("igemm", ours)] if cin % 64 == 0 and cout % 64 == 0 else []
     if whalo_ok(conv, cin, cout, _npix(x)):
         cands.append(("whalo", whalo))
+        if os.environ.get("RTSEG_CONV_WHALO2", "1") != "0":
+            cands.append(("whalo2", lambda: whalo(2)))  # both output tiles per wave, K split
     if stem_ok(conv, x):
         cands.append(("stem", stem))
     cands.append(("miopen", miopen))

@@ -130,23 +130,25 @@ def test_wres_routed_training_step(monkeypatch):
 WGRAD = [(2, 64, 17, 70, 64), (3, 128, 9, 40, 64), (1, 64, 6, 33, 192), (8, 64, 66, 256, 64), (2, 128, 16, 64, 128)]
 
 
+@pytest.mark.parametrize("variant", [1, 2])
 @pytest.mark.parametrize("geom", WGRAD)
 @pytest.mark.parametrize("channels_last", [False, True])
-def test_whalo_wgrad(geom, channels_last):
+def test_whalo_wgrad(geom, channels_last, variant):
     """Halo-tiled weight gradient (csrc/kernels/conv_whalo.hip) vs fp32 PyTorch on the same bf16
     operands: partial tiles, several channel pairs, split-K over many tiles (two-stage slab
-    reduction), both parameter layouts; deterministic."""
+    reduction), both parameter layouts; deterministic.  Variant 2: both output tiles per wave,
+    the tile's K sub-steps split across the two wave halves and summed through LDS."""
     n, cin, h, w, cout = geom
     g = torch.Generator().manual_seed(4)
     cl = dict(memory_format=torch.channels_last)
     x = _t((n, cin, h, w), g).contiguous(**cl)
     dy = _t((n, cout, h, w), g).contiguous(**cl)
-    dw = torch.ops.rtseg.conv_whalo_wgrad(x, dy, 3, 3, [1, 1], [1, 1], [1, 1], channels_last)
+    dw = torch.ops.rtseg.conv_whalo_wgrad(x, dy, 3, 3, [1, 1], [1, 1], [1, 1], channels_last, variant)
     ref = torch.nn.grad.conv2d_weight(x.float(), (cout, cin, 3, 3), dy.float(), 1, 1, 1)
     assert dw.shape == ref.shape and dw.dtype == torch.float32
     assert dw.is_contiguous(memory_format=torch.channels_last) == channels_last or cin == 1
     _close(dw, ref, 1e-3)
-    assert torch.equal(torch.ops.rtseg.conv_whalo_wgrad(x, dy, 3, 3, [1, 1], [1, 1], [1, 1], channels_last), dw)
+    assert torch.equal(torch.ops.rtseg.conv_whalo_wgrad(x, dy, 3, 3, [1, 1], [1, 1], [1, 1], channels_last, variant), dw)
 
 
 # register-weight halo conv (csrc/kernels/conv_hreg.hip): (n, cin, h, w, cout), Cin % 64, Cout % 128
