@@ -376,7 +376,7 @@ template <typename T, int V, int ACT, bool RES, bool BITS>
 __device__ __forceinline__ void apply_rows(const T* __restrict__ x, const T* __restrict__ res,
                                            const float* __restrict__ scale_shift, T* __restrict__ y,
                                            int64_t M, int C, uint8_t* __restrict__ bits, T* __restrict__ y2,
-                                           int64_t ld2) {
+                                           int64_t ld2, bool rev) {
   const int cv = C / V;
   const int cvi = threadIdx.x % cv;
   const int c0 = cvi * V;
@@ -385,6 +385,7 @@ __device__ __forceinline__ void apply_rows(const T* __restrict__ x, const T* __r
   for (int j = 0; j < V; ++j) { sc[j] = scale_shift[c0 + j]; sh[j] = scale_shift[C + c0 + j]; }
   const int64_t rstep = static_cast<int64_t>(gridDim.x) * (blockDim.x / cv);
   auto one = [&](int64_t row) {
+    if (rev) row = M - 1 - row;
     const int64_t off = row * C + c0;
     float f[V], r[V];
     VecIO<T, V>::load(x + off, f);
@@ -415,9 +416,10 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x,
                                                        const float* __restrict__ scale_shift,
                                                        T* __restrict__ y, int64_t M, int C,
                                                        uint8_t* __restrict__ bits = nullptr,
-                                                       T* __restrict__ y2 = nullptr, int64_t ld2 = 0) {
+                                                       T* __restrict__ y2 = nullptr, int64_t ld2 = 0,
+                                                       bool rev = false) {
   if (blockDim.x % (C / V) == 0) {  // block-uniform
-    apply_rows<T, V, ACT, RES, BITS>(x, res, scale_shift, y, M, C, bits, y2, ld2);
+    apply_rows<T, V, ACT, RES, BITS>(x, res, scale_shift, y, M, C, bits, y2, ld2, rev);
     return;
   }
   extern __shared__ __attribute__((aligned(16))) float coef[];  // [2][C]
@@ -479,7 +481,7 @@ template <typename T, int V, int ACT, int MASK>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y,
     const float* __restrict__ mean_invstd, const float* __restrict__ scale_shift, int64_t M, int C,
-    float* __restrict__ part, const T* __restrict__ dy2, int64_t ld2) {
+    float* __restrict__ part, const T* __restrict__ dy2, int64_t ld2, int order) {
   extern __shared__ __attribute__((aligned(16))) float sm[];  // coef[2C] | mean[C] | partials
   float* coef = sm;
   float* mu = sm + 2 * C;
@@ -492,32 +494,40 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
 #pragma unroll
   for (int j = 0; j < V; ++j) { s[j] = 0.f; q[j] = 0.f; }
   if (g.my_r < g.rpi) {
-    int64_t r0, r1;
-    block_rows(M, g.rpi, r0, r1);
     float m[V];
 #pragma unroll
     for (int j = 0; j < V; ++j) m[j] = mu[c0 + j];
-    int64_t r = r0 + g.my_r;
-    for (; r + 3 * g.rpi < r1; r += 4 * g.rpi) {  // four rows (8-12 loads) in flight
+    auto acc4 = [&](int64_t ra, int64_t rb, int64_t rc, int64_t rd) {  // four rows (8-12 loads) in flight
       float ga[V], xa[V], gb[V], xb[V], gc[V], xc[V], gd[V], xd[V];
-      load_g<T, V, ACT, MASK>(dy, dy2, x, y, coef, C, r * C + c0, r * ld2 + c0, c0, ga, xa);
-      load_g<T, V, ACT, MASK>(dy, dy2, x, y, coef, C, (r + g.rpi) * C + c0, (r + g.rpi) * ld2 + c0, c0, gb, xb);
-      load_g<T, V, ACT, MASK>(dy, dy2, x, y, coef, C, (r + 2 * g.rpi) * C + c0, (r + 2 * g.rpi) * ld2 + c0, c0,
-                              gc, xc);
-      load_g<T, V, ACT, MASK>(dy, dy2, x, y, coef, C, (r + 3 * g.rpi) * C + c0, (r + 3 * g.rpi) * ld2 + c0, c0,
-                              gd, xd);
+      load_g<T, V, ACT, MASK>(dy, dy2, x, y, coef, C, ra * C + c0, ra * ld2 + c0, c0, ga, xa);
+      load_g<T, V, ACT, MASK>(dy, dy2, x, y, coef, C, rb * C + c0, rb * ld2 + c0, c0, gb, xb);
+      load_g<T, V, ACT, MASK>(dy, dy2, x, y, coef, C, rc * C + c0, rc * ld2 + c0, c0, gc, xc);
+      load_g<T, V, ACT, MASK>(dy, dy2, x, y, coef, C, rd * C + c0, rd * ld2 + c0, c0, gd, xd);
 #pragma unroll
       for (int j = 0; j < V; ++j) {
         s[j] += (ga[j] + gb[j]) + (gc[j] + gd[j]);
         q[j] += (ga[j] * (xa[j] - m[j]) + gb[j] * (xb[j] - m[j])) +
                 (gc[j] * (xc[j] - m[j]) + gd[j] * (xd[j] - m[j]));
       }
-    }
-    for (; r < r1; r += g.rpi) {
+    };
+    auto acc1 = [&](int64_t r) {
       float ga[V], xa[V];
       load_g<T, V, ACT, MASK>(dy, dy2, x, y, coef, C, r * C + c0, r * ld2 + c0, c0, ga, xa);
 #pragma unroll
       for (int j = 0; j < V; ++j) { s[j] += ga[j]; q[j] += ga[j] * (xa[j] - m[j]); }
+    };
+    if (order == 0) {  // block-contiguous row ranges
+      int64_t r0, r1;
+      block_rows(M, g.rpi, r0, r1);
+      int64_t r = r0 + g.my_r;
+      for (; r + 3 * g.rpi < r1; r += 4 * g.rpi) acc4(r, r + g.rpi, r + 2 * g.rpi, r + 3 * g.rpi);
+      for (; r < r1; r += g.rpi) acc1(r);
+    } else {  // grid-stride sweep over the whole tensor, from the last row down (order 1) or up (2)
+      const int64_t S = static_cast<int64_t>(gridDim.x) * g.rpi;
+      const int64_t e = order == 1 ? M - 1 : 0, d = order == 1 ? -1 : 1;
+      int64_t v = static_cast<int64_t>(blockIdx.x) * g.rpi + g.my_r;
+      for (; v + 3 * S < M; v += 4 * S) acc4(e + d * v, e + d * (v + S), e + d * (v + 2 * S), e + d * (v + 3 * S));
+      for (; v < M; v += S) acc1(e + d * v);
     }
   }
   __syncthreads();  // coef/mu region is reused below only after every thread is done
@@ -584,7 +594,7 @@ __device__ __forceinline__ void bwd_apply_rows(const T* __restrict__ dy, const T
                                                const float* __restrict__ scale_shift,
                                                const float* __restrict__ kcoef, T* __restrict__ dx,
                                                T* __restrict__ dres, int64_t M, int C,
-                                               const T* __restrict__ dy2, int64_t ld2) {
+                                               const T* __restrict__ dy2, int64_t ld2, bool rev) {
   const int cv = C / V;
   const int c0 = (threadIdx.x % cv) * V;
   float cf[2 * V], k0[V], k1[V], k2[V], mu[V];  // cf: scale | shift (pre-activation mask)
@@ -600,6 +610,7 @@ __device__ __forceinline__ void bwd_apply_rows(const T* __restrict__ dy, const T
   }
   const int64_t rstep = static_cast<int64_t>(gridDim.x) * (blockDim.x / cv);
   auto one = [&](int64_t row) {
+    if (rev) row = M - 1 - row;
     const int64_t off = row * C + c0;
     float g[V], xv[V], o[V];
     load_dy<T, V>(dy, dy2, off, row * ld2 + c0, g);
@@ -635,9 +646,9 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
     const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y,
     const float* __restrict__ mean_invstd, const float* __restrict__ scale_shift,
     const float* __restrict__ kcoef, T* __restrict__ dx, T* __restrict__ dres, int64_t M, int C,
-    const T* __restrict__ dy2, int64_t ld2) {
+    const T* __restrict__ dy2, int64_t ld2, bool rev) {
   if (blockDim.x % (C / V) == 0) {  // block-uniform
-    bwd_apply_rows<T, V, ACT, MASK, DRES>(dy, x, y, mean_invstd, scale_shift, kcoef, dx, dres, M, C, dy2, ld2);
+    bwd_apply_rows<T, V, ACT, MASK, DRES>(dy, x, y, mean_invstd, scale_shift, kcoef, dx, dres, M, C, dy2, ld2, rev);
     return;
   }
   extern __shared__ __attribute__((aligned(16))) float sm[];  // coef[2C] | mu[C] | k[3C]
@@ -1022,6 +1033,21 @@ void launch_bn_eval_coeffs(int C, const float* w, const float* b, const float* r
                                                          scale_shift);
 }
 
+// Traversal order of the streaming passes, for reuse through the 256 MiB Infinity Cache: a pass
+// that starts where the previous pass over the same tensors ended re-reads what that pass left
+// resident.  RTSEG_BN_L3ORDER bits: 1 = backward reduce sweeps down from the last row, 2 = it sweeps
+// up grid-stride (neither: block-contiguous ranges), 4 = backward apply from the last row,
+// 8 = forward apply from the last row (its input's tail is what the producing conv wrote last).
+// Default 14: the reduce ends at the tail of (dy, x), the backward apply starts there.  DDRNet-23
+// b32 1024x2048: 537.2 (order 0) -> 543.0 images/s (profiles/r5_l3order).  Read once.
+static int l3_order() {
+  static const int v = [] {
+    const char* e = std::getenv("RTSEG_BN_L3ORDER");
+    return e ? std::atoi(e) : 14;
+  }();
+  return v;
+}
+
 static int apply_grid(int64_t work) {
   int64_t g = (work + 511) / 512;  // two vectors per thread
   // cap 1024 (4 blocks per CU): forward apply / backward apply of the 537 MB layer 906 -> 859 / 2209 ->
@@ -1066,10 +1092,11 @@ static void apply_t(const void* x, const void* res, const float* ss, void* y, in
   if (res)
     bn_apply_kernel<T, V, ACT, true><<<grid, 256, lds, st>>>(
         static_cast<const T*>(x), static_cast<const T*>(res), ss, static_cast<T*>(y), M, C, nullptr,
-        static_cast<T*>(y2), ld2);
+        static_cast<T*>(y2), ld2, (l3_order() & 8) != 0);
   else
     bn_apply_kernel<T, V, ACT, false><<<grid, 256, lds, st>>>(
-        static_cast<const T*>(x), nullptr, ss, static_cast<T*>(y), M, C, nullptr, static_cast<T*>(y2), ld2);
+        static_cast<const T*>(x), nullptr, ss, static_cast<T*>(y), M, C, nullptr, static_cast<T*>(y2), ld2,
+        (l3_order() & 8) != 0);
 }
 
 template <typename T, int V, int ACT>
@@ -1079,10 +1106,11 @@ static void apply_bits_t(const void* x, const void* res, const float* ss, void* 
   if (res != nullptr)
     bn_apply_kernel<T, V, ACT, true, true><<<apply_grid(work), 256, sizeof(float) * 2 * C, st>>>(
         static_cast<const T*>(x), static_cast<const T*>(res), ss, static_cast<T*>(y), M, C, bits,
-        static_cast<T*>(y2), ld2);
+        static_cast<T*>(y2), ld2, (l3_order() & 8) != 0);
   else
     bn_apply_kernel<T, V, ACT, false, true><<<apply_grid(work), 256, sizeof(float) * 2 * C, st>>>(
-        static_cast<const T*>(x), nullptr, ss, static_cast<T*>(y), M, C, bits, static_cast<T*>(y2), ld2);
+        static_cast<const T*>(x), nullptr, ss, static_cast<T*>(y), M, C, bits, static_cast<T*>(y2), ld2,
+        (l3_order() & 8) != 0);
 }
 
 // (Residual +) activation forward that also writes the derivative bit mask (kMaskBits):
@@ -1124,7 +1152,7 @@ static void bwd_reduce_t(const void* dy, const void* x, const void* y, const flo
   const size_t lds = sizeof(float) * (3 * C + 2 * rpi * C);
   bn_bwd_reduce_kernel<T, V, ACT, MASK><<<G, 256, lds, st>>>(
       static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(y), mi, ss, M, C,
-      part, static_cast<const T*>(dy2), ld2);
+      part, static_cast<const T*>(dy2), ld2, (l3_order() & 1) ? 1 : (l3_order() & 2) ? 2 : 0);
 }
 
 template <typename T, int V, int ACT, int MASK, bool DRES>
@@ -1135,7 +1163,8 @@ static void bwd_apply_t(const void* dy, const void* x, const void* y, const floa
   const size_t lds = sizeof(float) * 6 * C;
   bn_bwd_apply_kernel<T, V, ACT, MASK, DRES><<<apply_grid(work), 256, lds, st>>>(
       static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(y), mi, ss, k,
-      static_cast<T*>(dx), static_cast<T*>(dres), M, C, static_cast<const T*>(dy2), ld2);
+      static_cast<T*>(dx), static_cast<T*>(dres), M, C, static_cast<const T*>(dy2), ld2,
+      (l3_order() & 4) != 0);
 }
 
 #define RT_ACT_MASK_DISPATCH(FN, ...)                                                   \

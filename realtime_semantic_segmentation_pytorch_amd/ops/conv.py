@@ -198,7 +198,70 @@ def _order(cands):
         cands.sort(key=lambda c: c[0] != "hreg2")
     if os.environ.get("RTSEG_CONV_STEM") == "1":
         cands.sort(key=lambda c: c[0] != "stem")
+    if os.environ.get("RTSEG_CONV_GEMM") == "1":
+        cands.sort(key=lambda c: c[0] != "gemm")
     return cands
+
+
+# ----------------------------------------------------------------------------- pointwise GEMMs
+def gemm_ok(conv) -> bool:
+    """1 x 1, no padding, stride 1 or 2, ungrouped: each pass is one plain GEMM over the
+    channels-last pixel rows (hipBLASLt).  This is the candidate for the pointwise passes the
+    implicit-GEMM kernels lose to MIOpen: DDRNet-23's DAPPM 1024 -> 256 at 2 x 4 to 16 x 32, the
+    compression 1 x 1s, and the strided 1 x 1 shortcuts' data / weight gradients.
+    ``RTSEG_CONV_GEMM=0``: off; ``=1``: first (forced)."""
+    return (os.environ.get("RTSEG_CONV_GEMM") != "0" and tuple(conv.kernel_size) == (1, 1)
+            and tuple(conv.padding) == (0, 0) and tuple(conv.dilation) == (1, 1)
+            and getattr(conv, "groups", 1) == 1 and tuple(conv.stride) in ((1, 1), (2, 2)))
+
+
+def _rows(t: torch.Tensor) -> torch.Tensor:
+    """[N*H*W, C] view of a channels-last NCHW tensor (a copy if it is not channels-last dense)."""
+    return t.permute(0, 2, 3, 1).reshape(-1, t.shape[1])
+
+
+def _subsample(x: torch.Tensor, s: int) -> torch.Tensor:
+    """The pixels a stride-s 1 x 1 conv reads (pad 0: rows and columns 0, s, 2s, ...)."""
+    return x if s == 1 else x[:, :, ::s, ::s].contiguous(memory_format=torch.channels_last)
+
+
+def _from_rows(r: torch.Tensor, n: int, h: int, w: int) -> torch.Tensor:
+    return r.view(n, h, w, r.shape[1]).permute(0, 3, 1, 2)
+
+
+def gemm_fwd(x: torch.Tensor, wk: torch.Tensor, s: int) -> torch.Tensor:
+    """y = x W^T per pixel: [P, Cin] x [Cin, Cout], the output rows are y's channels-last memory."""
+    xs = _subsample(x, s)
+    y = torch.mm(_rows(xs), wk.reshape(wk.shape[0], -1).t())
+    return _from_rows(y, xs.shape[0], xs.shape[2], xs.shape[3])
+
+
+def gemm_dgrad(dy: torch.Tensor, wk: torch.Tensor, x_shape, s: int, addend=None) -> torch.Tensor:
+    """dx = dy W per output pixel, scattered to the rows / columns the stride read (the rest
+    stay zero, or the addend's): one addmm when s == 1."""
+    wm = wk.reshape(wk.shape[0], -1)  # [Cout, Cin]
+    n, cin, h, w = x_shape
+    if s == 1:
+        r = torch.mm(_rows(dy), wm) if addend is None else torch.addmm(_rows(addend), _rows(dy), wm)
+        return _from_rows(r, n, h, w)
+    sub = _from_rows(torch.mm(_rows(dy), wm), n, dy.shape[2], dy.shape[3])
+    if addend is None:
+        dx = torch.zeros((n, cin, h, w), dtype=dy.dtype, device=dy.device).contiguous(memory_format=torch.channels_last)
+        dx[:, :, ::s, ::s] = sub
+    else:
+        dx = addend.clone(memory_format=torch.channels_last)
+        dx[:, :, ::s, ::s] += sub
+    return dx
+
+
+def gemm_wgrad(x: torch.Tensor, dy: torch.Tensor, s: int) -> torch.Tensor:
+    """dW = dy^T x over the pixels the stride read: [Cout, P] x [P, Cin], fp32 out."""
+    a, b = _rows(dy).t(), _rows(_subsample(x, s))
+    try:
+        dw = torch.mm(a, b, out_dtype=torch.float32)  # fp32 accumulator written as is
+    except (RuntimeError, TypeError):
+        dw = torch.mm(a, b).float()
+    return dw.view(dw.shape[0], dw.shape[1], 1, 1)
 
 
 def _autocast_bf16(x: torch.Tensor) -> bool:
@@ -471,6 +534,8 @@ def _conv_fwd(x, weight, conv, stats):
         y, part = ops().conv_mfma(x, wk, stride, padding, dilation, stats, None, None, 0)
     elif impl == "stem":
         y, part = ops().conv_stem(x, wk, stride, padding, dilation, stats)
+    elif impl == "gemm":
+        y = gemm_fwd(x, wk, stride[0])
     else:
         y = F.conv2d(x, wk.permute(0, 3, 1, 2), None, stride, padding, dilation)
         y = y.contiguous(memory_format=torch.channels_last)
@@ -654,6 +719,13 @@ def _fwd_impl(x, wk, conv, key, stats) -> str:
         cands.append(("mfma", lambda: ops().conv_mfma(x, wk, stride, padding, dilation, stats, None, None, 0)))
     elif stem_ok(conv, x):
         cands.append(("stem", lambda: ops().conv_stem(x, wk, stride, padding, dilation, stats)))
+    if gemm_ok(conv):
+        def gemm():
+            y = gemm_fwd(x, wk, stride[0])
+            if stats:
+                ops().bn_stats_sums(y)
+
+        cands.append(("gemm", gemm))
     if not cands:
         return "miopen"
 
@@ -707,10 +779,12 @@ def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None):
     if hreg_ok(conv, cout, cin, _npix(x)):
         cands.append(("hreg", hreg))
         cands.append(("hreg2", lambda: hreg(2)))
+    if gemm_ok(conv):
+        cands.append(("gemm", lambda: gemm_dgrad(dy, wk, x.shape, stride[0], addend)))
     cands.append(("miopen", miopen))
     name, fn = cands[_choose(("dgrad",) + key, _order(cands))]
     dx = fn()
-    if addend is not None and name not in ("igemm", "halo", "wres", "hreg", "hreg2"):
+    if addend is not None and name not in ("igemm", "halo", "wres", "hreg", "hreg2", "gemm"):
         dx = dx + addend
     return dx
 
@@ -783,6 +857,8 @@ def _wgrad(x, dy, wk, conv, key, stride, padding, dilation):
             cands.append(("whalo2", lambda: whalo(2)))  # both output tiles per wave, K split
     if stem_ok(conv, x):
         cands.append(("stem", stem))
+    if gemm_ok(conv):
+        cands.append(("gemm", lambda: gemm_wgrad(x, dy, stride[0])))
     cands.append(("miopen", miopen))
     cands = _order(cands)
     dw = cands[_choose(("wgrad",) + key, cands)][1]()
