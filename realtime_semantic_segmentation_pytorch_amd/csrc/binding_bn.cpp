@@ -92,7 +92,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_stats_finalize(
                               fptr(w), fptr(b), fptr_mut(rmean), fptr_mut(rvar), nbt_ptr(nbt),
                               static_cast<float>(momentum), static_cast<float>(eps),
                               mi.data_ptr<float>(), ss.data_ptr<float>(), sums.data_ptr<double>(),
-                              cur_stream(), part.data_ptr<float>() + static_cast<int64_t>(G) * 2 * C);
+                              cur_stream(), part.data_ptr<float>() + static_cast<int64_t>(G) * 2 * C,
+                              SlabScratch(G, C, part).ptr());
   return {mi, ss, sums};
 }
 
@@ -107,7 +108,7 @@ at::Tensor bn_stats_sums(const at::Tensor& x, bool shift) {
   at::Tensor sums = at::empty({2 * C + 1}, x.options().dtype(at::kDouble));
   launch_bn_slab_to_sums(part.data_ptr<float>(), G, C, static_cast<double>(rows_of(x)),
                          sums.data_ptr<double>(), cur_stream(),
-                         part.data_ptr<float>() + static_cast<int64_t>(G) * 2 * C);
+                         part.data_ptr<float>() + static_cast<int64_t>(G) * 2 * C, SlabScratch(G, C, part).ptr());
   return sums;
 }
 
@@ -236,7 +237,8 @@ at::Tensor bn_bwd_sums(const std::optional<at::Tensor>& dy, const at::Tensor& x,
   at::Tensor part = bwd_slab(dyp, g2, x, opt_y(y, mask), mi, ss, act, mask, G);
   const int C = static_cast<int>(x.size(1));
   at::Tensor bsums = at::empty({2 * C}, x.options().dtype(at::kDouble));
-  launch_bn_slab_to_sums(part.data_ptr<float>(), G, C, -1.0, bsums.data_ptr<double>(), cur_stream());
+  launch_bn_slab_to_sums(part.data_ptr<float>(), G, C, -1.0, bsums.data_ptr<double>(), cur_stream(), nullptr,
+                         SlabScratch(G, C, part).ptr());
   return bsums;
 }
 
@@ -271,7 +273,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bwd_coeffs_impl(
   launch_bn_bwd_finalize(part.defined() ? part.data_ptr<float>() : nullptr, G, sums_p, cnt, C,
                          fptr(w), mi.data_ptr<float>(), batch_stats ? 1 : 0, k.data_ptr<float>(),
                          want_dw ? dw.data_ptr<float>() : nullptr,
-                         want_dw ? db.data_ptr<float>() : nullptr, cur_stream());
+                         want_dw ? db.data_ptr<float>() : nullptr, cur_stream(),
+                         part.defined() && !sums_p ? SlabScratch(G, C, part).ptr() : nullptr);
   return {k, dw, db};
 }
 

@@ -94,7 +94,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_finalize_slab(
   launch_bn_finalize_partials(part.data_ptr<float>(), static_cast<int>(part.size(0)), C, count, fptr(w), fptr(b),
                               fptr_mut(rmean), fptr_mut(rvar), nbt_ptr(nbt), static_cast<float>(momentum),
                               static_cast<float>(eps), mi.data_ptr<float>(), ss.data_ptr<float>(),
-                              sums.data_ptr<double>(), cur_stream());
+                              sums.data_ptr<double>(), cur_stream(), nullptr,
+                              SlabScratch(static_cast<int>(part.size(0)), C, part).ptr());
   return {mi, ss, sums};
 }
 
@@ -106,7 +107,7 @@ at::Tensor bn_slab_sums(const at::Tensor& part, double count) {
   const int C = static_cast<int>(part.size(1) / 2);
   at::Tensor sums = at::empty({2 * C + 1}, part.options().dtype(at::kDouble));
   launch_bn_slab_to_sums(part.data_ptr<float>(), static_cast<int>(part.size(0)), C, count, sums.data_ptr<double>(),
-                         cur_stream());
+                         cur_stream(), nullptr, SlabScratch(static_cast<int>(part.size(0)), C, part).ptr());
   return sums;
 }
 

@@ -69,9 +69,13 @@ void launch_bn_stats(const void* x, int dtype, int64_t M, int C, float* part, in
 void launch_bn_finalize_partials(const float* part, int G, int C, double count, const float* w,
                                  const float* b, float* rmean, float* rvar, int64_t* nbt,
                                  float momentum, float eps, float* mean_invstd, float* scale_shift,
-                                 double* sums_out, hipStream_t st, const float* pivot = nullptr);
+                                 double* sums_out, hipStream_t st, const float* pivot = nullptr,
+                                 double* scratch = nullptr);
 void launch_bn_slab_to_sums(const float* part, int G, int C, double count, double* sums,
-                            hipStream_t st, const float* pivot = nullptr);
+                            hipStream_t st, const float* pivot = nullptr, double* scratch = nullptr);
+// Row splits of a G-row statistics slab the finalize launchers pre-reduce when given a scratch of
+// bn_slab_splits(G) * 2C doubles (1: no pre-pass, no scratch needed).
+int bn_slab_splits(int G);
 void launch_bn_finalize(const double* sums, int C, const float* w, const float* b, float* rmean,
                         float* rvar, int64_t* nbt, float momentum, float eps, float* mean_invstd,
                         float* scale_shift, hipStream_t st);
@@ -91,7 +95,7 @@ void launch_bn_bwd_reduce(const void* dy, const void* x, const void* y, const fl
                           float* part, int G, hipStream_t st, const void* dy2 = nullptr, int64_t ld2 = 0);
 void launch_bn_bwd_finalize(const float* part, int G, const double* sums, const double* count_ptr,
                             int C, const float* w, const float* mean_invstd, int batch_stats,
-                            float* kcoef, float* dw, float* db, hipStream_t st);
+                            float* kcoef, float* dw, float* db, hipStream_t st, double* scratch = nullptr);
 void launch_bn_bwd_apply(const void* dy, const void* x, const void* y, const float* mean_invstd,
                          const float* scale_shift, const float* kcoef, void* dx, void* dres,
                          int dtype, int64_t M, int C, int act, int mask, hipStream_t st,

@@ -23,6 +23,7 @@
 // V-channel vector, bit j = activation derivative of channel c0+j is 1), which replaces
 // the 2-byte-per-element re-read of y in both backward passes by 1/8 byte.
 #include <cstdlib>
+#include <type_traits>
 
 #include "rtseg_common.h"
 #include "rtseg_launch.h"
@@ -213,16 +214,17 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ x, 
 constexpr int kFinWaves = 16;
 constexpr int kFinBlock = kFinWaves * 64;
 
-__device__ __forceinline__ void reduce_slab64(const float* __restrict__ part, int G, int C, int c,
+template <typename P>
+__device__ __forceinline__ void reduce_slab64(const P* __restrict__ part, int g0, int G, int C, int c,
                                               double* red) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   double a = 0.0, b = 0.0;
   if (c < C) {
     const int64_t rs = 2 * static_cast<int64_t>(C);
-    const float* p = part + c;
-    int gi = w;
+    const P* p = part + c;
+    int gi = g0 + w;
     for (; gi + 7 * kFinWaves < G; gi += 8 * kFinWaves) {  // 8 rows (16 loads) in flight per lane
-      float fa[8], fb[8];
+      P fa[8], fb[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         fa[k] = p[(gi + kFinWaves * k) * rs];
@@ -244,6 +246,23 @@ __device__ __forceinline__ void reduce_slab64(const float* __restrict__ part, in
     red[64 + lane] = tb;
   }
   __syncthreads();
+}
+
+// Row-split pre-pass of a tall slab: block (x, y) reduces rows [y * per, (y + 1) * per) of 64
+// channels into fp64 row y of out [S][2C].  One block per 64 channels reading a whole 2048-row
+// slab (1 MiB at C = 64) is bound by one CU's load bandwidth (~13 us per backward BN); split over
+// S = G / 128 blocks it is a few microseconds, and the finalize then reads S fp64 rows.  The
+// summation order is fixed (deterministic).
+__global__ void __launch_bounds__(kFinBlock) bn_slab_split_kernel(const float* __restrict__ part, int G, int C,
+                                                                  int per, double* __restrict__ out) {
+  __shared__ double red[kFinWaves * 128];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int g0 = blockIdx.y * per;
+  reduce_slab64<float>(part, g0, g0 + per < G ? g0 + per : G, C, c, red);
+  if (threadIdx.x < 64 && c < C) {
+    out[static_cast<int64_t>(blockIdx.y) * 2 * C + c] = red[threadIdx.x];
+    out[static_cast<int64_t>(blockIdx.y) * 2 * C + C + c] = red[64 + threadIdx.x];
+  }
 }
 
 __device__ __forceinline__ void finalize_channel(int c, int C, double sum, double sumsq,
@@ -277,14 +296,15 @@ __device__ __forceinline__ void unshift(const float* pivot, int c, double count,
 
 // Fused: slab reduce + finalize (+ sums[2C+1] for the backward's count).  ``pivot``: the shift
 // of a bn_stats slab (its row G), nullptr for a conv-epilogue slab (raw moments).
+template <typename P>
 __global__ void __launch_bounds__(kFinBlock) bn_finalize_partials_kernel(
-    const float* __restrict__ part, int G, int C, double count, const float* __restrict__ w,
+    const P* __restrict__ part, int G, int C, double count, const float* __restrict__ w,
     const float* __restrict__ b, float* __restrict__ rmean, float* __restrict__ rvar,
     int64_t* __restrict__ nbt, float momentum, float eps, float* __restrict__ mean_invstd,
     float* __restrict__ scale_shift, double* __restrict__ sums_out, const float* __restrict__ pivot) {
   __shared__ double red[kFinWaves * 128];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  reduce_slab64(part, G, C, c, red);
+  reduce_slab64<P>(part, 0, G, C, c, red);
   if (threadIdx.x < 64 && c < C) {
     double sum = red[threadIdx.x], sumsq = red[64 + threadIdx.x];
     unshift(pivot, c, count, sum, sumsq);
@@ -299,13 +319,14 @@ __global__ void __launch_bounds__(kFinBlock) bn_finalize_partials_kernel(
 }
 
 // SyncBN path, step 1: slab -> fp64 [2C+1] sums (all-reduced by the caller).
-__global__ void __launch_bounds__(kFinBlock) bn_slab_to_sums_kernel(const float* __restrict__ part, int G,
+template <typename P>
+__global__ void __launch_bounds__(kFinBlock) bn_slab_to_sums_kernel(const P* __restrict__ part, int G,
                                                               int C, double count,
                                                               double* __restrict__ sums,
                                                               const float* __restrict__ pivot) {
   __shared__ double red[kFinWaves * 128];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  reduce_slab64(part, G, C, c, red);
+  reduce_slab64<P>(part, 0, G, C, c, red);
   if (threadIdx.x < 64 && c < C) {
     double sum = red[threadIdx.x], sumsq = red[64 + threadIdx.x];
     unshift(pivot, c, count, sum, sumsq);
@@ -552,14 +573,15 @@ __device__ __forceinline__ void bwd_finalize_channel(int c, int C, double sg, do
 }
 
 // Slab (or already-reduced sums, SyncBN) -> dx coefficients + parameter grads.
+template <typename P>
 __global__ void __launch_bounds__(kFinBlock) bn_bwd_finalize_kernel(
-    const float* __restrict__ part, int G, const double* __restrict__ sums,
+    const P* __restrict__ part, int G, const double* __restrict__ sums,
     const double* __restrict__ count_ptr, int C, const float* __restrict__ w,
     const float* __restrict__ mean_invstd, int batch_stats, float* __restrict__ kcoef,
     float* __restrict__ dw, float* __restrict__ db) {
   __shared__ double red[kFinWaves * 128];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  if (!sums) reduce_slab64(part, G, C, c, red);
+  if (!sums) reduce_slab64<P>(part, 0, G, C, c, red);
   if (threadIdx.x < 64 && c < C) {
     const double sg = sums ? sums[c] : red[threadIdx.x];
     const double sgx = sums ? sums[C + c] : red[64 + threadIdx.x];
@@ -1005,18 +1027,48 @@ void launch_bn_stats(const void* x, int dtype, int64_t M, int C, float* part, in
   });
 }
 
+constexpr int kSplitRows = 128;
+
+// RTSEG_BN_SPLIT=0: off (A/B)
+int bn_slab_splits(int G) {
+  static const bool on = [] {
+    const char* e = std::getenv("RTSEG_BN_SPLIT");
+    return !(e && e[0] == '0');
+  }();
+  return on && G >= 4 * kSplitRows ? (G + kSplitRows - 1) / kSplitRows : 1;
+}
+
+// scratch (bn_slab_splits(G) * 2C doubles, or nullptr): the row-split pre-pass, then F(fp64 rows, S);
+// else F(the slab, G)
+template <typename F>
+static void with_split(const float* part, int G, int C, double* scratch, hipStream_t st, F&& f) {
+  const int S = bn_slab_splits(G);
+  if (scratch == nullptr || S <= 1 || part == nullptr) {
+    f(part, G);
+    return;
+  }
+  bn_slab_split_kernel<<<dim3((C + 63) / 64, S), kFinBlock, 0, st>>>(part, G, C, kSplitRows, scratch);
+  f(static_cast<const double*>(scratch), S);
+}
+
 void launch_bn_finalize_partials(const float* part, int G, int C, double count, const float* w,
                                  const float* b, float* rmean, float* rvar, int64_t* nbt,
                                  float momentum, float eps, float* mean_invstd, float* scale_shift,
-                                 double* sums_out, hipStream_t st, const float* pivot) {
-  bn_finalize_partials_kernel<<<(C + 63) / 64, kFinBlock, 0, st>>>(part, G, C, count, w, b, rmean, rvar,
-                                                             nbt, momentum, eps, mean_invstd,
-                                                             scale_shift, sums_out, pivot);
+                                 double* sums_out, hipStream_t st, const float* pivot, double* scratch) {
+  with_split(part, G, C, scratch, st, [&](const auto* p, int g) {
+    using P = std::remove_cv_t<std::remove_pointer_t<decltype(p)>>;
+    bn_finalize_partials_kernel<P><<<(C + 63) / 64, kFinBlock, 0, st>>>(p, g, C, count, w, b, rmean, rvar, nbt,
+                                                                     momentum, eps, mean_invstd, scale_shift,
+                                                                     sums_out, pivot);
+  });
 }
 
 void launch_bn_slab_to_sums(const float* part, int G, int C, double count, double* sums,
-                            hipStream_t st, const float* pivot) {
-  bn_slab_to_sums_kernel<<<(C + 63) / 64, kFinBlock, 0, st>>>(part, G, C, count, sums, pivot);
+                            hipStream_t st, const float* pivot, double* scratch) {
+  with_split(part, G, C, scratch, st, [&](const auto* p, int g) {
+    using P = std::remove_cv_t<std::remove_pointer_t<decltype(p)>>;
+    bn_slab_to_sums_kernel<P><<<(C + 63) / 64, kFinBlock, 0, st>>>(p, g, C, count, sums, pivot);
+  });
 }
 
 void launch_bn_finalize(const double* sums, int C, const float* w, const float* b,
@@ -1217,9 +1269,12 @@ void launch_bn_bwd_reduce(const void* dy, const void* x, const void* y, const fl
 
 void launch_bn_bwd_finalize(const float* part, int G, const double* sums, const double* count_ptr,
                             int C, const float* w, const float* mean_invstd, int batch_stats,
-                            float* kcoef, float* dw, float* db, hipStream_t st) {
-  bn_bwd_finalize_kernel<<<(C + 63) / 64, kFinBlock, 0, st>>>(part, G, sums, count_ptr, C, w,
-                                                        mean_invstd, batch_stats, kcoef, dw, db);
+                            float* kcoef, float* dw, float* db, hipStream_t st, double* scratch) {
+  with_split(sums ? nullptr : part, G, C, scratch, st, [&](const auto* p, int g) {
+    using P = std::remove_cv_t<std::remove_pointer_t<decltype(p)>>;
+    bn_bwd_finalize_kernel<P><<<(C + 63) / 64, kFinBlock, 0, st>>>(p, g, sums, count_ptr, C, w, mean_invstd,
+                                                                batch_stats, kcoef, dw, db);
+  });
 }
 
 template <typename T, int V, int ACT, int MASK>
