@@ -151,7 +151,8 @@ std::tuple<at::Tensor, at::Tensor> conv_stem(const at::Tensor& x, const at::Tens
 // dy [N,Cout,Ho,Wo] CL bf16, wt [Cin,KH,KW,Cout] bf16 -> dx [N,Cin,H,W] CL bf16
 at::Tensor conv_dgrad_impl(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
                            at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
-                           const std::optional<at::Tensor>& bias, const std::optional<at::Tensor>& addend, int kind) {
+                           const std::optional<at::Tensor>& bias, const std::optional<at::Tensor>& addend, int kind,
+                           const std::optional<at::Tensor>& addend_mask) {
   const bool halo = kind == 1, wres = kind == 2, hreg = kind == 3 || kind == 4;
   check_act(dy, "grad_output");
   TORCH_CHECK(x_size.size() == 4, "rtseg.conv_igemm_dgrad: x_size must be [N, Cin, H, W]");
@@ -191,6 +192,14 @@ at::Tensor conv_dgrad_impl(const at::Tensor& dy, const at::Tensor& wt, at::IntAr
     check_act(*addend, "addend");
     TORCH_CHECK(addend->sizes() == dx.sizes(), "rtseg.conv_igemm_dgrad: addend must match dx");
     g.res = addend->data_ptr();
+    if (addend_mask.has_value() && addend_mask->defined()) {  // dx += addend * mask (ops/bn.py kMaskBits)
+      TORCH_CHECK(addend_mask->is_cuda() && addend_mask->scalar_type() == at::kByte && addend_mask->is_contiguous() &&
+                      addend_mask->numel() * 8 == dx.numel() && g.cin % 8 == 0,
+                  "rtseg.conv_dgrad: addend_mask must be contiguous uint8 [numel(dx) / 8]");
+      g.amask = addend_mask->data_ptr<uint8_t>();
+    }
+  } else {
+    TORCH_CHECK(!(addend_mask.has_value() && addend_mask->defined()), "rtseg.conv_dgrad: addend_mask without addend");
   }
   if (halo) launch_conv_halo_dgrad(g, cur_stream());
   else if (wres) launch_conv_wres_dgrad(g, cur_stream());
@@ -203,28 +212,30 @@ at::Tensor conv_dgrad_impl(const at::Tensor& dy, const at::Tensor& wt, at::IntAr
 
 at::Tensor conv_igemm_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
                             at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
-                            const std::optional<at::Tensor>& bias, const std::optional<at::Tensor>& addend) {
-  return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, bias, addend, 0);
+                            const std::optional<at::Tensor>& bias, const std::optional<at::Tensor>& addend,
+                            const std::optional<at::Tensor>& addend_mask) {
+  return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, bias, addend, 0, addend_mask);
 }
 
 at::Tensor conv_halo_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
                            at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
-                           const std::optional<at::Tensor>& addend) {
-  return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, std::nullopt, addend, 1);
+                           const std::optional<at::Tensor>& addend, const std::optional<at::Tensor>& addend_mask) {
+  return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, std::nullopt, addend, 1, addend_mask);
 }
 
 at::Tensor conv_hreg_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
                            at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
-                           const std::optional<at::Tensor>& addend, int64_t rows_per_wave) {
+                           const std::optional<at::Tensor>& addend, int64_t rows_per_wave,
+                           const std::optional<at::Tensor>& addend_mask) {
   TORCH_CHECK(rows_per_wave == 1 || rows_per_wave == 2, "rtseg.conv_hreg_dgrad: rows_per_wave must be 1 or 2");
   return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, std::nullopt, addend,
-                         rows_per_wave == 2 ? 4 : 3);
+                         rows_per_wave == 2 ? 4 : 3, addend_mask);
 }
 
 at::Tensor conv_wres_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
                            at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
-                           const std::optional<at::Tensor>& addend) {
-  return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, std::nullopt, addend, 2);
+                           const std::optional<at::Tensor>& addend, const std::optional<at::Tensor>& addend_mask) {
+  return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, std::nullopt, addend, 2, addend_mask);
 }
 
 // x [N,Cin,H,W], dy [N,Cout,Ho,Wo] (CL bf16) -> dw fp32 [Cout,Cin,KH,KW]
@@ -332,18 +343,18 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
   m.def("conv_igemm(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats, "
         "Tensor? scale_shift, Tensor? residual, int act) -> (Tensor, Tensor)");
   m.def("conv_igemm_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
-        "Tensor? bias=None, Tensor? addend=None) -> Tensor");
+        "Tensor? bias=None, Tensor? addend=None, Tensor? addend_mask=None) -> Tensor");
   m.def("conv_halo(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats, "
         "Tensor? scale_shift, Tensor? residual, int act) -> (Tensor, Tensor)");
   m.def("conv_halo_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
-        "Tensor? addend=None) -> Tensor");
+        "Tensor? addend=None, Tensor? addend_mask=None) -> Tensor");
   m.def("conv_hreg(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats, "
         "int rows_per_wave=1) -> (Tensor, Tensor)");
   m.def("conv_hreg_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
-        "Tensor? addend=None, int rows_per_wave=1) -> Tensor");
+        "Tensor? addend=None, int rows_per_wave=1, Tensor? addend_mask=None) -> Tensor");
   m.def("conv_wres(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats) -> (Tensor, Tensor)");
   m.def("conv_wres_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
-        "Tensor? addend=None) -> Tensor");
+        "Tensor? addend=None, Tensor? addend_mask=None) -> Tensor");
   m.def("conv_stem(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats) -> (Tensor, Tensor)");
   m.def("conv_stem_wgrad_bn(Tensor x, Tensor dy, Tensor bn_input, Tensor kcoef, Tensor mean_invstd, "
         "Tensor scale_shift, int act, int kh, int kw, int[] stride, int[] padding, int[] dilation, "

@@ -171,6 +171,7 @@ struct ConvGeom {
   const void* res;
   int act;
   int n, h, w_in, cin, ho, wo, cout, kh, kw, sh, sw, ph, pw, dh, dw;
+  const uint8_t* amask = nullptr;  // data gradient: bit mask of the addend (res), see mask_addend4
 };
 // BN activation-derivative sources (= ops/bn.py MASK_*)
 enum BnMaskMode : int { kBnMaskNone = 0, kBnMaskFromY = 1, kBnMaskFromX = 2, kBnMaskBits = 3 };

@@ -182,5 +182,16 @@ __device__ __forceinline__ void bf16x4_unpack(uint2 r, float* f) {
   f[3] = bf16_to_f32(static_cast<uint16_t>(r.y >> 16));
 }
 
+// A residual-gradient addend handed over with its BN's activation mask (ops/bn.py, kMaskBits:
+// one bit per element, element e in bit e % 8 of byte e / 8): the 4 addend values of elements
+// e .. e + 3 (e % 4 == 0) where the mask is 0 become 0 -- the masked gradient g * relu'(z) is
+// never written out by the BN backward.
+__device__ __forceinline__ void mask_addend4(const uint8_t* __restrict__ m, int64_t e, float* r) {
+  const uint32_t b = static_cast<uint32_t>(m[e >> 3]) >> (e & 7);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (!((b >> q) & 1u)) r[q] = 0.f;
+}
+
 }  // namespace mdev
 }  // namespace rtseg

@@ -51,6 +51,7 @@ struct HaloArgs {
   const float* ss;         // EPI 1: inference BN [scale | shift] fp32 [2*cout]
   const uint16_t* res;     // EPI 1: residual, y's layout, or null
   const uint16_t* addend;  // EPI 0: bf16 tensor of y's layout added to the result, or null
+  const uint8_t* amask;    // EPI 0: bit mask of the addend (mask_addend4), or null
   int act;
   int H, W, C;             // gathered operand
   int Ho, Wo, cout;        // output
@@ -249,6 +250,7 @@ __global__ void __launch_bounds__(WM* WN * 64) halo_conv_kernel(const HaloArgs a
           if (a.addend != nullptr && sok) {
             float r[4];
             bf16x4_unpack(*reinterpret_cast<const uint2*>(a.addend + pend_off[tj] + co), r);
+            if (a.amask != nullptr) mask_addend4(a.amask, pend_off[tj] + co, r);
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[q] += r[q];
           }
@@ -542,6 +544,7 @@ void launch_conv_halo_dgrad(const ConvGeom& g, hipStream_t st) {
   k.w = static_cast<const uint16_t*>(g.w);
   k.y = static_cast<uint16_t*>(g.y);
   k.addend = static_cast<const uint16_t*>(g.res);
+  k.amask = g.amask;
   k.H = g.ho; k.W = g.wo; k.C = g.cout;
   k.Ho = g.h; k.Wo = g.w_in; k.cout = g.cin;
   k.wrow = g.kh * g.kw * g.cout;

@@ -47,6 +47,7 @@ struct HrArgs {
   uint16_t* y;             // output [N][Ho][Wo][cout]
   float* part;             // BN statistics slab [grid / ntiles][2 * cout], or null
   const uint16_t* addend;  // bf16 tensor of y's layout added to the result, or null
+  const uint8_t* amask;    // bit mask of the addend (mask_addend4), or null
   int H, W, C;             // gathered operand
   int Ho, Wo, cout;
   int cch;                 // 64-channel chunks of C
@@ -175,6 +176,7 @@ __global__ void __launch_bounds__(2 * kTH / RPW * 64) hreg_conv_kernel(const HrA
           if (a.addend != nullptr && ok) {
             float r[4];
             bf16x4_unpack(*reinterpret_cast<const uint2*>(a.addend + off + co), r);
+            if (a.amask != nullptr) mask_addend4(a.amask, off + co, r);
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[q] += r[q];
           }
@@ -349,6 +351,7 @@ void launch_conv_hreg(const ConvGeom& g, int mode, void* wpack, hipStream_t st, 
   k.y = static_cast<uint16_t*>(g.y);
   k.part = dgrad ? nullptr : g.part;
   k.addend = dgrad ? static_cast<const uint16_t*>(g.res) : nullptr;
+  k.amask = dgrad ? g.amask : nullptr;
   const int grid = hreg_grid(k);
   if (grid <= 0) return;
   if (rows_per_wave == 2) {

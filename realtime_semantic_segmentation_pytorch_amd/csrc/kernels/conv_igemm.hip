@@ -68,6 +68,7 @@ struct IgArgs {
   const uint16_t* res;
   const float* bias;      // [cout] added to the accumulators first (transposed conv), or null
   const uint16_t* addend; // bf16 tensor of the output's layout added in the epilogue, or null
+  const uint8_t* amask;   // bit mask of the addend (mask_addend4), or null
   int act;
   int H, W, C;            // gathered operand [N][H][W][C]
   int Hv, Wv;             // virtual output grid
@@ -305,8 +306,10 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
               if constexpr (GB) {
                 const auto r = __builtin_amdgcn_raw_buffer_load_b64(sr, voff, 0, 0);
                 bf16x4_unpack(make_uint2(r[0], r[1]), sv);
+                if (EPI == 0 && a.amask != nullptr && voff < a.ybytes) mask_addend4(a.amask, voff >> 1, sv);
               } else if (ok && co < a.cout) {
                 bf16x4_unpack(*reinterpret_cast<const uint2*>(side + pend_off[tj] + co), sv);
+                if (EPI == 0 && a.amask != nullptr) mask_addend4(a.amask, pend_off[tj] + co, sv);
               }
             }
             if constexpr (EPI == 0 && STATS == 0) {
@@ -845,6 +848,7 @@ void launch_conv_igemm_dgrad(const ConvGeom& g, hipStream_t st) {
       k.y = static_cast<uint16_t*>(g.y);
       k.bias = g.scale_shift;  // dgrad launches reuse the field as an optional bias (transposed conv)
       k.addend = static_cast<const uint16_t*>(g.res);  // ... and res as an optional addend
+      k.amask = g.amask;
       k.H = g.ho; k.W = g.wo; k.C = g.cout;
       k.Hv = (g.h - a + g.sh - 1) / g.sh;
       k.Wv = (g.w_in - b + g.sw - 1) / g.sw;

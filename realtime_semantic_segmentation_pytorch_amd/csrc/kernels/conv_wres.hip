@@ -52,6 +52,7 @@ struct WresArgs {
   uint16_t* y;             // [N][Ho][Wo][cout]
   float* part;             // BN statistics slab [grid / ntiles][2 * cout], or null
   const uint16_t* addend;  // bf16 tensor of y's layout added to the result, or null
+  const uint8_t* amask;    // bit mask of the addend (mask_addend4), or null
   int H, W;                // gathered operand
   int Ho, Wo, cout;        // output
   int dh0, dw0;            // halo origin: input row of output row oy (tap-relative offset 0)
@@ -181,6 +182,7 @@ __global__ void __launch_bounds__(NW * 64) wres_conv_kernel(const WresArgs a) {
           if (a.addend != nullptr && ok) {
             float r[4];
             bf16x4_unpack(*reinterpret_cast<const uint2*>(a.addend + off + co), r);
+            if (a.amask != nullptr) mask_addend4(a.amask, off + co, r);
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[q] += r[q];
           }
@@ -342,6 +344,7 @@ void launch_conv_wres_fwd(const ConvGeom& g, hipStream_t st) {
   k.y = static_cast<uint16_t*>(g.y);
   k.part = g.part;
   k.addend = nullptr;
+  k.amask = nullptr;
   const int grid = wres_grid(k.mtiles, k.ntiles);
   if (grid <= 0) return;
   if (k.part != nullptr) wres_launch<1, 0>(k, grid, st);
@@ -357,6 +360,7 @@ void launch_conv_wres_dgrad(const ConvGeom& g, hipStream_t st) {
   k.y = static_cast<uint16_t*>(g.y);
   k.part = nullptr;
   k.addend = static_cast<const uint16_t*>(g.res);
+  k.amask = g.amask;
   const int grid = wres_grid(k.mtiles, k.ntiles);
   if (grid <= 0) return;
   wres_launch<0, 1>(k, grid, st);

@@ -31,6 +31,12 @@ MASK_NONE, MASK_FROM_Y, MASK_FROM_X, MASK_BITS = 0, 1, 2, 3
 _USE_BITS = os.environ.get("RTSEG_BN_BITS", "1") != "0"
 # residual-gradient hand-off to the upstream conv's dgrad (RTSEG_RES_HANDOFF=0: off, for A/B)
 _HANDOFF = os.environ.get("RTSEG_RES_HANDOFF", "1") != "0"
+# ... as the BN output's gradient + its activation bit mask, applied in the dgrad epilogue, so the
+# BN backward never writes the masked residual gradient.  Opt-in (RTSEG_MASKED_HANDOFF=1): on the
+# DDRNet-23 b32 step it measured 0.7 % slower than writing the masked gradient out (524.8 / 524.4
+# vs 528.5 images/s, profiles/r5_masked) -- the epilogue's per-lane mask-byte loads cost more
+# than the saved 2-byte-per-element write
+_MASKED_HANDOFF = os.environ.get("RTSEG_MASKED_HANDOFF", "0") == "1"
 
 
 def act_code(act) -> Optional[int]:
@@ -164,8 +170,18 @@ class _BNActFn(torch.autograd.Function):
                 if want_dw:
                     local = bsums.clone()
                 dist.all_reduce(bsums, group=ctx.pg)
+        # the residual gradient dy * act'(z) handed over unmaterialised: the conv's dgrad epilogue
+        # applies the bit mask to dy itself (ops/conv.py MaskedAddend) -- no dres write here
+        masked = (want_dres and ctx.handoff is not None and mask == MASK_BITS and dy is not None
+                  and dy2 is None and _MASKED_HANDOFF and x.dtype == torch.bfloat16
+                  and x.shape[1] % 8 == 0 and x.shape[1] <= 2048)  # one mask byte per 8 channels
         dx, dres, dw, db = ops().bn_backward(dy, x, y, bsums, sums, mi, ss, weight, ctx.act,
-                                             mask, want_dres, ctx.batch_stats, want_dw, None, dy2)
+                                             mask, want_dres and not masked, ctx.batch_stats, want_dw, None, dy2)
+        if masked:
+            from .conv import MaskedAddend
+
+            dres = MaskedAddend(dy, y)  # y holds the activation bits (MASK_BITS)
+            MASKED_HANDOFFS[0] += 1
         if local is not None:
             # parameter gradients are this rank's contribution (DDP averages them), as in torch's
             # SyncBatchNorm; only the input-gradient coefficients use the all-reduced sums
@@ -179,6 +195,7 @@ class _BNActFn(torch.autograd.Function):
                 dres if want_dres else None, None, None, None, None, None, None, None)
 
 
+MASKED_HANDOFFS = [0]  # residual gradients handed over as (gradient, bit mask) (tests)
 STEM_HANDOFFS = [0]  # BN backward dx passes handed to a stem conv's weight gradient (tests)
 
 

@@ -36,6 +36,8 @@ from __future__ import annotations
 
 import os
 
+from typing import NamedTuple
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -618,6 +620,27 @@ def _stem_wgrad_bn(x, conv, wdtype, dy, fused):
     return like_param(dw.to(wdtype), w)
 
 
+class MaskedAddend(NamedTuple):
+    """A residual branch's gradient ``g * act'(z)`` handed to the dgrad of the conv whose input
+    is the residual (ops/bn.py) WITHOUT being written out: the BN output's gradient ``g`` and the
+    BN's 1-bit activation mask (kMaskBits: element e in bit e % 8 of byte e / 8, channels-last
+    order).  The routed dgrad kernels apply the mask in their addend epilogue
+    (``addend_mask``); other implementations take :meth:`materialize`."""
+    g: torch.Tensor
+    bits: torch.Tensor
+
+    def materialize(self) -> torch.Tensor:
+        n, c, h, w = self.g.shape
+        shifts = torch.arange(8, device=self.bits.device, dtype=torch.uint8)
+        m = (self.bits.view(-1, 1) >> shifts) & 1  # [numel / 8, 8] in channels-last element order
+        m = m.view(n, h, w, c).permute(0, 3, 1, 2)
+        return self.g * m.to(self.g.dtype)
+
+
+def _plain(addend):
+    return addend.materialize() if isinstance(addend, MaskedAddend) else addend
+
+
 def _conv_bwd(x, wk, conv, key, dy, want_dx, want_dw, wdtype, addend=None, on_dx=None):
     """(dx (+ addend) | None, dw | None) of a routed conv.  ``on_dx(dx)`` runs between the data
     and the weight gradient (the early SyncBN all-reduce of the producer BN)."""
@@ -629,7 +652,7 @@ def _conv_bwd(x, wk, conv, key, dy, want_dx, want_dw, wdtype, addend=None, on_dx
     if want_dx:
         dx = _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend)
     elif addend is not None:
-        dx = addend
+        dx = _plain(addend)
     if on_dx is not None and want_dx:
         on_dx(dx)  # dx is the input's whole gradient (a handed-off residual gradient included)
     if want_dw:
@@ -742,25 +765,40 @@ def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None):
     """dx (+ addend: a residual branch's gradient, added in our kernel's epilogue)."""
     cin, cout = conv.in_channels, conv.out_channels
     wt = []
+    amask = None  # the addend's activation bit mask (MaskedAddend), applied in our epilogues
+    if isinstance(addend, MaskedAddend):
+        if addend.g.dtype == torch.bfloat16 and addend.g.is_contiguous(memory_format=torch.channels_last) \
+                and addend.g.data_ptr() % 16 == 0 and addend.bits.is_contiguous() and cin % 8 == 0:
+            addend, amask = addend.g, addend.bits
+        else:
+            addend = addend.materialize()
     if addend is not None:
         addend = addend.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         if addend.data_ptr() % 16:
             addend = addend.clone(memory_format=torch.channels_last)
+    plain = []  # the masked addend written out, for the implementations without a mask epilogue
+
+    def addend_plain():
+        if amask is None:
+            return addend
+        if not plain:
+            plain.append(MaskedAddend(addend, amask).materialize())
+        return plain[0]
 
     def ours():
         if not wt:  # [Cin, KH, KW, Cout] bf16, the dgrad B operand
             wt.append(weight_crsk(conv, wk))
-        return ops().conv_igemm_dgrad(dy, wt[0], list(x.shape), stride, padding, dilation, None, addend)
+        return ops().conv_igemm_dgrad(dy, wt[0], list(x.shape), stride, padding, dilation, None, addend, amask)
 
     def halo():
         if not wt:
             wt.append(weight_crsk(conv, wk))
-        return ops().conv_halo_dgrad(dy, wt[0], list(x.shape), stride, padding, dilation, addend)
+        return ops().conv_halo_dgrad(dy, wt[0], list(x.shape), stride, padding, dilation, addend, amask)
 
     def wres():
         if not wt:
             wt.append(weight_crsk(conv, wk))
-        return ops().conv_wres_dgrad(dy, wt[0], list(x.shape), stride, padding, dilation, addend)
+        return ops().conv_wres_dgrad(dy, wt[0], list(x.shape), stride, padding, dilation, addend, amask)
 
     def miopen():
         return torch.ops.aten.convolution_backward(dy, x, wk.permute(0, 3, 1, 2), None, stride, padding, dilation, False,
@@ -769,7 +807,8 @@ def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None):
     def hreg(rows_per_wave=1):
         if not wt:
             wt.append(weight_crsk(conv, wk))
-        return ops().conv_hreg_dgrad(dy, wt[0], list(x.shape), stride, padding, dilation, addend, rows_per_wave)
+        return ops().conv_hreg_dgrad(dy, wt[0], list(x.shape), stride, padding, dilation, addend, rows_per_wave,
+                                     amask)
 
     cands = [("igemm", ours)] if cout % 64 == 0 and cin % 8 == 0 else []
     if halo_ok(conv, cout, cin):
@@ -780,12 +819,12 @@ def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None):
         cands.append(("hreg", hreg))
         cands.append(("hreg2", lambda: hreg(2)))
     if gemm_ok(conv):
-        cands.append(("gemm", lambda: gemm_dgrad(dy, wk, x.shape, stride[0], addend)))
+        cands.append(("gemm", lambda: gemm_dgrad(dy, wk, x.shape, stride[0], addend_plain())))
     cands.append(("miopen", miopen))
     name, fn = cands[_choose(("dgrad",) + key, _order(cands))]
     dx = fn()
     if addend is not None and name not in ("igemm", "halo", "wres", "hreg", "hreg2", "gemm"):
-        dx = dx + addend
+        dx = dx + addend_plain()
     return dx
 
 

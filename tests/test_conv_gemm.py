@@ -129,3 +129,13 @@ def test_gemm_routed_downsample_block(monkeypatch, block):
         assert ok(rel(gp0[n], g), rel(gp1[n], g), 2e-2), (n, rel(gp0[n], g), rel(gp1[n], g))
     assert calls[0] == {"gemm_fwd", "gemm_dgrad", "gemm_wgrad"}, calls[0]
     assert not calls[1], calls[1]
+
+
+def test_masked_addend_materialize_cpu():
+    """MaskedAddend (ops/conv.py): the channels-last bit order of the BN activation mask."""
+    g = torch.randn(2, 16, 3, 5).to(torch.bfloat16).contiguous(**CL)
+    m = torch.rand(2, 16, 3, 5) > 0.5
+    flat = m.permute(0, 2, 3, 1).reshape(-1, 8).to(torch.uint8)  # element e -> byte e // 8, bit e % 8
+    bits = (flat << torch.arange(8, dtype=torch.uint8)).sum(1).to(torch.uint8)
+    out = conv_mod.MaskedAddend(g, bits).materialize()
+    assert torch.equal(out, g * m.to(g.dtype))

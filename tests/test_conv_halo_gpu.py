@@ -11,6 +11,26 @@ from realtime_semantic_segmentation_pytorch_amd import ops
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
+
+def _mask_bits(shape, seed):
+    """Random activation bit mask of a channels-last bf16 tensor (ops/bn.py kMaskBits layout)."""
+    g = torch.Generator().manual_seed(seed)
+    n = shape[0] * shape[1] * shape[2] * shape[3] // 8
+    return torch.randint(0, 256, (n,), generator=g, dtype=torch.uint8).to(DEV)
+
+
+def _addend_ref(add, bits, mode):
+    """What the dgrad epilogue adds: nothing, the addend, or the addend where its mask bit is set
+    (element e of the channels-last order in bit e % 8 of byte e / 8)."""
+    if not mode:
+        return 0.0
+    a = add.float()
+    if mode != "masked":
+        return a
+    n, c, h, w = add.shape
+    m = torch.stack([(bits >> i) & 1 for i in range(8)], dim=1).reshape(n, h, w, c).permute(0, 3, 1, 2)
+    return a * m.float()
+
 # (n, cin, h, w, cout, kh, kw, ph, pw)
 GEOMS = [
     (2, 64, 17, 70, 64, 3, 3, 1, 1),
@@ -88,7 +108,7 @@ def test_halo_bn_epilogue(act, with_res):
 
 
 @pytest.mark.parametrize("geom", GEOMS)
-@pytest.mark.parametrize("with_addend", [False, True])
+@pytest.mark.parametrize("with_addend", [False, True, "masked"])
 def test_halo_dgrad(geom, with_addend):
     n, cin, h, w, cout, kh, kw, ph, pw = geom
     x, wt = _case(n, cin, h, w, cout, kh, kw, seed=2)
@@ -99,10 +119,11 @@ def test_halo_dgrad(geom, with_addend):
     add = torch.randn(x.shape, generator=g).to(DEV, torch.bfloat16).contiguous(**cl)
     if cout % 64 or cin % 64:
         pytest.skip("dgrad reduces over Cout and produces Cin: both must be 64-channel multiples")
+    bits = _mask_bits(add.shape, 7)
     dx = torch.ops.rtseg.conv_halo_dgrad(dy, wt.permute(1, 2, 3, 0).contiguous(), list(x.shape), [1, 1], [ph, pw],
-                                         [1, 1], add if with_addend else None)
+                                         [1, 1], add if with_addend else None, bits if with_addend == "masked" else None)
     ref = torch.nn.grad.conv2d_input(x.shape, wt.float(), dy.float(), 1, (ph, pw), 1)
-    _close(dx, ref + add.float() if with_addend else ref, 2e-2)
+    _close(dx, ref + _addend_ref(add, bits, with_addend), 2e-2)
 
 
 def test_halo_routed_training_step(monkeypatch):

@@ -10,6 +10,26 @@ from realtime_semantic_segmentation_pytorch_amd import ops
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
+
+def _mask_bits(shape, seed):
+    """Random activation bit mask of a channels-last bf16 tensor (ops/bn.py kMaskBits layout)."""
+    g = torch.Generator().manual_seed(seed)
+    n = shape[0] * shape[1] * shape[2] * shape[3] // 8
+    return torch.randint(0, 256, (n,), generator=g, dtype=torch.uint8).to(DEV)
+
+
+def _addend_ref(add, bits, mode):
+    """What the dgrad epilogue adds: nothing, the addend, or the addend where its mask bit is set
+    (element e of the channels-last order in bit e % 8 of byte e / 8)."""
+    if not mode:
+        return 0.0
+    a = add.float()
+    if mode != "masked":
+        return a
+    n, c, h, w = add.shape
+    m = torch.stack([(bits >> i) & 1 for i in range(8)], dim=1).reshape(n, h, w, c).permute(0, 3, 1, 2)
+    return a * m.float()
+
 # (n, cin, h, w, cout, k, stride, dilation) -- odd sizes, partial tiles, strides, dilation
 GEOMS = [
     (2, 64, 17, 23, 64, 3, 1, 1),
@@ -152,15 +172,17 @@ def _handoff_nodes(out):
     return hit
 
 
-@pytest.mark.parametrize("with_addend", [False, True])
+@pytest.mark.parametrize("with_addend", [False, True, "masked"])
 def test_igemm_dgrad_addend(with_addend):
     x, wt = _case(2, 64, 17, 23, 64, 3, 2, 1, seed=5)
     dy = torch.randn(2, 64, 9, 12, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     add = torch.randn(x.shape, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    bits = _mask_bits(x.shape, 6)
     dx = torch.ops.rtseg.conv_igemm_dgrad(dy, wt.permute(1, 2, 3, 0).contiguous(), list(x.shape), [2, 2], [1, 1],
-                                          [1, 1], None, add if with_addend else None)
+                                          [1, 1], None, add if with_addend else None,
+                                          bits if with_addend == "masked" else None)
     ref = torch.nn.grad.conv2d_input(x.shape, wt.float(), dy.float(), 2, 1, 1)
-    _close(dx, ref + add.float() if with_addend else ref, 2e-2)
+    _close(dx, ref + _addend_ref(add, bits, with_addend), 2e-2)
 
 
 def test_residual_grad_handoff_matches_plain_add(monkeypatch):
@@ -176,8 +198,10 @@ def test_residual_grad_handoff_matches_plain_add(monkeypatch):
     x0 = torch.randn(2, 64, 24, 40, device=DEV).contiguous(memory_format=torch.channels_last)
     gy = torch.randn(2, 64, 24, 40, device=DEV)
     res = {}
-    for on in (True, False):
-        monkeypatch.setattr(bn_mod, "_HANDOFF", on)
+    for on in ("masked", True, False):
+        monkeypatch.setattr(bn_mod, "_HANDOFF", bool(on))
+        monkeypatch.setattr(bn_mod, "_MASKED_HANDOFF", on == "masked")
+        before = bn_mod.MASKED_HANDOFFS[0]
         net.zero_grad(set_to_none=True)
         x = x0.to(torch.bfloat16).requires_grad_(True)
         with torch.autocast("cuda", dtype=torch.bfloat16):
@@ -186,7 +210,12 @@ def test_residual_grad_handoff_matches_plain_add(monkeypatch):
         (y.float() * gy).sum().backward()
         res[on] = (nodes, x.grad.float().clone(),
                    {n: p.grad.float().clone() for n, p in net.named_parameters() if p.grad is not None})
+        assert (bn_mod.MASKED_HANDOFFS[0] > before) == (on == "masked")
     assert res[True][0] >= 2 and res[False][0] == 0
+    # the masked hand-off adds exactly the values the written-out residual gradient held (g or 0)
+    assert torch.equal(res["masked"][1], res[True][1])
+    for n, g in res[True][2].items():
+        assert torch.equal(res["masked"][2][n], g), n
     _close(res[True][1], res[False][1], 2e-2)
     for n, g in res[False][2].items():
         _close(res[True][2][n], g, 2e-2)

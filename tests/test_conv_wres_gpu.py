@@ -13,6 +13,26 @@ from realtime_semantic_segmentation_pytorch_amd import ops
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
+
+def _mask_bits(shape, seed):
+    """Random activation bit mask of a channels-last bf16 tensor (ops/bn.py kMaskBits layout)."""
+    g = torch.Generator().manual_seed(seed)
+    n = shape[0] * shape[1] * shape[2] * shape[3] // 8
+    return torch.randint(0, 256, (n,), generator=g, dtype=torch.uint8).to(DEV)
+
+
+def _addend_ref(add, bits, mode):
+    """What the dgrad epilogue adds: nothing, the addend, or the addend where its mask bit is set
+    (element e of the channels-last order in bit e % 8 of byte e / 8)."""
+    if not mode:
+        return 0.0
+    a = add.float()
+    if mode != "masked":
+        return a
+    n, c, h, w = add.shape
+    m = torch.stack([(bits >> i) & 1 for i in range(8)], dim=1).reshape(n, h, w, c).permute(0, 3, 1, 2)
+    return a * m.float()
+
 # forward geometries (n, h, w, cout), Cin = 64
 FWD = [(2, 17, 70, 64), (3, 8, 64, 128), (1, 5, 7, 64), (8, 130, 256, 64), (2, 33, 97, 192)]
 # data-gradient geometries (n, h, w, cin) of forward convs with Cout = 64
@@ -54,7 +74,7 @@ def test_wres_forward_and_stats(geom):
 
 
 @pytest.mark.parametrize("geom", DGRAD)
-@pytest.mark.parametrize("with_addend", [False, True])
+@pytest.mark.parametrize("with_addend", [False, True, "masked"])
 def test_wres_dgrad(geom, with_addend):
     n, h, w, cin = geom
     g = torch.Generator().manual_seed(2)
@@ -62,10 +82,11 @@ def test_wres_dgrad(geom, with_addend):
     wt = _t((64, cin, 3, 3), g, 1 / 24)
     dy = _t((n, 64, h, w), g).contiguous(**cl)
     add = _t((n, cin, h, w), g).contiguous(**cl)
+    bits = _mask_bits(add.shape, 3)
     dx = torch.ops.rtseg.conv_wres_dgrad(dy, wt.permute(1, 2, 3, 0).contiguous(), [n, cin, h, w], [1, 1], [1, 1],
-                                         [1, 1], add if with_addend else None)
+                                         [1, 1], add if with_addend else None, bits if with_addend == "masked" else None)
     ref = torch.nn.grad.conv2d_input((n, cin, h, w), wt.float(), dy.float(), 1, 1, 1)
-    _close(dx, ref + add.float() if with_addend else ref, 2e-2)
+    _close(dx, ref + _addend_ref(add, bits, with_addend), 2e-2)
 
 
 def test_wres_rejects_other_shapes():
@@ -178,7 +199,7 @@ def test_hreg_forward_and_stats(geom, rpw):
 
 @pytest.mark.parametrize("rpw", [1, 2])
 @pytest.mark.parametrize("geom", HREG)
-@pytest.mark.parametrize("with_addend", [False, True])
+@pytest.mark.parametrize("with_addend", [False, True, "masked"])
 def test_hreg_dgrad(geom, with_addend, rpw):
     """Data gradient of the forward conv (n, cout -> cin roles swapped: the dgrad reduces over the
     forward Cout and produces the forward Cin, so geometry (n, a, h, w, b) tests a conv b -> a)."""
@@ -188,7 +209,9 @@ def test_hreg_dgrad(geom, with_addend, rpw):
     wt = _t((cout_fwd, cin_fwd, 3, 3), g, 1 / (3 * cout_fwd ** 0.5))
     dy = _t((n, cout_fwd, h, w), g).contiguous(**cl)
     add = _t((n, cin_fwd, h, w), g).contiguous(**cl)
+    bits = _mask_bits(add.shape, 4)
     dx = torch.ops.rtseg.conv_hreg_dgrad(dy, wt.permute(1, 2, 3, 0).contiguous(), [n, cin_fwd, h, w], [1, 1], [1, 1],
-                                         [1, 1], add if with_addend else None, rpw)
+                                         [1, 1], add if with_addend else None, rpw,
+                                         bits if with_addend == "masked" else None)
     ref = torch.nn.grad.conv2d_input((n, cin_fwd, h, w), wt.float(), dy.float(), 1, 1, 1)
-    _close(dx, ref + add.float() if with_addend else ref, 2e-2)
+    _close(dx, ref + _addend_ref(add, bits, with_addend), 2e-2)
