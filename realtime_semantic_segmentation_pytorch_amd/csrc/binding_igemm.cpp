@@ -152,7 +152,8 @@ std::tuple<at::Tensor, at::Tensor> conv_stem(const at::Tensor& x, const at::Tens
 at::Tensor conv_dgrad_impl(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
                            at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
                            const std::optional<at::Tensor>& bias, const std::optional<at::Tensor>& addend, int kind,
-                           const std::optional<at::Tensor>& addend_mask) {
+                           const std::optional<at::Tensor>& addend_mask,
+                           const std::optional<at::Tensor>& phase_addend) {
   const bool halo = kind == 1, wres = kind == 2, hreg = kind == 3 || kind == 4;
   check_act(dy, "grad_output");
   TORCH_CHECK(x_size.size() == 4, "rtseg.conv_igemm_dgrad: x_size must be [N, Cin, H, W]");
@@ -201,6 +202,14 @@ at::Tensor conv_dgrad_impl(const at::Tensor& dy, const at::Tensor& wt, at::IntAr
   } else {
     TORCH_CHECK(!(addend_mask.has_value() && addend_mask->defined()), "rtseg.conv_dgrad: addend_mask without addend");
   }
+  if (phase_addend.has_value() && phase_addend->defined()) {  // added to output phase (0, 0) only
+    TORCH_CHECK(kind == 0, "rtseg.conv_dgrad: phase_addend is an igemm dgrad option");
+    check_act(*phase_addend, "phase_addend");
+    TORCH_CHECK(phase_addend->size(0) == g.n && phase_addend->size(1) == g.cin &&
+                    phase_addend->size(2) == (g.h + g.sh - 1) / g.sh && phase_addend->size(3) == (g.w_in + g.sw - 1) / g.sw,
+                "rtseg.conv_igemm_dgrad: phase_addend must be [N, Cin, ceil(H / sh), ceil(W / sw)]");
+    g.res_phase0 = phase_addend->data_ptr();
+  }
   if (halo) launch_conv_halo_dgrad(g, cur_stream());
   else if (wres) launch_conv_wres_dgrad(g, cur_stream());
   else if (hreg) {
@@ -213,14 +222,16 @@ at::Tensor conv_dgrad_impl(const at::Tensor& dy, const at::Tensor& wt, at::IntAr
 at::Tensor conv_igemm_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
                             at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
                             const std::optional<at::Tensor>& bias, const std::optional<at::Tensor>& addend,
-                            const std::optional<at::Tensor>& addend_mask) {
-  return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, bias, addend, 0, addend_mask);
+                            const std::optional<at::Tensor>& addend_mask,
+                            const std::optional<at::Tensor>& phase_addend) {
+  return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, bias, addend, 0, addend_mask, phase_addend);
 }
 
 at::Tensor conv_halo_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
                            at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
                            const std::optional<at::Tensor>& addend, const std::optional<at::Tensor>& addend_mask) {
-  return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, std::nullopt, addend, 1, addend_mask);
+  return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, std::nullopt, addend, 1, addend_mask,
+                         std::nullopt);
 }
 
 at::Tensor conv_hreg_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
@@ -229,13 +240,14 @@ at::Tensor conv_hreg_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntAr
                            const std::optional<at::Tensor>& addend_mask) {
   TORCH_CHECK(rows_per_wave == 1 || rows_per_wave == 2, "rtseg.conv_hreg_dgrad: rows_per_wave must be 1 or 2");
   return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, std::nullopt, addend,
-                         rows_per_wave == 2 ? 4 : 3, addend_mask);
+                         rows_per_wave == 2 ? 4 : 3, addend_mask, std::nullopt);
 }
 
 at::Tensor conv_wres_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
                            at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
                            const std::optional<at::Tensor>& addend, const std::optional<at::Tensor>& addend_mask) {
-  return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, std::nullopt, addend, 2, addend_mask);
+  return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, std::nullopt, addend, 2, addend_mask,
+                         std::nullopt);
 }
 
 // x [N,Cin,H,W], dy [N,Cout,Ho,Wo] (CL bf16) -> dw fp32 [Cout,Cin,KH,KW]
@@ -343,7 +355,7 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
   m.def("conv_igemm(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats, "
         "Tensor? scale_shift, Tensor? residual, int act) -> (Tensor, Tensor)");
   m.def("conv_igemm_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
-        "Tensor? bias=None, Tensor? addend=None, Tensor? addend_mask=None) -> Tensor");
+        "Tensor? bias=None, Tensor? addend=None, Tensor? addend_mask=None, Tensor? phase_addend=None) -> Tensor");
   m.def("conv_halo(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats, "
         "Tensor? scale_shift, Tensor? residual, int act) -> (Tensor, Tensor)");
   m.def("conv_halo_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "

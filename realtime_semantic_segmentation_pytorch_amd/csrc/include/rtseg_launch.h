@@ -172,6 +172,10 @@ struct ConvGeom {
   int act;
   int n, h, w_in, cin, ho, wo, cout, kh, kw, sh, sw, ph, pw, dh, dw;
   const uint8_t* amask = nullptr;  // data gradient: bit mask of the addend (res), see mask_addend4
+  // igemm data gradient: a second addend indexed by the pixels of output phase (0, 0) (the even
+  // rows / columns of a stride-2 dx, [N][ceil(H/2)][ceil(W/2)][Cin]): the data gradient of a
+  // stride-2 1 x 1 shortcut on the same input, computed as a plain GEMM (ops/conv.py _TwinConvFn)
+  const void* res_phase0 = nullptr;
 };
 // BN activation-derivative sources (= ops/bn.py MASK_*)
 enum BnMaskMode : int { kBnMaskNone = 0, kBnMaskFromY = 1, kBnMaskFromX = 2, kBnMaskBits = 3 };

@@ -69,6 +69,7 @@ struct IgArgs {
   const float* bias;      // [cout] added to the accumulators first (transposed conv), or null
   const uint16_t* addend; // bf16 tensor of the output's layout added in the epilogue, or null
   const uint8_t* amask;   // bit mask of the addend (mask_addend4), or null
+  const uint16_t* vaddend; // addend indexed by the virtual pixel m ([M][cout]), or null
   int act;
   int H, W, C;            // gathered operand [N][H][W][C]
   int Hv, Wv;             // virtual output grid
@@ -320,6 +321,12 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
               if (side != nullptr) {  // e.g. a residual branch's gradient
                 #pragma unroll
                 for (int q = 0; q < 4; ++q) v[q] += sv[q];
+              }
+              if (a.vaddend != nullptr && ok && co < a.cout) {  // e.g. a strided 1 x 1 shortcut's dx
+                float pv[4];
+                bf16x4_unpack(*reinterpret_cast<const uint2*>(a.vaddend + static_cast<int64_t>(m) * a.cout + co), pv);
+                #pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] += pv[q];
               }
             }
             if constexpr (EPI == 1) {
@@ -849,6 +856,7 @@ void launch_conv_igemm_dgrad(const ConvGeom& g, hipStream_t st) {
       k.bias = g.scale_shift;  // dgrad launches reuse the field as an optional bias (transposed conv)
       k.addend = static_cast<const uint16_t*>(g.res);  // ... and res as an optional addend
       k.amask = g.amask;
+      k.vaddend = (a == 0 && b == 0) ? static_cast<const uint16_t*>(g.res_phase0) : nullptr;
       k.H = g.ho; k.W = g.wo; k.C = g.cout;
       k.Hv = (g.h - a + g.sh - 1) / g.sh;
       k.Wv = (g.w_in - b + g.sw - 1) / g.sw;

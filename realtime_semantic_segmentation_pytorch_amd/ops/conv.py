@@ -641,16 +641,17 @@ def _plain(addend):
     return addend.materialize() if isinstance(addend, MaskedAddend) else addend
 
 
-def _conv_bwd(x, wk, conv, key, dy, want_dx, want_dw, wdtype, addend=None, on_dx=None):
+def _conv_bwd(x, wk, conv, key, dy, want_dx, want_dw, wdtype, addend=None, on_dx=None, phase_addend=None):
     """(dx (+ addend) | None, dw | None) of a routed conv.  ``on_dx(dx)`` runs between the data
-    and the weight gradient (the early SyncBN all-reduce of the producer BN)."""
+    and the weight gradient (the early SyncBN all-reduce of the producer BN).  ``phase_addend``:
+    added to dx's even rows / columns (see :func:`_dgrad`)."""
     stride, padding, dilation = _geom(conv)
     dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     if dy.data_ptr() % 16:
         dy = dy.clone(memory_format=torch.channels_last)
     dx = dw = None
     if want_dx:
-        dx = _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend)
+        dx = _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend, phase_addend)
     elif addend is not None:
         dx = _plain(addend)
     if on_dx is not None and want_dx:
@@ -660,6 +661,11 @@ def _conv_bwd(x, wk, conv, key, dy, want_dx, want_dw, wdtype, addend=None, on_dx
         if dw.dtype != wdtype:
             dw = like_param(dw.to(wdtype), conv.weight)
     return dx, dw
+
+
+# RTSEG_TWIN_PHASE=0: the twin node's strided 1 x 1 data gradient runs as its own pass (A/B)
+_PHASE_FUSE = os.environ.get("RTSEG_TWIN_PHASE", "1") != "0"
+PHASE_FUSED = [0]  # twin backward passes that took the phase-addend path (tests)
 
 
 class _TwinConvFn(torch.autograd.Function):
@@ -694,6 +700,24 @@ class _TwinConvFn(torch.autograd.Function):
         # the other's dx), while a strided 1 x 1 shortcut's often autotunes to MIOpen, where the
         # addend would cost a separate add (profiles/r4_stem)
         order = sorted((0, 1), key=lambda i: ctx.convs[i].kernel_size[0] * ctx.convs[i].kernel_size[1])
+        small, big = order
+        if (want_dx and dy1 is not None and dy2 is not None and _PHASE_FUSE and gemm_ok(ctx.convs[small])
+                and tuple(ctx.convs[small].stride) == (2, 2) and tuple(ctx.convs[big].stride) == (2, 2)
+                and ctx.convs[big].in_channels % 8 == 0):
+            # the strided 1 x 1 shortcut's data gradient is one GEMM over its output pixels, added
+            # by the 3 x 3 conv's dgrad to its even-row / even-column phase: no zero-filled
+            # full-size dx, no separate accumulation
+            dy_s, wk_s = pairs[small]
+            dy_s = dy_s.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            sub = _from_rows(torch.mm(_rows(dy_s), wk_s.reshape(wk_s.shape[0], -1)), x.shape[0], dy_s.shape[2],
+                             dy_s.shape[3])
+            PHASE_FUSED[0] += 1
+            _, dws[small] = _conv_bwd(x, wk_s, ctx.convs[small], ctx.keys[small], dy_s, False,
+                                      ctx.needs_input_grad[1 + small], ctx.wdtypes[small])
+            dy_b, wk_b = pairs[big]
+            dx, dws[big] = _conv_bwd(x, wk_b, ctx.convs[big], ctx.keys[big], dy_b, True, ctx.needs_input_grad[1 + big],
+                                     ctx.wdtypes[big], dx, phase_addend=sub)
+            return dx, dws[0], dws[1], None, None
         for i in order:
             dy, wk = pairs[i]
             if dy is None:
@@ -761,8 +785,10 @@ def _fwd_impl(x, wk, conv, key, stats) -> str:
     return cands[_choose(("fwd", stats) + key, _order(cands))][0]
 
 
-def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None):
-    """dx (+ addend: a residual branch's gradient, added in our kernel's epilogue)."""
+def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None, phase_addend=None):
+    """dx (+ addend: a residual branch's gradient, added in our kernel's epilogue) (+ phase_addend
+    on the even rows / columns of a stride-2 dx: a strided 1 x 1 shortcut's data gradient, added
+    in the epilogue of the igemm launch of output phase (0, 0))."""
     cin, cout = conv.in_channels, conv.out_channels
     wt = []
     amask = None  # the addend's activation bit mask (MaskedAddend), applied in our epilogues
@@ -788,7 +814,8 @@ def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None):
     def ours():
         if not wt:  # [Cin, KH, KW, Cout] bf16, the dgrad B operand
             wt.append(weight_crsk(conv, wk))
-        return ops().conv_igemm_dgrad(dy, wt[0], list(x.shape), stride, padding, dilation, None, addend, amask)
+        return ops().conv_igemm_dgrad(dy, wt[0], list(x.shape), stride, padding, dilation, None, addend, amask,
+                                      phase_addend)
 
     def halo():
         if not wt:
@@ -823,6 +850,8 @@ def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None):
     cands.append(("miopen", miopen))
     name, fn = cands[_choose(("dgrad",) + key, _order(cands))]
     dx = fn()
+    if phase_addend is not None and name != "igemm":
+        dx[:, :, ::stride[0], ::stride[1]] += phase_addend
     if addend is not None and name not in ("igemm", "halo", "wres", "hreg", "hreg2", "gemm"):
         dx = dx + addend_plain()
     return dx

@@ -89,6 +89,7 @@ def test_gemm_routed_downsample_block(monkeypatch, block):
     x0 = torch.randn(2, 64, 32, 96, device="cuda").contiguous(**CL)
     gy = torch.randn(2, 128, 16, 48, device="cuda")
     res, calls = [], []
+    monkeypatch.setattr(conv_mod, "_PHASE_FUSE", False)  # the shortcut dgrad as its own (GEMM) pass
     for name in ("gemm_fwd", "gemm_dgrad", "gemm_wgrad"):
         def spy(*a, _f=getattr(conv_mod, name), _n=name, **k):
             calls[-1].add(_n)
@@ -139,3 +140,47 @@ def test_masked_addend_materialize_cpu():
     bits = (flat << torch.arange(8, dtype=torch.uint8)).sum(1).to(torch.uint8)
     out = conv_mod.MaskedAddend(g, bits).materialize()
     assert torch.equal(out, g * m.to(g.dtype))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("block", ["RB"])  # RBB's twin is two 1 x 1s (stride 1 and 2): not fused
+def test_twin_phase_fused_shortcut_dgrad(monkeypatch, block):
+    """A downsampling block's strided 1 x 1 shortcut dgrad as a GEMM added by the 3 x 3 dgrad's
+    phase-(0, 0) launch (ops/conv.py _TwinConvFn, RTSEG_TWIN_PHASE) vs the separate pass: each
+    against an fp32 CPU run of the block, the fused path within 1.5 x the other's error (+ a
+    bf16 floor), and the fused path really ran."""
+    import copy
+
+    from realtime_semantic_segmentation_pytorch_amd import ops
+    from realtime_semantic_segmentation_pytorch_amd.models import ddrnet
+
+    assert ops.load(), "HIP extension must load on the GPU box"
+    monkeypatch.setenv("RTSEG_TWIN_CONV", "1")
+    torch.manual_seed(0)
+    net = ops.convert_batchnorm(getattr(ddrnet, block)(64, 128, 2)).cuda().to(**CL).train()
+    x0 = torch.randn(2, 64, 34, 98, device="cuda").contiguous(**CL)
+    gy = torch.randn(2, 128, 17, 49, device="cuda")
+    res = []
+    for on in (True, False):
+        monkeypatch.setattr(conv_mod, "_PHASE_FUSE", on)
+        before = conv_mod.PHASE_FUSED[0]
+        net.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = net(x)
+        (y.float() * gy).sum().backward()
+        assert (conv_mod.PHASE_FUSED[0] > before) == on
+        res.append((y.float().detach(), x.grad.float().clone(),
+                    {n: p.grad.float().clone() for n, p in net.named_parameters()}))
+    ref = copy.deepcopy(net).cpu().float()
+    ref.zero_grad(set_to_none=True)
+    xr = x0.cpu().clone().requires_grad_(True)
+    (ref(xr) * gy.cpu()).sum().backward()
+    (_, gx0, gp0), (_, gx1, gp1) = res
+
+    def rel(a, b):
+        return ((a.cpu() - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+    assert rel(gx0, xr.grad) <= max(1.5 * rel(gx1, xr.grad), 2e-2), (rel(gx0, xr.grad), rel(gx1, xr.grad))
+    for n, p in ref.named_parameters():
+        assert rel(gp0[n], p.grad) <= max(1.5 * rel(gp1[n], p.grad), 2e-2), n

@@ -219,3 +219,27 @@ def test_residual_grad_handoff_matches_plain_add(monkeypatch):
     _close(res[True][1], res[False][1], 2e-2)
     for n, g in res[False][2].items():
         _close(res[True][2][n], g, 2e-2)
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 17, 23, 128), (1, 128, 16, 32, 64)])
+@pytest.mark.parametrize("with_addend", [False, True])
+def test_igemm_dgrad_phase_addend(shape, with_addend):
+    """Stride-2 3 x 3 dgrad with a phase-(0, 0) addend: added to exactly the even rows / columns
+    of dx (odd sizes: the last phase-(0, 0) row / column included), on top of a full addend."""
+    n, cin, h, w, cout = shape
+    x, wt = _case(n, cin, h, w, cout, 3, 2, 1, seed=9)
+    ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    cl = dict(memory_format=torch.channels_last)
+    dy = torch.randn(n, cout, ho, wo, device=DEV).to(torch.bfloat16).contiguous(**cl)
+    add = torch.randn(x.shape, device=DEV).to(torch.bfloat16).contiguous(**cl)
+    ph = torch.randn(n, cin, (h + 1) // 2, (w + 1) // 2, device=DEV).to(torch.bfloat16).contiguous(**cl)
+    dx = torch.ops.rtseg.conv_igemm_dgrad(dy, wt.permute(1, 2, 3, 0).contiguous(), list(x.shape), [2, 2], [1, 1],
+                                          [1, 1], None, add if with_addend else None, None, ph)
+    ref = torch.nn.grad.conv2d_input(x.shape, wt.float(), dy.float(), 2, 1, 1)
+    if with_addend:
+        ref = ref + add.float()
+    ref[:, :, ::2, ::2] += ph.float()
+    _close(dx, ref, 2e-2)
+    with pytest.raises(RuntimeError, match="phase_addend"):
+        torch.ops.rtseg.conv_igemm_dgrad(dy, wt.permute(1, 2, 3, 0).contiguous(), list(x.shape), [2, 2], [1, 1],
+                                         [1, 1], None, None, None, ph[:, :, 1:])

@@ -39,6 +39,7 @@ def main():
         "wres": lambda: r.conv_wres(x, wk, [1, 1], [1, 1], [1, 1], a.stats),
         "wres_dg": lambda: r.conv_wres_dgrad(dy, wtr, list(x.shape), [1, 1], [1, 1], [1, 1]),
         "whalo": lambda: r.conv_whalo_wgrad(x, dy, 3, 3, [1, 1], [1, 1], [1, 1]),
+        "whalo2": lambda: r.conv_whalo_wgrad(x, dy, 3, 3, [1, 1], [1, 1], [1, 1], False, 2),
         "hreg": lambda: r.conv_hreg(x, wk, [1, 1], [1, 1], [1, 1], a.stats),
         "hreg_dg": lambda: r.conv_hreg_dgrad(dy, wtr, list(x.shape), [1, 1], [1, 1], [1, 1]),
         "hreg2": lambda: r.conv_hreg(x, wk, [1, 1], [1, 1], [1, 1], a.stats, 2),
