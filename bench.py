@@ -221,6 +221,18 @@ def main():
         elapsed = float(t.item())
     loss_val = float(loss)
 
+    probe_out = os.environ.get("RTSEG_PROBE_OPS")
+    if probe_out and rank == 0:  # one extra step: large non-kernel aten ops (tools/probe_step_ops.py)
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from tools.probe_step_ops import OpProbe
+
+        probe = OpProbe()
+        with probe:
+            step()
+        torch.cuda.synchronize()
+        with open(probe_out, "w") as f:
+            f.write(probe.report())
+
     if a.profile_steps > 0 and rank == 0:
         from torch.profiler import ProfilerActivity, profile
 

@@ -35,6 +35,7 @@ likewise for ``conv_wres``.
 from __future__ import annotations
 
 import os
+import weakref
 
 from typing import NamedTuple
 
@@ -546,6 +547,29 @@ def _conv_fwd(x, weight, conv, stats):
     return y, part, wk, key
 
 
+# Routed-conv nodes by input tensor (weak on both sides): a later consumer of the same tensor that
+# is NOT downstream of the conv (a sibling, e.g. the skip of DDRNet's bilateral-fusion upsample,
+# whose other consumer is the fusion's 3 x 3 conv) may hand its gradient to the conv's dgrad
+# epilogue -- if, at its backward, the conv node has not run yet (consumer_for / ran flag).
+_CONSUMERS = weakref.WeakValueDictionary()  # id(input tensor) -> routed-conv node
+
+
+def _register_consumer(x: torch.Tensor, node) -> None:
+    if x.requires_grad:
+        _CONSUMERS[id(x)] = node
+
+
+def consumer_for(t: torch.Tensor):
+    """The routed-conv node registered for exactly this tensor (same object: id and in_key) whose
+    backward has not run and whose addend slot is free (see _register_consumer), or None."""
+    node = _CONSUMERS.get(id(t))
+    if node is None or node.ran or node.addend_slot is not None:
+        return None
+    if node.in_key != (t.data_ptr(), tuple(t.shape), t.dtype):
+        return None
+    return node
+
+
 class _ConvFn(torch.autograd.Function):
     """y (+ BN statistics slab) = conv(x, w); backward via our dgrad / wgrad or MIOpen."""
 
@@ -558,6 +582,8 @@ class _ConvFn(torch.autograd.Function):
         # residual branch's gradient to fuse into the dgrad epilogue (see ops.bn)
         ctx.in_key = (x.data_ptr(), tuple(x.shape), x.dtype)
         ctx.addend_slot = None
+        ctx.ran = not ctx.needs_input_grad[0]  # consumer_for: only a node that will produce dx
+        _register_consumer(x, ctx)
         ctx.wdtype = weight.dtype
         # a multi-rank SyncBN node that produced x: its backward all-reduce is issued from this
         # node's backward, between dgrad and wgrad (ops.bn.syncbn_bwd_early)
@@ -577,7 +603,10 @@ class _ConvFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy, _dpart):
+        ctx.ran = True
         if dy is None:
+            if ctx.addend_slot:  # a handed-over gradient is this input's whole gradient now
+                return _plain(ctx.addend_slot.pop()), None, None, None
             return None, None, None, None
         x, wk = ctx.saved_tensors
         fused = ctx.bn_fuse_slot.pop() if ctx.bn_fuse_slot else None

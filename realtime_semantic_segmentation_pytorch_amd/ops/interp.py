@@ -7,7 +7,9 @@ swiftnet.py:60-70, bisenetv2.py:213-218 ...).
 """
 from __future__ import annotations
 
+import os
 import threading
+import weakref
 from contextlib import contextmanager
 from typing import Optional, Sequence
 
@@ -17,6 +19,9 @@ import torch.nn.functional as F
 from ._ext import use_hip, ops
 
 ACT_CODES = {None: 0, "none": 0, "relu": 1, "relu6": 2}
+# skip-gradient hand-off to a sibling routed conv (RTSEG_SKIP_HANDOFF=0: off, for A/B)
+_SKIP_HANDOFF = os.environ.get("RTSEG_SKIP_HANDOFF", "1") != "0"
+SKIP_HANDOFFS = [0]  # backward passes that handed the skip gradient over (tests)
 
 
 def _torch_act(y: torch.Tensor, act: int) -> torch.Tensor:
@@ -36,6 +41,15 @@ class _InterpFn(torch.autograd.Function):
         ctx.in_hw = (x.shape[2], x.shape[3])
         ctx.cl = x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous()
         ctx.has_skip = skip is not None
+        # a routed conv that also reads the skip tensor (a sibling consumer, e.g. DDRNet's
+        # bilateral-fusion 3 x 3 conv on x_high): the skip gradient may go to its dgrad epilogue
+        ctx.skip_conv = None
+        if skip is not None and _SKIP_HANDOFF and ctx.needs_input_grad[1]:
+            from .conv import consumer_for
+
+            node = consumer_for(skip)
+            if node is not None:
+                ctx.skip_conv = weakref.ref(node)
         if act:
             ctx.save_for_backward(y)
         return y
@@ -49,6 +63,13 @@ class _InterpFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gx = ops().interp_backward(g, ctx.in_hw[0], ctx.in_hw[1], ctx.align, ctx.cl)
         gs = g if (ctx.has_skip and ctx.needs_input_grad[1]) else None
+        if gs is not None and ctx.skip_conv is not None:
+            node = ctx.skip_conv()
+            if node is not None and not node.ran and node.addend_slot is None:
+                # the conv node has not run: it adds gs in its dgrad epilogue (no accumulation add)
+                node.addend_slot = [gs]
+                gs = None
+                SKIP_HANDOFFS[0] += 1
         return gx, gs, None, None, None, None
 
 
