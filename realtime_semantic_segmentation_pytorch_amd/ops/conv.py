@@ -856,9 +856,10 @@ def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None, phase_a
             wt.append(weight_crsk(conv, wk))
         return ops().conv_wres_dgrad(dy, wt[0], list(x.shape), stride, padding, dilation, addend, amask)
 
-    def miopen():
-        return torch.ops.aten.convolution_backward(dy, x, wk.permute(0, 3, 1, 2), None, stride, padding, dilation, False,
-                                                   [0, 0], 1, [True, False, False])[0]
+    def miopen():  # the addend costs MIOpen a separate add: timed with it
+        r = torch.ops.aten.convolution_backward(dy, x, wk.permute(0, 3, 1, 2), None, stride, padding, dilation, False,
+                                                [0, 0], 1, [True, False, False])[0]
+        return r if addend is None else r + addend_plain()
 
     def hreg(rows_per_wave=1):
         if not wt:
@@ -877,12 +878,11 @@ def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None, phase_a
     if gemm_ok(conv):
         cands.append(("gemm", lambda: gemm_dgrad(dy, wk, x.shape, stride[0], addend_plain())))
     cands.append(("miopen", miopen))
-    name, fn = cands[_choose(("dgrad",) + key, _order(cands))]
+    # a pass with an addend is its own autotune key: our kernels fuse the add, MIOpen pays for it
+    name, fn = cands[_choose(("dgrad",) + key + (("+addend",) if addend is not None else ()), _order(cands))]
     dx = fn()
     if phase_addend is not None and name != "igemm":
         dx[:, :, ::stride[0], ::stride[1]] += phase_addend
-    if addend is not None and name not in ("igemm", "halo", "wres", "hreg", "hreg2", "gemm"):
-        dx = dx + addend_plain()
     return dx
 
 
