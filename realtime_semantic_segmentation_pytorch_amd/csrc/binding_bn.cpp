@@ -144,8 +144,12 @@ std::tuple<at::Tensor, at::Tensor> bn_eval_coeffs(const std::optional<at::Tensor
   return {mi, ss};
 }
 
+// slice_only: out2 (a channel slice of a wider channels-last buffer) is the only output -- the
+// concat-then-BN sites (ops.cat_bn_act) write each part's normalised channels straight into the
+// concatenated output; returns out2
 at::Tensor bn_apply(const at::Tensor& x, const at::Tensor& scale_shift,
-                    const std::optional<at::Tensor>& res, int64_t act, const std::optional<at::Tensor>& out2) {
+                    const std::optional<at::Tensor>& res, int64_t act, const std::optional<at::Tensor>& out2,
+                    bool slice_only) {
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   check_cl(x, "x");
   const void* rp = nullptr;
@@ -156,9 +160,11 @@ at::Tensor bn_apply(const at::Tensor& x, const at::Tensor& scale_shift,
     rp = res->data_ptr();
   }
   const Slice o2 = slice_of(out2, x, "out2");
-  at::Tensor y = at::empty_like(x);
-  launch_bn_apply(x.data_ptr(), rp, scale_shift.data_ptr<float>(), y.data_ptr(), dtype_code(x),
-                  rows_of(x), static_cast<int>(x.size(1)), static_cast<int>(act), cur_stream(), o2.p, o2.ld);
+  TORCH_CHECK(!slice_only || o2.p != nullptr, "rtseg.bn_apply: slice_only needs out2");
+  at::Tensor y = slice_only ? *out2 : at::empty_like(x);
+  launch_bn_apply(x.data_ptr(), rp, scale_shift.data_ptr<float>(), slice_only ? nullptr : y.data_ptr(),
+                  dtype_code(x), rows_of(x), static_cast<int>(x.size(1)), static_cast<int>(act), cur_stream(), o2.p,
+                  o2.ld);
   return y;
 }
 
@@ -330,7 +336,8 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
         "Tensor(b!)? running_var, Tensor(c!)? num_batches_tracked, float momentum, float eps) -> (Tensor, Tensor)");
   m.def("bn_eval_coeffs(Tensor? weight, Tensor? bias, Tensor running_mean, Tensor running_var, "
         "float eps) -> (Tensor, Tensor)");
-  m.def("bn_apply(Tensor x, Tensor scale_shift, Tensor? residual, int act, Tensor(a!)? out2=None) -> Tensor");
+  m.def("bn_apply(Tensor x, Tensor scale_shift, Tensor? residual, int act, Tensor(a!)? out2=None, "
+        "bool slice_only=False) -> Tensor");
   m.def("bn_apply_bits(Tensor x, Tensor scale_shift, Tensor? residual, int act, Tensor(a!)? out2=None) "
         "-> (Tensor, Tensor)");
   m.def("bn_bwd_sums(Tensor? grad, Tensor x, Tensor? y, Tensor mean_invstd, Tensor scale_shift, "

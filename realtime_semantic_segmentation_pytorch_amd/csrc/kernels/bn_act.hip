@@ -382,7 +382,7 @@ __device__ __forceinline__ void apply_one(const T* __restrict__ x, const T* __re
     f[j] = act_fwd<ACT>(z);
     if constexpr (BITS) b |= (act_grad_pre<ACT>(1.f, z) != 0.f ? 1u : 0u) << j;
   }
-  VecIO<T, V>::store(y + off, f);
+  if (y != nullptr) VecIO<T, V>::store(y + off, f);  // null: the concat slice is the only output
   if (y2 != nullptr) VecIO<T, V>::store(y2 + (i / cv) * ld2 + c0, f);  // the concat-buffer copy
   if constexpr (BITS) bits[i] = static_cast<uint8_t>(b);  // vector i = byte i (off / V)
 }
@@ -419,7 +419,7 @@ __device__ __forceinline__ void apply_rows(const T* __restrict__ x, const T* __r
       f[j] = act_fwd<ACT>(z);
       if constexpr (BITS) b |= (act_grad_pre<ACT>(1.f, z) != 0.f ? 1u : 0u) << j;
     }
-    VecIO<T, V>::store(y + off, f);
+    if (y != nullptr) VecIO<T, V>::store(y + off, f);
     if (y2 != nullptr) VecIO<T, V>::store(y2 + row * ld2 + c0, f);
     if constexpr (BITS) bits[row * cv + cvi] = static_cast<uint8_t>(b);
   };

@@ -73,8 +73,8 @@ class CGBlock(nn.Module):
 
     def forward(self, x):
         p = self.conv(x)
-        y = ops.bn_act(torch.cat([self.loc(p), self.sur(p)], dim=1), self.joi[0], self.joi[1],
-                       act_module=self.joi[1])
+        # BN(+PReLU) of the joint feature loc || sur, the concat never materialised (ops.cat_bn_act)
+        y = ops.cat_bn_act([self.loc(p), self.sur(p)], self.joi[0], self.joi[1], act_module=self.joi[1])
         if self.use_skip and self.res_type == "LRL":
             y = y + x
         y = ops.gate(y, self.glo(y.mean(dim=(2, 3)))[:, :, None, None], sigmoid=True)

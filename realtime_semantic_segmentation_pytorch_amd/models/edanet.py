@@ -37,8 +37,9 @@ class DownsamplingBlock(nn.Module):
 
     def forward(self, x):
         c = self.conv(x)  # (autocast: the pooled fp32 input joins in the conv's dtype, see enet.InitialBlock)
-        y = torch.cat([c, self.pool(x).to(c.dtype)], dim=1)
-        return ops.bn_act(y, self.bn_act[0], self.bn_act[1], act_module=self.bn_act[1])
+        # BN + act of conv || pool straight into the concat layout (ops.cat_bn_act)
+        return ops.cat_bn_act([c, self.pool(x).to(c.dtype)], self.bn_act[0], self.bn_act[1],
+                              act_module=self.bn_act[1])
 
 
 class EDABlock(nn.Module):

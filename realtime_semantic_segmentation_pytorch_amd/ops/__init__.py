@@ -14,7 +14,7 @@ from .bn import (bn_act, bn_stats_begin, bias_add, act_code as bn_act_code, fuse
 from .detail import detail_loss, detail_loss_reference, detail_target_reference
 from .postprocess import colorize, colorize_reference
 from .confmat import confusion_matrix, confusion_matrix_reference
-from .concat import ConcatSink
+from .concat import ConcatSink, cat_bn_act
 from .dwconv import DepthwiseConv2d, convert_depthwise, depthwise_ok, dw_conv2d, dw_conv_bn_stats
 from .pool import (avg_pool2d, max_pool2d, adaptive_avg_pool2d, convert_pooling, AvgPool2d, MaxPool2d,
                    AdaptiveAvgPool2d, MaxUnpool2d, max_pool2d_with_indices, max_unpool2d, AdaptiveMaxPool2d,
@@ -43,5 +43,5 @@ __all__ = [
     "PrunedConv2d", "convert_pruned_convs", "pruned_conv2d", "has_dead_taps",
     "FusedSGD", "FusedAdam", "FusedAdamW", "conv_ok", "conv_bn_stats", "twin_conv_bn_stats", "conv_bn_act_eval", "conv_bn_act", "conv_forward", "RoutedConv2d", "GroupedConv2d", "convert_routed_convs", "invalidate_weight_shadows",
     "TransposedConv2d", "conv_transpose2d", "convert_transposed_convs", "deconv_ok", "gate", "gate_reference", "activation", "convert_activations", "channel_shuffle", "convert_pixel_shuffle", "pixel_shuffle", "pixel_unshuffle", "AugmentSpec", "augment_batch", "augment_reference", "draw_params",
-    "ConcatSink", "bn_act", "bn_stats_begin", "bias_add", "bn_act_code", "bn_fused_ok", "convert_batchnorm", "FusedBatchNorm2d", "FusedSyncBatchNorm",
+    "ConcatSink", "cat_bn_act", "bn_act", "bn_stats_begin", "bias_add", "bn_act_code", "bn_fused_ok", "convert_batchnorm", "FusedBatchNorm2d", "FusedSyncBatchNorm",
 ]

@@ -100,3 +100,123 @@ class _CatSinkFn(torch.autograd.Function):
             else:
                 grads.append(sl)
         return (None, *grads)
+
+
+# --------------------------------------------------------------------------- concat -> BN
+# ``act(bn(torch.cat(parts, 1)))`` -- CGNet's joint feature (loc || sur, reference
+# models/cgnet.py:90-110), EDANet's / ENet-family downsamplers (conv || pool, edanet.py:26-45):
+# BatchNorm is per channel, so the concat's statistics are the parts' statistics side by side and
+# each part can be normalised straight into its channel slice of the output.  Forward: per-part
+# statistics (``bn_stats_sums``), ONE finalize over the joined sums (running stats updated once),
+# per-part apply into the output slice (``bn_apply(slice_only=True)``); backward: per-part BN
+# backward reading its slice of the output gradient at the row stride (``grad2``).  No concat is
+# materialised either way, and the parts' gradients are never slice copies.
+from .bn import (ACT_NONE, MASK_FROM_X, MASK_NONE, _aligned_cl, _sync_group, act_code,  # noqa: E402
+                 bump_write_generation, eval_coeffs, fused_ok)
+from ._ext import ops as _ops, use_hip as _use_hip  # noqa: E402
+
+CAT_BN_CALLS = [0]  # forward passes that took the fused path (tests)
+
+
+def _cat_bn_ok(parts, bn, code) -> bool:
+    if not _ENABLED or len(parts) < 2 or not _use_hip(parts[0], "bn") or code not in (0, 1, 2):
+        return False
+    if torch.onnx.is_in_onnx_export() or torch.jit.is_tracing():
+        return False
+    p0 = parts[0]
+    if p0.dim() != 4 or p0.dtype not in (torch.bfloat16, torch.float32) or not fused_ok(p0, bn, code):
+        return False
+    if _sync_group(bn) is not None:
+        return False
+    vec = 16 // p0.element_size()
+    off = 0
+    for p in parts:
+        if (p.dim() != 4 or p.dtype != p0.dtype or p.device != p0.device or p.shape[0] != p0.shape[0]
+                or p.shape[2:] != p0.shape[2:] or p.shape[1] % vec or p.shape[1] // vec > 256):
+            return False
+        off += p.shape[1]
+    return off == bn.num_features and off % vec == 0
+
+
+class _CatBNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, bn, code, weight, bias, *parts):
+        parts = tuple(_aligned_cl(p) for p in parts)
+        n, h, w = parts[0].shape[0], parts[0].shape[2], parts[0].shape[3]
+        widths = [p.shape[1] for p in parts]
+        offs = [sum(widths[:i]) for i in range(len(widths))]
+        c = sum(widths)
+        out = torch.empty((n, c, h, w), dtype=parts[0].dtype, device=parts[0].device,
+                          memory_format=torch.channels_last)
+        use_batch = bn.training or not bn.track_running_stats or bn.running_mean is None
+        if use_batch:
+            track = bn.track_running_stats and bn.training and bn.running_mean is not None
+            ps = [_ops().bn_stats_sums(p) for p in parts]  # [2Cp + 1]: sum, second moment, count
+            sums = torch.cat([s[:cp] for s, cp in zip(ps, widths)] + [s[cp:2 * cp] for s, cp in zip(ps, widths)]
+                             + [ps[0][-1:]])
+            mi, ss = _ops().bn_finalize(sums, weight, bias, bn.running_mean if track else None,
+                                        bn.running_var if track else None,
+                                        bn.num_batches_tracked if track else None, float(bn.momentum), float(bn.eps))
+            if track:
+                bump_write_generation()  # running stats rewritten through raw pointers
+        else:
+            sums = None
+            mi, ss = eval_coeffs(bn)
+
+        def sl(t, o, cp):  # [2C] -> the part's [2Cp] (first half, second half)
+            return torch.cat((t[o:o + cp], t[c + o:c + o + cp]))
+
+        for p, o, cp in zip(parts, offs, widths):
+            _ops().bn_apply(p, sl(ss, o, cp), None, code, out[:, o:o + cp], True)
+        CAT_BN_CALLS[0] += 1
+        ctx.widths, ctx.offs, ctx.code, ctx.use_batch, ctx.c = widths, offs, code, use_batch, c
+        ctx.has_w = weight is not None
+        ctx.save_for_backward(mi, ss, sums, weight, *parts)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        mi, ss, sums, weight, *parts = ctx.saved_tensors
+        g = _aligned_cl(g)
+        c = ctx.c
+        mask = MASK_NONE if ctx.code == ACT_NONE else MASK_FROM_X
+        want_dw = ctx.has_w and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
+        dxs, dws, dbs = [], [], []
+
+        def sl(t, o, cp):
+            return torch.cat((t[o:o + cp], t[c + o:c + o + cp]))
+
+        for i, (p, o, cp) in enumerate(zip(parts, ctx.offs, ctx.widths)):
+            sums_p = torch.cat((sums[o:o + cp], sums[c + o:c + o + cp], sums[2 * c:])) if sums is not None else None
+            w_p = weight[o:o + cp] if weight is not None else None
+            dx, _, dw, db = _ops().bn_backward(None, p, None, None, sums_p, sl(mi, o, cp), sl(ss, o, cp), w_p,
+                                               ctx.code, mask, False, ctx.use_batch, want_dw, None, g[:, o:o + cp])
+            dxs.append(dx if ctx.needs_input_grad[4 + i] else None)
+            dws.append(dw)
+            dbs.append(db)
+        dwt = torch.cat(dws).to(weight.dtype) if want_dw else None
+        dbt = torch.cat(dbs).to(weight.dtype) if want_dw else None
+        return (None, None, dwt if ctx.needs_input_grad[2] else None, dbt if ctx.needs_input_grad[3] else None,
+                *dxs)
+
+
+def cat_bn_act(parts, bn, act=None, act_module=None):
+    """``act(bn(torch.cat(parts, dim=1)))`` without the concat (see above); ``act``: a fused
+    activation (code / str / module) -- any other activation module runs on the BN output."""
+    code = act if isinstance(act, int) else act_code(act)
+    post = None
+    if code is None:  # e.g. PReLU: the BN into the concat layout, then the activation module
+        code, post = ACT_NONE, (act_module if act_module is not None else act)
+    parts = list(parts)
+    if parts[0].is_cuda and any(p.dtype != parts[0].dtype for p in parts):
+        dt = parts[0].dtype
+        for p in parts[1:]:
+            dt = torch.promote_types(dt, p.dtype)
+        parts = [p.to(dt) for p in parts]
+    if _cat_bn_ok(parts, bn, code):
+        y = _CatBNFn.apply(bn, code, bn.weight, bn.bias, *parts)
+    else:
+        from .bn import bn_act
+
+        y = bn_act(torch.cat(parts, dim=1), bn, code)
+    return post(y) if post is not None else y

@@ -95,3 +95,64 @@ def test_stdc_module_sink_matches_torch_cat(stride, monkeypatch):
     assert rel(dx1, dx0) < 2e-2, rel(dx1, dx0)
     for k in g0:
         assert rel(g1[k], g0[k]) < 3e-2, (k, rel(g1[k], g0[k]))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("act", ["relu", "none", "prelu"])
+@pytest.mark.parametrize("train", [True, False])
+def test_cat_bn_act_matches_cat_then_bn(dtype, act, train):
+    """ops.cat_bn_act (per-part statistics, one finalize, per-part apply into the output slice,
+    per-part backward on the gradient slice) vs bn_act of the materialised torch.cat: output,
+    part gradients, BN parameter gradients and running statistics."""
+    from realtime_semantic_segmentation_pytorch_amd.models.modules import Activation
+
+    torch.manual_seed(0)
+    widths = (32, 16, 24) if dtype == torch.bfloat16 else (12, 8, 4)
+    c = sum(widths)
+    bn = ops.convert_batchnorm(torch.nn.Sequential(torch.nn.BatchNorm2d(c))).cuda()[0]
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+        bn.running_mean.uniform_(-0.2, 0.2)
+        bn.running_var.uniform_(0.5, 2.0)
+    bn.train(train)
+    actm = Activation(act).cuda().to(dtype)  # (PReLU's weight in the activation dtype: no autocast here)
+    parts0 = [(torch.randn(2, w, 9, 14, device="cuda") * (1 + i) + i).to(dtype).contiguous(
+        memory_format=torch.channels_last) for i, w in enumerate(widths)]
+    g = torch.randn(2, c, 9, 14, device="cuda")
+    res = []
+    for fused in (True, False):
+        b = copy.deepcopy(bn)
+        a = copy.deepcopy(actm)
+        parts = [p.clone().requires_grad_(True) for p in parts0]
+        before = concat_mod.CAT_BN_CALLS[0]
+        if fused:
+            y = ops.cat_bn_act(parts, b, a, act_module=a)
+            assert concat_mod.CAT_BN_CALLS[0] == before + 1
+        else:
+            y = ops.bn_act(torch.cat(parts, dim=1), b, a, act_module=a)
+        (y.float() * g).sum().backward()
+        res.append((y.float().detach(), [p.grad.float() for p in parts], b.weight.grad.clone(), b.bias.grad.clone(),
+                    b.running_mean.clone(), b.running_var.clone()))
+    (y0, gp0, gw0, gb0, rm0, rv0), (y1, gp1, gw1, gb1, rm1, rv1) = res
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(y0, y1, atol=tol, rtol=tol)
+    for a_, b_ in zip(gp0, gp1):
+        torch.testing.assert_close(a_, b_, atol=tol * b_.abs().max().item(), rtol=tol)
+    torch.testing.assert_close(gw0, gw1, atol=tol * gw1.abs().max().item(), rtol=tol)
+    torch.testing.assert_close(gb0, gb1, atol=tol * gb1.abs().max().item(), rtol=tol)
+    torch.testing.assert_close(rm0, rm1, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(rv0, rv1, atol=1e-5, rtol=1e-5)
+
+
+def test_cgnet_block_uses_cat_bn():
+    """CGNet's context-guided block runs its joint BN + PReLU through cat_bn_act on the GPU."""
+    from realtime_semantic_segmentation_pytorch_amd.models.cgnet import CGBlock
+
+    blk = ops.convert_batchnorm(CGBlock(64, 64, 1, 2)).cuda().to(memory_format=torch.channels_last).train()
+    x = torch.randn(2, 64, 16, 24, device="cuda").contiguous(memory_format=torch.channels_last)
+    before = concat_mod.CAT_BN_CALLS[0]
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = blk(x)
+    y.float().sum().backward()
+    assert concat_mod.CAT_BN_CALLS[0] == before + 1
