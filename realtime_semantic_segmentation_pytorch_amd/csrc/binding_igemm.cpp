@@ -53,7 +53,7 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::
   if (stem) {
     TORCH_CHECK(conv_stem_supported(g),
                 "rtseg.conv_stem: needs Cin == 3, 3 x 3 / pad 1 / stride 1 or 2, Cout % 16 == 0 and <= 64, even W");
-    TORCH_CHECK(!(scale_shift.has_value() && scale_shift->defined()), "rtseg.conv_stem: no inference BN epilogue");
+    TORCH_CHECK(!(residual.has_value() && residual->defined()), "rtseg.conv_stem: no residual epilogue");
   } else if (halo) {
     TORCH_CHECK(conv_halo_supported(g, 0),
                 "rtseg.conv_halo: needs stride 1, taps within 3 x 3, Cin % 64 == 0, Cout % 64 == 0");
@@ -146,6 +146,12 @@ std::tuple<at::Tensor, at::Tensor> conv_wres(const at::Tensor& x, const at::Tens
 std::tuple<at::Tensor, at::Tensor> conv_stem(const at::Tensor& x, const at::Tensor& wk, at::IntArrayRef stride,
                                              at::IntArrayRef padding, at::IntArrayRef dilation, bool stats) {
   return conv_fwd_impl(x, wk, stride, padding, dilation, stats, std::nullopt, std::nullopt, 0, 5);
+}
+
+// ... with a BN (+ activation) epilogue on the fp32 accumulators: act(conv(x) * scale + shift)
+at::Tensor conv_stem_bn_act(const at::Tensor& x, const at::Tensor& wk, at::IntArrayRef stride, at::IntArrayRef padding,
+                            at::IntArrayRef dilation, const at::Tensor& scale_shift, int64_t act) {
+  return std::get<0>(conv_fwd_impl(x, wk, stride, padding, dilation, false, scale_shift, std::nullopt, act, 5));
 }
 
 // dy [N,Cout,Ho,Wo] CL bf16, wt [Cin,KH,KW,Cout] bf16 -> dx [N,Cin,H,W] CL bf16
@@ -368,6 +374,8 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
   m.def("conv_wres_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
         "Tensor? addend=None, Tensor? addend_mask=None) -> Tensor");
   m.def("conv_stem(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats) -> (Tensor, Tensor)");
+  m.def("conv_stem_bn_act(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, Tensor scale_shift, "
+        "int act) -> Tensor");
   m.def("conv_stem_wgrad_bn(Tensor x, Tensor dy, Tensor bn_input, Tensor kcoef, Tensor mean_invstd, "
         "Tensor scale_shift, int act, int kh, int kw, int[] stride, int[] padding, int[] dilation, "
         "bool channels_last) -> Tensor");
@@ -391,6 +399,7 @@ TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
   m.impl("conv_igemm_wgrad", &rtseg::conv_igemm_wgrad);
   m.impl("conv_whalo_wgrad", &rtseg::conv_whalo_wgrad);
   m.impl("conv_stem", &rtseg::conv_stem);
+  m.impl("conv_stem_bn_act", &rtseg::conv_stem_bn_act);
   m.impl("conv_stem_wgrad_bn", &rtseg::conv_stem_wgrad_bn);
   m.impl("conv_stem_wgrad", &rtseg::conv_stem_wgrad);
 }

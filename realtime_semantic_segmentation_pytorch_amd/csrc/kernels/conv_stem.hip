@@ -93,8 +93,14 @@ __device__ __forceinline__ void stage_input(const StemArgs& a, uint32_t* l32, in
     if (tid + 256 * e < kTotal) l32[tid + 256 * e] = v[e];
 }
 
-template <int S, int NT, int STATS>
+// BNA: 0 = the raw conv output (+ STATS), else the training BN applied in the epilogue from the
+// fp32 accumulators -- y = act(conv * scale + shift), act = BNA - 1 (none / ReLU / ReLU6): the
+// stem BN's forward apply as a recompute of the (K = 27) conv from the 0.4 GB image instead of a
+// pass over the 2.1 GB conv output (ops/bn.py; the conv output itself is still written by the
+// statistics launch, for the BN backward)
+template <int S, int NT, int STATS, int BNA = 0>
 __global__ void __launch_bounds__(256) stem_fwd_kernel(const StemArgs a) {
+  static_assert(!(STATS && BNA), "statistics come from the raw conv output");
   constexpr int TH = 8;  // 4 waves x 2 rows
   using T = StemTile<S, TH>;
   __shared__ uint32_t l32[T::R * T::DW];
@@ -122,6 +128,18 @@ __global__ void __launch_bounds__(256) stem_fwd_kernel(const StemArgs a) {
   }
   int ko[8];
   k_offsets<T::PX>(h, ko);
+
+  float bsc[BNA ? NT : 1][4], bsh[BNA ? NT : 1][4];  // this lane's channels' BN scale / shift
+  if constexpr (BNA != 0) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = 4 * NT * h + 4 * t + r;
+        bsc[t][r] = a.ss[co];
+        bsh[t][r] = a.ss[a.cout + co];
+      }
+  }
 
   float ts[NT][4], tq[NT][4];
 #pragma unroll
@@ -152,6 +170,13 @@ __global__ void __launch_bounds__(256) stem_fwd_kernel(const StemArgs a) {
       for (int t = 0; t < NT; ++t) {
         f32x4_t c = {0.f, 0.f, 0.f, 0.f};
         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t], bf, c, 0, 0, 0);
+        if constexpr (BNA != 0) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float z = fmaf(c[r], bsc[t][r], bsh[t][r]);
+            c[r] = BNA == 2 ? fmaxf(z, 0.f) : BNA == 3 ? fminf(fmaxf(z, 0.f), 6.f) : z;
+          }
+        }
         pk[2 * t] = pack2(c[0], c[1]);
         pk[2 * t + 1] = pack2(c[2], c[3]);
         if constexpr (STATS) {
@@ -389,18 +414,21 @@ bool stem_fill(StemArgs& k, const ConvGeom& g, int th) {
 int stem_grid(int mtiles) { return std::max(1, std::min(mtiles, 2048)); }
 
 template <int S, int NT>
-void fwd_launch(const StemArgs& k, int grid, hipStream_t st) {
+void fwd_launch(const StemArgs& k, int grid, hipStream_t st, int bna) {
   if (k.part != nullptr) stem_fwd_kernel<S, NT, 1><<<grid, 256, 0, st>>>(k);
+  else if (bna == 1) stem_fwd_kernel<S, NT, 0, 1><<<grid, 256, 0, st>>>(k);
+  else if (bna == 2) stem_fwd_kernel<S, NT, 0, 2><<<grid, 256, 0, st>>>(k);
+  else if (bna == 3) stem_fwd_kernel<S, NT, 0, 3><<<grid, 256, 0, st>>>(k);
   else stem_fwd_kernel<S, NT, 0><<<grid, 256, 0, st>>>(k);
 }
 
 template <int S>
-void fwd_dispatch(const StemArgs& k, int grid, hipStream_t st) {
+void fwd_dispatch(const StemArgs& k, int grid, hipStream_t st, int bna) {
   switch (k.cout / 16) {
-    case 1: fwd_launch<S, 1>(k, grid, st); break;
-    case 2: fwd_launch<S, 2>(k, grid, st); break;
-    case 3: fwd_launch<S, 3>(k, grid, st); break;
-    default: fwd_launch<S, 4>(k, grid, st); break;
+    case 1: fwd_launch<S, 1>(k, grid, st, bna); break;
+    case 2: fwd_launch<S, 2>(k, grid, st, bna); break;
+    case 3: fwd_launch<S, 3>(k, grid, st, bna); break;
+    default: fwd_launch<S, 4>(k, grid, st, bna); break;
   }
 }
 
@@ -442,9 +470,11 @@ void launch_conv_stem_fwd(const ConvGeom& g, hipStream_t st) {
   k.w = static_cast<const uint16_t*>(g.w);
   k.y = static_cast<uint16_t*>(g.y);
   k.part = g.part;
+  k.ss = g.scale_shift;  // the BN epilogue (no statistics then)
+  const int bna = g.scale_shift != nullptr ? g.act + 1 : 0;
   const int grid = stem_grid(k.mtiles);
-  if (g.sh == 2) fwd_dispatch<2>(k, grid, st);
-  else fwd_dispatch<1>(k, grid, st);
+  if (g.sh == 2) fwd_dispatch<2>(k, grid, st, bna);
+  else fwd_dispatch<1>(k, grid, st, bna);
 }
 
 int64_t conv_stem_wgrad_ws_elems(const ConvGeom& g) {

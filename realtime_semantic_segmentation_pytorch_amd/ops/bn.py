@@ -37,6 +37,8 @@ _HANDOFF = os.environ.get("RTSEG_RES_HANDOFF", "1") != "0"
 # vs 528.5 images/s, profiles/r5_masked) -- the epilogue's per-lane mask-byte loads cost more
 # than the saved 2-byte-per-element write
 _MASKED_HANDOFF = os.environ.get("RTSEG_MASKED_HANDOFF", "0") == "1"
+# the stem BN's forward apply as a recompute of the stem conv (RTSEG_STEM_BN_RECOMPUTE=0: off, A/B)
+_STEM_BN_RECOMPUTE = os.environ.get("RTSEG_STEM_BN_RECOMPUTE", "1") != "0"
 
 
 def act_code(act) -> Optional[int]:
@@ -104,8 +106,18 @@ class _BNActFn(torch.autograd.Function):
             mask = MASK_FROM_X
         else:
             mask = MASK_BITS if _USE_BITS else MASK_FROM_Y
+        # a stem conv produced x (batch statistics, no residual / concat slice): the apply is a
+        # recompute of that K = 27 conv from the 0.4 GB image with the BN + act epilogue on its
+        # fp32 accumulators (conv_stem_bn_act) -- no pass over the 2.1 GB x
+        sprod = x.grad_fn if (use_batch_stats and residual is None and out2 is None and _STEM_BN_RECOMPUTE
+                              and mask in (MASK_NONE, MASK_FROM_X) and x.dtype == torch.bfloat16) else None
+        stem_io = getattr(sprod, "stem_io", None)
         # out2: this output's channel slice of a concat buffer (ops/concat.py), stored too
-        if mask == MASK_BITS:
+        if stem_io is not None:
+            xi, wk, st, pd, dl = stem_io
+            y, bits = ops().conv_stem_bn_act(xi, wk, st, pd, dl, ss, act), None
+            STEM_RECOMPUTES[0] += 1
+        elif mask == MASK_BITS:
             y, bits = ops().bn_apply_bits(x, ss, residual, act, out2)
         else:
             y, bits = ops().bn_apply(x, ss, residual, act, out2), None
@@ -196,6 +208,7 @@ class _BNActFn(torch.autograd.Function):
 
 
 MASKED_HANDOFFS = [0]  # residual gradients handed over as (gradient, bit mask) (tests)
+STEM_RECOMPUTES = [0]  # stem BN forward applies run as conv_stem_bn_act (tests)
 STEM_HANDOFFS = [0]  # BN backward dx passes handed to a stem conv's weight gradient (tests)
 
 

@@ -594,6 +594,9 @@ class _ConvFn(torch.autograd.Function):
         # weight gradient (conv_stem_wgrad_bn) instead of writing dx to HBM
         ctx.bn_fuse_slot = [] if (_STEM_BN_FUSE and not x.requires_grad and stem_ok(conv, x)
                                   and conv.out_channels in (16, 32, 64)) else None
+        # ... and its forward apply recomputes this conv from the image with the BN epilogue
+        # (conv_stem_bn_act) instead of re-reading y
+        ctx.stem_io = ((x, wk) + tuple(_geom(conv))) if ctx.bn_fuse_slot is not None else None
         if part is not None:
             ctx.mark_non_differentiable(part)
         # the statistics slab never gets a gradient: without this autograd would allocate and

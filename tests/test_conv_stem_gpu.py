@@ -240,3 +240,57 @@ def test_stem_bn_backward_fused(monkeypatch, act, second_consumer, cout):
 
     for a, b, name in zip(res[0], res[1], ("conv.weight", "bn.weight", "bn.bias")):
         assert rel(a, b) < 1e-2, (name, rel(a, b))
+
+
+@pytest.mark.parametrize("geom", [(2, 17, 70, 64, 2), (1, 9, 130, 32, 1), (3, 33, 66, 16, 2)])
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_stem_bn_act_epilogue(geom, act):
+    """conv_stem_bn_act: act(conv(x) * scale + shift) from the fp32 accumulators vs fp32 PyTorch."""
+    n, h, w, cout, s = geom
+    g = torch.Generator().manual_seed(4)
+    x = _t((n, 3, h, w), g).contiguous(memory_format=torch.channels_last)
+    wt = _t((cout, 3, 3, 3), g, 0.2)
+    ss = torch.cat([torch.rand(cout, generator=g) + 0.5, torch.randn(cout, generator=g)]).to(DEV)
+    y = torch.ops.rtseg.conv_stem_bn_act(x, wt.permute(0, 2, 3, 1).contiguous(), [s, s], [1, 1], [1, 1], ss, act)
+    ref = F.conv2d(x.float(), wt.float(), None, s, 1) * ss[:cout].view(1, -1, 1, 1) + ss[cout:].view(1, -1, 1, 1)
+    ref = ref.relu() if act == 1 else ref.clamp(0, 6) if act == 2 else ref
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    _close(y, ref, 1e-2)
+
+
+@pytest.mark.parametrize("act", ["relu", "none"])
+def test_stem_bn_forward_recompute(monkeypatch, act):
+    """A training stem ConvBNAct: the BN's forward apply recomputed from the image
+    (conv_stem_bn_act, ops/bn.py) vs the apply over the stored conv output -- outputs, BN running
+    statistics and gradients agree to bf16 rounding, and the recompute really ran."""
+    from realtime_semantic_segmentation_pytorch_amd.models.modules import ConvBNAct
+    from realtime_semantic_segmentation_pytorch_amd.ops import bn as bn_mod
+
+    torch.manual_seed(0)
+    net0 = ops.convert_batchnorm(ConvBNAct(3, 32, 3, 2, act_type=act)).to(DEV).to(memory_format=torch.channels_last)
+    x = torch.randn(2, 3, 40, 132, device=DEV).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(2, 32, 20, 66, device=DEV)
+    res = []
+    for on in (True, False):
+        import copy
+
+        net = copy.deepcopy(net0).train()
+        monkeypatch.setattr(bn_mod, "_STEM_BN_RECOMPUTE", on)
+        before = bn_mod.STEM_RECOMPUTES[0]
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = net(x)
+        (y.float() * gy).sum().backward()
+        assert (bn_mod.STEM_RECOMPUTES[0] > before) == on
+        bn = [m for m in net.modules() if isinstance(m, torch.nn.BatchNorm2d)][0]
+        res.append((y.float().detach(), {n: p.grad.float().clone() for n, p in net.named_parameters()},
+                    bn.running_mean.clone(), bn.running_var.clone()))
+    (y0, g0, m0, v0), (y1, g1, m1, v1) = res
+
+    def rel(a, b):
+        return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+    assert rel(y0, y1) < 1e-2
+    torch.testing.assert_close(m0, m1)
+    torch.testing.assert_close(v0, v1)
+    for n_, g_ in g1.items():
+        assert rel(g0[n_], g_) < 2e-2, n_
