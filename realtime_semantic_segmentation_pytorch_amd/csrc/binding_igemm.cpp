@@ -42,7 +42,8 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::
                                                  at::IntArrayRef padding, at::IntArrayRef dilation, bool stats,
                                                  const std::optional<at::Tensor>& scale_shift,
                                                  const std::optional<at::Tensor>& residual, int64_t act, int kind) {
-  const bool halo = kind == 1, wres = kind == 2, hreg = kind == 3 || kind == 4, stem = kind == 5;
+  // kind 7: the stem kernel's statistics without the output stores
+  const bool halo = kind == 1, wres = kind == 2, hreg = kind == 3 || kind == 4, stem = kind == 5 || kind == 7;
   check_act(x, "input");
   TORCH_CHECK(wk.is_cuda() && wk.dim() == 4 && wk.scalar_type() == at::kBFloat16 && wk.is_contiguous() &&
                   wk.size(3) == x.size(1),
@@ -69,7 +70,7 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::
   }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   at::Tensor y = at::empty({g.n, g.cout, g.ho, g.wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  g.x = x.data_ptr(); g.w = wk.data_ptr(); g.y = y.data_ptr();
+  g.x = x.data_ptr(); g.w = wk.data_ptr(); g.y = kind == 7 ? nullptr : y.data_ptr();
   g.part = nullptr; g.scale_shift = nullptr; g.res = nullptr; g.act = static_cast<int>(act);
   at::Tensor part;
   if (stats) {
@@ -143,9 +144,40 @@ std::tuple<at::Tensor, at::Tensor> conv_wres(const at::Tensor& x, const at::Tens
 }
 
 // the 3-channel stem kernel (conv_stem.hip): 3 x 3 / pad 1 / stride 1 or 2, Cout % 16 <= 64
+// store = false (with stats): the statistics only; y is returned allocated but never written -- the
+// stem BN recomputes it wherever it is needed (ops/bn.py, conv_stem_bn_act / _bn_sums / _wgrad_bn)
 std::tuple<at::Tensor, at::Tensor> conv_stem(const at::Tensor& x, const at::Tensor& wk, at::IntArrayRef stride,
-                                             at::IntArrayRef padding, at::IntArrayRef dilation, bool stats) {
-  return conv_fwd_impl(x, wk, stride, padding, dilation, stats, std::nullopt, std::nullopt, 0, 5);
+                                             at::IntArrayRef padding, at::IntArrayRef dilation, bool stats,
+                                             bool store) {
+  TORCH_CHECK(store || stats, "rtseg.conv_stem: store = false needs stats");
+  return conv_fwd_impl(x, wk, stride, padding, dilation, stats, std::nullopt, std::nullopt, 0, store ? 5 : 7);
+}
+
+// the stem BN's backward reduction [slabs, 2 cout] (sum g', sum g' (x - mean)) with the conv
+// output x recomputed from the image instead of read back (conv_stem.hip, STATS 2)
+at::Tensor conv_stem_bn_sums(const at::Tensor& x, const at::Tensor& wk, at::IntArrayRef stride,
+                             at::IntArrayRef padding, at::IntArrayRef dilation, const at::Tensor& dy,
+                             const at::Tensor& mean_invstd, const at::Tensor& scale_shift, int64_t act) {
+  check_act(x, "input");
+  check_act(dy, "grad_output");
+  TORCH_CHECK(wk.is_cuda() && wk.dim() == 4 && wk.scalar_type() == at::kBFloat16 && wk.is_contiguous() &&
+                  wk.size(3) == x.size(1),
+              "rtseg.conv_stem_bn_sums: weights must be contiguous bf16 [Cout, KH, KW, Cin]");
+  ConvGeom g = geom(x.size(0), x.size(1), x.size(2), x.size(3), wk.size(0), wk.size(1), wk.size(2), stride, padding,
+                    dilation);
+  TORCH_CHECK(conv_stem_supported(g), "rtseg.conv_stem_bn_sums: not a stem geometry");
+  TORCH_CHECK(dy.size(0) == g.n && dy.size(1) == g.cout && dy.size(2) == g.ho && dy.size(3) == g.wo,
+              "rtseg.conv_stem_bn_sums: grad_output does not match the geometry");
+  TORCH_CHECK(mean_invstd.is_cuda() && mean_invstd.scalar_type() == at::kFloat && mean_invstd.numel() == 2 * g.cout &&
+                  scale_shift.is_cuda() && scale_shift.scalar_type() == at::kFloat && scale_shift.numel() == 2 * g.cout,
+              "rtseg.conv_stem_bn_sums: coefficients must be fp32 [2 cout]");
+  TORCH_CHECK(act >= 0 && act <= 2, "rtseg.conv_stem_bn_sums: bad activation");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  at::Tensor part = at::empty({conv_stem_slabs(g), 2 * g.cout}, x.options().dtype(at::kFloat));
+  g.x = x.data_ptr(); g.w = wk.data_ptr(); g.y = const_cast<void*>(dy.data_ptr());
+  launch_conv_stem_bn_sums(g, mean_invstd.data_ptr<float>(), scale_shift.data_ptr<float>(), static_cast<int>(act),
+                           part.data_ptr<float>(), cur_stream());
+  return part;
 }
 
 // ... with a BN (+ activation) epilogue on the fp32 accumulators: act(conv(x) * scale + shift)
@@ -324,10 +356,11 @@ at::Tensor conv_stem_wgrad_bn(const at::Tensor& x, const at::Tensor& dy, const a
                               const at::Tensor& kcoef, const at::Tensor& mean_invstd,
                               const at::Tensor& scale_shift, int64_t act, int64_t kh, int64_t kw,
                               at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
-                              bool channels_last) {
+                              bool channels_last, const std::optional<at::Tensor>& wk) {
   check_act(x, "input");
   check_act(dy, "grad_output");
-  check_act(xb, "bn_input");
+  const bool rc = wk.has_value() && wk->defined();  // recompute the BN input (xb may be a placeholder)
+  if (!rc) check_act(xb, "bn_input");
   ConvGeom g = geom(x.size(0), x.size(1), x.size(2), x.size(3), dy.size(1), kh, kw, stride, padding, dilation);
   TORCH_CHECK(g.ho == dy.size(2) && g.wo == dy.size(3) && g.n == dy.size(0) && xb.sizes() == dy.sizes(),
               "rtseg.conv_stem_wgrad_bn: grad_output / bn_input do not match the geometry");
@@ -348,8 +381,12 @@ at::Tensor conv_stem_wgrad_bn(const at::Tensor& x, const at::Tensor& dy, const a
   at::Tensor dw = at::empty({g.cout, g.cin, g.kh, g.kw},
                             x.options().dtype(at::kFloat).memory_format(channels_last ? at::MemoryFormat::ChannelsLast
                                                                                       : at::MemoryFormat::Contiguous));
-  const StemBnBwd bn{xb.data_ptr(), kcoef.data_ptr<float>(), mean_invstd.data_ptr<float>(),
-                     scale_shift.data_ptr<float>(), static_cast<int>(act)};
+  if (rc)
+    TORCH_CHECK(wk->is_cuda() && wk->scalar_type() == at::kBFloat16 && wk->is_contiguous() && wk->numel() == 27 * C,
+                "rtseg.conv_stem_wgrad_bn: wk must be contiguous bf16 [Cout, 3, 3, 3]");
+  StemBnBwd bn{rc ? nullptr : xb.data_ptr(), kcoef.data_ptr<float>(), mean_invstd.data_ptr<float>(),
+               scale_shift.data_ptr<float>(), static_cast<int>(act)};
+  if (rc) bn.w = wk->data_ptr();
   launch_conv_stem_wgrad(g, ws.data_ptr<float>(), dw.data_ptr<float>(), channels_last, cur_stream(), &bn);
   return dw;
 }
@@ -373,12 +410,15 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
   m.def("conv_wres(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats) -> (Tensor, Tensor)");
   m.def("conv_wres_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
         "Tensor? addend=None, Tensor? addend_mask=None) -> Tensor");
-  m.def("conv_stem(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats) -> (Tensor, Tensor)");
+  m.def("conv_stem(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats, bool store=True) "
+        "-> (Tensor, Tensor)");
   m.def("conv_stem_bn_act(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, Tensor scale_shift, "
         "int act) -> Tensor");
+  m.def("conv_stem_bn_sums(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, Tensor dy, "
+        "Tensor mean_invstd, Tensor scale_shift, int act) -> Tensor");
   m.def("conv_stem_wgrad_bn(Tensor x, Tensor dy, Tensor bn_input, Tensor kcoef, Tensor mean_invstd, "
         "Tensor scale_shift, int act, int kh, int kw, int[] stride, int[] padding, int[] dilation, "
-        "bool channels_last) -> Tensor");
+        "bool channels_last, Tensor? wk=None) -> Tensor");
   m.def("conv_stem_wgrad(Tensor x, Tensor dy, int kh, int kw, int[] stride, int[] padding, int[] dilation, "
         "bool channels_last=False) -> Tensor");
   m.def("conv_whalo_wgrad(Tensor x, Tensor dy, int kh, int kw, int[] stride, int[] padding, int[] dilation, "
@@ -400,6 +440,7 @@ TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
   m.impl("conv_whalo_wgrad", &rtseg::conv_whalo_wgrad);
   m.impl("conv_stem", &rtseg::conv_stem);
   m.impl("conv_stem_bn_act", &rtseg::conv_stem_bn_act);
+  m.impl("conv_stem_bn_sums", &rtseg::conv_stem_bn_sums);
   m.impl("conv_stem_wgrad_bn", &rtseg::conv_stem_wgrad_bn);
   m.impl("conv_stem_wgrad", &rtseg::conv_stem_wgrad);
 }

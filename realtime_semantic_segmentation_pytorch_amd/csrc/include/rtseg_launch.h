@@ -238,17 +238,21 @@ void launch_conv_hreg(const ConvGeom& g, int mode, void* wpack, hipStream_t st, 
 // (+ BN statistics slab of conv_stem_slabs(g) rows) and weight gradient (g.x = x, g.y = dy).
 bool conv_stem_supported(const ConvGeom& g);
 int conv_stem_slabs(const ConvGeom& g);
+// stem BN backward reduction with the conv recomputed from the image (g.y = the BN output's gradient)
+void launch_conv_stem_bn_sums(const ConvGeom& g, const float* mean_invstd, const float* scale_shift, int act,
+                              float* part, hipStream_t st);
 void launch_conv_stem_fwd(const ConvGeom& g, hipStream_t st);
 int64_t conv_stem_wgrad_ws_elems(const ConvGeom& g);
 // BN-fused weight gradient: g.y is the gradient of act(BN(conv output)); the BN backward's apply
 // pass (dx = k0 (g - k1 - (xb - mean) k2), g masked by act'(xb * sc + sh)) runs in the dy staging.
 // act: 0 none, 1 ReLU, 2 ReLU6.  Cout of 16, 32 or 64.
 struct StemBnBwd {
-  const void* xb;
+  const void* xb;           // the BN input (the conv output), or null with w set
   const float* kcoef;
   const float* mean_invstd;
   const float* scale_shift;
   int act;
+  const void* w = nullptr;  // KRSC stem weights: recompute the BN input from the image instead
 };
 void launch_conv_stem_wgrad(const ConvGeom& g, float* ws, float* dw, bool krsc, hipStream_t st,
                             const StemBnBwd* bn = nullptr);

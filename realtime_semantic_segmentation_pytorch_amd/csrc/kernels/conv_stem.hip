@@ -22,6 +22,7 @@
 #include "rtseg_mfma_dev.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace rtseg {
 
@@ -93,43 +94,89 @@ __device__ __forceinline__ void stage_input(const StemArgs& a, uint32_t* l32, in
     if (tid + 256 * e < kTotal) l32[tid + 256 * e] = v[e];
 }
 
+// input rows with every pixel padded to 4 channels (8 bytes, the 4th zero): pixel q of staged row r
+// at uint2 index r * PX + q (the same rows / pixels as stage_input).  The forward's B fragment of
+// lane half h -- taps 2h and 2h + 1, 4 channels each -- is then two 8-byte LDS reads instead of
+// eight 2-byte gathers with their selects and packs (33 VALU per MFMA: profiles/r5_stempmc)
+template <int S, int TH>
+__device__ __forceinline__ void stage_input4(const StemArgs& a, uint2* l64, int n, int oy0, int ox0, int tid) {
+  using T = StemTile<S, TH>;
+  constexpr int PP = T::PX / 2;  // pixel pairs per row
+  constexpr int kTotal = T::R * PP, kPer = (kTotal + 255) / 256;
+  const int iw0 = ox0 * S - 2;
+  const uint32_t* x32 = reinterpret_cast<const uint32_t*>(a.x);
+  uint32_t d[kPer][3];
+#pragma unroll
+  for (int e = 0; e < kPer; ++e) {
+    const int pi = tid + 256 * e;
+    const int r = pi / PP, pp = pi - r * PP;
+    const int ih = oy0 * S - 1 + r, iwp = iw0 + 2 * pp;
+    d[e][0] = d[e][1] = d[e][2] = 0u;
+    if (pi < kTotal && static_cast<unsigned>(ih) < static_cast<unsigned>(a.H) && iwp >= 0 && iwp < a.W) {
+      const uint32_t* src = x32 + ((static_cast<int64_t>(n) * a.H + ih) * a.W + iwp) * 3 / 2;
+      d[e][0] = src[0]; d[e][1] = src[1]; d[e][2] = src[2];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < kPer; ++e) {
+    const int pi = tid + 256 * e;
+    if (pi >= kTotal) continue;
+    const int r = pi / PP, pp = pi - r * PP;
+    // two pixels (c0 c1 c2 | c0 c1 c2) -> (c0 c1 c2 0) (c0 c1 c2 0)
+    *reinterpret_cast<uint4*>(l64 + r * T::PX + 2 * pp) =
+        uint4{d[e][0], d[e][1] & 0xffffu, (d[e][1] >> 16) | (d[e][2] << 16), d[e][2] >> 16};
+  }
+}
+
 // BNA: 0 = the raw conv output (+ STATS), else the training BN applied in the epilogue from the
 // fp32 accumulators -- y = act(conv * scale + shift), act = BNA - 1 (none / ReLU / ReLU6): the
 // stem BN's forward apply as a recompute of the (K = 27) conv from the 0.4 GB image instead of a
 // pass over the 2.1 GB conv output (ops/bn.py; the conv output itself is still written by the
 // statistics launch, for the BN backward)
+// STATS 2: the stem BN's BACKWARD reduction with the conv recomputed -- per channel
+// sum g' and sum g' (x - mean), g' = dy masked by act'(x * scale + shift) (act = BNA - 1), x = the
+// bf16-rounded conv output exactly as the statistics launch stored it, read from the 0.4 GB image
+// instead of the 2.1 GB stored x; no output stores.  Same [grid][2 cout] slab as the forward
+// statistics (the BN backward finalize's input)
 template <int S, int NT, int STATS, int BNA = 0>
 __global__ void __launch_bounds__(256) stem_fwd_kernel(const StemArgs a) {
-  static_assert(!(STATS && BNA), "statistics come from the raw conv output");
+  static_assert(!(STATS == 1 && BNA), "statistics come from the raw conv output");
+  static_assert(STATS != 2 || BNA != 0, "the backward reduction needs the activation");
   constexpr int TH = 8;  // 4 waves x 2 rows
   using T = StemTile<S, TH>;
-  __shared__ uint32_t l32[T::R * T::DW];
+  __shared__ __attribute__((aligned(16))) uint2 l64[T::R * T::PX];
   __shared__ float red[4][2][64];
-  const uint16_t* l16 = reinterpret_cast<const uint16_t*>(l32);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int h = lane >> 4, px = lane & 15;
   const int G = gridDim.x;
   const int lb = xcd_logical(blockIdx.x, G);
 
-  // A fragments: weights [row m = px][k 8h + j]; row m of tile t is output channel
-  // cout_of(t, m) = 4 NT (m >> 2) + 4 t + (m & 3), so the C rows 4h .. 4h + 3 of the NT tiles are
-  // the 4 NT CONSECUTIVE channels 4 NT h .. of one pixel in a lane: 16-byte stores
-  bf16x8_t wf[NT];
+  // A fragments, K = tap * 4 + channel (the 4th channel zero): K block 0 = taps 0..7, block 1 =
+  // tap 8 (lane half 0 only).  Row m of tile t is output channel cout_of(t, m) =
+  // 4 NT (m >> 2) + 4 t + (m & 3), so the C rows 4h .. 4h + 3 of the NT tiles are the 4 NT
+  // CONSECUTIVE channels 4 NT h .. of one pixel in a lane: 16-byte stores
+  bf16x8_t wf[2][NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
-    s16x8_t v;
     const int co = 4 * NT * (px >> 2) + 4 * t + (px & 3);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = 8 * h + j;
-      v[j] = k < 27 ? static_cast<short>(a.w[co * 27 + k]) : short(0);
+    for (int kb = 0; kb < 2; ++kb) {
+      s16x8_t v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 8 * h + j, tap = 8 * kb + (k >> 2), ch = k & 3;
+        v[j] = (tap < 9 && ch < 3) ? static_cast<short>(a.w[co * 27 + tap * 3 + ch]) : short(0);
+      }
+      wf[kb][t] = __builtin_bit_cast(bf16x8_t, v);
     }
-    wf[t] = __builtin_bit_cast(bf16x8_t, v);
   }
-  int ko[8];
-  k_offsets<T::PX>(h, ko);
+  // this lane half's two taps (2h, 2h + 1): staged-pixel offsets from the output pixel's (row 0, tap 0)
+  const int t0 = 2 * h, t1 = 2 * h + 1;
+  const int off0 = (t0 / 3) * T::PX + t0 % 3 + 1, off1 = (t1 / 3) * T::PX + t1 % 3 + 1;
+  const int off8 = 2 * T::PX + 2 + 1;  // tap 8 (lane half 0)
 
   float bsc[BNA ? NT : 1][4], bsh[BNA ? NT : 1][4];  // this lane's channels' BN scale / shift
+  float bmu[STATS == 2 ? NT : 1][4];                   // ... and mean (backward reduction)
   if constexpr (BNA != 0) {
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -138,6 +185,7 @@ __global__ void __launch_bounds__(256) stem_fwd_kernel(const StemArgs a) {
         const int co = 4 * NT * h + 4 * t + r;
         bsc[t][r] = a.ss[co];
         bsh[t][r] = a.ss[a.cout + co];
+        if constexpr (STATS == 2) bmu[t][r] = a.mi[co];
       }
   }
 
@@ -151,25 +199,59 @@ __global__ void __launch_bounds__(256) stem_fwd_kernel(const StemArgs a) {
     const int tx = mt % a.tilesW, t2 = mt / a.tilesW;
     const int n = t2 / a.tilesH, oy0 = (t2 % a.tilesH) * TH, ox0 = tx * kTW;
     __syncthreads();  // the previous tile's fragment reads are done
-    stage_input<S, TH>(a, l32, n, oy0, ox0, tid);
+    stage_input4<S, TH>(a, l64, n, oy0, ox0, tid);
     __syncthreads();
 #pragma unroll 2
     for (int g = 0; g < 8; ++g) {
       const int oyl = 2 * wid + (g >> 2), oxl = (g & 3) * 16 + px;
-      const int base = oyl * S * T::PX * 3 + (oxl * S + 1) * 3;
-      s16x8_t b;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) b[j] = ko[j] >= 0 ? static_cast<short>(l16[base + ko[j]]) : short(0);
-      const bf16x8_t bf = __builtin_bit_cast(bf16x8_t, b);
+      const int pb = oyl * S * T::PX + oxl * S;
+      const uint2 q0 = l64[pb + off0], q1 = l64[pb + off1], q8 = l64[pb + off8];
+      const bf16x8_t bf = __builtin_bit_cast(bf16x8_t, uint4{q0.x, q0.y, q1.x, q1.y});
+      const bf16x8_t bf8 = __builtin_bit_cast(bf16x8_t, h == 0 ? uint4{q8.x, q8.y, 0u, 0u} : uint4{0u, 0u, 0u, 0u});
       const int oy = oy0 + oyl, ox = ox0 + oxl;
       const bool ok = oy < a.Ho && ox < a.Wo;
-      uint16_t* yp =
-          a.y + ((static_cast<int64_t>(n) * a.Ho + (ok ? oy : 0)) * a.Wo + (ok ? ox : 0)) * a.cout + 4 * NT * h;
+      const int64_t poff = ((static_cast<int64_t>(n) * a.Ho + (ok ? oy : 0)) * a.Wo + (ok ? ox : 0)) * a.cout + 4 * NT * h;
+      uint16_t* yp = a.y + poff;
+      uint32_t gk[STATS == 2 ? 2 * NT : 1];  // the lane's 4 NT gradient values (STATS 2)
+      if constexpr (STATS == 2) {
+#pragma unroll
+        for (int v = 0; v < 2 * NT; ++v) gk[v] = 0u;
+        if (ok) {
+          if constexpr (NT % 2 == 0) {
+#pragma unroll
+            for (int v = 0; v < NT / 2; ++v) {
+              const uint4 q = reinterpret_cast<const uint4*>(a.dy + poff)[v];
+              gk[4 * v] = q.x; gk[4 * v + 1] = q.y; gk[4 * v + 2] = q.z; gk[4 * v + 3] = q.w;
+            }
+          } else {
+#pragma unroll
+            for (int v = 0; v < NT; ++v) {
+              const uint2 q = reinterpret_cast<const uint2*>(a.dy + poff)[v];
+              gk[2 * v] = q.x; gk[2 * v + 1] = q.y;
+            }
+          }
+        }
+      }
       uint32_t pk[2 * NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         f32x4_t c = {0.f, 0.f, 0.f, 0.f};
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t], bf, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[0][t], bf, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[1][t], bf8, c, 0, 0, 0);
+        if constexpr (STATS == 2) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const uint32_t w2 = gk[2 * t + (r >> 1)];
+            const float g = (r & 1) ? __uint_as_float(w2 & 0xffff0000u) : __uint_as_float(w2 << 16);
+            const float xr = bf16_to_f32(f32_to_bf16(c[r]));  // the stored conv output's value
+            const float z = fmaf(xr, bsc[t][r], bsh[t][r]);
+            const bool live = BNA == 1 ? true : BNA == 2 ? z > 0.f : (z > 0.f && z < 6.f);
+            const float gm = (ok && live) ? g : 0.f;
+            ts[t][r] += gm;
+            tq[t][r] = fmaf(gm, xr - bmu[t][r], tq[t][r]);
+          }
+          continue;
+        }
         if constexpr (BNA != 0) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -179,7 +261,7 @@ __global__ void __launch_bounds__(256) stem_fwd_kernel(const StemArgs a) {
         }
         pk[2 * t] = pack2(c[0], c[1]);
         pk[2 * t + 1] = pack2(c[2], c[3]);
-        if constexpr (STATS) {
+        if constexpr (STATS == 1) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float u = ok ? c[r] : 0.f;
@@ -188,7 +270,7 @@ __global__ void __launch_bounds__(256) stem_fwd_kernel(const StemArgs a) {
           }
         }
       }
-      if (ok) {
+      if (ok && STATS != 2 && a.y != nullptr) {  // null y: statistics only (the recompute path)
         if constexpr (NT % 2 == 0) {
 #pragma unroll
           for (int v = 0; v < NT / 2; ++v)
@@ -244,13 +326,19 @@ __device__ __forceinline__ float bn_dx(float g, float xv, int j, const float* k0
 }
 
 // weight gradient partials: block b writes ws[b][k 32][cout] (k >= 27 rows are zero)
-template <int S, int NT, int BNF = 0>
+// RC (BN-fused only): the BN input x is not read back but recomputed from the staged image rows
+// (one v_mfma_f32_16x16x32_bf16 per 16 pixels x 16 channels, the forward kernel's fragments) and
+// rounded to bf16 exactly as the forward's statistics launch stored it
+template <int S, int NT, int BNF = 0, int RC = 0>
 __global__ void __launch_bounds__(256) stem_wgrad_kernel(const StemArgs a) {
+  static_assert(RC == 0 || BNF != 0, "the recompute feeds the fused BN backward");
   constexpr int TH = 4;  // 4 waves x 1 row of 64 pixels (2 MFMA K-steps of 32 pixels)
   constexpr int CP = 16 * NT + 2;  // dy row pitch (elements)
+  constexpr int XP = 16 * NT + 8;  // recomputed-x row pitch (elements; 16-byte rows)
   using T = StemTile<S, TH>;
   __shared__ uint32_t l32[T::R * T::DW];
   __shared__ uint16_t dyl[TH * kTW * CP];
+  __shared__ __attribute__((aligned(16))) uint16_t xl[RC ? TH * kTW * XP : 8];
   const uint16_t* l16 = reinterpret_cast<const uint16_t*>(l32);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int h = lane >> 4, c16 = lane & 15;
@@ -275,6 +363,22 @@ __global__ void __launch_bounds__(256) stem_wgrad_kernel(const StemArgs a) {
   // BN-fused: a thread always stages the same channel vector (V divides 256): its coefficients
   // stay in registers
   static_assert(BNF == 0 || 256 % V == 0, "BN-fused stem wgrad needs V | 256");
+  bf16x8_t wf[RC ? NT : 1];  // RC: forward A fragments (see stem_fwd_kernel)
+  int kof[8];
+  if constexpr (RC != 0) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      s16x8_t v;
+      const int co = 4 * NT * (c16 >> 2) + 4 * t + (c16 & 3);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 8 * h + j;
+        v[j] = k < 27 ? static_cast<short>(a.w[co * 27 + k]) : short(0);
+      }
+      wf[t] = __builtin_bit_cast(bf16x8_t, v);
+    }
+    k_offsets<T::PX>(h, kof);
+  }
   float k0[8], k1[8], k2[8], mu[8], sc[8], sh[8];
   if constexpr (BNF != 0) {
     const int c0 = 8 * (tid % V);
@@ -305,7 +409,34 @@ __global__ void __launch_bounds__(256) stem_wgrad_kernel(const StemArgs a) {
       if (oy < a.Ho && ox < a.Wo) {
         const int64_t off = ((static_cast<int64_t>(n) * a.Ho + oy) * a.Wo + ox) * C + 8 * v;
         q[i] = *reinterpret_cast<const uint4*>(a.dy + off);
-        if constexpr (BNF != 0) xq[i] = *reinterpret_cast<const uint4*>(a.xb + off);
+        if constexpr (BNF != 0 && RC == 0) xq[i] = *reinterpret_cast<const uint4*>(a.xb + off);
+      }
+    }
+    if constexpr (RC != 0) {
+      // the tile's conv output, recomputed while the dy loads are in flight: wave wid = tile row
+      __syncthreads();  // every wave's image rows are staged
+#pragma unroll
+      for (int gi = 0; gi < 4; ++gi) {
+        const int oxl = gi * 16 + c16;
+        const int base = wid * S * T::PX * 3 + (oxl * S + 1) * 3;
+        s16x8_t b;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b[j] = kof[j] >= 0 ? static_cast<short>(l16[base + kof[j]]) : short(0);
+        const bf16x8_t bf = __builtin_bit_cast(bf16x8_t, b);
+        uint16_t* xp = xl + (wid * kTW + oxl) * XP + 4 * NT * h;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          f32x4_t c = {0.f, 0.f, 0.f, 0.f};
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t], bf, c, 0, 0, 0);
+          *reinterpret_cast<uint2*>(xp + 4 * t) = uint2{pack2(c[0], c[1]), pack2(c[2], c[3])};
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) {
+        const int e = tid + 256 * i;
+        const int p = e / V, v = e - p * V;
+        xq[i] = *reinterpret_cast<const uint4*>(xl + p * XP + 8 * v);
       }
     }
     if constexpr (BNF != 0) {
@@ -432,22 +563,30 @@ void fwd_dispatch(const StemArgs& k, int grid, hipStream_t st, int bna) {
   }
 }
 
-template <int S, int BNF>
+template <int S, int BNF, int RC>
 void wgrad_dispatch(const StemArgs& k, int grid, hipStream_t st) {
   switch (k.cout / 16) {
-    case 1: stem_wgrad_kernel<S, 1, BNF><<<grid, 256, 0, st>>>(k); break;
-    case 2: stem_wgrad_kernel<S, 2, BNF><<<grid, 256, 0, st>>>(k); break;
+    case 1: stem_wgrad_kernel<S, 1, BNF, RC><<<grid, 256, 0, st>>>(k); break;
+    case 2: stem_wgrad_kernel<S, 2, BNF, RC><<<grid, 256, 0, st>>>(k); break;
     case 3:
       if constexpr (BNF == 0) stem_wgrad_kernel<S, 3, 0><<<grid, 256, 0, st>>>(k);  // (BN-fused: V = 6 does not divide 256)
       break;
-    default: stem_wgrad_kernel<S, 4, BNF><<<grid, 256, 0, st>>>(k); break;
+    default: stem_wgrad_kernel<S, 4, BNF, RC><<<grid, 256, 0, st>>>(k); break;
   }
 }
 
 template <int BNF>
-void wgrad_dispatch_s(const StemArgs& k, int grid, int s, hipStream_t st) {
-  if (s == 2) wgrad_dispatch<2, BNF>(k, grid, st);
-  else wgrad_dispatch<1, BNF>(k, grid, st);
+void wgrad_dispatch_s(const StemArgs& k, int grid, int s, hipStream_t st, bool rc = false) {
+  if constexpr (BNF == 0) {
+    if (s == 2) wgrad_dispatch<2, 0, 0>(k, grid, st);
+    else wgrad_dispatch<1, 0, 0>(k, grid, st);
+  } else if (rc) {
+    if (s == 2) wgrad_dispatch<2, BNF, 1>(k, grid, st);
+    else wgrad_dispatch<1, BNF, 1>(k, grid, st);
+  } else {
+    if (s == 2) wgrad_dispatch<2, BNF, 0>(k, grid, st);
+    else wgrad_dispatch<1, BNF, 0>(k, grid, st);
+  }
 }
 
 }  // namespace
@@ -477,6 +616,38 @@ void launch_conv_stem_fwd(const ConvGeom& g, hipStream_t st) {
   else fwd_dispatch<1>(k, grid, st, bna);
 }
 
+// stem BN backward reduction with the conv recomputed (STATS 2): g.x = image, g.w = KRSC weights,
+// g.y = dy (the BN output's gradient), part [conv_stem_slabs(g)][2 cout]
+void launch_conv_stem_bn_sums(const ConvGeom& g, const float* mean_invstd, const float* scale_shift, int act,
+                              float* part, hipStream_t st) {
+  StemArgs k{};
+  if (!stem_fill(k, g, 8)) return;
+  k.x = static_cast<const uint16_t*>(g.x);
+  k.w = static_cast<const uint16_t*>(g.w);
+  k.dy = static_cast<const uint16_t*>(g.y);
+  k.mi = mean_invstd;
+  k.ss = scale_shift;
+  k.part = part;
+  const int grid = stem_grid(k.mtiles);
+  auto go = [&](auto s_tag) {
+    constexpr int S = decltype(s_tag)::value;
+    auto nt = [&](auto nt_tag) {
+      constexpr int NT = decltype(nt_tag)::value;
+      if (act == 1) stem_fwd_kernel<S, NT, 2, 2><<<grid, 256, 0, st>>>(k);
+      else if (act == 2) stem_fwd_kernel<S, NT, 2, 3><<<grid, 256, 0, st>>>(k);
+      else stem_fwd_kernel<S, NT, 2, 1><<<grid, 256, 0, st>>>(k);
+    };
+    switch (k.cout / 16) {
+      case 1: nt(std::integral_constant<int, 1>{}); break;
+      case 2: nt(std::integral_constant<int, 2>{}); break;
+      case 3: nt(std::integral_constant<int, 3>{}); break;
+      default: nt(std::integral_constant<int, 4>{}); break;
+    }
+  };
+  if (g.sh == 2) go(std::integral_constant<int, 2>{});
+  else go(std::integral_constant<int, 1>{});
+}
+
 int64_t conv_stem_wgrad_ws_elems(const ConvGeom& g) {
   StemArgs k{};
   if (!stem_fill(k, g, 4)) return 0;
@@ -496,10 +667,12 @@ void launch_conv_stem_wgrad(const ConvGeom& g, float* ws, float* dw, bool krsc, 
     wgrad_dispatch_s<0>(k, grid, g.sh, st);
   } else {
     k.xb = static_cast<const uint16_t*>(bn->xb);
+    k.w = static_cast<const uint16_t*>(bn->w);  // non-null: recompute x instead of reading xb
     k.kc = bn->kcoef; k.mi = bn->mean_invstd; k.ss = bn->scale_shift;
-    if (bn->act == 0) wgrad_dispatch_s<1>(k, grid, g.sh, st);
-    else if (bn->act == 1) wgrad_dispatch_s<2>(k, grid, g.sh, st);
-    else wgrad_dispatch_s<3>(k, grid, g.sh, st);
+    const bool rc = bn->w != nullptr;
+    if (bn->act == 0) wgrad_dispatch_s<1>(k, grid, g.sh, st, rc);
+    else if (bn->act == 1) wgrad_dispatch_s<2>(k, grid, g.sh, st, rc);
+    else wgrad_dispatch_s<3>(k, grid, g.sh, st, rc);
   }
   const int n = 27 * g.cout;
   stem_wgrad_reduce<<<(n + 63) / 64, 1024, 0, st>>>(ws, grid, g.cout, dw, krsc ? 1 : 0);

@@ -169,7 +169,10 @@ class _FusedTail:
         use_batch = bn.training or not bn.track_running_stats or bn.running_mean is None
         if not use_batch:
             return ops.conv_bn_act_eval(x, conv, bn, post, residual)
-        r = ops.conv_bn_stats(x, conv)
+        # a stem whose BN recomputes the conv output from the image: no 2.1 GB store (ops/bn.py)
+        store = not (residual is None and sink is None and post in (0, 1, 2)
+                     and ops.stem_store_skippable(x, conv, bn))
+        r = ops.conv_bn_stats(x, conv, store=store)
         if r is None:
             return None
         y, part = r

@@ -23,7 +23,7 @@ from .tapconv import TapConv2d, convert_tap_convs, tap_conv2d, tapconv_ok
 from .dilated import (DilatedGroupConv2d, convert_dilated_group_convs, dilated_group_conv2d, dilated_group_ok,
                       PrunedConv2d, convert_pruned_convs, pruned_conv2d, has_dead_taps)
 from .optim import FusedAdam, FusedAdamW, FusedSGD
-from .conv import (conv_ok, conv_bn_stats, twin_conv_bn_stats, conv_bn_act_eval, conv_bn_act, conv_forward, RoutedConv2d, GroupedConv2d,
+from .conv import (conv_ok, conv_bn_stats, stem_store_skippable, twin_conv_bn_stats, conv_bn_act_eval, conv_bn_act, conv_forward, RoutedConv2d, GroupedConv2d,
                    convert_routed_convs, invalidate_weight_shadows)
 from .deconv import TransposedConv2d, conv_transpose2d, convert_transposed_convs, deconv_ok
 from .gate import gate, gate_reference
@@ -41,7 +41,7 @@ __all__ = [
     "AdaptiveAvgPool2d", "AdaptiveMaxPool2d", "adaptive_max_pool2d", "MaxUnpool2d", "max_pool2d_with_indices", "max_unpool2d", "TapConv2d", "convert_tap_convs", "tap_conv2d", "tapconv_ok",
     "DilatedGroupConv2d", "convert_dilated_group_convs", "dilated_group_conv2d", "dilated_group_ok",
     "PrunedConv2d", "convert_pruned_convs", "pruned_conv2d", "has_dead_taps",
-    "FusedSGD", "FusedAdam", "FusedAdamW", "conv_ok", "conv_bn_stats", "twin_conv_bn_stats", "conv_bn_act_eval", "conv_bn_act", "conv_forward", "RoutedConv2d", "GroupedConv2d", "convert_routed_convs", "invalidate_weight_shadows",
+    "FusedSGD", "FusedAdam", "FusedAdamW", "conv_ok", "conv_bn_stats", "stem_store_skippable", "twin_conv_bn_stats", "conv_bn_act_eval", "conv_bn_act", "conv_forward", "RoutedConv2d", "GroupedConv2d", "convert_routed_convs", "invalidate_weight_shadows",
     "TransposedConv2d", "conv_transpose2d", "convert_transposed_convs", "deconv_ok", "gate", "gate_reference", "activation", "convert_activations", "channel_shuffle", "convert_pixel_shuffle", "pixel_shuffle", "pixel_unshuffle", "AugmentSpec", "augment_batch", "augment_reference", "draw_params",
     "ConcatSink", "cat_bn_act", "bn_act", "bn_stats_begin", "bias_add", "bn_act_code", "bn_fused_ok", "convert_batchnorm", "FusedBatchNorm2d", "FusedSyncBatchNorm",
 ]

@@ -117,6 +117,9 @@ class _BNActFn(torch.autograd.Function):
             xi, wk, st, pd, dl = stem_io
             y, bits = ops().conv_stem_bn_act(xi, wk, st, pd, dl, ss, act), None
             STEM_RECOMPUTES[0] += 1
+        elif not getattr(x.grad_fn, "y_stored", True):  # (never expected) give x its values first
+            _stem_materialize(x.grad_fn, x)
+            y, bits = ops().bn_apply(x, ss, residual, act, out2), None
         elif mask == MASK_BITS:
             y, bits = ops().bn_apply_bits(x, ss, residual, act, out2)
         else:
@@ -212,12 +215,32 @@ STEM_RECOMPUTES = [0]  # stem BN forward applies run as conv_stem_bn_act (tests)
 STEM_HANDOFFS = [0]  # BN backward dx passes handed to a stem conv's weight gradient (tests)
 
 
+def _stem_materialize(node, x: torch.Tensor) -> None:
+    """Write a stats-only stem launch's conv output into its (allocated, unwritten) tensor ``x``:
+    the fallback for a consumer that needs the stored values after all."""
+    xi, wk, st, pd, dl = node.stem_io
+    with torch.no_grad():
+        x.copy_(ops().conv_stem(xi, wk, st, pd, dl, False)[0])
+    node.y_stored = True
+
+
 def _stem_handoff(ctx, stem, dy, x, y, mi, ss, sums, weight, want_dw):
     """BN backward whose dx pass runs in the producing stem conv's weight gradient: only the
     reduction + finalize here (``bn_bwd_coeffs``), the coefficients handed to the conv node, and a
     zero-stride placeholder returned as dx (no HBM traffic).  On the flagship this is DDRNet-23's
     first BN, at half resolution: the largest tensor of the step (2.1 GB at batch 32)."""
     bsums = local = None
+    stem_io = getattr(stem, "stem_io", None)
+    recompute = stem_io is not None and _STEM_BN_RECOMPUTE and x.dtype == torch.bfloat16
+
+    def reduce_sums():  # [2C] fp64 (sum g', sum g' (x - mean)) of this rank
+        if recompute:  # the conv output recomputed from the image, not read back (conv_stem.hip)
+            xi, wk, st, pd, dl = stem_io
+            slab = ops().conv_stem_bn_sums(xi, wk, st, pd, dl, dy, mi, ss, ctx.act)
+            STEM_RECOMPUTES[0] += 1
+            return ops().bn_slab_sums(slab, -1.0)[: 2 * x.shape[1]]
+        return ops().bn_bwd_sums(dy, x, y, mi, ss, ctx.act, ctx.mask, None)
+
     if ctx.pg is not None:  # SyncBN: the reduction is all-reduced as usual (early if issued)
         early = ctx.early.pop() if ctx.early else None
         if early is not None:
@@ -228,10 +251,12 @@ def _stem_handoff(ctx, stem, dy, x, y, mi, ss, sums, weight, want_dw):
             else:
                 ctx.bn_module._rtseg_no_early = True
         if bsums is None:
-            bsums = ops().bn_bwd_sums(dy, x, y, mi, ss, ctx.act, ctx.mask, None)
+            bsums = reduce_sums()
             if want_dw:
                 local = bsums.clone()
             dist.all_reduce(bsums, group=ctx.pg)
+    elif recompute:
+        bsums = reduce_sums()
     k, dw, db = ops().bn_bwd_coeffs(dy, x, y, bsums, sums, mi, ss, weight, ctx.act, ctx.mask,
                                     ctx.batch_stats, want_dw)
     if local is not None:
@@ -242,6 +267,8 @@ def _stem_handoff(ctx, stem, dy, x, y, mi, ss, sums, weight, want_dw):
     act, mask, batch = ctx.act, ctx.mask, ctx.batch_stats  # (act codes 0 / 1 / 2 = the kernel's)
 
     def full():  # the plain dx (the conv output had another consumer)
+        if not getattr(stem, "y_stored", True):
+            _stem_materialize(stem, x)
         return ops().bn_backward(dy, x, y, bsums, sums, mi, ss, weight, act, mask, False, batch, False,
                                  None, None)[0]
 

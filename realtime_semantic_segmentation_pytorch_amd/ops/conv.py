@@ -515,8 +515,9 @@ def _db_pick(entry, names):
 
 
 # ----------------------------------------------------------------------------- autograd node
-def _conv_fwd(x, weight, conv, stats):
-    """(y, BN statistics slab | None, KRSC bf16 weight, autotune key) of a routed conv."""
+def _conv_fwd(x, weight, conv, stats, store=True):
+    """(y, BN statistics slab | None, KRSC bf16 weight, autotune key) of a routed conv.
+    ``store=False`` (the stem kernel with statistics only): y is allocated, never written."""
     stride, padding, dilation = _geom(conv)
     cout, cin, kh, kw = weight.shape
     key = (tuple(x.shape), cout, kh, kw, tuple(stride), tuple(padding), tuple(dilation))
@@ -536,7 +537,7 @@ def _conv_fwd(x, weight, conv, stats):
     elif impl == "mfma":
         y, part = ops().conv_mfma(x, wk, stride, padding, dilation, stats, None, None, 0)
     elif impl == "stem":
-        y, part = ops().conv_stem(x, wk, stride, padding, dilation, stats)
+        y, part = ops().conv_stem(x, wk, stride, padding, dilation, stats, store or not stats)
     elif impl == "gemm":
         y = gemm_fwd(x, wk, stride[0])
     else:
@@ -574,8 +575,14 @@ class _ConvFn(torch.autograd.Function):
     """y (+ BN statistics slab) = conv(x, w); backward via our dgrad / wgrad or MIOpen."""
 
     @staticmethod
-    def forward(ctx, x, weight, conv, stats):
-        y, part, wk, key = _conv_fwd(x, weight, conv, stats)
+    def forward(ctx, x, weight, conv, stats, store=True):
+        # store=False: a stem whose BN recomputes the conv output wherever it needs it (ops/bn.py):
+        # the statistics launch writes no 2.1 GB y (honoured only on the stem kernel's fused path)
+        stem_fused = (_STEM_BN_FUSE and not x.requires_grad and stem_ok(conv, x)
+                      and conv.out_channels in (16, 32, 64))
+        store = store or not (stem_fused and stats and _impl_is_stem(x, weight, conv, stats))
+        y, part, wk, key = _conv_fwd(x, weight, conv, stats, store)
+        ctx.y_stored = store
         ctx.save_for_backward(x, wk)
         ctx.conv, ctx.key = conv, key
         # identity of the input, so a residual-add node downstream can hand this node the
@@ -592,8 +599,7 @@ class _ConvFn(torch.autograd.Function):
         # a 3-channel stem conv on an input that needs no gradient: a following batch-statistics
         # BN may hand its backward over (ops.bn), and the BN's dx pass runs inside this conv's
         # weight gradient (conv_stem_wgrad_bn) instead of writing dx to HBM
-        ctx.bn_fuse_slot = [] if (_STEM_BN_FUSE and not x.requires_grad and stem_ok(conv, x)
-                                  and conv.out_channels in (16, 32, 64)) else None
+        ctx.bn_fuse_slot = [] if stem_fused else None
         # ... and its forward apply recomputes this conv from the image with the BN epilogue
         # (conv_stem_bn_act) instead of re-reading y
         ctx.stem_io = ((x, wk) + tuple(_geom(conv))) if ctx.bn_fuse_slot is not None else None
@@ -609,12 +615,12 @@ class _ConvFn(torch.autograd.Function):
         ctx.ran = True
         if dy is None:
             if ctx.addend_slot:  # a handed-over gradient is this input's whole gradient now
-                return _plain(ctx.addend_slot.pop()), None, None, None
-            return None, None, None, None
+                return _plain(ctx.addend_slot.pop()), None, None, None, None
+            return None, None, None, None, None
         x, wk = ctx.saved_tensors
         fused = ctx.bn_fuse_slot.pop() if ctx.bn_fuse_slot else None
         if fused is not None:
-            return None, _stem_wgrad_bn(x, ctx.conv, ctx.wdtype, dy, fused), None, None
+            return None, _stem_wgrad_bn(x, ctx.conv, ctx.wdtype, dy, fused, wk, ctx.y_stored), None, None, None
         addend = ctx.addend_slot.pop() if ctx.addend_slot else None
         node, ctx.bn_node = ctx.bn_node, None
         on_dx = None
@@ -625,14 +631,38 @@ class _ConvFn(torch.autograd.Function):
                 syncbn_bwd_early(node, dx)
         dx, dw = _conv_bwd(x, wk, ctx.conv, ctx.key, dy, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
                            ctx.wdtype, addend, on_dx)
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
+def _impl_is_stem(x, weight, conv, stats) -> bool:
+    """Whether the forward of this stem conv runs on the stem kernel (its autotune decision)."""
+    stride, padding, dilation = _geom(conv)
+    cout, cin, kh, kw = weight.shape
+    key = (tuple(x.shape), cout, kh, kw, tuple(stride), tuple(padding), tuple(dilation))
+    return _fwd_impl(x, weight_krsc(conv), conv, key, stats) == "stem"
+
+
+def stem_store_skippable(x: torch.Tensor, conv: nn.Module, bn: nn.Module) -> bool:
+    """A training stem ConvBNAct whose BN (batch statistics, no residual / concat slice, a fused
+    activation) will recompute the stem conv's output from the image in forward and backward
+    (ops/bn.py): its statistics launch need not store the output (``conv_bn_stats(store=False)``)."""
+    from .bn import _STEM_BN_RECOMPUTE
+
+    return (_STEM_NO_STORE and _STEM_BN_RECOMPUTE and _STEM_BN_FUSE and use_hip(x, "conv") and torch.is_grad_enabled()
+            and conv.weight.requires_grad and not x.requires_grad and bn.training and not padded_ok(conv)
+            and stem_ok(conv, x) and conv.out_channels in (16, 32, 64))
+
+
+# RTSEG_STEM_NO_STORE=1: the stem's statistics launch stores no output and the fused weight
+# gradient recomputes the BN input instead of reading it.  Opt-in: on DDRNet-23 b32 the recompute
+# inside the weight gradient cost +0.46 ms against the 0.2 ms the skipped store saves
+# (profiles/r5_stemrc); the forward apply and the backward reduction recompute either way
+_STEM_NO_STORE = os.environ.get("RTSEG_STEM_NO_STORE", "0") == "1"
 # RTSEG_STEM_BN_FUSE=0: the stem's BN backward writes dx as before (A/B, tests)
 _STEM_BN_FUSE = os.environ.get("RTSEG_STEM_BN_FUSE", "1") != "0"
 
 
-def _stem_wgrad_bn(x, conv, wdtype, dy, fused):
+def _stem_wgrad_bn(x, conv, wdtype, dy, fused, wk=None, stored=True):
     """Weight gradient of a stem conv whose output went through a batch-statistics BN that handed
     its backward over (``fused`` = (bn output grad, bn input, kcoef, mean_invstd, scale_shift,
     act, dummy, full)): the BN's dx is formed while the kernel stages it.  ``dy`` -- what autograd
@@ -644,7 +674,9 @@ def _stem_wgrad_bn(x, conv, wdtype, dy, fused):
     w = conv.weight
     cl = w.dim() == 4 and w.is_contiguous(memory_format=torch.channels_last) and not w.is_contiguous()
     if dy is dummy or (dy is not None and dy.dim() == 4 and dy.stride() == (0, 0, 0, 0)):
-        dw = ops().conv_stem_wgrad_bn(x, g, xb, kc, mi, ss, act, 3, 3, stride, padding, dilation, cl)
+        # a stats-only stem launch stored no BN input: the kernel recomputes it from the image
+        rc = wk if (not stored and wk is not None and wk.dtype == torch.bfloat16) else None
+        dw = ops().conv_stem_wgrad_bn(x, g, xb, kc, mi, ss, act, 3, 3, stride, padding, dilation, cl, rc)
     else:
         d = full() + dy.to(g.dtype)
         d = d.contiguous(memory_format=torch.channels_last)
@@ -966,15 +998,15 @@ def _wgrad(x, dy, wk, conv, key, stride, padding, dilation):
 
 
 # ----------------------------------------------------------------------------- public entry points
-def conv_bn_stats(x: torch.Tensor, conv: nn.Conv2d):
+def conv_bn_stats(x: torch.Tensor, conv: nn.Conv2d, store: bool = True):
     """Training forward of a conv followed by batch-statistics BN: (y, slab | None).  The slab
     holds the BN statistics of y when our kernel produced y (else ``ops.bn_act`` computes
-    them).  None -> the caller's stock path."""
+    them).  None -> the caller's stock path.  ``store=False``: see :func:`stem_store_skippable`."""
     if x.dtype != torch.bfloat16:
         x = x.to(torch.bfloat16)
     if x.data_ptr() % 16:
         x = x.clone(memory_format=torch.channels_last)
-    return _apply(x, conv, True)
+    return _apply(x, conv, True, store)
 
 
 def conv_bn_act_eval(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, act_code: int, residual=None):
@@ -1138,15 +1170,15 @@ def padded_ok(conv: nn.Module) -> bool:
             and conv.groups == 1 and os.environ.get("RTSEG_PAD_COUT", "1") != "0")
 
 
-def _apply(x: torch.Tensor, conv: nn.Module, stats: bool):
+def _apply(x: torch.Tensor, conv: nn.Module, stats: bool, store: bool = True):
     """:class:`_ConvFn` on ``conv``'s weight -> (y, statistics slab | None).  A :func:`padded_ok`
     conv runs on its weight zero-padded to the next 64 output channels (all three passes then
     fit the MFMA kernels) and returns the real channels as a dense channels-last tensor."""
     if not padded_ok(conv):
-        return _ConvFn.apply(x, conv.weight, conv, stats)
+        return _ConvFn.apply(x, conv.weight, conv, stats, store)
     cp = -(-conv.out_channels // 64) * 64
     wp = F.pad(conv.weight, (0, 0, 0, 0, 0, 0, 0, cp - conv.out_channels))
-    y, _ = _ConvFn.apply(x, wp, _DenseView(conv, wp), False)
+    y, _ = _ConvFn.apply(x, wp, _DenseView(conv, wp), False, True)
     return y[:, :conv.out_channels].contiguous(memory_format=torch.channels_last), None
 
 
@@ -1160,7 +1192,7 @@ def grouped_as_dense(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
         x = x.to(torch.bfloat16)
         if not x.is_contiguous(memory_format=torch.channels_last) or x.data_ptr() % 16:
             x = x.clone(memory_format=torch.channels_last)
-        y, _ = _ConvFn.apply(x, wd, _DenseView(conv, wd), False)
+        y, _ = _ConvFn.apply(x, wd, _DenseView(conv, wd), False, True)
         return bias_add(y, conv.bias) if conv.bias is not None else y
     return pruned_conv2d(x, wd, conv.bias, conv.stride, conv.padding, conv.dilation, 1)
 

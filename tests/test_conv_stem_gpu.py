@@ -258,14 +258,17 @@ def test_stem_bn_act_epilogue(geom, act):
     _close(y, ref, 1e-2)
 
 
+@pytest.mark.parametrize("no_store", [True, False])
 @pytest.mark.parametrize("act", ["relu", "none"])
-def test_stem_bn_forward_recompute(monkeypatch, act):
+def test_stem_bn_forward_recompute(monkeypatch, act, no_store):
     """A training stem ConvBNAct: the BN's forward apply recomputed from the image
     (conv_stem_bn_act, ops/bn.py) vs the apply over the stored conv output -- outputs, BN running
     statistics and gradients agree to bf16 rounding, and the recompute really ran."""
     from realtime_semantic_segmentation_pytorch_amd.models.modules import ConvBNAct
     from realtime_semantic_segmentation_pytorch_amd.ops import bn as bn_mod
+    from realtime_semantic_segmentation_pytorch_amd.ops import conv as conv_mod
 
+    monkeypatch.setattr(conv_mod, "_STEM_NO_STORE", no_store)  # stats-only launch + wgrad recompute
     torch.manual_seed(0)
     net0 = ops.convert_batchnorm(ConvBNAct(3, 32, 3, 2, act_type=act)).to(DEV).to(memory_format=torch.channels_last)
     x = torch.randn(2, 3, 40, 132, device=DEV).contiguous(memory_format=torch.channels_last)
@@ -279,6 +282,16 @@ def test_stem_bn_forward_recompute(monkeypatch, act):
         before = bn_mod.STEM_RECOMPUTES[0]
         with torch.autocast("cuda", dtype=torch.bfloat16):
             y = net(x)
+        seen, stack, stored = set(), [y.grad_fn], []
+        while stack:  # the stem conv node: its statistics launch stored no output when recomputing
+            fn = stack.pop()
+            if fn is None or id(fn) in seen:
+                continue
+            seen.add(id(fn))
+            if hasattr(fn, "y_stored"):
+                stored.append(fn.y_stored)
+            stack.extend(f for f, _ in fn.next_functions)
+        assert stored == [not (on and no_store)], stored
         (y.float() * gy).sum().backward()
         assert (bn_mod.STEM_RECOMPUTES[0] > before) == on
         bn = [m for m in net.modules() if isinstance(m, torch.nn.BatchNorm2d)][0]
@@ -294,3 +307,32 @@ def test_stem_bn_forward_recompute(monkeypatch, act):
     torch.testing.assert_close(v0, v1)
     for n_, g_ in g1.items():
         assert rel(g0[n_], g_) < 2e-2, n_
+
+
+@pytest.mark.parametrize("geom", [(2, 17, 70, 64, 2), (1, 9, 130, 32, 1), (3, 33, 66, 16, 2)])
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_stem_bn_backward_sums_recompute(geom, act):
+    """conv_stem_bn_sums (the stem BN's backward reduction with the conv output recomputed from the
+    image) vs the same sums over the stored bf16 conv output in fp64: sum g' and sum g' (x - mean),
+    g' = dy masked by act'(x * scale + shift)."""
+    n, h, w, cout, s = geom
+    g = torch.Generator().manual_seed(6)
+    x = _t((n, 3, h, w), g).contiguous(memory_format=torch.channels_last)
+    wt = _t((cout, 3, 3, 3), g, 0.2)
+    wk = wt.permute(0, 2, 3, 1).contiguous()
+    y, _ = torch.ops.rtseg.conv_stem(x, wk, [s, s], [1, 1], [1, 1], False)  # the stored conv output
+    dy = _t(y.shape, g).contiguous(memory_format=torch.channels_last)
+    mean = torch.randn(cout, generator=g) * 0.1
+    mi = torch.cat([mean, torch.rand(cout, generator=g) + 0.5]).to(DEV)
+    ss = torch.cat([torch.rand(cout, generator=g) + 0.5, torch.randn(cout, generator=g) * 0.3]).to(DEV)
+    slab = torch.ops.rtseg.conv_stem_bn_sums(x, wk, [s, s], [1, 1], [1, 1], dy, mi, ss, act)
+    got = slab.double().sum(0)
+    xd, gd = y.double(), dy.double()
+    z = xd * ss[:cout].double().view(1, -1, 1, 1) + ss[cout:].double().view(1, -1, 1, 1)
+    live = torch.ones_like(z, dtype=torch.bool) if act == 0 else (z > 0) if act == 1 else (z > 0) & (z < 6)
+    gm = torch.where(live, gd, torch.zeros_like(gd))
+    ref_s = gm.sum((0, 2, 3))
+    ref_q = (gm * (xd - mi[:cout].double().view(1, -1, 1, 1))).sum((0, 2, 3))
+    scale = gd.abs().sum((0, 2, 3)).max().item()
+    torch.testing.assert_close(got[:cout], ref_s, atol=1e-4 * scale, rtol=1e-4)
+    torch.testing.assert_close(got[cout:], ref_q, atol=1e-4 * scale * xd.abs().max().item(), rtol=1e-4)

@@ -45,6 +45,18 @@ def main():
         "hreg2": lambda: r.conv_hreg(x, wk, [1, 1], [1, 1], [1, 1], a.stats, 2),
         "hreg2_dg": lambda: r.conv_hreg_dgrad(dy, wtr, list(x.shape), [1, 1], [1, 1], [1, 1], None, 2),
     }
+    if a.kind.startswith("stem"):  # the 3-channel stem at DDRNet-23's geometry (cin = 3, stride 2)
+        xs = torch.randn(a.batch, 3, h, w, device="cuda", dtype=torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+        ws = (torch.randn(cout, 3, 3, 3, device="cuda") * 0.2).to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()
+        ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+        dys = torch.randn(a.batch, cout, ho, wo, device="cuda", dtype=torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+        ss = torch.cat([torch.ones(cout), torch.zeros(cout)]).cuda()
+        fns["stem_stats"] = lambda: r.conv_stem(xs, ws, [2, 2], [1, 1], [1, 1], True)
+        fns["stem_nostore"] = lambda: r.conv_stem(xs, ws, [2, 2], [1, 1], [1, 1], True, False)
+        fns["stem_apply"] = lambda: r.conv_stem_bn_act(xs, ws, [2, 2], [1, 1], [1, 1], ss, 1)
+        fns["stem_wgrad"] = lambda: r.conv_stem_wgrad(xs, dys, 3, 3, [2, 2], [1, 1], [1, 1], True)
     fn = fns[a.kind]
     for _ in range(a.iters):
         fn()
