@@ -320,3 +320,24 @@ def test_block_diagonal_grouped_conv_identity(groups, cout, cg, k):
     y.backward(g)
     ref.backward(g)
     torch.testing.assert_close(w.grad, w2.grad)
+
+
+def test_cat_bn_act_cpu_matches_cat_then_bn():
+    """ops.cat_bn_act on the CPU: the concat + BatchNorm (+ ReLU / PReLU module) of the reference
+    formulation, including the running statistics (GPU kernels: tests/test_concat_gpu.py)."""
+    import copy
+
+    from realtime_semantic_segmentation_pytorch_amd import ops
+    from realtime_semantic_segmentation_pytorch_amd.models.modules import Activation
+
+    torch.manual_seed(0)
+    parts = [torch.randn(2, 8, 5, 7), torch.randn(2, 16, 5, 7) + 1.0]
+    for act in ("relu", "prelu"):
+        bn = torch.nn.BatchNorm2d(24).train()
+        actm = Activation(act)
+        b2, a2 = copy.deepcopy(bn), copy.deepcopy(actm)
+        y = ops.cat_bn_act(parts, bn, actm, act_module=actm)
+        ref = a2(b2(torch.cat(parts, dim=1)))
+        torch.testing.assert_close(y, ref)
+        torch.testing.assert_close(bn.running_mean, b2.running_mean)
+        torch.testing.assert_close(bn.running_var, b2.running_var)
