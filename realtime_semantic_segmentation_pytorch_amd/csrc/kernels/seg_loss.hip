@@ -677,6 +677,210 @@ __global__ void __launch_bounds__(256) seg_ce_bwd_run(
   }
 }
 
+// Round-5 form of the run kernel (the default; RTSEG_LOSS_BWD_RUN=1 selects the form above).
+// Same (output row, run) work split and the same LDS row buffer R, three changes:
+//  * per-pixel metadata packed into 6 bytes (lse pre-scaled by log2 e, and a 16-bit word holding
+//    the label and the selection code -- the weight is a function of (code, label), evaluated per
+//    pixel in the run loop): 44 -> 37 KB of LDS per block, 4 blocks per CU instead of 3; the
+//    tile's metadata loads are issued together (unrolled) before any of them is used;
+//  * logits pre-scaled by log2 e and shifted by the run's largest lse, the shift undone in the
+//    per-pixel weight: per pixel and class one FMA, one v_exp_f32 and two FMAs (the round-5
+//    form above: 7 VALU + exp).  A run whose lse spans more than 2^60 falls back to a per-pixel
+//    shift;
+//  * the one-hot term -w [c == y] leaves the class loop: after the row buffer is complete each
+//    thread subtracts its pixels' weights from R[r][j][y] / R[r][j1][y] with LDS float atomics
+//    (no two lanes of one instruction address one cell).
+template <typename T, int TH, int TW, int NC>
+__global__ void __launch_bounds__(256) seg_ce_bwd_run2(
+    const T* __restrict__ x, LossGeo g, int ignore,
+    const float* __restrict__ cw, const float* __restrict__ pix_loss,
+    const float* __restrict__ pix_lse, const double* __restrict__ stats, int mode,
+    const float* __restrict__ grad_out, float* __restrict__ gacc, int64_t asn, int64_t asc,
+    int64_t ash, int64_t asw) {
+  static_assert(NC > 0 && NC < 255, "run form needs the class count at compile time");
+  constexpr float kL2E = 1.4426950408889634f;
+  constexpr int PIT = (TH * TW + 255) / 256;  // metadata items per thread (launch: 256 threads)
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  __shared__ int tx0[TW], tx1[TW], ty0[TH], ty1[TH], jlo[TW + 4], jhi[TW + 4];  // BW <= TW + 2
+  __shared__ float tlx[TW], tly[TH];
+  __shared__ float plse[TH * TW];      // lse * log2 e
+  __shared__ uint16_t pcode[TH * TW];  // label | selection code << 8 (code 0: no gradient)
+  const TileGeo t = tile_geo<TH, TW>(g);
+  const int BW = t.BW, RS = BW | 1;
+  const int nx = t.ox1 - t.ox0 + 1, ny = t.oy1 - t.oy0 + 1;
+  float* L = sm;                          // [BH][BW][CP]
+  float* R = L + t.BH * t.BW * t.CP;      // [TH][RS][NC]: classes innermost
+  for (int k = threadIdx.x; k < TW; k += blockDim.x) {
+    int a0, a1; float l;
+    g.mw.map(min(t.ox0 + k, t.ox1), a0, a1, l);
+    tx0[k] = a0 - t.bx0; tx1[k] = a1 - t.bx0; tlx[k] = l;
+  }
+  for (int k = threadIdx.x; k < TH; k += blockDim.x) {
+    int a0, a1; float l;
+    g.mh.map(min(t.oy0 + k, t.oy1), a0, a1, l);
+    ty0[k] = a0 - t.by0; ty1[k] = a1 - t.by0; tly[k] = l;
+  }
+  const SelRule rule = load_rule(stats, mode);
+  const float go = *grad_out;
+  {
+    float pl[PIT], ls[PIT];
+    int yy[PIT];
+#pragma unroll
+    for (int it = 0; it < PIT; ++it) {  // all loads first
+      const int p = threadIdx.x + it * 256;
+      const int r = p / TW, k = p - (p / TW) * TW;
+      pl[it] = 0.f; ls[it] = 0.f; yy[it] = -1;
+      if (p < TH * TW && r < ny && k < nx) {
+        const int oy = t.oy0 + r, ox = t.ox0 + k;
+        const int64_t pi = (static_cast<int64_t>(t.n) * g.oh + oy) * g.ow + ox;
+        const int64_t y = label_at(g, t.n, oy, ox);
+        yy[it] = (y == ignore || y < 0 || y >= NC) ? -1 : static_cast<int>(y);
+        pl[it] = pix_loss[pi];
+        ls[it] = pix_lse[pi];
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < PIT; ++it) {
+      const int p = threadIdx.x + it * 256;
+      if (p >= TH * TW) break;
+      int code = 0;
+      if (yy[it] >= 0) {
+        if (rule.mode != MODE_OHEM) code = 3;
+        else if (pl[it] > rule.T) code = 1;
+        else if (pl[it] == rule.T) code = 2;
+      }
+      plse[p] = ls[it] * kL2E;
+      pcode[p] = static_cast<uint16_t>(code == 0 ? 0 : (yy[it] | (code << 8)));
+    }
+  }
+  for (int j = threadIdx.x; j < TW + 4; j += blockDim.x) { jlo[j] = nx; jhi[j] = -1; }
+  stage_logits<T, TH, NC>(x, g, t, L, nullptr, false);  // syncs: tables and pixels visible too
+  for (int k = threadIdx.x; k < nx; k += blockDim.x) {
+    const int j = tx0[k];
+    if (k == 0 || tx0[k - 1] != j) jlo[j] = k;
+    if (k == nx - 1 || tx0[k + 1] != j) jhi[j] = k;
+  }
+  __syncthreads();
+  // gradient weight of a pixel from its code word (0 when it carries no gradient)
+  auto weight = [&](int cw16) -> float {
+    const int code = cw16 >> 8;
+    const float w = code == 1 ? rule.a : code == 2 ? rule.b : code == 3 ? rule.a * (cw ? cw[cw16 & 255] : 1.f) : 0.f;
+    return w * go;
+  };
+  const int rj = threadIdx.x;
+  const bool item = rj < TH * BW;
+  const int r = item ? rj / BW : 0, j = item ? rj - (rj / BW) * BW : 0;
+  const bool run = item && r < ny && jlo[j] <= jhi[j];
+  const int k0 = run ? jlo[j] : 0, k1 = run ? jhi[j] : -1;
+  const int j1 = run ? tx1[k0] : j;  // == j: no right column (the clamped last low-res column)
+  float a0[NC], a1[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) { a0[c] = 0.f; a1[c] = 0.f; }
+  if (run) {
+    float m = -INFINITY, mn = INFINITY;
+    for (int k = k0; k <= k1; ++k) {
+      if (pcode[r * TW + k] == 0) continue;
+      const float v = plse[r * TW + k];
+      m = fmaxf(m, v); mn = fminf(mn, v);
+    }
+    if (m != -INFINITY) {
+      const bool wide = m - mn > 60.f;
+      const float sh = wide ? 0.f : m;
+      const float ly = tly[r];
+      const float* q00 = L + (ty0[r] * t.BW + j) * t.CP;
+      const float* q10 = L + (ty1[r] * t.BW + j) * t.CP;
+      const float* q01 = L + (ty0[r] * t.BW + j1) * t.CP;
+      const float* q11 = L + (ty1[r] * t.BW + j1) * t.CP;
+      float u[NC], d[NC];  // log2-scaled left tap (shifted) and right-minus-left
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const float left = q00[c] + ly * (q10[c] - q00[c]);
+        const float right = q01[c] + ly * (q11[c] - q01[c]);
+        u[c] = fmaf(left, kL2E, -sh);
+        d[c] = (right - left) * kL2E;
+      }
+      if (!wide) {
+        for (int k = k0; k <= k1; ++k) {
+          const int cwd = pcode[r * TW + k];
+          if (cwd == 0) continue;
+          const float lx = tlx[k];
+          const float s = weight(cwd) * __builtin_amdgcn_exp2f(m - plse[r * TW + k]);
+          const float wa = s * (1.f - lx), wb = s * lx;
+#pragma unroll
+          for (int c = 0; c < NC; ++c) {
+            const float e = __builtin_amdgcn_exp2f(fmaf(lx, d[c], u[c]));
+            a0[c] = fmaf(wa, e, a0[c]);
+            a1[c] = fmaf(wb, e, a1[c]);
+          }
+        }
+      } else {
+        for (int k = k0; k <= k1; ++k) {
+          const int cwd = pcode[r * TW + k];
+          if (cwd == 0) continue;
+          const float lx = tlx[k];
+          const float s = weight(cwd), ls = plse[r * TW + k];
+          const float wa = s * (1.f - lx), wb = s * lx;
+#pragma unroll
+          for (int c = 0; c < NC; ++c) {
+            const float e = __builtin_amdgcn_exp2f(fmaf(lx, d[c], u[c]) - ls);
+            a0[c] = fmaf(wa, e, a0[c]);
+            a1[c] = fmaf(wb, e, a1[c]);
+          }
+        }
+      }
+    }
+  }
+  if (j1 == j) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) { a0[c] += a1[c]; a1[c] = 0.f; }
+  }
+  if (item) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) R[(r * RS + j) * NC + c] = a0[c];
+  }
+  __syncthreads();
+  if (item && j1 != j) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) R[(r * RS + j1) * NC + c] += a1[c];
+  }
+  __syncthreads();
+  if (run) {  // one-hot terms: lanes of one instruction address distinct (row, column) cells
+    float* ra = R + (r * RS + j) * NC;
+    float* rb = R + (r * RS + j1) * NC;
+    for (int k = k0; k <= k1; ++k) {
+      const int cwd = pcode[r * TW + k];
+      if (cwd == 0) continue;
+      const int y = cwd & 255;
+      const float w = weight(cwd), lx = tlx[k];
+      if (j1 == j) {
+        atomicAdd(ra + y, -w);
+      } else {
+        atomicAdd(ra + y, -w * (1.f - lx));
+        atomicAdd(rb + y, -w * lx);
+      }
+    }
+  }
+  __syncthreads();
+  for (int cj = threadIdx.x; cj < NC * BW; cj += blockDim.x) {
+    const int jj = cj / NC, c = cj - (cj / NC) * NC;
+    float* dst = gacc + t.n * asn + c * asc + t.by0 * ash + (t.bx0 + jj) * asw;
+    int ic = ty0[0];
+    float a = 0.f, b = 0.f;
+    for (int rr = 0; rr < ny; ++rr) {
+      const int i0 = ty0[rr];
+      while (ic < i0) {
+        if (a != 0.f) atomicAdd(dst + static_cast<int64_t>(ic) * ash, a);
+        a = b; b = 0.f; ++ic;
+      }
+      const float v = R[(rr * RS + jj) * NC + c];
+      if (ty1[rr] == i0) a += v;
+      else { const float l = tly[rr]; a += (1.f - l) * v; b += l * v; }
+    }
+    if (a != 0.f) atomicAdd(dst + static_cast<int64_t>(ic) * ash, a);
+    if (b != 0.f && ic + 1 < t.BH) atomicAdd(dst + static_cast<int64_t>(ic + 1) * ash, b);
+  }
+}
+
 // fp32 accumulator (same strides as the gradient tensor) -> gradient dtype
 template <typename G>
 __global__ void __launch_bounds__(256) cast_out_kernel(const float* __restrict__ acc,
@@ -805,6 +1009,20 @@ static void bwd_run(const SegLossArgs& a, const LossGeo& g, const float* grad_ou
 }
 
 template <typename T, int TH, int TW, int NC>
+static void bwd_run2(const SegLossArgs& a, const LossGeo& g, const float* grad_out, hipStream_t st) {
+  const int bh = static_cast<int>((TH - 1) * g.mh.scale) + 3;
+  const int bw = static_cast<int>((TW - 1) * g.mw.scale) + 3;
+  const size_t lds = sizeof(float) * (static_cast<size_t>(bh) * bw * (g.c | 1) +
+                                      static_cast<size_t>(g.c) * TH * (bw | 1));
+  auto k = seg_ce_bwd_run2<T, TH, TW, NC>;
+  allow_lds(k, lds);
+  k<<<tiles_of<TH, TW>(g), 256, lds, st>>>(
+      static_cast<const T*>(a.logits.data), g, a.ignore_index, a.class_weight,
+      a.pix_loss, a.pix_lse, a.stats, a.mode, grad_out, a.acc, a.acc_sn, a.acc_sc, a.acc_sh,
+      a.acc_sw);
+}
+
+template <typename T, int TH, int TW, int NC>
 static void bwd_tile(const SegLossArgs& a, const LossGeo& g, const float* grad_out,
                      hipStream_t st) {
   const int bh = static_cast<int>((TH - 1) * g.mh.scale) + 3;
@@ -837,12 +1055,15 @@ static void bwd_t(const SegLossArgs& a, const LossGeo& g, const float* grad_out,
   // head's backward ran 10x slower per pixel than DDRNet's x8, profiles/r4_zoo_models); 8 x 64
   // tiles fit four blocks per CU
   const bool fine = (g.mh.scale > 0.2f || g.mw.scale > 0.2f) && g.mh.scale <= 1.f && g.mw.scale <= 1.f;
+  const char* rf = std::getenv("RTSEG_LOSS_BWD_RUN");
+  const char run_form = rf != nullptr && rf[0] != 0 ? rf[0] : '2';
   if (g.c == 19) {
     if (fine) bwd_tile<T, 8, 64, 19>(a, g, grad_out, st);
-    else if ((static_cast<int>(127 * g.mw.scale) + 3) * 14 <= 256 &&
-             (std::getenv("RTSEG_LOSS_BWD_RUN") == nullptr || std::getenv("RTSEG_LOSS_BWD_RUN")[0] != '0'))
-      bwd_run<T, 14, 128, 19>(a, g, grad_out, st);  // one (row, run) item per thread; =0: round-4 form
-    else bwd_tile<T, 16, 128, 19>(a, g, grad_out, st);
+    else if ((static_cast<int>(127 * g.mw.scale) + 3) * 14 <= 256 && run_form != '0') {
+      // one (row, run) item per thread; =1: the first run form, =0: round-4 form
+      if (run_form == '1') bwd_run<T, 14, 128, 19>(a, g, grad_out, st);
+      else bwd_run2<T, 14, 128, 19>(a, g, grad_out, st);
+    } else bwd_tile<T, 16, 128, 19>(a, g, grad_out, st);
   } else if (g.c <= 32) {
     if (fine) bwd_tile<T, 8, 64, 0>(a, g, grad_out, st);
     else bwd_tile<T, 16, 128, 0>(a, g, grad_out, st);

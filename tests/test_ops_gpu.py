@@ -163,3 +163,28 @@ def test_loss_no_host_sync():
     finally:
         torch.cuda.set_sync_debug_mode("default")
     assert math.isfinite(float(loss))
+
+
+@pytest.mark.parametrize("form", ["0", "1", "2"])
+@pytest.mark.parametrize("scale", [2.0, 200.0])  # 200: a run's lse spans > 2^60 -> per-pixel shift
+@pytest.mark.parametrize("align", [True, False])
+def test_loss_bwd_run_forms(monkeypatch, form, scale, align):
+    """The x8 upsampled 19-class backward: round-4 tile form (0), first run form (1) and the packed
+    run form with the exp2 shift and LDS one-hot terms (2, default) against the fp32 reference."""
+    _lib_loaded()
+    monkeypatch.setenv("RTSEG_LOSS_BWD_RUN", form)
+    torch.manual_seed(11)
+    logits = (torch.randn(2, 19, 24, 40, device=DEV) * scale).contiguous(memory_format=torch.channels_last)
+    logits.requires_grad_(True)
+    labels = _labels(2, 192, 320, 19, seed=12)
+    for mode in (ops.MODE_OHEM, 1):
+        logits.grad = None
+        loss = ops.seg_cross_entropy(logits, labels.to(torch.uint8), mode=mode, align_corners=align)
+        lr_ = logits.detach().clone().requires_grad_(True)
+        ref = ops.seg_cross_entropy_reference(lr_, labels, mode=mode, align_corners=align)
+        torch.testing.assert_close(loss, ref, atol=1e-4, rtol=1e-4)
+        loss.backward()
+        ref.backward()
+        assert torch.isfinite(logits.grad).all()
+        torch.testing.assert_close(logits.grad, lr_.grad, atol=1e-6 + 1e-3 * lr_.grad.abs().max().item(),
+                                   rtol=1e-3)

@@ -43,7 +43,13 @@ class OpProbe(TorchDispatchMode):
             if big >= self.min_numel:
                 shapes = tuple(tuple(t.shape) for t in ts[:2])
                 dts = tuple(str(t.dtype)[6:] for t in ts[:2] + outs[:1])
-                self.hits[(name, shapes, dts, _site())] += 1
+                site = _site()
+                if site == "?":  # backward engine: name the autograd node that produced the operand
+                    node = torch._C._current_autograd_node()
+                    if node is not None:
+                        nxt = [type(f).__name__ if f is not None else "-" for f, _ in node.next_functions][:3]
+                        site = f"bwd:{node.name()}->{','.join(nxt)}"
+                self.hits[(name, shapes, dts, site)] += 1
         return out
 
     def report(self) -> str:
