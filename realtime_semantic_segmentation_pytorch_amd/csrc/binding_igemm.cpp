@@ -191,7 +191,7 @@ at::Tensor conv_dgrad_impl(const at::Tensor& dy, const at::Tensor& wt, at::IntAr
                            at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
                            const std::optional<at::Tensor>& bias, const std::optional<at::Tensor>& addend, int kind,
                            const std::optional<at::Tensor>& addend_mask,
-                           const std::optional<at::Tensor>& phase_addend) {
+                           const std::optional<at::Tensor>& phase_addend, bool fused_phases = false) {
   const bool halo = kind == 1, wres = kind == 2, hreg = kind == 3 || kind == 4;
   check_act(dy, "grad_output");
   TORCH_CHECK(x_size.size() == 4, "rtseg.conv_igemm_dgrad: x_size must be [N, Cin, H, W]");
@@ -215,6 +215,8 @@ at::Tensor conv_dgrad_impl(const at::Tensor& dy, const at::Tensor& wt, at::IntAr
     TORCH_CHECK(!(bias.has_value() && bias->defined()), "rtseg.conv_hreg_dgrad: no bias");
   } else {
     TORCH_CHECK(conv_igemm_supported(g, 1), "rtseg.conv_igemm_dgrad: needs Cout % 64 == 0, Cin % 8 == 0");
+    TORCH_CHECK(!fused_phases || conv_igemm_dgrad_fused_ok(g),
+                "rtseg.conv_igemm_dgrad: fused phases need a strided conv with H % sh == 0, W % sw == 0");
   }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
   at::Tensor dx = at::empty({g.n, g.cin, g.h, g.w_in}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
@@ -253,7 +255,11 @@ at::Tensor conv_dgrad_impl(const at::Tensor& dy, const at::Tensor& wt, at::IntAr
   else if (hreg) {
     at::Tensor wpack = at::empty({conv_hreg_pack_elems(g, 1)}, wt.options());
     launch_conv_hreg(g, 1, wpack.data_ptr(), cur_stream(), kind == 4 ? 2 : 1);
-  } else launch_conv_igemm_dgrad(g, cur_stream());
+  } else if (fused_phases) {
+    launch_conv_igemm_dgrad_fused(g, cur_stream());
+  } else {
+    launch_conv_igemm_dgrad(g, cur_stream());
+  }
   return dx;
 }
 
@@ -261,8 +267,9 @@ at::Tensor conv_igemm_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntA
                             at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
                             const std::optional<at::Tensor>& bias, const std::optional<at::Tensor>& addend,
                             const std::optional<at::Tensor>& addend_mask,
-                            const std::optional<at::Tensor>& phase_addend) {
-  return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, bias, addend, 0, addend_mask, phase_addend);
+                            const std::optional<at::Tensor>& phase_addend, bool fused_phases) {
+  return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, bias, addend, 0, addend_mask, phase_addend,
+                         fused_phases);
 }
 
 at::Tensor conv_halo_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
@@ -398,7 +405,8 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
   m.def("conv_igemm(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats, "
         "Tensor? scale_shift, Tensor? residual, int act) -> (Tensor, Tensor)");
   m.def("conv_igemm_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
-        "Tensor? bias=None, Tensor? addend=None, Tensor? addend_mask=None, Tensor? phase_addend=None) -> Tensor");
+        "Tensor? bias=None, Tensor? addend=None, Tensor? addend_mask=None, Tensor? phase_addend=None, "
+        "bool fused_phases=False) -> Tensor");
   m.def("conv_halo(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats, "
         "Tensor? scale_shift, Tensor? residual, int act) -> (Tensor, Tensor)");
   m.def("conv_halo_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "

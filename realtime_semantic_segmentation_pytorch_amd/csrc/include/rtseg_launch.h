@@ -196,6 +196,10 @@ void launch_conv_igemm_fwd(const ConvGeom& g, hipStream_t st);
 // g.scale_shift, when set, is a [Cin] bias added to dx (the forward of a transposed conv);
 // g.res, when set, is a bf16 tensor of dx's layout added to dx (a residual branch's gradient);
 void launch_conv_igemm_dgrad(const ConvGeom& g, hipStream_t st);
+// the same data gradient of a strided conv with every output phase in ONE launch (padding taps
+// even out the phases' tap counts); needs H % sh == 0, W % sw == 0 -- conv_igemm_dgrad_fused_ok
+bool conv_igemm_dgrad_fused_ok(const ConvGeom& g);
+void launch_conv_igemm_dgrad_fused(const ConvGeom& g, hipStream_t st);
 // g.x = x [N,H,W,Cin], g.y = dy [N,Ho,Wo,Cout]; ws fp32 of conv_igemm_wgrad_ws_elems(g);
 // dw fp32 [Cout][Cin][KH][KW]
 int64_t conv_igemm_wgrad_ws_elems(const ConvGeom& g);

@@ -55,6 +55,8 @@ namespace {
 using namespace mdev;
 
 constexpr int kMaxTaps = kIgemmMaxTaps;
+constexpr int kMaxPhases = 16;
+constexpr int kNullTap = 0xff;  // tap_wt of a padding tap (fused phases): zero weights, no gather
 
 // 64 zero bytes: the DMA source of padding taps / rows past the edge
 __device__ uint4 g_igemm_zero[4];
@@ -78,6 +80,9 @@ struct IgArgs {
   int sh, sw;             // input pixel = (hv*sh + dh[t], wv*sw + dw[t])
   int wrow;               // weight row stride (elements) = KT * C
   int ntap, cch, nk;      // taps, 64-channel chunks per tap, K-steps per tile
+  int nph;                // output phases per launch (fused dgrad of a strided conv), else 1
+  int wide;               // 16-byte epilogue stores (channel-group pairs swapped across half-waves)
+  int phase_off[kMaxPhases];  // phase q: oph | opw << 8 (nph > 1; taps of phase q at q * ntap)
   int M, mtiles, ntiles;
   FastDiv fwv, fhv;
   uint32_t xbytes;        // bytes of the gathered operand (<= 2^31: buffer range, GB kernels)
@@ -113,7 +118,9 @@ __device__ __forceinline__ void bdma16x2(__amdgpu_buffer_rsrc_t r, uint32_t v0, 
 // store / load the output-layout tensors (y, residual, addend) through range-checked buffer
 // resources too: a pixel past M or a channel past Cout gets an out-of-range offset (the store is
 // dropped, the load returns 0) instead of an exec-mask branch around every 8-byte access.
-template <int BM, int BN, int WM, int WN, int NST, int EPI, int STATS, int GB>
+// PH: fused output phases (launch_conv_igemm_dgrad_fused; a.nph > 1), a separate instantiation so
+// that the phase bookkeeping costs the other launches no registers
+template <int BM, int BN, int WM, int WN, int NST, int EPI, int STATS, int GB, int PH = 0>
 __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs a) {
   constexpr int NW = WM * WN;
   constexpr int TI = BN / WN / 32;  // 32-channel MFMA tiles per wave
@@ -164,7 +171,14 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
   uint32_t roff[GB ? PI : 1];
   const uint16_t* pbase[GB ? 1 : PI];
   int phb[PI], pwb[PI];
-  auto set_rows = [&](int mt) {
+  // fused phases: tile t = spatial tile t / nph of phase t % nph (the phases of one spatial tile
+  // are neighbouring tiles of the walk: adjacent blocks of one XCD share its dy rows in L2 and
+  // fill complementary pixels of the same dx lines)
+  const int P = PH ? a.nph : 1;
+  int st_phase = 0;
+  auto set_rows = [&](int tile) {
+    int mt = tile;
+    if (PH) { mt = tile / P; st_phase = tile - mt * P; }
 #pragma unroll
     for (int e = 0; e < PI; ++e) {
       const int m = mt * BM + (wid * PI + e) * 8 + lr8;
@@ -187,14 +201,16 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
   auto stage = [&]() {
     // uniform indices -> scalar (SMEM) tap-table loads: a VGPR-indexed kernarg load is a VMEM
     // load whose s_waitcnt vmcnt(0) would drain the whole DMA ring every K-step
-    const int tv = a.taps[__builtin_amdgcn_readfirstlane(st_t)];
+    const int tv = a.taps[__builtin_amdgcn_readfirstlane(st_phase * a.ntap + st_t)];
+    const bool null_tap = PH && tap_wt(tv) == kNullTap;  // uniform
     const int dh = tap_dh(tv), dw = tap_dw(tv);
     const int c0 = __builtin_amdgcn_readfirstlane(st_c) * 64;
     const int woff = tap_wt(tv) * a.C + c0;
     const uint32_t base = lds_addr(lds + st_buf * STAGE);
 #pragma unroll
     for (int e = 0; e < WI; ++e) {
-      const void* src = wok[e] ? static_cast<const void*>(wsrc[e] + woff) : static_cast<const void*>(g_igemm_zero);
+      const void* src = wok[e] && !null_tap ? static_cast<const void*>(wsrc[e] + woff)
+                                            : static_cast<const void*>(g_igemm_zero);
       dma16(src, base + (wid * WI + e) * 1024);
     }
     if constexpr (GB) {
@@ -206,7 +222,7 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
         uint32_t v[2];
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-          const bool ok = static_cast<unsigned>(phb[e + q] + dh) < static_cast<unsigned>(a.H) &&
+          const bool ok = !null_tap && static_cast<unsigned>(phb[e + q] + dh) < static_cast<unsigned>(a.H) &&
                           static_cast<unsigned>(pwb[e + q] + dw) < static_cast<unsigned>(a.W);
           v[q] = ok ? roff[e + q] + delta : 0x80000000u;
         }
@@ -217,7 +233,7 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
 #pragma unroll
       for (int e = 0; e < PI; ++e) {
         const int hi = phb[e] + dh, wi = pwb[e] + dw;
-        const bool ok = static_cast<unsigned>(hi) < static_cast<unsigned>(a.H) &&
+        const bool ok = !null_tap && static_cast<unsigned>(hi) < static_cast<unsigned>(a.H) &&
                         static_cast<unsigned>(wi) < static_cast<unsigned>(a.W);
         const uint16_t* src = pbase[e] + static_cast<int64_t>(hi * a.W + wi) * a.C + c0;
         dma16(ok ? static_cast<const void*>(src) : static_cast<const void*>(g_igemm_zero),
@@ -266,7 +282,16 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
 #pragma unroll
   for (int k = 0; k < NPS; ++k) pst[k] = 0.f;
 
-  auto pack_tile = [&](int mt) __attribute__((always_inline)) {
+  auto pack_tile = [&](int tile) __attribute__((always_inline)) {
+    int mt = tile, oph = a.oph, opw = a.opw;
+    bool phase0 = true;
+    if (PH) {
+      mt = tile / P;
+      const int q = tile - mt * P;
+      oph = a.phase_off[q] & 0xff;
+      opw = a.phase_off[q] >> 8;
+      phase0 = q == 0;
+    }
     {
       // BN statistics of this tile: per-lane partial sums over the lane's TJ pixels
       float ts[STATS ? TI : 1][16], tq[STATS ? TI : 1][16];
@@ -283,7 +308,7 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
         uint32_t wv, hv;
         const uint32_t t = a.fwv.divmod(static_cast<uint32_t>(ok ? m : 0), wv);
         const uint32_t n = a.fhv.divmod(t, hv);
-        const int ho = static_cast<int>(hv) * a.osh + a.oph, wo = static_cast<int>(wv) * a.osw + a.opw;
+        const int ho = static_cast<int>(hv) * a.osh + oph, wo = static_cast<int>(wv) * a.osw + opw;
         if constexpr (GB) {
           poff[tj] = ok ? ((n * static_cast<uint32_t>(a.Ho) + ho) * static_cast<uint32_t>(a.Wo) + wo) *
                               static_cast<uint32_t>(a.cout) * 2u
@@ -293,8 +318,15 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
         }
         #pragma unroll
         for (int ti = 0; ti < TI; ++ti) {
+          // channel groups in pairs (g2, g2 + 1): lane l < 32 holds channels 8g + 0..3 of pixel l,
+          // lane l + 32 channels 8g + 4..7 of the same pixel; one v_permlane32_swap per dword
+          // gives lanes < 32 channels 8 g2 .. 8 g2 + 7 and lanes >= 32 the next 8 -> one 16-byte
+          // store per pair instead of two 8-byte ones (WIDE: RTSEG_IGEMM_WIDE_STORE=0 off, A/B)
           #pragma unroll
-          for (int g = 0; g < 4; ++g) {
+          for (int g2 = 0; g2 < 4; g2 += 2) {
+          uint2 pkp[2];
+          #pragma unroll
+          for (int g = g2; g < g2 + 2; ++g) {
             const int co = co_lane + ti * 32 + 8 * g;
             float v[4];
             #pragma unroll
@@ -322,7 +354,7 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
                 #pragma unroll
                 for (int q = 0; q < 4; ++q) v[q] += sv[q];
               }
-              if (a.vaddend != nullptr && ok && co < a.cout) {  // e.g. a strided 1 x 1 shortcut's dx
+              if (a.vaddend != nullptr && phase0 && ok && co < a.cout) {  // e.g. a strided 1 x 1 shortcut's dx
                 float pv[4];
                 bf16x4_unpack(*reinterpret_cast<const uint2*>(a.vaddend + static_cast<int64_t>(m) * a.cout + co), pv);
                 #pragma unroll
@@ -345,11 +377,14 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
             uint2 pk;
             pk.x = pack2(v[0], v[1]);
             pk.y = pack2(v[2], v[3]);
-            if constexpr (GB) {
-              typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
-              __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pk.x, pk.y}, yr, voff, 0, 0);
-            } else if (ok && co < a.cout) {
-              *reinterpret_cast<uint2*>(a.y + pend_off[tj] + co) = pk;
+            pkp[g - g2] = pk;
+            if (!a.wide) {
+              if constexpr (GB) {
+                typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+                __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pk.x, pk.y}, yr, voff, 0, 0);
+              } else if (ok && co < a.cout) {
+                *reinterpret_cast<uint2*>(a.y + pend_off[tj] + co) = pk;
+              }
             }
             if constexpr (STATS) {
               // statistics of the fp32 conv outputs, straight from the accumulators: STATS == 1
@@ -362,6 +397,24 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
                 tq[ti][4 * g + q] = fmaf(v[q], v[q], tq[ti][4 * g + q]);
               }
             }
+          }
+          if (a.wide) {
+            {
+              const auto rx = __builtin_amdgcn_permlane32_swap(pkp[0].x, pkp[1].x, false, false);
+              const auto ry = __builtin_amdgcn_permlane32_swap(pkp[0].y, pkp[1].y, false, false);
+              pkp[0].x = rx[0]; pkp[1].x = rx[1];
+              pkp[0].y = ry[0]; pkp[1].y = ry[1];
+            }
+            const int co = co_lane + ti * 32 + 8 * g2 + 4 * fhi;  // lanes >= 32: the next group
+            if constexpr (GB) {
+              typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+              const uint32_t voff = co < a.cout ? poff[tj] + static_cast<uint32_t>(co) * 2u : 0x80000000u;
+              __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{pkp[0].x, pkp[0].y, pkp[1].x, pkp[1].y}, yr, voff, 0, 0);
+            } else {
+              if (ok && co < a.cout)
+                *reinterpret_cast<uint4*>(a.y + pend_off[tj] + co) = make_uint4(pkp[0].x, pkp[0].y, pkp[1].x, pkp[1].y);
+            }
+          }
           }
           #pragma unroll
           for (int r = 0; r < 16; ++r) acc[ti][tj][r] = 0.f;
@@ -726,26 +779,29 @@ int persistent_grid(int mtiles, int ntiles) {
 }
 
 void fill_common(IgArgs& k, const Cfg& c, int n) {
+  if (k.nph < 1) k.nph = 1;
+  const char* we = std::getenv("RTSEG_IGEMM_WIDE_STORE");  // read per launch (A/B in one process)
+  k.wide = (we != nullptr && we[0] == '0') ? 0 : 1;
   k.M = n * k.Hv * k.Wv;
-  k.mtiles = (k.M + c.bm - 1) / c.bm;
+  k.mtiles = (k.M + c.bm - 1) / c.bm * k.nph;  // nph > 1: every phase walks the same pixel tiles
   k.ntiles = (k.cout + c.bn - 1) / c.bn;
   k.nk = k.ntap * k.cch;
   k.fwv = FastDiv::make(static_cast<uint32_t>(k.Wv));
   k.fhv = FastDiv::make(static_cast<uint32_t>(k.Hv));
 }
 
-template <int EPI, int STATS, int GB>
+template <int EPI, int STATS, int GB, int PH = 0>
 void launch_cfg(const IgArgs& k, const Cfg& c, int grid, hipStream_t st) {
   switch (c.id) {
-    case 0: igemm_gather_kernel<256, 64, 4, 2, 3, EPI, STATS, GB><<<grid, 512, 0, st>>>(k); break;
-    case 2: igemm_gather_kernel<512, 64, 8, 1, 2, EPI, STATS, GB><<<grid, 512, 0, st>>>(k); break;
+    case 0: igemm_gather_kernel<256, 64, 4, 2, 3, EPI, STATS, GB, PH><<<grid, 512, 0, st>>>(k); break;
+    case 2: igemm_gather_kernel<512, 64, 8, 1, 2, EPI, STATS, GB, PH><<<grid, 512, 0, st>>>(k); break;
     case 3:
-      if constexpr (EPI == 0) igemm_gather_kernel<256, 256, 2, 4, 2, 0, STATS, GB><<<grid, 512, 0, st>>>(k);
+      if constexpr (EPI == 0) igemm_gather_kernel<256, 256, 2, 4, 2, 0, STATS, GB, PH><<<grid, 512, 0, st>>>(k);
       break;
     case 4:
-      if constexpr (EPI == 0) igemm_gather_kernel<512, 128, 4, 2, 2, 0, STATS, GB><<<grid, 512, 0, st>>>(k);
+      if constexpr (EPI == 0) igemm_gather_kernel<512, 128, 4, 2, 2, 0, STATS, GB, PH><<<grid, 512, 0, st>>>(k);
       break;
-    default: igemm_gather_kernel<256, 128, 4, 2, 3, EPI, STATS, GB><<<grid, 512, 0, st>>>(k); break;
+    default: igemm_gather_kernel<256, 128, 4, 2, 3, EPI, STATS, GB, PH><<<grid, 512, 0, st>>>(k); break;
   }
 }
 
@@ -776,6 +832,11 @@ __global__ void slab_compact_kernel(const float* __restrict__ in, int rows, int 
 void launch_gather(const IgArgs& k, const Cfg& c, hipStream_t st) {
   const int grid = persistent_grid(k.mtiles, k.ntiles);
   if (grid <= 0) return;
+  if (k.nph > 1) {  // fused dgrad phases: data-gradient epilogue only
+    if (use_buffer_gather(k)) launch_cfg<0, 0, 1, 1>(k, c, grid, st);
+    else launch_cfg<0, 0, 0, 1>(k, c, grid, st);
+    return;
+  }
   if (k.ss != nullptr) launch_cfg<1, 0>(k, c, grid, st);
   else if (k.part != nullptr) launch_cfg<0, 1>(k, c, grid, st);
   else launch_cfg<0, 0>(k, c, grid, st);
@@ -882,6 +943,77 @@ void launch_conv_igemm_dgrad(const ConvGeom& g, hipStream_t st) {
       fill_common(k, c, g.n);
       launch_gather(k, c, st);
     }
+}
+
+// Fused phases: the sh x sw output phases of a strided conv's data gradient in ONE launch.  The
+// per-phase launches above each re-read all of dy for a quarter (stride 2) of dx and write dx in
+// 1-pixel-wide strips; here tile t is spatial tile t / nph of phase t % nph, so the phases of one
+// spatial tile run on neighbouring blocks of one XCD: dy is read from HBM about once and each dx
+// line is completed in L2 before it is written back.  Phases have 1..4 taps (3 x 3, stride 2):
+// shorter ones are padded with null taps (zero weights, no gather) to one K length, which costs
+// MFMA work -- the autotuner weighs it against the per-phase form per shape.
+bool conv_igemm_dgrad_fused_ok(const ConvGeom& g) {
+  if (g.sh * g.sw <= 1 || g.sh * g.sw > kMaxPhases) return false;
+  if (g.h % g.sh != 0 || g.w_in % g.sw != 0) return false;
+  if (!conv_igemm_supported(g, 1)) return false;
+  int maxt = 0;
+  for (int a = 0; a < g.sh; ++a)
+    for (int b = 0; b < g.sw; ++b) {
+      int n = 0;
+      for (int i = 0; i < g.kh; ++i)
+        for (int j = 0; j < g.kw; ++j)
+          n += (((a + g.ph - i * g.dh) % g.sh + g.sh) % g.sh == 0) && (((b + g.pw - j * g.dw) % g.sw + g.sw) % g.sw == 0);
+      maxt = std::max(maxt, n);
+    }
+  return maxt >= 1 && maxt * g.sh * g.sw <= kMaxTaps;
+}
+
+void launch_conv_igemm_dgrad_fused(const ConvGeom& g, hipStream_t st) {
+  if (!conv_igemm_dgrad_fused_ok(g)) return;
+  const Cfg c = dgrad_cfg(g);
+  IgArgs k{};
+  k.x = static_cast<const uint16_t*>(g.x);
+  k.w = static_cast<const uint16_t*>(g.w);
+  k.y = static_cast<uint16_t*>(g.y);
+  k.bias = g.scale_shift;
+  k.addend = static_cast<const uint16_t*>(g.res);
+  k.amask = g.amask;
+  k.vaddend = static_cast<const uint16_t*>(g.res_phase0);  // phase 0 is (0, 0)
+  k.H = g.ho; k.W = g.wo; k.C = g.cout;
+  k.Hv = g.h / g.sh;
+  k.Wv = g.w_in / g.sw;
+  k.Ho = g.h; k.Wo = g.w_in; k.cout = g.cin;
+  k.osh = g.sh; k.osw = g.sw; k.oph = 0; k.opw = 0; k.sh = 1; k.sw = 1;
+  k.wrow = g.kh * g.kw * g.cout;
+  k.cch = g.cout / 64;
+  const int64_t xb = static_cast<int64_t>(g.n) * g.ho * g.wo * g.cout * 2;
+  k.xbytes = xb <= (int64_t{1} << 31) ? static_cast<uint32_t>(xb) : 0u;
+  const int64_t yb = static_cast<int64_t>(g.n) * g.h * g.w_in * g.cin * 2;
+  k.ybytes = yb <= (int64_t{1} << 31) ? static_cast<uint32_t>(yb) : 0u;
+  int cnt[kMaxPhases] = {};
+  int tp[kMaxPhases][kMaxTaps];
+  int maxt = 0;
+  k.nph = g.sh * g.sw;
+  for (int a = 0; a < g.sh; ++a)
+    for (int b = 0; b < g.sw; ++b) {
+      const int q = a * g.sw + b;
+      k.phase_off[q] = a | (b << 8);
+      for (int i = 0; i < g.kh; ++i) {
+        const int vh = a + g.ph - i * g.dh;
+        if (((vh % g.sh) + g.sh) % g.sh != 0) continue;
+        for (int j = 0; j < g.kw; ++j) {
+          const int vw = b + g.pw - j * g.dw;
+          if (((vw % g.sw) + g.sw) % g.sw != 0) continue;
+          tp[q][cnt[q]++] = pack_tap(vh / g.sh, vw / g.sw, i * g.kw + j, i, j);
+        }
+      }
+      maxt = std::max(maxt, cnt[q]);
+    }
+  k.ntap = maxt;
+  for (int q = 0; q < k.nph; ++q)
+    for (int t = 0; t < maxt; ++t) k.taps[q * maxt + t] = t < cnt[q] ? tp[q][t] : pack_tap(0, 0, kNullTap);
+  fill_common(k, c, g.n);
+  launch_gather(k, c, st);
 }
 
 namespace {

@@ -875,11 +875,11 @@ def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None, phase_a
             plain.append(MaskedAddend(addend, amask).materialize())
         return plain[0]
 
-    def ours():
+    def ours(fused=False):
         if not wt:  # [Cin, KH, KW, Cout] bf16, the dgrad B operand
             wt.append(weight_crsk(conv, wk))
         return ops().conv_igemm_dgrad(dy, wt[0], list(x.shape), stride, padding, dilation, None, addend, amask,
-                                      phase_addend)
+                                      phase_addend, fused)
 
     def halo():
         if not wt:
@@ -903,6 +903,9 @@ def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None, phase_a
                                      amask)
 
     cands = [("igemm", ours)] if cout % 64 == 0 and cin % 8 == 0 else []
+    if cands and os.environ.get("RTSEG_CONV_DGRAD_PH", "1") != "0" and \
+            _fused_phases_ok(x, conv, stride, padding, dilation):  # =0: per-phase launches only (A/B)
+        cands.append(("igemm_ph", lambda: ours(True)))
     if halo_ok(conv, cout, cin):
         cands.append(("halo", halo))
     if wres_ok(conv, cout, cin, _npix(x)):
@@ -916,9 +919,25 @@ def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None, phase_a
     # a pass with an addend is its own autotune key: our kernels fuse the add, MIOpen pays for it
     name, fn = cands[_choose(("dgrad",) + key + (("+addend",) if addend is not None else ()), _order(cands))]
     dx = fn()
-    if phase_addend is not None and name != "igemm":
+    if phase_addend is not None and name not in ("igemm", "igemm_ph"):
         dx[:, :, ::stride[0], ::stride[1]] += phase_addend
     return dx
+
+
+def _fused_phases_ok(x, conv, stride, padding, dilation) -> bool:
+    """Whether the igemm data gradient can run every output phase of this strided conv in one
+    launch (csrc conv_igemm_dgrad_fused_ok): H, W divisible by the stride, <= 16 phases, and the
+    phases' tap tables, padded to the longest, within the kernel's 49 entries."""
+    sh, sw = stride
+    if sh * sw <= 1 or sh * sw > 16 or x.shape[2] % sh or x.shape[3] % sw:
+        return False
+    kh, kw = conv.kernel_size
+    ph, pw = padding
+    dh, dw = dilation
+    maxt = max(sum(1 for i in range(kh) for j in range(kw)
+                   if (a + ph - i * dh) % sh == 0 and (b + pw - j * dw) % sw == 0)
+               for a in range(sh) for b in range(sw))
+    return 1 <= maxt and maxt * sh * sw <= 49
 
 
 def find_conv_consumer(t: torch.Tensor, r: torch.Tensor, max_nodes: int = 64):

@@ -276,3 +276,45 @@ def test_skip_grad_handoff_bilateral_fusion(monkeypatch):
         _close(res[True][k], res[False][k], 1e-2)
     for n, g in res[False][3].items():
         _close(res[True][3][n], g, 1e-2)
+
+
+@pytest.mark.parametrize("case", [
+    (2, 64, 16, 24, 64, 3, 2, 1),     # 3 x 3 / 2: phases of 1, 2, 2, 4 taps (null-tap padding)
+    (2, 128, 32, 16, 128, 3, 2, 1),
+    (2, 64, 24, 32, 128, 3, 4, 1),    # 3 x 3 / 4 (DDRNet's x4 fusion): 16 phases, 7 of them empty
+    (2, 64, 16, 16, 128, 1, 2, 0),    # 1 x 1 / 2 shortcut: 1 phase with a tap, 3 all-null
+    (3, 32, 40, 48, 64, 3, 2, 1),     # Cin 32 (16-byte rows), tiles past M
+])
+@pytest.mark.parametrize("extras", ["none", "addend", "phase_addend"])
+def test_igemm_dgrad_fused_phases(case, extras):
+    """Data gradient of a strided conv with every output phase in one launch (fused_phases=True)
+    against the fp32 reference and against the per-phase launches (same accumulation order per
+    output pixel: bitwise equal)."""
+    n, cin, h, w, cout, k, s, p = case
+    x, wt = _case(n, cin, h, w, cout, k, s, 1, seed=21)
+    ho, wo = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+    cl = dict(memory_format=torch.channels_last)
+    g = torch.Generator(device="cpu").manual_seed(22)
+    dy = torch.randn(n, cout, ho, wo, generator=g).to(DEV, torch.bfloat16).contiguous(**cl)
+    add = torch.randn(x.shape, generator=g).to(DEV, torch.bfloat16).contiguous(**cl) if extras == "addend" else None
+    ph = (torch.randn(n, cin, h // s, w // s, generator=g).to(DEV, torch.bfloat16).contiguous(**cl)
+          if extras == "phase_addend" else None)
+    wtr = wt.permute(1, 2, 3, 0).contiguous()
+    args = (dy, wtr, list(x.shape), [s, s], [p, p], [1, 1], None, add, None, ph)
+    fused = torch.ops.rtseg.conv_igemm_dgrad(*args, True)
+    split = torch.ops.rtseg.conv_igemm_dgrad(*args, False)
+    ref = torch.nn.grad.conv2d_input(x.shape, wt.float(), dy.float(), s, p, 1)
+    if add is not None:
+        ref = ref + add.float()
+    if ph is not None:
+        ref[:, :, ::s, ::s] += ph.float()
+    _close(fused, ref, 2e-2)
+    assert torch.equal(fused, split)
+
+
+def test_igemm_dgrad_fused_phases_rejects():
+    x, wt = _case(1, 64, 15, 16, 64, 3, 2, 1)  # H % 2 != 0
+    dy = torch.randn(1, 64, 8, 8, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    with pytest.raises(RuntimeError, match="fused phases"):
+        torch.ops.rtseg.conv_igemm_dgrad(dy, wt.permute(1, 2, 3, 0).contiguous(), list(x.shape), [2, 2], [1, 1],
+                                         [1, 1], None, None, None, None, True)

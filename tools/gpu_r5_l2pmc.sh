@@ -17,3 +17,6 @@ done
 python3 $R/tools/pmc_summary.py $OUT/*_p1 --filter rtseg > $OUT/summary.txt || exit 1
 rm -rf $OUT/*_p1
 cat $OUT/summary.txt
+cd $R
+RTSEG_PROBE_OPS=$OUT/step_ops.txt timeout -k 10 400 python -u bench.py --steps 2 --warmup 2 > $OUT/probe_bench.log 2>&1 || { tail -n 20 $OUT/probe_bench.log; exit 1; }
+cat $OUT/step_ops.txt
