@@ -57,6 +57,18 @@ __device__ __forceinline__ int tap_ci(int v) { return static_cast<int>(static_ca
 
 __device__ __forceinline__ bf16x8_t as_frag(uint4 v) { return __builtin_bit_cast(bf16x8_t, v); }
 
+// 16-byte epilogue stores from 32 x 32 MFMA accumulators whose rows are channels (T21 of the
+// CDNA guide): lane l < 32 holds channels 8g + 0..3 of pixel l, lane l + 32 channels 8g + 4..7 of
+// the same pixel.  For the channel-group pair (g, g + 1) -- pk0 / pk1 this lane's packed bf16 x 4
+// of groups g / g + 1 -- one v_permlane32_swap per dword leaves lanes < 32 holding channels
+// 8g .. 8g + 7 and lanes >= 32 channels 8g + 8 .. 8g + 15: one 16-byte store per lane at channel
+// 8g + 8 * (lane >= 32) (= the lane's group-g channel + 4 * (lane >= 32)) instead of two 8-byte ones.
+__device__ __forceinline__ uint4 pair_swap16(uint2 pk0, uint2 pk1) {
+  const auto rx = __builtin_amdgcn_permlane32_swap(pk0.x, pk1.x, false, false);
+  const auto ry = __builtin_amdgcn_permlane32_swap(pk0.y, pk1.y, false, false);
+  return make_uint4(rx[0], ry[0], rx[1], ry[1]);
+}
+
 __device__ __forceinline__ float epi_act(float v, int act) {
   if (act == kActReLU) return fmaxf(v, 0.f);
   if (act == kActReLU6) return fminf(fmaxf(v, 0.f), 6.f);

@@ -240,6 +240,7 @@ __global__ void __launch_bounds__(WM* WN * 64) halo_conv_kernel(const HaloArgs a
       pend_off[tj] = ((static_cast<int64_t>(n) * a.Ho + (ok ? oy : 0)) * a.Wo + (ok ? ox : 0)) * a.cout;
 #pragma unroll
       for (int ti = 0; ti < TI; ++ti) {
+        uint2 pkp[2];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int co = co_lane + ti * 32 + 8 * g;
@@ -274,7 +275,12 @@ __global__ void __launch_bounds__(WM* WN * 64) halo_conv_kernel(const HaloArgs a
           uint2 pk;
           pk.x = pack2(v[0], v[1]);
           pk.y = pack2(v[2], v[3]);
-          if (sok && !(a.dbg & 1)) *reinterpret_cast<uint2*>(a.y + pend_off[tj] + co) = pk;
+          pkp[g & 1] = pk;
+          if (g & 1) {  // 16-byte store of the group pair (g - 1, g): pair_swap16
+            const uint4 w = pair_swap16(pkp[0], pkp[1]);
+            const int c16 = co - 8 + 4 * fhi;
+            if (ok && c16 < a.cout && !(a.dbg & 1)) *reinterpret_cast<uint4*>(a.y + pend_off[tj] + c16) = w;
+          }
           if constexpr (STATS) {  // statistics of the fp32 outputs (the accumulators)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {

@@ -167,6 +167,7 @@ __global__ void __launch_bounds__(2 * kTH / RPW * 64) hreg_conv_kernel(const HrA
       const int64_t off = ((static_cast<int64_t>(n) * a.Ho + (ok ? oy : 0)) * a.Wo + (ok ? ox : 0)) * a.cout;
 #pragma unroll
       for (int ti = 0; ti < 2; ++ti) {
+        uint2 pkp[2];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int co = co_lane + ti * 32 + 8 * g;
@@ -183,7 +184,11 @@ __global__ void __launch_bounds__(2 * kTH / RPW * 64) hreg_conv_kernel(const HrA
           uint2 pk;
           pk.x = pack2(v[0], v[1]);
           pk.y = pack2(v[2], v[3]);
-          if (ok) *reinterpret_cast<uint2*>(a.y + off + co) = pk;
+          pkp[g & 1] = pk;
+          if (g & 1) {  // 16-byte store of the group pair (g - 1, g): pair_swap16
+            const uint4 w = pair_swap16(pkp[0], pkp[1]);
+            if (ok) *reinterpret_cast<uint4*>(a.y + off + co - 8 + 4 * fhi) = w;
+          }
           if constexpr (STATS) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {

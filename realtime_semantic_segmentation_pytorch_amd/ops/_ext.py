@@ -35,6 +35,9 @@ def load(build_if_missing: bool = True) -> bool:
             return True
         try:
             path = _build.LIB_PATH
+            override = os.environ.get("RTSEG_LIB_PATH")  # a prebuilt library (A/B of two builds)
+            if override:
+                path, build_if_missing = override, False
             if build_if_missing:
                 try:
                     path = _build.build()
