@@ -63,6 +63,16 @@ __device__ __forceinline__ bf16x8_t as_frag(uint4 v) { return __builtin_bit_cast
 // of groups g / g + 1 -- one v_permlane32_swap per dword leaves lanes < 32 holding channels
 // 8g .. 8g + 7 and lanes >= 32 channels 8g + 8 .. 8g + 15: one 16-byte store per lane at channel
 // 8g + 8 * (lane >= 32) (= the lane's group-g channel + 4 * (lane >= 32)) instead of two 8-byte ones.
+// The inverse for loads: a 16-byte load at the same per-lane channel (8g + 8 * (lane >= 32)),
+// swapped back, gives this lane's words of groups g and g + 1 (lo[0] / lo[1]) -- one 16-byte load
+// instead of two 8-byte ones.  Every lane must execute it (a cross-lane exchange).
+__device__ __forceinline__ void pair_unswap16(uint4 raw, uint2& g0, uint2& g1) {
+  const auto rx = __builtin_amdgcn_permlane32_swap(raw.x, raw.z, false, false);
+  const auto ry = __builtin_amdgcn_permlane32_swap(raw.y, raw.w, false, false);
+  g0 = make_uint2(rx[0], ry[0]);
+  g1 = make_uint2(rx[1], ry[1]);
+}
+
 __device__ __forceinline__ uint4 pair_swap16(uint2 pk0, uint2 pk1) {
   const auto rx = __builtin_amdgcn_permlane32_swap(pk0.x, pk1.x, false, false);
   const auto ry = __builtin_amdgcn_permlane32_swap(pk0.y, pk1.y, false, false);

@@ -173,17 +173,26 @@ __global__ void __launch_bounds__(NW * 64) wres_conv_kernel(const WresArgs a) {
       const int64_t off = ((static_cast<int64_t>(n) * a.Ho + (ok ? oy : 0)) * a.Wo + (ok ? ox : 0)) * a.cout;
 #pragma unroll
       for (int ti = 0; ti < 2; ++ti) {
-        uint2 pkp[2];
+        uint2 pkp[2], adp[2];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int co = co_lane + ti * 32 + 8 * g;
+          if ((g & 1) == 0 && FLIP == 1 && a.addend != nullptr && a.amask == nullptr) {  // uniform: 16-byte addend load
+            uint4 raw = make_uint4(0u, 0u, 0u, 0u);
+            if (ok) raw = *reinterpret_cast<const uint4*>(a.addend + off + co + 4 * fhi);
+            pair_unswap16(raw, adp[0], adp[1]);
+          }
           float v[4];
 #pragma unroll
           for (int q = 0; q < 4; ++q) v[q] = acc[ti][tj][4 * g + q];
-          if (a.addend != nullptr && ok) {
+          if (FLIP == 1 && a.addend != nullptr && ok) {
             float r[4];
-            bf16x4_unpack(*reinterpret_cast<const uint2*>(a.addend + off + co), r);
-            if (a.amask != nullptr) mask_addend4(a.amask, off + co, r);
+            if (a.amask == nullptr) {
+              bf16x4_unpack(adp[g & 1], r);
+            } else {
+              bf16x4_unpack(*reinterpret_cast<const uint2*>(a.addend + off + co), r);
+              mask_addend4(a.amask, off + co, r);
+            }
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[q] += r[q];
           }
