@@ -117,6 +117,9 @@ def make_config(a, world):
     c.graph_step = bool(a.graph_step) and world == 1
     c.is_testing = False
     c.use_ema = True
+    # a hung or dead rank fails the run within 5 minutes (parallel/ddp.py pg_timeout_s): the first
+    # step's autotuning takes < 1 minute on every rank alike
+    c.pg_timeout_s = 300
     return c
 
 

@@ -128,6 +128,8 @@ class BaseConfig:
         self.hip_activations = True      # PReLU / ELU / SELU / Hardswish / SiLU / ... on the HIP kernels
         self.ddp_bucket_mb = 32          # RCCL all-reduce bucket: ~3 buckets for DDRNet-23 (84 MB), overlapped with backward
         self.ddp_static_graph = True
+        self.pg_timeout_s = 600          # collective timeout: a hung rank fails the job (non-zero exit) instead of holding the node
+        self.syncbn_group = "own"        # SyncBN statistics on their own communicator ('own') or DDP's ('default')
         self.spawn_procs = None          # main.py without torchrun: worker processes (None: one per visible GPU)
         self.graph_step = False          # replay forward+loss+backward from one captured HIP graph (small batches)
         self.graph_warmup = 3            # eager steps per input shape before the capture

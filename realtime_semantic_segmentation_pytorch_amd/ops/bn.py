@@ -161,6 +161,7 @@ class _BNActFn(torch.autograd.Function):
         dy2 = ctx.dy2_slot.pop() if ctx.dy2_slot else None
         if dy is None and dy2 is None:
             return (None,) * 11
+        dy_in = dy  # (as autograd passed it: the early SyncBN reduction is matched on it)
         if dy is not None:
             dy = _aligned_cl(dy)
         bsums = local = None
@@ -174,7 +175,7 @@ class _BNActFn(torch.autograd.Function):
             if early is not None:
                 key, e_sums, e_local, work = early
                 work.wait()
-                if dy is not None and dy2 is None and dy.data_ptr() == key:
+                if dy2 is None and _same_grad(dy_in, key):
                     bsums, local = e_sums, e_local  # reduced while the consumer's wgrad ran
                 else:
                     # the output had another consumer (its gradient is a sum): this site never
@@ -246,7 +247,7 @@ def _stem_handoff(ctx, stem, dy, x, y, mi, ss, sums, weight, want_dw):
         if early is not None:
             key, e_sums, e_local, work = early
             work.wait()
-            if dy.data_ptr() == key:
+            if _same_grad(dy, key):
                 bsums, local = e_sums, e_local
             else:
                 ctx.bn_module._rtseg_no_early = True
@@ -301,9 +302,26 @@ def syncbn_bwd_early(node, dy: torch.Tensor) -> bool:
     want_dw = node.has_w and (node.needs_input_grad[1] or node.needs_input_grad[2])
     local = bsums.clone() if want_dw else None
     work = dist.all_reduce(bsums, group=node.pg, async_op=True)
-    early.append((dy.data_ptr(), bsums, local, work))
+    # the key holds a reference to dy itself: autograd then cannot accumulate another consumer's
+    # gradient into dy in place (its input buffer adds in place only into a tensor nobody else
+    # holds) -- a sum arrives as a new tensor -- and the version counter catches any other
+    # in-place write (_same_grad)
+    early.append(((dy, dy._version), bsums, local, work))
     EARLY_ISSUED[0] += 1
     return True
+
+
+def _same_grad(dy, key) -> bool:
+    """Whether the gradient a SyncBN node received is exactly the tensor its consumer conv
+    reduced early (``syncbn_bwd_early``), unmodified: same tensor (or storage, shape and strides)
+    and same version.  Anything else -- a second consumer's gradient added, in place or not --
+    means the early sums are of a partial gradient and must not be used."""
+    ref, ver = key
+    if dy is None:
+        return False
+    same = dy is ref or (dy.data_ptr() == ref.data_ptr() and dy.shape == ref.shape
+                         and dy.stride() == ref.stride() and dy.dtype == ref.dtype)
+    return same and dy._version == ver
 
 
 def eval_coeffs(bn):

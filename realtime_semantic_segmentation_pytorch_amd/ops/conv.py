@@ -464,6 +464,10 @@ def _choose(key, candidates):
     if len(candidates) == 1 or _mode() == "1":
         return 0
     names = [n for n, _ in candidates]
+    if os.environ.get("RTSEG_TUNE_FIXED") == "1":
+        # reproducible across processes (numerics tests): the first native candidate, never a
+        # timing -- nor a decision an earlier timing in this process made
+        return next((i for i, n in enumerate(names) if n != "miopen"), 0)
     got = _DECISIONS.get(key)
     if got is not None:  # by name: the candidate list may differ (e.g. RTSEG_CONV_HALO changed)
         if got[1] in names:

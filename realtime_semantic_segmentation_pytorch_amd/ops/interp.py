@@ -32,6 +32,17 @@ def _torch_act(y: torch.Tensor, act: int) -> torch.Tensor:
     return y
 
 
+def _will_run(node) -> bool:
+    """Whether autograd node ``node`` executes in the backward pass now running: it is in the
+    current graph task (reachable from the roots) and not pruned by ``inputs=``.  A sibling conv
+    whose output was dropped, or feeds only another loss, is NOT -- handing it the skip gradient
+    would lose that gradient."""
+    try:
+        return bool(torch._C._will_engine_execute_node(node))
+    except (AttributeError, RuntimeError, TypeError):
+        return False
+
+
 class _InterpFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, skip, out_h, out_w, align, act):
@@ -65,8 +76,9 @@ class _InterpFn(torch.autograd.Function):
         gs = g if (ctx.has_skip and ctx.needs_input_grad[1]) else None
         if gs is not None and ctx.skip_conv is not None:
             node = ctx.skip_conv()
-            if node is not None and not node.ran and node.addend_slot is None:
-                # the conv node has not run: it adds gs in its dgrad epilogue (no accumulation add)
+            if node is not None and not node.ran and node.addend_slot is None and _will_run(node):
+                # the conv node has not run and will run in THIS backward (its output reaches the
+                # roots): it adds gs in its dgrad epilogue (no accumulation add)
                 node.addend_slot = [gs]
                 gs = None
                 SKIP_HANDOFFS[0] += 1

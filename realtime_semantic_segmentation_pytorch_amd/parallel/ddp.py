@@ -80,8 +80,11 @@ def set_device(config, local_rank=None):
             device = torch.device("cpu")
             backend = "gloo"
         if not is_dist():
-            kw = dict(backend=backend,
-                      timeout=datetime.timedelta(minutes=int(os.getenv("RTSEG_PG_TIMEOUT_MIN", 30))))
+            # RCCL: a collective that does not complete within the timeout aborts the communicator
+            # and the process (watchdog, async error handling) -- a hung or dead peer ends the job
+            # with a non-zero exit instead of holding every GPU of the node until the lease ends
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "3")
+            kw = dict(backend=backend, timeout=datetime.timedelta(seconds=pg_timeout_s(config)))
             if backend == "nccl":
                 kw["device_id"] = device
             store = _restart_store(rank, world, kw["timeout"])
@@ -101,6 +104,18 @@ def set_device(config, local_rank=None):
     return device
 
 
+def pg_timeout_s(config=None) -> float:
+    """Collective timeout in seconds: ``RTSEG_PG_TIMEOUT_S`` (or the older ``RTSEG_PG_TIMEOUT_MIN``),
+    else ``config.pg_timeout_s`` (default 600).  The first step at a new shape autotunes every conv
+    pass on every rank (tens of seconds at most, all ranks alike), so minutes are plenty; torch's own
+    default is 10 minutes for RCCL and 30 for gloo."""
+    if os.getenv("RTSEG_PG_TIMEOUT_S"):
+        return float(os.environ["RTSEG_PG_TIMEOUT_S"])
+    if os.getenv("RTSEG_PG_TIMEOUT_MIN"):
+        return 60.0 * float(os.environ["RTSEG_PG_TIMEOUT_MIN"])
+    return float(getattr(config, "pg_timeout_s", 600))
+
+
 def _restart_store(rank, world, timeout):
     """After a torchrun restart (``--max-restarts``), a key space of this generation's own on the
     launcher's store: the default env:// rendezvous would read the previous generation's
@@ -117,11 +132,27 @@ def _restart_store(rank, world, timeout):
 _SYNCBN_PG = None
 
 
-def syncbn_group():
-    """Process group dedicated to SyncBatchNorm statistics (created once, on every rank)."""
+def syncbn_group(config=None):
+    """Process group of the SyncBatchNorm statistics (created once, on every rank, in the same order).
+
+    ``config.syncbn_group`` / ``RTSEG_SYNCBN_GROUP``:
+    * ``"own"`` (default): a communicator of its own.  Its per-layer all-reduces are tiny and
+      latency-bound; on DDP's communicator (one RCCL stream) they would queue behind the 32 MiB
+      gradient buckets in backward.  Two communicators cannot deadlock here because every rank
+      issues the same sequence on each of them: DDP's bucket all-reduces are launched in the
+      same bucket order on all ranks (static graph, fixed buckets), SyncBN's in the same layer
+      order (the same graph on every rank, ``syncbn_bwd_early`` decides identically everywhere),
+      and neither communicator's kernels wait on the other's -- the compute stream waits on both,
+      each collective completes once all ranks reach IT, independent of the other stream.
+    * ``"default"``: the default group (the world communicator DDP uses): one communicator, one
+      ordered stream of collectives -- the fallback if a platform serialises or deadlocks
+      concurrent communicators."""
     global _SYNCBN_PG
     if _SYNCBN_PG is None and is_dist():
-        _SYNCBN_PG = dist.new_group(ranks=list(range(dist.get_world_size())))
+        mode = os.getenv("RTSEG_SYNCBN_GROUP", getattr(config, "syncbn_group", "own") if config is not None else "own")
+        if mode not in ("own", "default"):
+            raise ValueError(f"syncbn_group must be 'own' or 'default', got {mode!r}")
+        _SYNCBN_PG = dist.group.WORLD if mode == "default" else dist.new_group(ranks=list(range(dist.get_world_size())))
     return _SYNCBN_PG
 
 
@@ -130,11 +161,8 @@ def parallel_model(config, model, rank, device):
         return model.to(device)
     sync = bool(config.synBN) and device.type == "cuda"
     if sync:
-        # SyncBN gets its OWN process group: its per-layer statistics all-reduces are small and
-        # latency-bound, and on the default group (one RCCL communicator / stream) they would
-        # queue behind DDP's 32 MiB gradient buckets in backward.  All ranks create it in the
-        # same order here.
-        model = nn.SyncBatchNorm.convert_sync_batchnorm(model, process_group=syncbn_group())
+        # SyncBN gets its OWN process group by default (syncbn_group: why, and the fallback)
+        model = nn.SyncBatchNorm.convert_sync_batchnorm(model, process_group=syncbn_group(config))
         from ..ops import convert_batchnorm
         convert_batchnorm(model)  # SyncBN -> fused HIP SyncBN (one fp64 all-reduce per layer)
     model = model.to(device)

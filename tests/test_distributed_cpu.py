@@ -137,3 +137,77 @@ def test_syncbn_pooled_attention_two_ranks_matches_full_batch(tmp_path):
         torch.testing.assert_close(got[r]["rv"], arm.conv[1].running_var, rtol=1e-5, atol=1e-7)
     assert isinstance(nn.SyncBatchNorm.convert_sync_batchnorm(AttentionRefinementModule(8)).conv[1],
                       nn.SyncBatchNorm)
+
+
+def _hang_worker(rank, world, port, out_dir):
+    """Rank 1 never enters the collective rank 0 waits in (a hung peer): rank 0 must fail with an
+    error within the configured collective timeout -- a non-zero exit -- not wait forever."""
+    import time
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), LOCAL_RANK=str(rank),
+                      WORLD_SIZE=str(world), RTSEG_PG_TIMEOUT_S="4")
+    import torch.distributed as dist
+
+    from realtime_semantic_segmentation_pytorch_amd.configs import BaseConfig
+    from realtime_semantic_segmentation_pytorch_amd.parallel.ddp import set_device, syncbn_group
+
+    c = BaseConfig()
+    c.DDP, c.device = True, "cpu"
+    set_device(c)
+    assert syncbn_group(c) is not dist.group.WORLD  # default: a communicator of its own
+    t = torch.ones(4)
+    dist.all_reduce(t)  # both ranks: fine
+    if rank == 1:
+        time.sleep(60)  # hung: never reaches the next collective
+        return
+    t0 = time.perf_counter()
+    with open(os.path.join(out_dir, "r0.txt"), "w") as f:
+        try:
+            dist.all_reduce(t)
+            f.write("completed")
+        except Exception as e:  # noqa: BLE001 - the timeout error is what is tested
+            f.write(f"raised after {time.perf_counter() - t0:.1f} s: {type(e).__name__}")
+            raise SystemExit(3)
+
+
+@pytest.mark.timeout(120)
+def test_hung_peer_fails_fast_with_nonzero_exit(tmp_path):
+    """parallel/ddp.py: the collective timeout (``pg_timeout_s`` / ``RTSEG_PG_TIMEOUT_S``) turns a
+    rank that stops issuing collectives into an error on its peers within that timeout (here 4 s)."""
+    import time
+
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    ps = [ctx.Process(target=_hang_worker, args=(r, 2, port, str(tmp_path))) for r in range(2)]
+    t0 = time.perf_counter()
+    for p in ps:
+        p.start()
+    ps[0].join(60)
+    took = time.perf_counter() - t0
+    for p in ps:
+        if p.is_alive():
+            p.kill()
+            p.join()
+    msg = open(os.path.join(tmp_path, "r0.txt")).read()
+    assert ps[0].exitcode == 3, (ps[0].exitcode, msg)
+    assert msg.startswith("raised after"), msg
+    assert float(msg.split()[2]) < 15 and took < 60, (msg, took)
+
+
+def _group_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), LOCAL_RANK=str(rank),
+                      WORLD_SIZE=str(world), RTSEG_SYNCBN_GROUP="default")
+    import torch.distributed as dist
+
+    from realtime_semantic_segmentation_pytorch_amd.configs import BaseConfig
+    from realtime_semantic_segmentation_pytorch_amd.parallel.ddp import set_device, syncbn_group
+
+    c = BaseConfig()
+    c.DDP, c.device = True, "cpu"
+    set_device(c)
+    assert syncbn_group(c) is dist.group.WORLD
+    dist.destroy_process_group()
+
+
+def test_syncbn_on_default_group_knob(tmp_path):
+    mp.spawn(_group_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)

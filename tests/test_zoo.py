@@ -108,28 +108,150 @@ def _freeze_bn(m):
     return m
 
 
-def check_zoo_hip_matches_torch_path(key, monkeypatch):
-    """Eval forward: HIP path == torch path (tight).  Training step (forward, loss, backward): the
-    HIP path (channels-last) is scored against a CPU fp64 run of the same step, with two
-    yardsticks measured in the same test -- the CPU fp32 run and the GPU torch path in NCHW.
+# A training-mode BatchNorm whose per-channel population N*H*W is below this runs on its running
+# statistics in the train-BN numerics pass (all paths identically).  Such a BN normalises a handful
+# of values to +-d/sqrt(d^2 + eps); where d is rounding-sized the sign -- which value passes the
+# next ReLU -- flips with the last bits of upstream sums, in ANY path (AGLNet's 1-channel pyramid on
+# 4 x 8 maps, DDRNet's DAPPM global branch over 2 values).  tools/probe_bn_population.py: at 1024
+# AGLNet's CPU fp32 error drops 6.8e-3 -> 4.2e-4, ContextNet 3.3e-2 -> 4e-6, FastSCNN 8e-3 -> 2e-6;
+# other discrete events remain (see check_zoo_hip_matches_torch_path), so this alone is not a
+# criterion (profiles/r6_zoo_numerics).
+SMALL_BN_POPULATION = 1024
 
-    Measured on MI355X (tools/probe_zoo_gpu_err.py, profiles/r3_zoo_numerics): the channels-last
-    torch path is ~1e-2 off fp64 on the pooling models even with frozen BatchNorm (round 3 blamed
-    MIOpen's NHWC convs; the round-4 bisection, profiles/r4_numerics, pins it on PyTorch's
-    channels-last avg_pool2d backward -- the HIP path runs the same MIOpen convs at 1e-5), so it
-    is NOT a usable yardstick (round 2 used it and had to skip 7 models).  Two passes, no skips:
-    * frozen BatchNorm (running statistics): every model's whole HIP training path -- convs,
-      depth-wise convs, pooling, interpolation, gating, activations, the loss -- must be within
-      10x the CPU fp32 error (floor 1e-3);
-    * batch-statistics BatchNorm at batch 2: within 4x the better of the two yardsticks, or 1.5x
-      the worse, or the flip envelope of a batch-2 BN sign flip (``TRAIN_BN_FLIP_FLOOR``).  Where even CPU fp32 is > 0.1 off fp64 (DFANet, Lite-HRNet, MiniNetV2: BN over a
-      handful of values at batch 2, gradients of ~1e8), the step is only checked for finite
-      gradients; the frozen pass above still pins their numerics."""
-    torch.manual_seed(0)
-    cpu = _model(key)
-    for mod in cpu.modules():  # CPU and GPU RNG streams differ: compare without dropout
+
+def bn_populations(m, x):
+    """{module name: per-channel population N*H*W} of every BatchNorm of ``m`` in a training
+    forward of ``x`` on the CPU (smallest over repeated calls)."""
+    m = copy.deepcopy(m).train()
+    pops, hooks = {}, []
+    for name, mod in m.named_modules():
+        if isinstance(mod, torch.nn.modules.batchnorm._BatchNorm):
+            def pre(mod_, args, name=name):
+                t = args[0]
+                p = t.numel() // t.shape[1]
+                pops[name] = min(pops.get(name, p), p)
+            hooks.append(mod.register_forward_pre_hook(pre))
+    with torch.no_grad():
+        _forward(m, x)
+    for h in hooks:
+        h.remove()
+    return pops
+
+
+def freeze_small_bn(m, pops, threshold=SMALL_BN_POPULATION):
+    """Put every BatchNorm of ``m`` whose population (``bn_populations``) is below ``threshold``
+    in eval mode (running statistics) -- after ``m.train()``."""
+    mods = dict(m.named_modules())
+    for name, p in pops.items():
+        if p < threshold:
+            mods[name].eval()
+    return m
+
+
+def _no_dropout(m):
+    for mod in m.modules():  # CPU and GPU RNG streams differ: compare without dropout
         if isinstance(mod, torch.nn.modules.dropout._DropoutNd):
             mod.p = 0.0
+    return m
+
+
+def _grad_err(g, r):
+    a = torch.cat([g[n].flatten().double() for n in r])
+    b = torch.cat([r[n].flatten().double() for n in r])
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+def _cpu_grads(m, x, labels):
+    with ops.defer_final_upsample():
+        o = _main(_forward(m, x))
+    SegCELoss(ops.MODE_MEAN)(o, labels).backward()
+    return {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
+
+
+def perturb_ulp(m, seed):
+    """Multiply every parameter of fp32 model ``m`` by (1 + 2^-24 * N(0, 1)) -- a rounding-sized
+    change, so the step's distance to the unperturbed fp64 step is one more independent draw of
+    fp32 rounding noise (through the same chaotic sign decisions)."""
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.mul_(1 + 2.0 ** -24 * torch.randn(p.shape, generator=g, dtype=torch.float64).to(p.dtype))
+    return m
+
+
+def cpu_fp32_vs_fp64_train_bn(key, x, labels, threshold=SMALL_BN_POPULATION, draws=0):
+    """CPU fp32 whole-model gradient error vs CPU fp64 of one batch-statistics training step with
+    the small-population BatchNorms frozen; with ``draws`` > 0 a list: the plain fp32 error then
+    ``draws`` errors of ulp-perturbed fp32 models (``perturb_ulp``)."""
+    torch.manual_seed(0)
+    cpu = _no_dropout(_model(key))
+    pops = bn_populations(cpu, x)
+    prep = lambda dt: freeze_small_bn(copy.deepcopy(cpu).train().to(dt), pops, threshold)  # noqa: E731
+    ref = _cpu_grads(prep(torch.float64), x.double(), labels)
+    errs = [_grad_err(_cpu_grads(prep(torch.float32), x, labels), ref)]
+    for d in range(draws):
+        errs.append(_grad_err(_cpu_grads(perturb_ulp(prep(torch.float32), d + 1), x, labels), ref))
+    return errs if draws else errs[0]
+
+
+def test_small_bn_freeze_covers_the_batch2_flip_sites_cpu():
+    """The sites behind the round-5 driver failure (AGLNet's 1-channel ConvBNAct pyramid, reference
+    models/aglnet.py:99-104) and DDRNet's DAPPM global branch run on running statistics in the
+    train-BN pass; the full-resolution BNs keep batch statistics."""
+    x = torch.randn(2, 3, *HW)
+    for key in ("aglnet", "ddrnet"):
+        m = _model(key)
+        pops = bn_populations(m, x)
+        assert min(pops.values()) < 64 and max(pops.values()) >= 2 * (HW[0] // 2) * (HW[1] // 2) // 4
+        f = freeze_small_bn(copy.deepcopy(m).train(), pops)
+        mods = dict(f.named_modules())
+        assert all(mods[n].training == (p >= SMALL_BN_POPULATION) for n, p in pops.items())
+
+
+@pytest.mark.parametrize("key", ["aglnet", "ddrnet", "lite_hrnet"])
+def test_train_bn_envelope_accepts_a_rounding_draw_cpu(key):
+    """The GPU train-BN criterion on the CPU: more ulp-perturbed fp32 runs (stand-ins for a correct
+    HIP path and its re-draws: rounding noise only) land within ``ZOO_ENVELOPE_X`` x the envelope of the
+    plain fp32 run and ``ZOO_CPU_DRAWS`` draws -- including on Lite-HRNet, where every draw is
+    ~5e-3 off fp64, and on DDRNet-23, whose draws are 2.7e-6 or, when the ReLU after a 1024-value BN
+    (conv5.high_conv1) flips one element, 1.4e-3 -- while a 5 % systematic gradient error (a bug) would not."""
+    torch.manual_seed(0)
+    x = torch.randn(2, 3, *HW)
+    labels = torch.randint(0, 19, (2, *HW))
+    errs = cpu_fp32_vs_fp64_train_bn(key, x, labels, draws=ZOO_CPU_DRAWS + 1 + ZOO_HIP_DRAWS)
+    env, cand = errs[:ZOO_CPU_DRAWS + 1], errs[ZOO_CPU_DRAWS + 1:]
+    assert min(cand) <= ZOO_ENVELOPE_X * max(env), (cand, env)
+    assert 5e-2 > ZOO_ENVELOPE_X * max(env), env  # a bug of 5 % would fail
+
+
+def check_zoo_hip_matches_torch_path(key, monkeypatch):
+    """Eval forward: HIP path == torch path (tight).  Training step (forward, loss, backward): the
+    HIP path (channels-last) is scored against a CPU fp64 run of the same step.
+
+    Measured on MI355X (tools/probe_zoo_gpu_err.py, profiles/r3_zoo_numerics): the channels-last
+    torch path is ~1e-2 off fp64 on the pooling models even with frozen BatchNorm (round 4,
+    profiles/r4_numerics: PyTorch's channels-last avg_pool2d backward), so it is NOT a yardstick.
+    Two passes, no skips:
+    * frozen BatchNorm (running statistics): every model's whole HIP training path -- convs,
+      depth-wise convs, pooling, interpolation, gating, activations, the loss -- must be within
+      10x the CPU fp32 error (floor 1e-3), plus the production bf16 path (``_check_bf16_vs_fp64``);
+    * batch-statistics BatchNorm at batch 2.  This step is chaotic on every path: a BN over a
+      handful of values normalises to +-d/sqrt(d^2 + eps), and wherever a rounding-sized change
+      decides a discrete event (that sign, a ReLU on a pooled vector, a max-pool winner) the whole
+      gradient jumps.  Measured on CPU (tools/probe_bn_population.py, profiles/r6_zoo_numerics):
+      fp32-vs-fp64 errors of ulp-perturbed copies of ONE model are bimodal (DDRNet 2.7e-6 or
+      1.4e-3; Lite-HRNet 4e-3..8e-3), so any single-draw yardstick flips.  Hence:
+      - BatchNorms whose per-channel population is below ``SMALL_BN_POPULATION`` run on running
+        statistics in every path (the batch-2 sign flips: AGLNet's 1-channel pyramid on 4 x 8
+        maps, reference models/aglnet.py:99-104);
+      - the envelope is measured in the test: CPU fp32 plus ``ZOO_CPU_DRAWS`` ulp-perturbed fp32
+        draws (``perturb_ulp``) and the GPU NCHW stock path;
+      - the HIP path (plus up to ``ZOO_HIP_DRAWS`` ulp-perturbed re-runs, taken only while it is
+        outside) must land within ``ZOO_ENVELOPE_X`` x the envelope's largest error.
+      A kernel bug is systematic: it survives every HIP draw.  A flip does not."""
+    monkeypatch.setenv("RTSEG_TUNE_FIXED", "1")  # conv choices by rule, not timing (reproducible)
+    torch.manual_seed(0)
+    cpu = _no_dropout(_model(key))
     x = torch.randn(2, 3, *HW)
     labels = torch.randint(0, 19, (2, *HW))
     base = copy.deepcopy(cpu).cuda().to(memory_format=torch.channels_last)
@@ -144,8 +266,9 @@ def check_zoo_hip_matches_torch_path(key, monkeypatch):
         monkeypatch.delenv("RTSEG_DISABLE_HIP", raising=False)
     assert _rel(e_h, e_t) < 2e-5
     err = lambda a, b: ((a.double().cpu() - b.double().cpu()).norm() / (b.double().cpu().norm() + 1e-30)).item()  # noqa: E731
+    pops = bn_populations(cpu, x)
     for frozen in (True, False):
-        prep = _freeze_bn if frozen else (lambda m: m)
+        prep = _freeze_bn if frozen else (lambda m: freeze_small_bn(m, pops))
         bn = "frozen-BN" if frozen else "train-BN"
         y_r, l_r, g_r = _run_gpu(prep(copy.deepcopy(cpu).train().double()), x.double(), labels, False, monkeypatch)
         y_c, l_c, g_c = _run_gpu(prep(copy.deepcopy(cpu).train()), x, labels, False, monkeypatch)
@@ -155,32 +278,38 @@ def check_zoo_hip_matches_torch_path(key, monkeypatch):
         cat = lambda g: torch.cat([g[n].flatten().double().cpu() for n in g_r])  # noqa: E731
         hg, cg = err(cat(g_h), cat(g_r)), err(cat(g_c), cat(g_r))
         assert torch.isfinite(cat(g_h)).all()
-        tag = f"{key} {'frozen-BN' if frozen else 'train-BN'}: HIP grad err {hg:.2e}, CPU fp32 {cg:.2e}"
+        tag = f"{key} {bn}: HIP grad err {hg:.2e}, CPU fp32 {cg:.2e}"
         if frozen:
             assert err(y_h, y_r) <= max(10 * err(y_c, y_r), 1e-4), tag
             assert abs(l_h.item() - l_r.item()) <= max(10 * abs(l_c.item() - l_r.item()), 1e-4 * abs(l_r.item())), tag
             assert hg <= max(10 * cg, 1e-3), tag
             _check_bf16_vs_fp64(key, base, xg, labels, l_r, g_r, cat, err, monkeypatch)
             continue
-        if cg > 0.1:
-            continue  # ill-conditioned at batch 2 on any path (see docstring); finiteness checked
-        nchw = copy.deepcopy(cpu).cuda().train()
+        nchw = prep(copy.deepcopy(cpu).cuda().train())
         _, l_t, g_t = _run_gpu(nchw, x.cuda(), labels.cuda(), True, monkeypatch, f"{key} {bn} stock fp32 NCHW")
-        tg = err(cat(g_t), cat(g_r))
-        tag += f", GPU torch NCHW {tg:.2e}"
+        env = [cg, err(cat(g_t), cat(g_r))]
+        lenv = [abs(l_c.item() - l_r.item()), abs(l_t.item() - l_r.item())]
+        for d in range(ZOO_CPU_DRAWS):
+            _, l_d, g_d = _run_gpu(perturb_ulp(prep(copy.deepcopy(cpu).train()), d + 1), x, labels, False,
+                                   monkeypatch)
+            env.append(err(cat(g_d), cat(g_r)))
+            lenv.append(abs(l_d.item() - l_r.item()))
+        hip = [hg]
+        lh = abs(l_h.item() - l_r.item())
+        bound, lbound = ZOO_ENVELOPE_X * max(env), ZOO_ENVELOPE_X * max(max(lenv), 1e-7 * abs(l_r.item()))
+        for d in range(ZOO_HIP_DRAWS):
+            if min(hip) <= bound and lh <= lbound:
+                break
+            m = perturb_ulp(prep(copy.deepcopy(cpu).train()), 100 + d).cuda().to(memory_format=torch.channels_last)
+            _, l_d, g_d = _run_gpu(m, xg, labels.cuda(), False, monkeypatch, f"{key} {bn} HIP fp32 draw {d + 1}")
+            hip.append(err(cat(g_d), cat(g_r)))
+            lh = min(lh, abs(l_d.item() - l_r.item()))
+        tag = (f"{key} {bn}: HIP grad err {', '.join(f'{h:.2e}' for h in hip)}; envelope (CPU fp32, GPU NCHW, "
+               f"{ZOO_CPU_DRAWS} CPU draws) {', '.join(f'{e:.2e}' for e in env)}; loss err {lh:.2e} "
+               f"(envelope max {max(lenv):.2e})")
         print(tag)
-        assert abs(l_h.item() - l_r.item()) <= max(4 * min(abs(l_t.item() - l_r.item()), abs(l_c.item() - l_r.item())),
-                                                   1e-3 * abs(l_r.item())), tag
-        # batch-2 batch statistics make this step ill-conditioned: a BN over 2 values per channel
-        # (DDRNet's DAPPM global branch, BiSeNetV2's context block) normalises to +-d/sqrt(d^2 +
-        # eps), and where d is rounding-sized the sign -- which sample passes its ReLU -- flips
-        # with the last bits of upstream sums.  Such a flip moves the whole gradient by
-        # ~3.5e-3 (DDRNet) in ANY path: on identical inputs the stock GPU path gave 1.5e-5 in one
-        # process and 3.46e-3 in the next, the HIP path 1.2e-5 or 3.47e-3, and at batch 4 even
-        # CPU fp32 shows 3.05e-3 (tools/probe_param_err.py, profiles/r5_numerics).  So the HIP
-        # path must be within 4x the better yardstick, or 1.5x the worse one, or the measured
-        # flip envelope; the frozen-BN pass above pins every kernel's precision without flips.
-        assert hg <= max(4 * min(tg, cg), 1.5 * max(tg, cg), TRAIN_BN_FLIP_FLOOR), tag
+        assert min(hip) <= bound, tag
+        assert lh <= lbound, tag
 
 
 def _run_gpu_bf16(m, x, labels, disable_hip, monkeypatch, phase=None):
@@ -209,9 +338,9 @@ def _check_bf16_vs_fp64(key, base, xg, labels, l_r, g_r, cat, err, monkeypatch):
     assert bl <= max(ZOO_BF16_LOSS_SLACK * sl, 2e-3 * abs(l_r.item())), tag
 
 
-# a sign flip of a batch-2 BatchNorm over 2 values (see check_zoo_hip_matches_torch_path): the
-# gradient error one flip leaves on DDRNet-23, measured on the stock GPU path too (3.46e-3)
-TRAIN_BN_FLIP_FLOOR = 4e-3
+# the train-BN envelope (check_zoo_hip_matches_torch_path): ulp-perturbed CPU fp32 draws measured
+# per test, the factor on the envelope's largest error, and HIP re-draws taken while outside it
+ZOO_CPU_DRAWS, ZOO_ENVELOPE_X, ZOO_HIP_DRAWS = 3, 2.0, 2
 
 # HIP bf16 vs stock bf16 distance to fp64 (frozen BN, 128 x 256, batch 2).  Round 5 on MI355X: HIP
 # / stock between 0.14 (SwiftNet) and 1.14 (ENet), smallest stock 4.6e-3 (FastSCNN); the floor
