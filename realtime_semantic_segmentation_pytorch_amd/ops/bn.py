@@ -170,6 +170,10 @@ class _BNActFn(torch.autograd.Function):
         stem, ctx.stem_node = ctx.stem_node, None
         if stem is not None and dy is not None and dy2 is None and ctx.needs_input_grad[0]:
             return _stem_handoff(ctx, stem, dy, x, y, mi, ss, sums, weight, want_dw)
+        if not getattr(x.grad_fn, "y_stored", True):
+            # a stats-only stem launch (RTSEG_STEM_NO_STORE=1) never wrote x, and this backward
+            # reads it (the hand-off above was not taken: a second backward, another consumer)
+            _stem_materialize(x.grad_fn, x)
         if ctx.pg is not None:
             early = ctx.early.pop() if ctx.early else None
             if early is not None:
@@ -298,6 +302,8 @@ def syncbn_bwd_early(node, dy: torch.Tensor) -> bool:
     if (dy.dtype != x.dtype or dy.shape != x.shape or dy.data_ptr() % 16
             or not dy.is_contiguous(memory_format=torch.channels_last)):
         return False
+    if not getattr(x.grad_fn, "y_stored", True):
+        _stem_materialize(x.grad_fn, x)
     bsums = ops().bn_bwd_sums(dy, x, y, mi, ss, node.act, node.mask, None)
     want_dw = node.has_w and (node.needs_input_grad[1] or node.needs_input_grad[2])
     local = bsums.clone() if want_dw else None

@@ -367,8 +367,13 @@ def invalidate_weight_shadows(params) -> int:
     ``parallel/ddp.py`` calls this), raw-pointer writers other than the fused step.  Writes
     through ``p`` itself under ``torch.no_grad()`` (``load_state_dict``, ``p.copy_``) bump the
     version counter and need no call.  Returns the number of shadows invalidated."""
+    from ._ext import bump_write_generation
+
+    bump_write_generation()  # every (ptr, version, generation)-keyed cache: depth-wise, eval BN, w16
     n = 0
     for p in params:
+        if getattr(p, "_rtseg_dw_wt", None) is not None:
+            p._rtseg_dw_wt = None  # the depth-wise kernels' fp32 weight re-layout (ops/dwconv.py)
         sh = shadow_of(p)
         if sh is not None:
             sh.gen = sh.crsk_gen = -1
