@@ -45,9 +45,9 @@ def _data():
     g1 = torch.randn(2 * N, C, H, W, generator=g)
     g2 = torch.randn(2 * N, C, H, W, generator=g)
     # bf16-representable inputs and weights: the fp64 reference sees what the GPU path sees
-    rb = lambda t: t.to(torch.bfloat16).double()  # noqa: E731
-    return {"w0": rb(conv0.weight), "w1": rb(conv1.weight), "gamma": bn.weight.double(), "beta": bn.bias.double(),
-            "x": rb(x), "g1": g1.double(), "g2": g2.double()}
+    rb = lambda t: t.detach().to(torch.bfloat16).double()  # noqa: E731
+    return {"w0": rb(conv0.weight), "w1": rb(conv1.weight), "gamma": bn.weight.detach().double(),
+            "beta": bn.bias.detach().double(), "x": rb(x), "g1": g1.double(), "g2": g2.double()}
 
 
 def _reference(d):
