@@ -234,8 +234,8 @@ void launch_conv_wres_dgrad(const ConvGeom& g, hipStream_t st);
 bool conv_hreg_supported(const ConvGeom& g, int mode);
 int conv_hreg_slabs(const ConvGeom& g);
 int64_t conv_hreg_pack_elems(const ConvGeom& g, int mode);
-// rows_per_wave: 1 = 8 waves of 2 x 2 accumulator tiles, 2 = 4 waves of 2 x 4 tiles
-void launch_conv_hreg(const ConvGeom& g, int mode, void* wpack, hipStream_t st, int rows_per_wave = 1);
+// layout: 1 = 8 waves of 2 x 2 accumulator tiles, 2 = 4 waves of 2 x 4, 4 = 8 waves of 1 x 4
+void launch_conv_hreg(const ConvGeom& g, int mode, void* wpack, hipStream_t st, int layout = 1);
 
 // ---- conv_stem.hip ------------------------------------------------------------
 // 3-channel 3 x 3 stem conv (pad 1, stride 1 / 2, Cout % 16 == 0 and <= 64, even W): forward

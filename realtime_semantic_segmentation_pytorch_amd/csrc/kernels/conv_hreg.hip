@@ -25,6 +25,7 @@
 #include "rtseg_mfma_dev.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace rtseg {
 
@@ -69,18 +70,28 @@ __device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t r, uint32_t voff, 
       : "memory");
 }
 
-// RPW = tile rows per wave: 1 -> 8 waves (2 per SIMD, 2 x 2 accumulator tiles each); 2 -> 4 waves
-// (1 per SIMD, 2 x 4 tiles in the unified 512-register file): half the per-block weight stream
-// (every wave of a channel half reads the same fragments) for twice the B-fragment reads
-template <int STATS, int FLIP, int RPW>
-__global__ void __launch_bounds__(2 * kTH / RPW * 64) hreg_conv_kernel(const HrArgs a) {
-  constexpr int kNW = 2 * kTH / RPW, TJ = 2 * RPW;
+// Wave layouts (WL): NRG row groups x NCG channel groups of the 4 x 64-pixel x 128-channel tile;
+// each wave owns RPW = 4 / NRG tile rows (TJ = 2 RPW 32-pixel tiles) x TI = 4 / NCG 32-channel tiles.
+//  WL 1: 4 x 2 -> 8 waves of 2 x 2 tiles (2 per SIMD);
+//  WL 2: 2 x 2 -> 4 waves of 2 x 4 tiles (1 per SIMD, 512-register file): half the weight stream;
+//  WL 4: 2 x 4 -> 8 waves of 1 x 4 tiles: WL 2's weight stream (every A fragment feeds 4 MFMAs;
+//        the per-CU stream of WL 1 is ~64 B/clk, above the L2's ~56 B/clk/CU share) with WL 1's
+//        two waves per SIMD, for twice WL 1's B-fragment LDS reads (128 B/clk/CU of 256).
+template <int WL> struct HrLayout;
+template <> struct HrLayout<1> { static constexpr int NRG = 4, NCG = 2; };
+template <> struct HrLayout<2> { static constexpr int NRG = 2, NCG = 2; };
+template <> struct HrLayout<4> { static constexpr int NRG = 2, NCG = 4; };
+
+template <int STATS, int FLIP, int WL>
+__global__ void __launch_bounds__(HrLayout<WL>::NRG * HrLayout<WL>::NCG * 64) hreg_conv_kernel(const HrArgs a) {
+  constexpr int NRG = HrLayout<WL>::NRG, NCG = HrLayout<WL>::NCG;
+  constexpr int kNW = NRG * NCG, RPW = kTH / NRG, TJ = 2 * RPW, TI = 4 / NCG;
   __shared__ uint4 lds[2 * kHStage + kRed / 4];
-  float* const red = reinterpret_cast<float*>(lds + 2 * kHStage);  // [4 rows][sum, sumsq][128]
+  float* const red = reinterpret_cast<float*>(lds + 2 * kHStage);  // [row group][sum, sumsq][128]
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid >> 1, wn = wid & 1;  // pixel row of the tile, 64-channel half
+  const int wm = wid / NCG, wn = wid % NCG;  // row group of the tile, channel group
   const int G = gridDim.x;
   const int lb = xcd_logical(blockIdx.x, G);
   const int ntile = lb % a.ntiles;
@@ -120,12 +131,11 @@ __global__ void __launch_bounds__(2 * kTH / RPW * 64) hreg_conv_kernel(const HrA
     }
   };
 
-  // packed A fragments of (chunk c, tap t): [ti][ks], lane-contiguous 1 KiB each
-  const uint4* wbase = a.wp + (static_cast<int64_t>(co0 / 32 + wn * 2) * cch * 9 * 4) * 64 + lane;
+  const uint4* wbase = a.wp + (static_cast<int64_t>(co0 / 32 + wn * TI) * cch * 9 * 4) * 64 + lane;
   const int64_t ti_stride = static_cast<int64_t>(cch) * 9 * 4 * 64;
-  auto wload = [&](int g, bf16x8_t (&dst)[2][4]) {  // g = chunk * 9 + tap
+  auto wload = [&](int g, bf16x8_t (&dst)[TI][4]) {  // g = chunk * 9 + tap
 #pragma unroll
-    for (int ti = 0; ti < 2; ++ti)
+    for (int ti = 0; ti < TI; ++ti)
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) dst[ti][ks] = as_frag(wbase[ti * ti_stride + (g * 4 + ks) * 64]);
   };
@@ -134,9 +144,9 @@ __global__ void __launch_bounds__(2 * kTH / RPW * 64) hreg_conv_kernel(const HrA
   const int frow = lane & 31, fhi = lane >> 5;
   const int hrow0 = wm * RPW * kHW + frow;  // + (tj / 2) * kHW + (tj % 2) * 32 + tap shift
 
-  f32x16_t acc[2][TJ];
+  f32x16_t acc[TI][TJ];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < TJ; ++j)
 #pragma unroll
@@ -146,14 +156,14 @@ __global__ void __launch_bounds__(2 * kTH / RPW * 64) hreg_conv_kernel(const HrA
     for (int e = tid; e < kRed; e += kNW * 64) red[e] = 0.f;
   }
 
-  const int co_lane = co0 + wn * 64 + 4 * fhi;  // + ti * 32 + 8 g
+  const int co_lane = co0 + wn * (TI * 32) + 4 * fhi;  // + ti * 32 + 8 g
   auto epilogue = [&](int mt) __attribute__((always_inline)) {
     int n, oy0, ox0;
     tile_xyz(mt, n, oy0, ox0);
-    float ts[STATS ? 2 : 1][16], tq[STATS ? 2 : 1][16];
+    float ts[STATS ? TI : 1][16], tq[STATS ? TI : 1][16];
     if constexpr (STATS) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           ts[i][r] = 0.f;
@@ -166,7 +176,7 @@ __global__ void __launch_bounds__(2 * kTH / RPW * 64) hreg_conv_kernel(const HrA
       const bool ok = oy < a.Ho && ox < a.Wo;
       const int64_t off = ((static_cast<int64_t>(n) * a.Ho + (ok ? oy : 0)) * a.Wo + (ok ? ox : 0)) * a.cout;
 #pragma unroll
-      for (int ti = 0; ti < 2; ++ti) {
+      for (int ti = 0; ti < TI; ++ti) {
         uint2 pkp[2], adp[2];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -213,16 +223,16 @@ __global__ void __launch_bounds__(2 * kTH / RPW * 64) hreg_conv_kernel(const HrA
     }
     if constexpr (STATS) {
       // full per-tile wave reduction; every (row, channel) slot of red has one owning lane
-      float y1[32];
-      stats_stage1<2>(ts, tq, y1);
-      stats_stage2<2>(y1, lane, [&](int, int sq, int dc, float v) {
-        red[(wm * 2 + sq) * kBN + wn * 64 + 4 * fhi + dc] += v;
+      float y1[TI * 16];
+      stats_stage1<TI>(ts, tq, y1);
+      stats_stage2<TI>(y1, lane, [&](int, int sq, int dc, float v) {
+        red[(wm * 2 + sq) * kBN + wn * (TI * 32) + 4 * fhi + dc] += v;
       });
     }
   };
 
   // weights two taps ahead of their MFMAs: three register slots, K-steps g walked in threes
-  bf16x8_t wr[3][2][4];
+  bf16x8_t wr[3][TI][4];
   const int gtot = cch * 9;
   if (nsteps > 0) {
     halo_dma(0);
@@ -240,13 +250,14 @@ __global__ void __launch_bounds__(2 * kTH / RPW * 64) hreg_conv_kernel(const HrA
     if (c == 0 && q > 0) epilogue(mfirst + (q / cch - 1) * mstep);
     if (q + 1 < nsteps) halo_dma(q + 1);
     const uint4* hb = lds + (q & 1) * kHStage;
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int g = c * 9 + tap;  // this K-step's weights are in slot g % 3 (tap % 3 since 9 % 3 == 0)
+    // one tap: K-step g = c * 9 + 3 i + j, whose weights are in slot j (9 % 3 == 0)
+    auto tap_step = [&](int i, auto jc) __attribute__((always_inline)) {
+      constexpr int j = decltype(jc)::value;
+      const int tap = 3 * i + j;
+      const int g = c * 9 + tap;
       // prefetch the weights of K-step g + 2 (the next chunk's first taps, or the next tile's)
       const int gn = g + 2 < gtot ? g + 2 : g + 2 - gtot;
-      if (q * 9 + tap + 2 < nsteps * 9) wload(gn, wr[(tap + 2) % 3]);
-      const int i = tap / 3, j = tap % 3;
+      if (q * 9 + tap + 2 < nsteps * 9) wload(gn, wr[(j + 2) % 3]);
       const int sh = FLIP ? (2 - i) * kHW + (2 - j) : i * kHW + j;
       bf16x8_t bfg[2][TJ];
 #pragma unroll
@@ -259,24 +270,40 @@ __global__ void __launch_bounds__(2 * kTH / RPW * 64) hreg_conv_kernel(const HrA
         }
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int ti = 0; ti < 2; ++ti)
+        for (int ti = 0; ti < TI; ++ti)
 #pragma unroll
           for (int tj = 0; tj < TJ; ++tj)
-            acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wr[tap % 3][ti][ks], bfg[ks & 1][tj], acc[ti][tj],
-                                                                  0, 0, 0);
+            acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wr[j][ti][ks], bfg[ks & 1][tj], acc[ti][tj], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
+      }
+    };
+    if constexpr (WL == 4) {
+      // tap rows rolled: with 4 pixel tiles per wave, hoisting the 9 x 4 x 4 swizzled B-fragment
+      // addresses of a fully unrolled chunk out of the loop spilled
+#pragma unroll 1
+      for (int i = 0; i < 3; ++i) {
+        tap_step(i, std::integral_constant<int, 0>{});
+        tap_step(i, std::integral_constant<int, 1>{});
+        tap_step(i, std::integral_constant<int, 2>{});
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        tap_step(i, std::integral_constant<int, 0>{});
+        tap_step(i, std::integral_constant<int, 1>{});
+        tap_step(i, std::integral_constant<int, 2>{});
       }
     }
   }
   if (nsteps > 0) epilogue(mfirst + (my_tiles - 1) * mstep);
 
   if constexpr (STATS) {
-    // one slab row per block: the 4 pixel rows' sums of each channel in a fixed order
+    // one slab row per block: the row groups' sums of each channel in a fixed order
     __syncthreads();
     for (int e = tid; e < 2 * kBN; e += kNW * 64) {
       float s = 0.f;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) s += red[w * 2 * kBN + e];
+      for (int w = 0; w < NRG; ++w) s += red[w * 2 * kBN + e];
       const int sq = e >= kBN, cc = co0 + (sq ? e - kBN : e);
       a.part[static_cast<int64_t>(mfirst) * 2 * a.cout + (sq ? a.cout : 0) + cc] = s;
     }
@@ -351,7 +378,7 @@ int64_t conv_hreg_pack_elems(const ConvGeom& g, int mode) {  // bf16 elements of
 
 // forward (mode 0: g.x = x, g.w = wk [Cout][3][3][Cin]) or data gradient (mode 1: g.x = dy,
 // g.w = wt [Cin][3][3][Cout], g.res = addend); wpack: conv_hreg_pack_elems bf16 of scratch
-void launch_conv_hreg(const ConvGeom& g, int mode, void* wpack, hipStream_t st, int rows_per_wave) {
+void launch_conv_hreg(const ConvGeom& g, int mode, void* wpack, hipStream_t st, int layout) {
   HrArgs k{};
   const bool dgrad = mode == 1;
   if (!hreg_fill(k, g, dgrad)) return;
@@ -368,17 +395,16 @@ void launch_conv_hreg(const ConvGeom& g, int mode, void* wpack, hipStream_t st, 
   k.amask = dgrad ? g.amask : nullptr;
   const int grid = hreg_grid(k);
   if (grid <= 0) return;
-  if (rows_per_wave == 2) {
-    constexpr int T = 2 * kTH / 2 * 64;
-    if (dgrad) hreg_conv_kernel<0, 1, 2><<<grid, T, 0, st>>>(k);
-    else if (k.part != nullptr) hreg_conv_kernel<1, 0, 2><<<grid, T, 0, st>>>(k);
-    else hreg_conv_kernel<0, 0, 2><<<grid, T, 0, st>>>(k);
-    return;
-  }
-  constexpr int T = 2 * kTH * 64;
-  if (dgrad) hreg_conv_kernel<0, 1, 1><<<grid, T, 0, st>>>(k);
-  else if (k.part != nullptr) hreg_conv_kernel<1, 0, 1><<<grid, T, 0, st>>>(k);
-  else hreg_conv_kernel<0, 0, 1><<<grid, T, 0, st>>>(k);
+  auto go = [&](auto wl) {
+    constexpr int WL = decltype(wl)::value;
+    constexpr int T = HrLayout<WL>::NRG * HrLayout<WL>::NCG * 64;
+    if (dgrad) hreg_conv_kernel<0, 1, WL><<<grid, T, 0, st>>>(k);
+    else if (k.part != nullptr) hreg_conv_kernel<1, 0, WL><<<grid, T, 0, st>>>(k);
+    else hreg_conv_kernel<0, 0, WL><<<grid, T, 0, st>>>(k);
+  };
+  if (layout == 2) go(std::integral_constant<int, 2>{});
+  else if (layout == 4) go(std::integral_constant<int, 4>{});
+  else go(std::integral_constant<int, 1>{});
 }
 
 }  // namespace rtseg

@@ -147,6 +147,10 @@ def wres_ok(conv, reduce_c: int, out_c: int, npix: int) -> bool:
             and _fits32(npix, reduce_c))
 
 
+# the 8-wave 1 x 4-tile conv_hreg layout as an autotune candidate (RTSEG_CONV_HREG4=0: off, A/B)
+_HREG4 = os.environ.get("RTSEG_CONV_HREG4", "1") != "0"
+
+
 def hreg_ok(conv, reduce_c: int, out_c: int, npix: int) -> bool:
     """Shapes ``conv_hreg`` takes (``csrc/kernels/conv_hreg.hip``): 3 x 3, stride 1, pad 1, dilation
     1, a 64-channel multiple summed over, a 128-channel multiple produced.  Two candidates: "hreg"
@@ -199,6 +203,8 @@ def _order(cands):
         cands.sort(key=lambda c: c[0] != "hreg")
     if os.environ.get("RTSEG_CONV_HREG") == "2":
         cands.sort(key=lambda c: c[0] != "hreg2")
+    if os.environ.get("RTSEG_CONV_HREG") == "4":
+        cands.sort(key=lambda c: c[0] != "hreg4")
     if os.environ.get("RTSEG_CONV_STEM") == "1":
         cands.sort(key=lambda c: c[0] != "stem")
     if os.environ.get("RTSEG_CONV_GEMM") == "1":
@@ -541,8 +547,8 @@ def _conv_fwd(x, weight, conv, stats, store=True):
         y, part = ops().conv_halo(x, wk, stride, padding, dilation, stats, None, None, 0)
     elif impl == "wres":
         y, part = ops().conv_wres(x, wk, stride, padding, dilation, stats)
-    elif impl in ("hreg", "hreg2"):
-        y, part = ops().conv_hreg(x, wk, stride, padding, dilation, stats, 2 if impl == "hreg2" else 1)
+    elif impl in ("hreg", "hreg2", "hreg4"):
+        y, part = ops().conv_hreg(x, wk, stride, padding, dilation, stats, {"hreg2": 2, "hreg4": 4}.get(impl, 1))
     elif impl == "mfma":
         y, part = ops().conv_mfma(x, wk, stride, padding, dilation, stats, None, None, 0)
     elif impl == "stem":
@@ -835,6 +841,8 @@ def _fwd_impl(x, wk, conv, key, stats) -> str:
         if hreg_ok(conv, cin, cout, _npix(x)):
             cands.append(("hreg", lambda: ops().conv_hreg(x, wk, stride, padding, dilation, stats, 1)))
             cands.append(("hreg2", lambda: ops().conv_hreg(x, wk, stride, padding, dilation, stats, 2)))
+            if _HREG4:
+                cands.append(("hreg4", lambda: ops().conv_hreg(x, wk, stride, padding, dilation, stats, 4)))
     elif cin % 32 == 0 and cout % 8 == 0:
         cands.append(("mfma", lambda: ops().conv_mfma(x, wk, stride, padding, dilation, stats, None, None, 0)))
     elif stem_ok(conv, x):
@@ -922,6 +930,8 @@ def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None, phase_a
     if hreg_ok(conv, cout, cin, _npix(x)):
         cands.append(("hreg", hreg))
         cands.append(("hreg2", lambda: hreg(2)))
+        if _HREG4:
+            cands.append(("hreg4", lambda: hreg(4)))
     if gemm_ok(conv):
         cands.append(("gemm", lambda: gemm_dgrad(dy, wk, x.shape, stride[0], addend_plain())))
     cands.append(("miopen", miopen))

@@ -247,7 +247,9 @@ def check_zoo_hip_matches_torch_path(key, monkeypatch):
       - the envelope is measured in the test: CPU fp32 plus ``ZOO_CPU_DRAWS`` ulp-perturbed fp32
         draws (``perturb_ulp``) and the GPU NCHW stock path;
       - the HIP path (plus up to ``ZOO_HIP_DRAWS`` ulp-perturbed re-runs, taken only while it is
-        outside) must land within ``ZOO_ENVELOPE_X`` x the envelope's largest error.
+        outside) must land within ``ZOO_ENVELOPE_X`` x the envelope's largest error, or within
+        ``ZOO_SAME_LAYOUT_X`` x the stock path run on the same channels-last tensors (which shares
+        MIOpen's channels-last fp32 convs: SegNet is 3.0e-2 off fp64 on both, profiles/r6_zoo_numerics).
       A kernel bug is systematic: it survives every HIP draw.  A flip does not."""
     monkeypatch.setenv("RTSEG_TUNE_FIXED", "1")  # conv choices by rule, not timing (reproducible)
     torch.manual_seed(0)
@@ -294,9 +296,19 @@ def check_zoo_hip_matches_torch_path(key, monkeypatch):
                                    monkeypatch)
             env.append(err(cat(g_d), cat(g_r)))
             lenv.append(abs(l_d.item() - l_r.item()))
+        # the stock path on the SAME channels-last tensors: it shares MIOpen's channels-last fp32
+        # convs with the HIP path, whose rounding moves discrete decisions the NCHW / CPU runs do not
+        # (SegNet: max-unpool positions after a ReLU, 3.0e-2 on both paths, profiles/r6_zoo_numerics)
+        _, l_s, g_s = _run_gpu(prep(copy.deepcopy(base).train()), xg, labels.cuda(), True, monkeypatch,
+                               f"{key} {bn} stock fp32 channels-last")
+        sg, sl = err(cat(g_s), cat(g_r)), abs(l_s.item() - l_r.item())
         hip = [hg]
         lh = abs(l_h.item() - l_r.item())
-        bound, lbound = ZOO_ENVELOPE_X * max(env), ZOO_ENVELOPE_X * max(max(lenv), 1e-7 * abs(l_r.item()))
+        # within the rounding envelope, or no worse than stock PyTorch on the same layout (whose own
+        # avg_pool2d backward is ~1e-2 off on the pooling models: that clause only ever adds a pass
+        # where the HIP path matches stock)
+        bound = max(ZOO_ENVELOPE_X * max(env), ZOO_SAME_LAYOUT_X * sg)
+        lbound = max(ZOO_ENVELOPE_X * max(max(lenv), 1e-7 * abs(l_r.item())), ZOO_SAME_LAYOUT_X * sl)
         for d in range(ZOO_HIP_DRAWS):
             if min(hip) <= bound and lh <= lbound:
                 break
@@ -305,8 +317,8 @@ def check_zoo_hip_matches_torch_path(key, monkeypatch):
             hip.append(err(cat(g_d), cat(g_r)))
             lh = min(lh, abs(l_d.item() - l_r.item()))
         tag = (f"{key} {bn}: HIP grad err {', '.join(f'{h:.2e}' for h in hip)}; envelope (CPU fp32, GPU NCHW, "
-               f"{ZOO_CPU_DRAWS} CPU draws) {', '.join(f'{e:.2e}' for e in env)}; loss err {lh:.2e} "
-               f"(envelope max {max(lenv):.2e})")
+               f"{ZOO_CPU_DRAWS} CPU draws) {', '.join(f'{e:.2e}' for e in env)}; stock channels-last {sg:.2e}; "
+               f"loss err {lh:.2e} (envelope max {max(lenv):.2e}, stock channels-last {sl:.2e})")
         print(tag)
         assert min(hip) <= bound, tag
         assert lh <= lbound, tag
@@ -341,6 +353,7 @@ def _check_bf16_vs_fp64(key, base, xg, labels, l_r, g_r, cat, err, monkeypatch):
 # the train-BN envelope (check_zoo_hip_matches_torch_path): ulp-perturbed CPU fp32 draws measured
 # per test, the factor on the envelope's largest error, and HIP re-draws taken while outside it
 ZOO_CPU_DRAWS, ZOO_ENVELOPE_X, ZOO_HIP_DRAWS = 3, 2.0, 2
+ZOO_SAME_LAYOUT_X = 1.5  # ... or within this factor of the stock path on the same channels-last tensors
 
 # HIP bf16 vs stock bf16 distance to fp64 (frozen BN, 128 x 256, batch 2).  Round 5 on MI355X: HIP
 # / stock between 0.14 (SwiftNet) and 1.14 (ENet), smallest stock 4.6e-3 (FastSCNN); the floor
