@@ -43,7 +43,7 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::
                                                  const std::optional<at::Tensor>& scale_shift,
                                                  const std::optional<at::Tensor>& residual, int64_t act, int kind) {
   // kind 7: the stem kernel's statistics without the output stores
-  const bool halo = kind == 1, wres = kind == 2, hreg = kind == 3 || kind == 4 || kind == 8, stem = kind == 5 || kind == 7;
+  const bool halo = kind == 1, wres = kind == 2, hreg = kind == 3 || kind == 4 || kind == 8 || kind == 9, stem = kind == 5 || kind == 7;
   check_act(x, "input");
   TORCH_CHECK(wk.is_cuda() && wk.dim() == 4 && wk.scalar_type() == at::kBFloat16 && wk.is_contiguous() &&
                   wk.size(3) == x.size(1),
@@ -100,7 +100,7 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::
   else if (wres) launch_conv_wres_fwd(g, cur_stream());
   else if (hreg) {
     at::Tensor wpack = at::empty({conv_hreg_pack_elems(g, 0)}, wk.options());
-    launch_conv_hreg(g, 0, wpack.data_ptr(), cur_stream(), kind == 4 ? 2 : kind == 8 ? 4 : 1);
+    launch_conv_hreg(g, 0, wpack.data_ptr(), cur_stream(), kind == 4 ? 2 : kind == 8 ? 4 : kind == 9 ? 5 : 1);
   } else launch_conv_igemm_fwd(g, cur_stream());
   if (stats && part.size(0) > 256) {  // fold the per-tile rows so the BN finalize stays cheap
     const int rows = static_cast<int>(part.size(0));
@@ -128,14 +128,15 @@ std::tuple<at::Tensor, at::Tensor> conv_halo(const at::Tensor& x, const at::Tens
 }
 
 // the register-weight halo kernel (conv_hreg.hip): 3 x 3 stride-1 convs, Cin % 64, Cout % 128
-// (rows_per_wave = wave layout 1: 8 waves of 2 x 2 tiles; 2: 4 waves of 2 x 4; 4: 8 waves of 1 x 4)
+// (rows_per_wave = wave layout 1: 8 waves of 2 x 2 tiles; 2: 4 waves of 2 x 4; 4: 8 waves of 1 x 4;
+// 5: layout 4 with double-buffered accumulators, the epilogue drained beside the next tile's MFMAs)
 std::tuple<at::Tensor, at::Tensor> conv_hreg(const at::Tensor& x, const at::Tensor& wk, at::IntArrayRef stride,
                                              at::IntArrayRef padding, at::IntArrayRef dilation, bool stats,
                                              int64_t rows_per_wave) {
-  TORCH_CHECK(rows_per_wave == 1 || rows_per_wave == 2 || rows_per_wave == 4,
-              "rtseg.conv_hreg: rows_per_wave (wave layout) must be 1, 2 or 4");
+  TORCH_CHECK(rows_per_wave == 1 || rows_per_wave == 2 || rows_per_wave == 4 || rows_per_wave == 5,
+              "rtseg.conv_hreg: rows_per_wave (wave layout) must be 1, 2, 4 or 5");
   return conv_fwd_impl(x, wk, stride, padding, dilation, stats, std::nullopt, std::nullopt, 0,
-                       rows_per_wave == 2 ? 4 : rows_per_wave == 4 ? 8 : 3);
+                       rows_per_wave == 2 ? 4 : rows_per_wave == 4 ? 8 : rows_per_wave == 5 ? 9 : 3);
 }
 
 // the weights-resident halo kernel (conv_wres.hip): 3 x 3 stride-1 convs with Cin == 64
@@ -193,7 +194,7 @@ at::Tensor conv_dgrad_impl(const at::Tensor& dy, const at::Tensor& wt, at::IntAr
                            const std::optional<at::Tensor>& bias, const std::optional<at::Tensor>& addend, int kind,
                            const std::optional<at::Tensor>& addend_mask,
                            const std::optional<at::Tensor>& phase_addend, bool fused_phases = false) {
-  const bool halo = kind == 1, wres = kind == 2, hreg = kind == 3 || kind == 4 || kind == 8;
+  const bool halo = kind == 1, wres = kind == 2, hreg = kind == 3 || kind == 4 || kind == 8 || kind == 9;
   check_act(dy, "grad_output");
   TORCH_CHECK(x_size.size() == 4, "rtseg.conv_igemm_dgrad: x_size must be [N, Cin, H, W]");
   TORCH_CHECK(wt.is_cuda() && wt.dim() == 4 && wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() &&
@@ -255,7 +256,7 @@ at::Tensor conv_dgrad_impl(const at::Tensor& dy, const at::Tensor& wt, at::IntAr
   else if (wres) launch_conv_wres_dgrad(g, cur_stream());
   else if (hreg) {
     at::Tensor wpack = at::empty({conv_hreg_pack_elems(g, 1)}, wt.options());
-    launch_conv_hreg(g, 1, wpack.data_ptr(), cur_stream(), kind == 4 ? 2 : kind == 8 ? 4 : 1);
+    launch_conv_hreg(g, 1, wpack.data_ptr(), cur_stream(), kind == 4 ? 2 : kind == 8 ? 4 : kind == 9 ? 5 : 1);
   } else if (fused_phases) {
     launch_conv_igemm_dgrad_fused(g, cur_stream());
   } else {
@@ -284,10 +285,11 @@ at::Tensor conv_hreg_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntAr
                            at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
                            const std::optional<at::Tensor>& addend, int64_t rows_per_wave,
                            const std::optional<at::Tensor>& addend_mask) {
-  TORCH_CHECK(rows_per_wave == 1 || rows_per_wave == 2 || rows_per_wave == 4,
-              "rtseg.conv_hreg_dgrad: rows_per_wave (wave layout) must be 1, 2 or 4");
+  TORCH_CHECK(rows_per_wave == 1 || rows_per_wave == 2 || rows_per_wave == 4 || rows_per_wave == 5,
+              "rtseg.conv_hreg_dgrad: rows_per_wave (wave layout) must be 1, 2, 4 or 5");
   return conv_dgrad_impl(dy, wt, x_size, stride, padding, dilation, std::nullopt, addend,
-                         rows_per_wave == 2 ? 4 : rows_per_wave == 4 ? 8 : 3, addend_mask, std::nullopt);
+                         rows_per_wave == 2 ? 4 : rows_per_wave == 4 ? 8 : rows_per_wave == 5 ? 9 : 3, addend_mask,
+                         std::nullopt);
 }
 
 at::Tensor conv_wres_dgrad(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,

@@ -87,10 +87,10 @@ class _BNActFn(torch.autograd.Function):
             else:  # SyncBN: one all-reduce of (sum, sumsq, count) in fp64 over RCCL
                 if pending is not None:  # issued by bn_stats_begin (async): wait for it here
                     sums, work = pending
-                    work.wait()
-                else:
+                else:  # issued here, asynchronously as everywhere: the wait is the finalize's dependency
                     sums = ops().bn_slab_sums(part, count) if part is not None else ops().bn_stats_sums(x)
-                    dist.all_reduce(sums, group=pg)
+                    work = dist.all_reduce(sums, group=pg, async_op=True)
+                work.wait()
                 mi, ss = ops().bn_finalize(sums, weight, bias, rm, rv, nb, float(bn.momentum),
                                            float(bn.eps))
             if rm is not None:

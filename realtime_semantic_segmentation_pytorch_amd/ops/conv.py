@@ -149,6 +149,11 @@ def wres_ok(conv, reduce_c: int, out_c: int, npix: int) -> bool:
 
 # the 8-wave 1 x 4-tile conv_hreg layout as an autotune candidate (RTSEG_CONV_HREG4=0: off, A/B)
 _HREG4 = os.environ.get("RTSEG_CONV_HREG4", "1") != "0"
+# ... and the same layout with double-buffered accumulators: the epilogue of tile t drained beside
+# tile t + 1's MFMAs.  Opt-in (RTSEG_CONV_HREG5=1): measured neutral -- 359 vs 355 us (fwd + stats)
+# and 346 vs 349 us (dgrad) on the 128-channel layer, headline 566.2-567.0 images/s either way
+# (profiles/r6_hreg)
+_HREG5 = os.environ.get("RTSEG_CONV_HREG5", "0") == "1"
 
 
 def hreg_ok(conv, reduce_c: int, out_c: int, npix: int) -> bool:
@@ -205,6 +210,8 @@ def _order(cands):
         cands.sort(key=lambda c: c[0] != "hreg2")
     if os.environ.get("RTSEG_CONV_HREG") == "4":
         cands.sort(key=lambda c: c[0] != "hreg4")
+    if os.environ.get("RTSEG_CONV_HREG") == "5":
+        cands.sort(key=lambda c: c[0] != "hreg5")
     if os.environ.get("RTSEG_CONV_STEM") == "1":
         cands.sort(key=lambda c: c[0] != "stem")
     if os.environ.get("RTSEG_CONV_GEMM") == "1":
@@ -547,8 +554,9 @@ def _conv_fwd(x, weight, conv, stats, store=True):
         y, part = ops().conv_halo(x, wk, stride, padding, dilation, stats, None, None, 0)
     elif impl == "wres":
         y, part = ops().conv_wres(x, wk, stride, padding, dilation, stats)
-    elif impl in ("hreg", "hreg2", "hreg4"):
-        y, part = ops().conv_hreg(x, wk, stride, padding, dilation, stats, {"hreg2": 2, "hreg4": 4}.get(impl, 1))
+    elif impl in ("hreg", "hreg2", "hreg4", "hreg5"):
+        y, part = ops().conv_hreg(x, wk, stride, padding, dilation, stats,
+                                  {"hreg2": 2, "hreg4": 4, "hreg5": 5}.get(impl, 1))
     elif impl == "mfma":
         y, part = ops().conv_mfma(x, wk, stride, padding, dilation, stats, None, None, 0)
     elif impl == "stem":
@@ -843,6 +851,8 @@ def _fwd_impl(x, wk, conv, key, stats) -> str:
             cands.append(("hreg2", lambda: ops().conv_hreg(x, wk, stride, padding, dilation, stats, 2)))
             if _HREG4:
                 cands.append(("hreg4", lambda: ops().conv_hreg(x, wk, stride, padding, dilation, stats, 4)))
+            if _HREG5:
+                cands.append(("hreg5", lambda: ops().conv_hreg(x, wk, stride, padding, dilation, stats, 5)))
     elif cin % 32 == 0 and cout % 8 == 0:
         cands.append(("mfma", lambda: ops().conv_mfma(x, wk, stride, padding, dilation, stats, None, None, 0)))
     elif stem_ok(conv, x):
@@ -932,6 +942,8 @@ def _dgrad(x, dy, wk, conv, key, stride, padding, dilation, addend=None, phase_a
         cands.append(("hreg2", lambda: hreg(2)))
         if _HREG4:
             cands.append(("hreg4", lambda: hreg(4)))
+        if _HREG5:
+            cands.append(("hreg5", lambda: hreg(5)))
     if gemm_ok(conv):
         cands.append(("gemm", lambda: gemm_dgrad(dy, wk, x.shape, stride[0], addend_plain())))
     cands.append(("miopen", miopen))
@@ -1250,8 +1262,13 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Module, bn: nn.Module, act="none", res
                 if y is not None:
                     return y
             else:
+                from .bn import bn_stats_begin
+
                 y, part = conv_bn_stats(x, conv)
-                return bn_act(y, bn, code, residual=residual, act_module=act_module, part=part)
+                # SyncBN: the statistics all-reduce leaves from the conv's epilogue slab right away
+                # (async; None when not a multi-rank SyncBN) and bn_act waits at its finalize
+                pending = bn_stats_begin(y, bn, part)
+                return bn_act(y, bn, code, residual=residual, act_module=act_module, part=part, pending=pending)
     return bn_act(conv_forward(x, conv), bn, act, residual=residual, act_module=act_module)
 
 

@@ -176,7 +176,7 @@ def test_whalo_wgrad(geom, channels_last, variant):
 HREG = [(2, 64, 9, 70, 128), (1, 128, 17, 130, 128), (3, 192, 6, 40, 256), (8, 128, 66, 256, 128)]
 
 
-@pytest.mark.parametrize("rpw", [1, 2, 4])
+@pytest.mark.parametrize("rpw", [1, 2, 4, 5])
 @pytest.mark.parametrize("geom", HREG)
 def test_hreg_forward_and_stats(geom, rpw):
     n, cin, h, w, cout = geom
@@ -197,7 +197,7 @@ def test_hreg_forward_and_stats(geom, rpw):
     assert torch.equal(y2, y)
 
 
-@pytest.mark.parametrize("rpw", [1, 2, 4])
+@pytest.mark.parametrize("rpw", [1, 2, 4, 5])
 @pytest.mark.parametrize("geom", HREG)
 @pytest.mark.parametrize("with_addend", [False, True, "masked"])
 def test_hreg_dgrad(geom, with_addend, rpw):

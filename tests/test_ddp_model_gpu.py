@@ -47,7 +47,12 @@ def _batches():
     out = []
     for _ in range(STEPS):
         img = torch.randn(GLOBAL_BS, 3, *SIZE, generator=g)
-        out.append((img, _masks_like(g, GLOBAL_BS, SIZE[0], SIZE[1], 19, 255, "cpu")))
+        msk = _masks_like(g, GLOBAL_BS, SIZE[0], SIZE[1], 19, 255, "cpu")
+        # no ignored pixels: every image then has the same number of valid pixels, so DDP's average
+        # of the two half-batch mean losses IS the mean over the whole batch, and the 2-rank vs
+        # 1-process comparison measures numerics alone (round 5 bounded a structural 1e-2 instead)
+        msk = torch.where(msk == 255, torch.zeros_like(msk), msk)
+        out.append((img, msk))
     return out
 
 

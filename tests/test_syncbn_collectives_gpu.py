@@ -3,7 +3,9 @@ GPU; RCCL needs one GPU per rank).
 
 Per step, for DDRNet-23-slim + aux head (reference wiring utils/parallel.py:34-43):
 * exactly ONE forward SyncBN all-reduce ([2C+1] fp64 sums) and ONE backward all-reduce ([2C])
-  per SyncBatchNorm layer, all on the SyncBN process group (parallel/ddp.py:syncbn_group);
+  per SyncBatchNorm layer, all on the SyncBN process group (parallel/ddp.py:syncbn_group); the
+  forward ones asynchronous (issued from the producing conv's statistics slab, waited at the BN
+  finalize) at >= 80 % of the sites;
 * the backward ones mostly issued early, asynchronously, from the consumer conv's backward
   (ops.bn.syncbn_bwd_early) -- counted, and required to be > 0.  A site whose output turns out to
   have a second consumer wastes its early reduction once (step 1) and never issues early again;
@@ -88,6 +90,7 @@ def _run(rank, world, port, out):
         tr.train_step(imgs, masks)
         torch.cuda.synchronize()
         per_step.append({"fwd": sum(1 for k, odd, _ in calls if k == "sbn" and odd == 1),
+                         "fwd_async": sum(1 for k, odd, asy in calls if k == "sbn" and odd == 1 and asy),
                          "bwd": sum(1 for k, odd, _ in calls if k == "sbn" and odd == 0),
                          "other": sum(1 for k, _, _ in calls if k != "sbn"),
                          "early": bn_mod.EARLY_ISSUED[0] - e0,
@@ -122,6 +125,8 @@ def test_syncbn_and_ddp_collectives_per_step(tmp_path):
     cap = BUCKET_MB * 2 ** 20
     for i, st in enumerate(r["per_step"]):
         assert st["fwd"] == r["n_sbn"], st
+        # forward statistics all-reduces are issued asynchronously (waited at the BN finalize)
+        assert st["fwd_async"] >= 0.8 * st["fwd"], st
         assert st["early"] > 0, st
         assert st["bucket_numel"] == r["n_grad"], st  # every gradient element exactly once
         # the DDP allreduce hook's own dist.all_reduce calls (one per bucket): nothing else

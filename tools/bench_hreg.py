@@ -47,12 +47,12 @@ def main():
         flop = 2.0 * n * h * w * cin * cout * 9
         passes = {
             "fwd+st": {"igemm": lambda: r.conv_igemm(x, wk, [1, 1], [1, 1], [1, 1], True, None, None, 0)[0]}
-            | {f"hreg{k}": (lambda k=k: r.conv_hreg(x, wk, [1, 1], [1, 1], [1, 1], True, k)[0]) for k in (1, 2, 4)},
+            | {f"hreg{k}": (lambda k=k: r.conv_hreg(x, wk, [1, 1], [1, 1], [1, 1], True, k)[0]) for k in (1, 2, 4, 5)},
         }
         if cin % 128 == 0:  # the dgrad produces Cin channels: % 128
             passes["dgrad"] = {"igemm": lambda: r.conv_igemm_dgrad(dy, wtr, list(x.shape), [1, 1], [1, 1], [1, 1])} | {
                 f"hreg{k}": (lambda k=k: r.conv_hreg_dgrad(dy, wtr, list(x.shape), [1, 1], [1, 1], [1, 1], None, k))
-                for k in (1, 2, 4)}
+                for k in (1, 2, 4, 5)}
         for pname, fns in passes.items():
             ref = fns["igemm"]().float()
             row = []

@@ -46,6 +46,8 @@ def main():
         "hreg2_dg": lambda: r.conv_hreg_dgrad(dy, wtr, list(x.shape), [1, 1], [1, 1], [1, 1], None, 2),
         "hreg4": lambda: r.conv_hreg(x, wk, [1, 1], [1, 1], [1, 1], a.stats, 4),
         "hreg4_dg": lambda: r.conv_hreg_dgrad(dy, wtr, list(x.shape), [1, 1], [1, 1], [1, 1], None, 4),
+        "hreg5": lambda: r.conv_hreg(x, wk, [1, 1], [1, 1], [1, 1], a.stats, 5),
+        "hreg5_dg": lambda: r.conv_hreg_dgrad(dy, wtr, list(x.shape), [1, 1], [1, 1], [1, 1], None, 5),
     }
     if a.kind.startswith("stem"):  # the 3-channel stem at DDRNet-23's geometry (cin = 3, stride 2)
         xs = torch.randn(a.batch, 3, h, w, device="cuda", dtype=torch.bfloat16).contiguous(
