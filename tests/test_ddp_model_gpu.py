@@ -32,6 +32,11 @@ MODELS = {
     "ddrnet23slim_aux": {"model": "ddrnet", "arch_type": "DDRNet-23-slim", "use_aux": True},
 }
 GLOBAL_BS, SIZE, STEPS = 4, (128, 256), 2
+# fp32 step-1 update, 2 ranks vs 1 process (relative norm of the difference).  Measured on MI355X
+# with no ignored pixels (profiles/r6_start): DDRNet-23-slim 2.7e-3, BiSeNetV2 1.6e-2, STDC2 3.3e-2 --
+# batch-statistics BN over 4 random-init images amplifies reduction-order rounding (the same chaos
+# as tests/test_zoo.py's train-BN pass); the BN running statistics agree to 4e-8
+FP32_REL = {"ddrnet23slim_aux": 1e-2, "bisenetv2_aux": 5e-2, "stdc2_aux": 5e-2}
 
 
 def _port():
@@ -215,7 +220,7 @@ def test_ddp_two_ranks_match_one_process(tmp_path, name):
     cos, rel, ema_rel, bn_rel, cos2 = res[False]
     # fp32: reduction order (SyncBN fp64 sums) and DDP's average of the two half-batch mean losses
     # (the halves' valid-pixel counts differ) vs one mean over the whole batch
-    assert cos > 0.999 and rel < 5e-2 and ema_rel < 5e-2 and bn_rel < 1e-4, res[False]
+    assert cos > 0.999 and rel < FP32_REL[name] and ema_rel < FP32_REL[name] and bn_rel < 1e-4, res[False]
     cos, rel, ema_rel, bn_rel, cos2 = res[True]
     # bf16: at random init on a 4-image batch the bf16 gradient itself is noisy (per-parameter
     # cosine to fp64 ~0.93, tests/test_train_numerics_gpu.py), so two bf16 runs need not agree
