@@ -24,6 +24,7 @@
 #include "rtseg_vec.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 namespace rtseg {
@@ -70,14 +71,30 @@ __device__ __forceinline__ void load_wvec(const float* p, float* w) {
 // never re-reads y.  Deterministic: the host makes gridDim.x * kDwBlock a multiple of the
 // channel-vector count, so each thread keeps ONE channel vector for all its iterations and
 // accumulates it in registers; the block then sums its threads in a fixed order through LDS.
-template <typename T, int VEC, int MT, int KS, bool STATS = false>
+// CSW (channel-stationary weights, MT == 1 and KS > 0 only): the host sizes the grid so every
+// thread keeps ONE channel vector (gridDim.x * kDwBlock a multiple of the channel-vector count, as
+// for STATS), and the thread's KS x KS x VEC weights are loaded into registers once instead of
+// per output pixel -- the unrolled taps then issue only their input loads (KS^2 in flight).  Per
+// output that removes 9 x 32 B of weight loads against 9 x 16 B of activations (the reason an
+// unrolled 3 x 3 without it measured 4-5x slower: see launch_dw_fwd).
+template <typename T, int VEC, int MT, int KS, bool STATS = false, bool CSW = false>
 __global__ void __launch_bounds__(kDwBlock) dw_fwd_kernel(DwGeom g, DwDivs fd, const T* __restrict__ x,
                                                           const float* __restrict__ wt,
                                                           const float* __restrict__ bias, T* __restrict__ y,
                                                           float* __restrict__ part = nullptr) {
+  static_assert(!CSW || (MT == 1 && KS > 0), "channel-stationary weights: MT 1, compile-time taps");
   constexpr int OV = MT > 1 ? VEC * MT : VEC;  // output channels per thread
   const int cv_n = MT > 1 ? g.cin / VEC : g.cout / VEC;
   const uint32_t total = static_cast<uint32_t>(g.n) * g.ho * g.wo * cv_n;  // < 2^31 (host splits)
+  float wreg[CSW ? KS * KS : 1][CSW ? VEC : 1];
+  float breg[CSW ? VEC : 1];
+  if constexpr (CSW) {
+    const int co = static_cast<int>((blockIdx.x * kDwBlock + threadIdx.x) % static_cast<uint32_t>(cv_n)) * VEC;
+#pragma unroll
+    for (int t = 0; t < KS * KS; ++t) load_wvec<VEC>(wt + t * g.cout + co, wreg[t]);
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) breg[v] = bias ? bias[co + v] : 0.f;
+  }
   float ssum[STATS ? OV : 1], ssq[STATS ? OV : 1];
   if constexpr (STATS) {
 #pragma unroll
@@ -93,7 +110,10 @@ __global__ void __launch_bounds__(kDwBlock) dw_fwd_kernel(DwGeom g, DwDivs fd, c
     const int ci = cv * VEC;                             // first input channel (MT > 1)
     float acc[OV];
 #pragma unroll
-    for (int v = 0; v < OV; ++v) acc[v] = bias ? bias[co + v] : 0.f;
+    for (int v = 0; v < OV; ++v) {
+      if constexpr (CSW) acc[v] = breg[v];
+      else acc[v] = bias ? bias[co + v] : 0.f;
+    }
     const int hb = ho * g.sh - g.ph, wb = wo * g.sw - g.pw;
     // branch-free tap: clamped (always valid) load, product selected away outside the image
     auto tap = [&](int i, int j) {
@@ -103,7 +123,12 @@ __global__ void __launch_bounds__(kDwBlock) dw_fwd_kernel(DwGeom g, DwDivs fd, c
       const float* wp = wt + (i * g.kw + j) * g.cout + co;
       const T* xp = x + ((static_cast<int64_t>(n) * g.h + hc) * g.w + wc) * g.cin;
       float xv[VEC], wv[OV];
-      load_wvec<OV>(wp, wv);
+      if constexpr (CSW) {
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) wv[v] = wreg[KS > 0 ? i * KS + j : 0][v];
+      } else {
+        load_wvec<OV>(wp, wv);
+      }
       if constexpr (MT == 1) {
         Vec<T, VEC>::load(xp + co, xv);
       } else if constexpr (MT > 1) {
@@ -405,6 +430,14 @@ static int batch_chunk(int64_t per_image, int n) {
 
 static int64_t elem_bytes(int dtype) { return dtype == kF32 ? 4 : 2; }
 
+static int dw_stats_grid(int64_t items, int cv_n);
+
+// RTSEG_DW_CS=0: the 3 x 3 channel-stationary register-weight forward off (A/B)
+static bool dw_cs_enabled() {
+  static const bool on = [] { const char* e = std::getenv("RTSEG_DW_CS"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
 void launch_dw_fwd(const DwGeom& g0, int dtype, const void* x, const float* wt, const float* bias, void* y,
                    hipStream_t st) {
   const int mt = mt_of(g0.mult);
@@ -420,12 +453,20 @@ void launch_dw_fwd(const DwGeom& g0, int dtype, const void* x, const float* wt, 
     const char* xb = static_cast<const char*>(x) + static_cast<int64_t>(n0) * g.h * g.w * g.cin * eb;
     char* yb = static_cast<char*>(y) + static_cast<int64_t>(n0) * g.ho * g.wo * g.cout * eb;
     const DwDivs fd{FastDiv::make(cv_n), FastDiv::make(g.wo), FastDiv::make(g.ho)};
-    const int grid = stream_grid(per_img * g.n, kDwBlock);
+    const bool cs3 = mt == 1 && g.kh == 3 && g.kw == 3 && dw_cs_enabled();
+    const int grid = cs3 ? dw_stats_grid(per_img * g.n, cv_n) : stream_grid(per_img * g.n, kDwBlock);
     dw_dispatch(dtype, vec, g.mult, [&](auto t, auto v, auto m) {
       using T = decltype(t);
       constexpr int V = decltype(v)::value, M = decltype(m)::value;
-      // KS = 0: runtime tap loop.  A fully unrolled 3x3 (KS = 3) measured 4-5x slower on
-      // BiSeNetV2 (it re-loads all 9 taps' weights per output with no latency to hide).
+      if constexpr (M == 1) {
+        if (cs3) {  // 3 x 3, channel-stationary: weights in registers, 9 loads in flight
+          dw_fwd_kernel<T, V, 1, 3, false, true><<<grid, kDwBlock, 0, st>>>(
+              g, fd, reinterpret_cast<const T*>(xb), wt, bias, reinterpret_cast<T*>(yb));
+          return;
+        }
+      }
+      // KS = 0: runtime tap loop.  A fully unrolled 3x3 (KS = 3) WITHOUT register weights measured
+      // 4-5x slower on BiSeNetV2 (it re-loads all 9 taps' weights per output with no latency to hide)
       dw_fwd_kernel<T, V, M, 0><<<grid, kDwBlock, 0, st>>>(g, fd, reinterpret_cast<const T*>(xb), wt, bias,
                                                              reinterpret_cast<T*>(yb));
     });
@@ -478,6 +519,13 @@ void launch_dw_fwd_stats(const DwGeom& g0, int dtype, const void* x, const float
     dw_dispatch(dtype, vec, g.mult, [&](auto t, auto v, auto m) {
       using T = decltype(t);
       constexpr int V = decltype(v)::value, M = decltype(m)::value;
+      if constexpr (M == 1) {
+        if (g.kh == 3 && g.kw == 3 && dw_cs_enabled()) {  // the grid is channel-stationary already
+          dw_fwd_kernel<T, V, 1, 3, true, true><<<grid, kDwBlock, 0, st>>>(
+              g, fd, reinterpret_cast<const T*>(xb), wt, nullptr, reinterpret_cast<T*>(yb), part);
+          return;
+        }
+      }
       if constexpr (M != 0) {
         dw_fwd_kernel<T, V, M, 0, true><<<grid, kDwBlock, 0, st>>>(g, fd, reinterpret_cast<const T*>(xb), wt, nullptr,
                                                                      reinterpret_cast<T*>(yb), part);
