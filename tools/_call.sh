@@ -1,8 +1,7 @@
 set -o pipefail
-mkdir -p gpurun_out/r6_dw
-timeout -k 10 400 python -u -m pytest tests/test_dwconv_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r6_dw/tests.log 2>&1 || { tail -30 gpurun_out/r6_dw/tests.log; exit 1; }
-tail -1 gpurun_out/r6_dw/tests.log
-RTSEG_DW_CS=0 timeout -k 10 200 python -u tools/bench_dw.py > gpurun_out/r6_dw/bench_base.txt 2>&1 || exit 1
-timeout -k 10 200 python -u tools/bench_dw.py > gpurun_out/r6_dw/bench_cs.txt 2>&1 || exit 1
-cat gpurun_out/r6_dw/bench_base.txt gpurun_out/r6_dw/bench_cs.txt | grep -v amdgpu
-timeout -k 10 600 python -u -m pytest tests/test_syncbn_collectives_gpu.py -x -q --timeout 300 --timeout-method thread > gpurun_out/r6_dw/coll.log 2>&1; tail -3 gpurun_out/r6_dw/coll.log
+mkdir -p gpurun_out/r6_kd
+timeout -k 10 500 python -u bench.py --kd --batch 16 --steps 10 --warmup 4 --no-infer > gpurun_out/r6_kd/bench_kd_b16.json 2> gpurun_out/r6_kd/bench_kd.err || { tail -20 gpurun_out/r6_kd/bench_kd.err; exit 1; }
+tail -1 gpurun_out/r6_kd/bench_kd_b16.json | cut -c1-200
+PROF_SKIP=4 PROF_PER_STEP=2 timeout -k 10 600 bash tools/profile_bench.sh gpurun_out/r6_kd/prof --kd --batch 16 --steps 6 --warmup 4 > gpurun_out/r6_kd/prof.log 2>&1 || { tail -20 gpurun_out/r6_kd/prof.log; exit 1; }
+rm -f gpurun_out/r6_kd/prof/trace.csv.gz
+head -50 gpurun_out/r6_kd/prof/steady.txt | cut -c1-170
