@@ -188,6 +188,32 @@ at::Tensor conv_stem_bn_act(const at::Tensor& x, const at::Tensor& wk, at::IntAr
   return std::get<0>(conv_fwd_impl(x, wk, stride, padding, dilation, false, scale_shift, std::nullopt, act, 5));
 }
 
+// the 7 x 7 stem (conv_stem7.hip): x [N,3,H,W] CL bf16, wk [Cout,7,7,3] bf16 -> y [N,Cout,Ho,Wo] CL
+// bf16, = act(conv * scale + shift) when scale_shift is given (inference BN epilogue)
+at::Tensor conv_stem7(const at::Tensor& x, const at::Tensor& wk, at::IntArrayRef stride,
+                      const std::optional<at::Tensor>& scale_shift, int64_t act) {
+  check_act(x, "input");
+  TORCH_CHECK(wk.is_cuda() && wk.dim() == 4 && wk.scalar_type() == at::kBFloat16 && wk.is_contiguous() &&
+                  wk.size(1) == 7 && wk.size(2) == 7 && wk.size(3) == 3 && x.size(1) == 3,
+              "rtseg.conv_stem7: weights must be contiguous bf16 [Cout, 7, 7, 3] on a 3-channel input");
+  const int64_t pad[2] = {3, 3}, dil[2] = {1, 1};
+  ConvGeom g = geom(x.size(0), 3, x.size(2), x.size(3), wk.size(0), 7, 7, stride, pad, dil);
+  TORCH_CHECK(conv_stem7_supported(g), "rtseg.conv_stem7: needs stride 1 / 2, Cout % 16 <= 64, even W");
+  if (scale_shift.has_value() && scale_shift->defined()) {
+    TORCH_CHECK(scale_shift->is_cuda() && scale_shift->scalar_type() == at::kFloat &&
+                    scale_shift->numel() == 2 * g.cout && scale_shift->is_contiguous(),
+                "rtseg.conv_stem7: scale_shift must be fp32 [2 cout]");
+    TORCH_CHECK(act >= 0 && act <= 2, "rtseg.conv_stem7: bad activation");
+    g.scale_shift = scale_shift->data_ptr<float>();
+    g.act = static_cast<int>(act);
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  at::Tensor y = at::empty({g.n, g.cout, g.ho, g.wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  g.x = x.data_ptr(); g.w = wk.data_ptr(); g.y = y.data_ptr();
+  launch_conv_stem7_fwd(g, cur_stream());
+  return y;
+}
+
 // dy [N,Cout,Ho,Wo] CL bf16, wt [Cin,KH,KW,Cout] bf16 -> dx [N,Cin,H,W] CL bf16
 at::Tensor conv_dgrad_impl(const at::Tensor& dy, const at::Tensor& wt, at::IntArrayRef x_size,
                            at::IntArrayRef stride, at::IntArrayRef padding, at::IntArrayRef dilation,
@@ -424,6 +450,7 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
         "Tensor? addend=None, Tensor? addend_mask=None) -> Tensor");
   m.def("conv_stem(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats, bool store=True) "
         "-> (Tensor, Tensor)");
+  m.def("conv_stem7(Tensor x, Tensor wk, int[] stride, Tensor? scale_shift, int act) -> Tensor");
   m.def("conv_stem_bn_act(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, Tensor scale_shift, "
         "int act) -> Tensor");
   m.def("conv_stem_bn_sums(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, Tensor dy, "
@@ -452,6 +479,7 @@ TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
   m.impl("conv_whalo_wgrad", &rtseg::conv_whalo_wgrad);
   m.impl("conv_stem", &rtseg::conv_stem);
   m.impl("conv_stem_bn_act", &rtseg::conv_stem_bn_act);
+  m.impl("conv_stem7", &rtseg::conv_stem7);
   m.impl("conv_stem_bn_sums", &rtseg::conv_stem_bn_sums);
   m.impl("conv_stem_wgrad_bn", &rtseg::conv_stem_wgrad_bn);
   m.impl("conv_stem_wgrad", &rtseg::conv_stem_wgrad);

@@ -241,6 +241,10 @@ void launch_conv_hreg(const ConvGeom& g, int mode, void* wpack, hipStream_t st, 
 // 3-channel 3 x 3 stem conv (pad 1, stride 1 / 2, Cout % 16 == 0 and <= 64, even W): forward
 // (+ BN statistics slab of conv_stem_slabs(g) rows) and weight gradient (g.x = x, g.y = dy).
 bool conv_stem_supported(const ConvGeom& g);
+// 7 x 7 / pad 3 / stride 1 or 2 stem (conv_stem7.hip): Cin 3, Cout % 16 <= 64, even W; forward with
+// an optional inference BN (+ act) epilogue (g.scale_shift, g.act)
+bool conv_stem7_supported(const ConvGeom& g);
+void launch_conv_stem7_fwd(const ConvGeom& g, hipStream_t st);
 int conv_stem_slabs(const ConvGeom& g);
 // stem BN backward reduction with the conv recomputed from the image (g.y = the BN output's gradient)
 void launch_conv_stem_bn_sums(const ConvGeom& g, const float* mean_invstd, const float* scale_shift, int act,

@@ -1073,6 +1073,8 @@ def conv_bn_act_eval(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, act_code: 
                                      and residual.dim() == 4):
         return None
     cin, cout = conv.in_channels, conv.out_channels
+    if residual is None and stem7_ok(conv, x):
+        return _stem7_eval(x, conv, bn, act_code)
     if cout % 8 or cin % 32:
         return None
     x = x.to(torch.bfloat16)
@@ -1096,6 +1098,44 @@ def conv_bn_act_eval(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, act_code: 
         ops().bn_apply(y, ss, res, act_code)
 
     if _choose(key, [("igemm" if cin % 64 == 0 else "mfma", ours), ("miopen", theirs)]) != 0:
+        return None
+    return ours()
+
+
+def stem7_ok(conv: nn.Module, x: torch.Tensor) -> bool:
+    """A torchvision-style 7 x 7 / pad 3 / stride 2 (or 1) stem on 3 channels with <= 64 (% 16)
+    outputs and an even width: ``conv_stem7.hip`` (``RTSEG_CONV_STEM7=0``: off)."""
+    return (conv.in_channels == 3 and conv.groups == 1 and tuple(conv.kernel_size) == (7, 7)
+            and tuple(conv.padding) == (3, 3) and tuple(conv.dilation) == (1, 1)
+            and tuple(conv.stride) in ((1, 1), (2, 2)) and conv.out_channels % 16 == 0 and conv.out_channels <= 64
+            and conv.bias is None and x.dim() == 4 and x.shape[1] == 3 and x.shape[3] % 2 == 0
+            and conv.padding_mode == "zeros" and os.environ.get("RTSEG_CONV_STEM7", "1") != "0")
+
+
+def _stem7_eval(x: torch.Tensor, conv: nn.Module, bn: nn.Module, act_code: int):
+    """Inference ``act(BN_running(conv(x)))`` of a 7 x 7 stem in one pass (the BN + act on the
+    conv's fp32 accumulators), timed once per shape against MIOpen + the BN apply; None -> the
+    caller's path.  The KD teacher's ResNet-101 stem (BASELINE config 5): MIOpen took 1.1 ms per
+    batch-16 1024 x 2048 call channels-last, plus a BN pass over its 1 GB output
+    (tools/bench_stem7.py, profiles/r6_kd)."""
+    from .bn import eval_coeffs
+
+    x = x.to(torch.bfloat16)
+    if not x.is_contiguous(memory_format=torch.channels_last) or x.data_ptr() % 16:
+        x = x.contiguous(memory_format=torch.channels_last).clone(memory_format=torch.channels_last)
+    wk = weight_krsc(conv)
+    _, ss = eval_coeffs(bn)
+    stride = list(conv.stride)
+
+    def ours():
+        return ops().conv_stem7(x, wk, stride, ss, act_code)
+
+    def theirs():
+        y = F.conv2d(x, wk.permute(0, 3, 1, 2), None, stride, [3, 3], [1, 1])
+        ops().bn_apply(y, ss, None, act_code)
+
+    key = ("eval-stem7", tuple(x.shape), conv.out_channels, tuple(stride), act_code)
+    if _choose(key, [("stem7", ours), ("miopen", theirs)]) != 0:
         return None
     return ours()
 

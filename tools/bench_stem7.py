@@ -1,5 +1,6 @@
 """The KD teacher's ResNet stem (7 x 7 / 2, 3 -> 64, batch 16, 1024 x 2048, bf16) on MIOpen in each
-memory layout (the channels-last pick measured 1.5 ms per call in the KD profile, profiles/r6_kd).
+memory layout (the channels-last pick measured 1.5 ms per call in the KD profile, profiles/r6_kd),
+and the native conv_stem7.hip kernel (alone, and with the inference BN + ReLU epilogue).
 python tools/bench_stem7.py"""
 import os
 import sys
@@ -32,7 +33,13 @@ def main():
     xcl = x.contiguous(memory_format=torch.channels_last)
     wcl = w.contiguous(memory_format=torch.channels_last)
     ref = F.conv2d(x.float()[:1], w.float(), None, 2, 3)
-    for name, fn in [("nchw", lambda: F.conv2d(x, w, None, 2, 3)),
+    from realtime_semantic_segmentation_pytorch_amd import ops
+
+    assert ops.load()
+    wk = w.permute(0, 2, 3, 1).contiguous()
+    ss = torch.cat([torch.ones(64), torch.zeros(64)]).cuda()
+    for name, fn in [("rtseg conv_stem7", lambda: torch.ops.rtseg.conv_stem7(xcl, wk, [2, 2], None, 0)),
+                     ("rtseg conv_stem7 + BN/ReLU", lambda: torch.ops.rtseg.conv_stem7(xcl, wk, [2, 2], ss, 1)),("nchw", lambda: F.conv2d(x, w, None, 2, 3)),
                      ("channels_last", lambda: F.conv2d(xcl, wcl, None, 2, 3)),
                      ("nchw + to channels_last", lambda: F.conv2d(xcl.contiguous(), w, None, 2, 3).contiguous(
                          memory_format=torch.channels_last))]:
