@@ -109,10 +109,10 @@ def get_detail_loss_fn(config):
 
 def kd_loss_fn(config, outputs, outputsT):
     """Knowledge-distillation loss between student and (detached) teacher logits."""
-    outputs = ops.materialize(outputs)
     outputsT = ops.materialize(outputsT).detach()
-    if config.kd_loss_type == "kl_div":
+    if config.kd_loss_type == "kl_div":  # (deferred student logits: the upsample folds into the KD kernels)
         return ops.kd_kl_div(outputs, outputsT, config.kd_temperature)
+    outputs = ops.materialize(outputs)
     if config.kd_loss_type == "mse":
         return F.mse_loss(outputs, outputsT)
     raise NotImplementedError(f"Unsupported kd loss type: {config.kd_loss_type}")

@@ -45,6 +45,39 @@ static at::Tensor kd_kl_bwd(const at::Tensor& grad, const at::Tensor& s, const a
   return gs;
 }
 
+// KD with the student's final upsample folded in: s_lo at head resolution, t at full resolution
+static std::tuple<at::Tensor, at::Tensor> kd_kl_fwd_fold(const at::Tensor& s_lo, const at::Tensor& t,
+                                                         double temperature, bool align_corners) {
+  TORCH_CHECK(s_lo.is_cuda() && t.is_cuda() && s_lo.dim() == 4 && t.dim() == 4, "rtseg.kd_fold: 4-D GPU tensors");
+  TORCH_CHECK(temperature > 0.0, "rtseg.kd: temperature must be > 0");
+  TORCH_CHECK(kd_fold_ok(view4(s_lo), view4(t)), "rtseg.kd_fold: needs dense channels-last, 16-byte aligned "
+              "tensors of one dtype with the same batch and channels");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(t.device());
+  const int64_t npix = t.size(0) * t.size(2) * t.size(3);
+  auto f32 = t.options().dtype(at::kFloat);
+  at::Tensor loss = at::empty({}, f32);
+  at::Tensor lse = at::empty({2, npix}, f32);
+  at::Tensor part = at::empty({kd_partial_blocks(npix)}, t.options().dtype(at::kDouble));
+  launch_kd_fwd_fold(view4(s_lo), view4(t), align_corners, static_cast<float>(temperature), lse.data_ptr<float>(),
+                     part.data_ptr<double>(), loss.data_ptr<float>(), cur_stream());
+  return {loss, lse};
+}
+
+// -> the gradient of the FULL-resolution student logits (the upsample's backward maps it down)
+static at::Tensor kd_kl_bwd_fold(const at::Tensor& grad, const at::Tensor& s_lo, const at::Tensor& t,
+                                 const at::Tensor& lse, double temperature, bool align_corners) {
+  TORCH_CHECK(kd_fold_ok(view4(s_lo), view4(t)), "rtseg.kd_fold: bad tensors");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(t.device());
+  const int64_t npix = t.size(0) * t.size(2) * t.size(3);
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == 2 * npix,
+              "rtseg.kd_bwd: bad lse workspace");
+  at::Tensor g32 = grad.to(at::kFloat).contiguous();
+  at::Tensor gs = at::empty(t.sizes(), t.options().memory_format(at::MemoryFormat::ChannelsLast));
+  launch_kd_bwd_fold(view4(s_lo), view4(t), view4(gs), align_corners, static_cast<float>(temperature),
+                     lse.data_ptr<float>(), g32.data_ptr<float>(), cur_stream());
+  return gs;
+}
+
 // cm[target, argmax_c x] as int64 [C, C]
 static at::Tensor confmat(const at::Tensor& x, const at::Tensor& target, int64_t num_class, int64_t ignore) {
   TORCH_CHECK(x.dim() == 4 && x.size(1) == num_class, "rtseg.confmat: logits must be [N, num_class, H, W]");
@@ -205,6 +238,9 @@ static std::tuple<at::Tensor, at::Tensor, at::Tensor> colorize(const at::Tensor&
 TORCH_LIBRARY_FRAGMENT(rtseg, m) {
   m.def("kd_kl_fwd(Tensor s, Tensor t, float temperature) -> (Tensor, Tensor)");
   m.def("kd_kl_bwd(Tensor grad, Tensor s, Tensor t, Tensor lse, float temperature) -> Tensor");
+  m.def("kd_kl_fwd_fold(Tensor s_lo, Tensor t, float temperature, bool align_corners) -> (Tensor, Tensor)");
+  m.def("kd_kl_bwd_fold(Tensor grad, Tensor s_lo, Tensor t, Tensor lse, float temperature, bool align_corners) "
+        "-> Tensor");
   m.def("detail_loss_fwd(Tensor d, Tensor labels, Tensor wb, float thrs, float dice_coef, float bce_coef) "
         "-> (Tensor, Tensor, Tensor)");
   m.def("detail_loss_bwd(Tensor grad, Tensor d, Tensor y, Tensor sums, float dice_coef, float bce_coef) -> Tensor");
@@ -220,6 +256,8 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
 TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
   m.impl("kd_kl_fwd", &rtseg::kd_kl_fwd);
   m.impl("kd_kl_bwd", &rtseg::kd_kl_bwd);
+  m.impl("kd_kl_fwd_fold", &rtseg::kd_kl_fwd_fold);
+  m.impl("kd_kl_bwd_fold", &rtseg::kd_kl_bwd_fold);
   m.impl("detail_loss_fwd", &rtseg::detail_loss_fwd);
   m.impl("detail_loss_bwd", &rtseg::detail_loss_bwd);
   m.impl("colorize", &rtseg::colorize);

@@ -105,6 +105,13 @@ void launch_bn_bwd_apply(const void* dy, const void* x, const void* y, const flo
 // ---- kd_metrics.hip ---------------------------------------------------------
 int kd_partial_blocks(int64_t npix);
 // lse: [2, N*H*W] fp32 (student, teacher log-sum-exp of z/T); part: [kd_partial_blocks] fp64
+// KD with the student's final bilinear upsample folded in: s_lo [N][Hl][Wl][C] at head resolution,
+// t (and gs) at full resolution, dense channels-last; kd_fold_ok(s_lo, t) first
+bool kd_fold_ok(const Tensor4& s_lo, const Tensor4& t);
+void launch_kd_fwd_fold(const Tensor4& s_lo, const Tensor4& t, bool align, float temperature, float* lse, double* part,
+                        float* out, hipStream_t st);
+void launch_kd_bwd_fold(const Tensor4& s_lo, const Tensor4& t, const Tensor4& gs, bool align, float temperature,
+                        const float* lse, const float* gout, hipStream_t st);
 void launch_kd_fwd(const Tensor4& s, const Tensor4& t, float temperature, float* lse, double* part,
                    float* out, hipStream_t st);
 void launch_kd_bwd(const Tensor4& s, const Tensor4& t, const Tensor4& gs, float temperature,

@@ -124,9 +124,47 @@ __device__ __forceinline__ void stage_in(const T* __restrict__ g, int64_t first,
     lds[e] = g[first + e];
 }
 
+// Student logits at the head's resolution with the model's final bilinear upsample folded in
+// (ops/kd.py: the trainer's DeferredLogits): the staged student values of a full-resolution pixel
+// are interpolated from the low-resolution channels-last tensor -- the same arithmetic and bf16
+// rounding as interp.hip's interp_fwd_cl_pix_lds -- instead of read from a materialised full-
+// resolution copy (0.64 GB written and read twice per KD step at batch 16, 1024 x 2048).
+struct KdFold {
+  const void* lo;          // [N][Hl][Wl][C] dense channels-last
+  int hl, wl;
+  LinMap mh, mw;
+  FastDiv fw, fh;          // full-resolution W, H
+};
+
 template <typename T>
+__device__ __forceinline__ void stage_fold(const KdFold& f, int C, int64_t p0, int np, T* lds) {
+  const int i = threadIdx.x;
+  if (i >= np) return;
+  uint32_t ox, oy;
+  const uint32_t r1 = f.fw.divmod(static_cast<uint32_t>(p0 + i), ox);
+  const int n = static_cast<int>(f.fh.divmod(r1, oy));
+  int y0, y1, x0, x1;
+  float ly, lx;
+  f.mh.map(static_cast<int>(oy), y0, y1, ly);
+  f.mw.map(static_cast<int>(ox), x0, x1, lx);
+  const float w00 = (1.f - ly) * (1.f - lx), w01 = (1.f - ly) * lx, w10 = ly * (1.f - lx), w11 = ly * lx;
+  const T* b = static_cast<const T*>(f.lo) + static_cast<int64_t>(n) * f.hl * f.wl * C;
+  const T* p00 = b + (static_cast<int64_t>(y0) * f.wl + x0) * C;
+  const T* p01 = b + (static_cast<int64_t>(y0) * f.wl + x1) * C;
+  const T* p10 = b + (static_cast<int64_t>(y1) * f.wl + x0) * C;
+  const T* p11 = b + (static_cast<int64_t>(y1) * f.wl + x1) * C;
+  T* q = lds + i * C;
+  for (int c = 0; c < C; ++c) {
+    const float v = w00 * Io<T>::ld(p00 + c) + w01 * Io<T>::ld(p01 + c) + w10 * Io<T>::ld(p10 + c) +
+                    w11 * Io<T>::ld(p11 + c);
+    Io<T>::st(q + c, v);
+  }
+}
+
+template <typename T, bool FOLD = false>
 __global__ void __launch_bounds__(kKdPix) kd_fwd_cl_kernel(const T* __restrict__ s, const T* __restrict__ t, int C,
-                                                           int64_t npix, float inv_t, float* lse, double* part) {
+                                                           int64_t npix, float inv_t, float* lse, double* part,
+                                                           KdFold fold = {}) {
   extern __shared__ __attribute__((aligned(16))) unsigned char kd_lds[];
   T* ls = reinterpret_cast<T*>(kd_lds);
   T* lt = ls + kKdPix * C;
@@ -134,7 +172,8 @@ __global__ void __launch_bounds__(kKdPix) kd_fwd_cl_kernel(const T* __restrict__
   for (int64_t p0 = static_cast<int64_t>(blockIdx.x) * kKdPix; p0 < npix; p0 += static_cast<int64_t>(gridDim.x) * kKdPix) {
     const int np = static_cast<int>(npix - p0 < kKdPix ? npix - p0 : kKdPix);
     __syncthreads();
-    stage_in(s, p0 * C, static_cast<int64_t>(np) * C, ls);
+    if constexpr (FOLD) stage_fold(fold, C, p0, np, ls);
+    else stage_in(s, p0 * C, static_cast<int64_t>(np) * C, ls);
     stage_in(t, p0 * C, static_cast<int64_t>(np) * C, lt);
     __syncthreads();
     if (static_cast<int>(threadIdx.x) < np) {
@@ -165,10 +204,11 @@ __global__ void __launch_bounds__(kKdPix) kd_fwd_cl_kernel(const T* __restrict__
   if (threadIdx.x == 0) part[blockIdx.x] = acc;
 }
 
-template <typename T>
+template <typename T, bool FOLD = false>
 __global__ void __launch_bounds__(kKdPix) kd_bwd_cl_kernel(const T* __restrict__ s, const T* __restrict__ t,
                                                            T* __restrict__ gs, int C, int64_t npix, float inv_t,
-                                                           const float* lse, const float* gout, float coef) {
+                                                           const float* lse, const float* gout, float coef,
+                                                           KdFold fold = {}) {
   extern __shared__ __attribute__((aligned(16))) unsigned char kd_lds[];
   T* ls = reinterpret_cast<T*>(kd_lds);
   T* lt = ls + kKdPix * C;
@@ -176,7 +216,8 @@ __global__ void __launch_bounds__(kKdPix) kd_bwd_cl_kernel(const T* __restrict__
   for (int64_t p0 = static_cast<int64_t>(blockIdx.x) * kKdPix; p0 < npix; p0 += static_cast<int64_t>(gridDim.x) * kKdPix) {
     const int np = static_cast<int>(npix - p0 < kKdPix ? npix - p0 : kKdPix);
     __syncthreads();
-    stage_in(s, p0 * C, static_cast<int64_t>(np) * C, ls);
+    if constexpr (FOLD) stage_fold(fold, C, p0, np, ls);
+    else stage_in(s, p0 * C, static_cast<int64_t>(np) * C, ls);
     stage_in(t, p0 * C, static_cast<int64_t>(np) * C, lt);
     __syncthreads();
     if (static_cast<int>(threadIdx.x) < np) {
@@ -279,6 +320,56 @@ void launch_kd_fwd(const Tensor4& s, const Tensor4& t, float temperature, float*
   const double numel = static_cast<double>(npix) * s.c;
   const double scale = static_cast<double>(temperature) * temperature / numel;
   kd_finalize_kernel<<<1, kKdBlock, 0, st>>>(part, g, scale, out);
+}
+
+// student logits s_lo at head resolution, the model's final bilinear upsample to t's size folded
+// in (KdFold); t and gs dense channels-last at full resolution
+static KdFold make_fold(const Tensor4& s_lo, const Tensor4& t, bool align) {
+  KdFold f;
+  f.lo = s_lo.data;
+  f.hl = s_lo.h;
+  f.wl = s_lo.w;
+  f.mh = LinMap::make(s_lo.h, t.h, align);
+  f.mw = LinMap::make(s_lo.w, t.w, align);
+  f.fw = FastDiv::make(t.w);
+  f.fh = FastDiv::make(t.h);
+  return f;
+}
+
+bool kd_fold_ok(const Tensor4& s_lo, const Tensor4& t) {
+  return kd_cl_ok(s_lo) && kd_cl_ok(t) && s_lo.dtype == t.dtype && s_lo.c == t.c && s_lo.n == t.n &&
+         static_cast<int64_t>(t.n) * t.h * t.w < (int64_t{1} << 31);
+}
+
+void launch_kd_fwd_fold(const Tensor4& s_lo, const Tensor4& t, bool align, float temperature, float* lse, double* part,
+                        float* out, hipStream_t st) {
+  const int64_t npix = static_cast<int64_t>(t.n) * t.h * t.w;
+  const int g = kd_partial_blocks(npix);
+  const float inv_t = 1.f / temperature;
+  const KdFold f = make_fold(s_lo, t, align);
+  by_dtype(t.dtype, [&](auto tag) {
+    using T = decltype(tag);
+    kd_fwd_cl_kernel<T, true><<<g, kKdPix, kd_lds_bytes(t), st>>>(nullptr, static_cast<const T*>(t.data), t.c, npix,
+                                                                   inv_t, lse, part, f);
+  });
+  const double numel = static_cast<double>(npix) * t.c;
+  const double scale = static_cast<double>(temperature) * temperature / numel;
+  kd_finalize_kernel<<<1, kKdBlock, 0, st>>>(part, g, scale, out);
+}
+
+void launch_kd_bwd_fold(const Tensor4& s_lo, const Tensor4& t, const Tensor4& gs, bool align, float temperature,
+                        const float* lse, const float* gout, hipStream_t st) {
+  const int64_t npix = static_cast<int64_t>(t.n) * t.h * t.w;
+  const int g = kd_partial_blocks(npix);
+  const double numel = static_cast<double>(npix) * t.c;
+  const float coef = static_cast<float>(static_cast<double>(temperature) / numel);
+  const KdFold f = make_fold(s_lo, t, align);
+  by_dtype(t.dtype, [&](auto tag) {
+    using T = decltype(tag);
+    kd_bwd_cl_kernel<T, true><<<g, kKdPix, kd_lds_bytes(t), st>>>(nullptr, static_cast<const T*>(t.data),
+                                                                   static_cast<T*>(gs.data), t.c, npix, 1.f / temperature,
+                                                                   lse, gout, coef, f);
+  });
 }
 
 void launch_kd_bwd(const Tensor4& s, const Tensor4& t, const Tensor4& gs, float temperature,
