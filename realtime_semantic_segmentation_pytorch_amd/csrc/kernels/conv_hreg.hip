@@ -34,8 +34,6 @@ namespace {
 
 using namespace mdev;
 
-typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-
 constexpr int kTH = 4, kTW = 64;                       // output tile: 256 pixels
 constexpr int kHH = kTH + 2, kHW = kTW + 2;            // halo of one 64-channel chunk
 constexpr int kHRows = kHH * kHW;                      // 396
@@ -57,7 +55,7 @@ struct HrArgs {
   int cch;                 // 64-channel chunks of C
   int tilesW, tilesH, mtiles, ntiles;
   uint32_t xbytes;
-  int dbg;                 // RTSEG_HREG_DBG (A/B only): 1 = no epilogue, 2 = no statistics, 4 = no stores, 8 / 16 = sc1 / nt stores
+  int dbg;                 // RTSEG_HREG_DBG (A/B only): 1 = no epilogue, 2 = no statistics, 4 = no stores
 };
 
 __device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t lds_dst) {
@@ -222,16 +220,7 @@ __global__ void __launch_bounds__(HrLayout<WL>::NRG * HrLayout<WL>::NCG * 64) hr
             if (g & 1) {  // 16-byte group pair (g - 1, g): pair_swap16
               const uint4 w = pair_swap16(pkp[0], pkp[1]);
               if (ok && !(a.dbg & 4)) {
-                uint4* dst = reinterpret_cast<uint4*>(a.y + off + co - 8 + 4 * fhi);
-                if (a.dbg & 8) {  // cache-policy A/B: sc1 (the line leaves the XCD's L2)
-                  const u32x4_t wv = {w.x, w.y, w.z, w.w};
-                  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(wv) : "memory");
-                } else if (a.dbg & 16) {  // ... nt
-                  const u32x4_t wv = {w.x, w.y, w.z, w.w};
-                  asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(dst), "v"(wv) : "memory");
-                } else {
-                  *dst = w;
-                }
+                *reinterpret_cast<uint4*>(a.y + off + co - 8 + 4 * fhi) = w;
               }
             }
             if constexpr (STATS) {
