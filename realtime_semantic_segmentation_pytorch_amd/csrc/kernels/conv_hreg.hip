@@ -260,9 +260,10 @@ __global__ void __launch_bounds__(HrLayout<WL>::NRG * HrLayout<WL>::NCG * 64) hr
   for (int q = 0; q < nsteps; ++q) {
     const int c = q % cch;
     // this wave's halo DMA for chunk-step q landed (it is older than the weight loads of the
-    // two K-steps in flight: at most those 16 loads may still be outstanding); the barrier
-    // publishes every wave's halo and frees the other buffer (read by chunk-step q - 1)
-    vm_wait<16>();
+    // two K-steps in flight: at most those 2 x TI x 4 loads may still be outstanding -- with TI = 1
+    // a wait for 16 would let the prologue's DMA still be in flight); the barrier publishes every
+    // wave's halo and frees the other buffer (read by chunk-step q - 1)
+    vm_wait<8 * TI>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (c == 0 && q > 0) epilogue(mfirst + (q / cch - 1) * mstep);
@@ -497,7 +498,7 @@ __global__ void __launch_bounds__(512) hreg_db_kernel(const HrArgs a) {
   // previous tile's accumulators piece by piece between its taps
   auto run_chunk = [&](f32x16_t (&A)[TJ], f32x16_t (&D)[TJ], int q) __attribute__((always_inline)) {
     const int c = q % cch;
-    vm_wait<16>();
+    vm_wait<8>();  // (the two K-steps of weight loads in flight, 4 each)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (q + 1 < nsteps) halo_dma(q + 1);
