@@ -121,6 +121,7 @@ class BaseConfig:
         self.amp_dtype = "bf16"          # autocast dtype when amp_training: 'bf16' | 'fp16'
         self.channels_last = True        # NHWC activations (MIOpen/HIP kernels prefer it)
         self.cudnn_benchmark = False     # MIOpen find mode (exhaustive solver search) for convs left on MIOpen; opt-in (utils/runtime.py)
+        self.deterministic = False       # bit-reproducible steps across processes: no conv timing, MIOpen deterministic solvers (utils/runtime.py)
         self.fused_loss = True           # fold the final upsample into the HIP loss kernel
         self.fused_optimizer = True      # HIP multi-tensor optimizer step that also writes the EMA
         self.hip_depthwise = True        # depth-wise convs on the HIP kernels (else MIOpen)

@@ -81,7 +81,7 @@ _SPEC = [
     ("no_fused_loss", "true", {"dest": "no_fused_loss"}), ("ddp_bucket_mb", int, {}),
     ("gpu_aug", "true", {}), ("spawn_procs", int, {}), ("graph_step", "true", {}), ("synthetic_data", "true", {}), ("synthetic_len", int, {}),
     ("synthetic_learnable", "true", {}), ("synthetic_cell", int, {}), ("max_train_itrs", int, {}),
-    ("cudnn_benchmark", "true", {}),
+    ("cudnn_benchmark", "true", {}), ("deterministic", "true", {}),
     ("log_interval", int, {}), ("device", str, {}),
     ("no_fused_optimizer", "true", {"dest": "no_fused_optimizer"}),
 ]

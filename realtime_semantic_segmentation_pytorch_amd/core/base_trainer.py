@@ -51,7 +51,8 @@ class BaseTrainer:
             config.init_dependent_config()  # idempotent; main.py calls it too
         self.logger = get_logger(config, self.main_rank)
         # same find-mode policy as bench.py (which alone also drops the naive solvers)
-        configure_backend(getattr(config, "cudnn_benchmark", False), model=config.model)
+        configure_backend(getattr(config, "cudnn_benchmark", False), model=config.model,
+                          deterministic=getattr(config, "deterministic", False))
         self.device = set_device(config, self.local_rank)
         self.amp_dtype = torch.float16 if getattr(config, "amp_dtype", "bf16") == "fp16" else torch.bfloat16
         use_scaler = bool(config.amp_training) and self.amp_dtype == torch.float16 and self.device.type == "cuda"

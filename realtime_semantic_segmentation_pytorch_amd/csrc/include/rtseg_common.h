@@ -147,8 +147,8 @@ struct LinMap {
     else m.scale = static_cast<float>(in_size) / static_cast<float>(out_size);
     return m;
   }
-  // -> i0, i1 (= i0 or i0+1), lambda for i1
-  __device__ __forceinline__ void map(int o, int& i0, int& i1, float& l) const {
+  // -> i0, i1 (= i0 or i0+1), lambda for i1 (host too: the loss backward's tile classes)
+  __host__ __device__ __forceinline__ void map(int o, int& i0, int& i1, float& l) const {
     float src = align ? scale * static_cast<float>(o)
                       : fmaxf(scale * (static_cast<float>(o) + 0.5f) - 0.5f, 0.f);
     int f = static_cast<int>(src);

@@ -25,6 +25,12 @@
 //  * Backward recomputes the softmax per pixel, weights it by the device-side
 //    selection rule, and reduces the transpose of the bilinear map through LDS
 //    (row pass, then column pass); only block-border cells use global atomics.
+//  * Deterministic: the backward's tiles are launched in classes (tile row mod Py, tile column
+//    mod Px) whose low-resolution bounding boxes are pairwise disjoint, so every gradient cell
+//    takes at most one atomic add per launch and the launches run in a fixed stream order; every
+//    sum inside a block has one writer per cell and phase; the loss sums are per-block slabs
+//    reduced in a fixed order.  Same inputs -> the same bits, run to run and process to process.
+#include <algorithm>
 #include <cstdlib>
 
 #include "rtseg_common.h"
@@ -67,15 +73,22 @@ struct TileGeo {
   bool ident_h, ident_w;
 };
 
+// A launch over the tiles with tile row = py (mod Py) and tile column = px (mod Px); {0, 1, 0, 1}:
+// every tile
+struct TileClass {
+  int py, Py, px, Px;
+};
+
 template <int TH, int TW>
-__device__ __forceinline__ TileGeo tile_geo(const LossGeo& g) {
+__device__ __forceinline__ TileGeo tile_geo(const LossGeo& g, TileClass k = {0, 1, 0, 1}) {
   TileGeo t;
   const int tiles_x = (g.ow + TW - 1) / TW;
   const int tiles_y = (g.oh + TH - 1) / TH;
+  const int cx = (tiles_x - k.px + k.Px - 1) / k.Px, cy = (tiles_y - k.py + k.Py - 1) / k.Py;
   const int bid = blockIdx.x;
-  const int tx = bid % tiles_x;
-  const int ty = (bid / tiles_x) % tiles_y;
-  t.n = bid / (tiles_x * tiles_y);
+  const int tx = k.px + k.Px * (bid % cx);
+  const int ty = k.py + k.Py * ((bid / cx) % cy);
+  t.n = bid / (cx * cy);
   t.oy0 = ty * TH; t.ox0 = tx * TW;
   t.oy1 = min(t.oy0 + TH, g.oh) - 1; t.ox1 = min(t.ox0 + TW, g.ow) - 1;
   int a0, a1; float l;
@@ -324,7 +337,7 @@ __global__ void __launch_bounds__(256) radix_scan_kernel(double* stats,
 }
 
 __global__ void __launch_bounds__(256) sum_gt_kernel(const float* __restrict__ loss, int64_t total,
-                                                     double* stats) {
+                                                     const double* stats, double* __restrict__ slab) {
   if (stats[S_FLAG_TOPK] != 1.0) return;
   __shared__ double red[4];
   const float vk = __uint_as_float(static_cast<unsigned>(stats[S_PREFIX]));
@@ -335,12 +348,15 @@ __global__ void __launch_bounds__(256) sum_gt_kernel(const float* __restrict__ l
     if (l > vk) s += l;
   }
   s = block_sum(s, red);
-  if (threadIdx.x == 0 && s != 0.0) atomicAdd(stats + S_SUM_GT, s);
+  if (threadIdx.x == 0) slab[blockIdx.x] = s;  // summed in block order by seg_finalize2
 }
 
-__global__ void seg_finalize2(double* stats, float* out_loss) {
+__global__ void seg_finalize2(double* stats, const double* __restrict__ slab, int nblk, float* out_loss) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   if (stats[S_FLAG_TOPK] != 1.0) return;
+  double sgt = 0.0;
+  for (int i = 0; i < nblk; ++i) sgt += slab[i];
+  stats[S_SUM_GT] = sgt;
   const double k = stats[S_K];
   const double krem = stats[S_KREM];
   const float vk = __uint_as_float(static_cast<unsigned>(stats[S_PREFIX]));
@@ -430,11 +446,11 @@ __global__ void __launch_bounds__(256) seg_ce_bwd_tile(
     const float* __restrict__ cw, const float* __restrict__ pix_loss,
     const float* __restrict__ pix_lse, const double* __restrict__ stats, int mode,
     const float* __restrict__ grad_out, float* __restrict__ gacc, int64_t asn, int64_t asc,
-    int64_t ash, int64_t asw) {
+    int64_t ash, int64_t asw, TileClass cls) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   __shared__ int tx0[TW], tx1[TW], ty0[TH], ty1[TH], jlo[TW + 4], jhi[TW + 4];  // BW <= TW + 2
   __shared__ float tlx[TW], tly[TH];
-  const TileGeo t = tile_geo<TH, TW>(g);
+  const TileGeo t = tile_geo<TH, TW>(g, cls);
   const int C = NC > 0 ? NC : g.c;
   const int BW = t.BW, RS = BW | 1;
   const int nx = t.ox1 - t.ox0 + 1, ny = t.oy1 - t.oy0 + 1;
@@ -553,14 +569,14 @@ __global__ void __launch_bounds__(256) seg_ce_bwd_run(
     const float* __restrict__ cw, const float* __restrict__ pix_loss,
     const float* __restrict__ pix_lse, const double* __restrict__ stats, int mode,
     const float* __restrict__ grad_out, float* __restrict__ gacc, int64_t asn, int64_t asc,
-    int64_t ash, int64_t asw) {
+    int64_t ash, int64_t asw, TileClass cls) {
   static_assert(NC > 0, "run form needs the class count at compile time");
   extern __shared__ __attribute__((aligned(16))) float sm[];
   __shared__ int tx0[TW], tx1[TW], ty0[TH], ty1[TH], jlo[TW + 4], jhi[TW + 4];  // BW <= TW + 2
   __shared__ float tlx[TW], tly[TH];
   __shared__ float2 pwl[TH * TW];  // per tile pixel: (gradient weight, lse)
   __shared__ uint8_t plab[TH * TW];
-  const TileGeo t = tile_geo<TH, TW>(g);
+  const TileGeo t = tile_geo<TH, TW>(g, cls);
   const int BW = t.BW, RS = BW | 1;
   const int nx = t.ox1 - t.ox0 + 1, ny = t.oy1 - t.oy0 + 1;
   float* L = sm;                          // [BH][BW][CP]
@@ -696,7 +712,7 @@ __global__ void __launch_bounds__(256) seg_ce_bwd_run2(
     const float* __restrict__ cw, const float* __restrict__ pix_loss,
     const float* __restrict__ pix_lse, const double* __restrict__ stats, int mode,
     const float* __restrict__ grad_out, float* __restrict__ gacc, int64_t asn, int64_t asc,
-    int64_t ash, int64_t asw) {
+    int64_t ash, int64_t asw, TileClass cls) {
   static_assert(NC > 0 && NC < 255, "run form needs the class count at compile time");
   constexpr float kL2E = 1.4426950408889634f;
   constexpr int PIT = (TH * TW + 255) / 256;  // metadata items per thread (launch: 256 threads)
@@ -705,7 +721,7 @@ __global__ void __launch_bounds__(256) seg_ce_bwd_run2(
   __shared__ float tlx[TW], tly[TH];
   __shared__ float plse[TH * TW];      // lse * log2 e
   __shared__ uint16_t pcode[TH * TW];  // label | selection code << 8 (code 0: no gradient)
-  const TileGeo t = tile_geo<TH, TW>(g);
+  const TileGeo t = tile_geo<TH, TW>(g, cls);
   const int BW = t.BW, RS = BW | 1;
   const int nx = t.ox1 - t.ox0 + 1, ny = t.oy1 - t.oy0 + 1;
   float* L = sm;                          // [BH][BW][CP]
@@ -844,20 +860,24 @@ __global__ void __launch_bounds__(256) seg_ce_bwd_run2(
     for (int c = 0; c < NC; ++c) R[(r * RS + j1) * NC + c] += a1[c];
   }
   __syncthreads();
-  if (run) {  // one-hot terms: lanes of one instruction address distinct (row, column) cells
+  // one-hot terms in two phases, left taps then right taps: in each phase a cell (r, j) has one
+  // writing thread (j1 = j + 1 is injective), so the order of the adds is fixed
+  if (run) {
     float* ra = R + (r * RS + j) * NC;
+    for (int k = k0; k <= k1; ++k) {
+      const int cwd = pcode[r * TW + k];
+      if (cwd == 0) continue;
+      const float w = weight(cwd);
+      ra[cwd & 255] -= j1 == j ? w : w * (1.f - tlx[k]);
+    }
+  }
+  __syncthreads();
+  if (run && j1 != j) {
     float* rb = R + (r * RS + j1) * NC;
     for (int k = k0; k <= k1; ++k) {
       const int cwd = pcode[r * TW + k];
       if (cwd == 0) continue;
-      const int y = cwd & 255;
-      const float w = weight(cwd), lx = tlx[k];
-      if (j1 == j) {
-        atomicAdd(ra + y, -w);
-      } else {
-        atomicAdd(ra + y, -w * (1.f - lx));
-        atomicAdd(rb + y, -w * lx);
-      }
+      rb[cwd & 255] -= weight(cwd) * tlx[k];
     }
   }
   __syncthreads();
@@ -981,8 +1001,9 @@ static void fwd_t(const SegLossArgs& a, const LossGeo& g, hipStream_t st) {
                                             shifts[p], bits[p], p);
     radix_scan_kernel<<<1, 256, 0, st>>>(a.stats, a.hist + p * 2048, bits[p], p == 2, a.out_loss);
   }
-  sum_gt_kernel<<<grid, 256, 0, st>>>(a.pix_loss, total, a.stats);
-  seg_finalize2<<<1, 64, 0, st>>>(a.stats, a.out_loss);
+  // a.slab (one row per forward tile, >= grid doubles) is free again after seg_finalize1
+  sum_gt_kernel<<<grid, 256, 0, st>>>(a.pix_loss, total, a.stats, a.slab);
+  seg_finalize2<<<1, 64, 0, st>>>(a.stats, a.slab, grid, a.out_loss);
 }
 
 void launch_seg_loss_fwd(const SegLossArgs& a, hipStream_t st) {
@@ -994,6 +1015,34 @@ void launch_seg_loss_fwd(const SegLossArgs& a, hipStream_t st) {
   }
 }
 
+// Tile classes for the backward: the smallest strides (Py, Px) such that two tiles of one class
+// never share a low-resolution bounding-box cell (with one cell of margin, so a host/device
+// rounding difference in the map cannot matter)
+static int class_stride(const LinMap& m, int out, int T) {
+  const int tiles = (out + T - 1) / T;
+  auto lo = [&](int t) { int a0, a1; float l; m.map(t * T, a0, a1, l); return a0; };
+  auto hi = [&](int t) { int a0, a1; float l; m.map(std::min((t + 1) * T, out) - 1, a0, a1, l); return a1; };
+  for (int P = 1; P < tiles; ++P) {
+    bool ok = true;
+    for (int t = 0; t + P < tiles && ok; ++t) ok = hi(t) + 1 < lo(t + P);
+    if (ok) return P;
+  }
+  return std::max(tiles, 1);
+}
+
+// launch(cls, grid) once per tile class, in a fixed order
+template <int TH, int TW, typename F>
+static void for_tile_classes(const LossGeo& g, F&& launch) {
+  static const bool one = [] { const char* e = std::getenv("RTSEG_LOSS_ONE_CLASS"); return e && e[0] == '1'; }();
+  const int Py = one ? 1 : class_stride(g.mh, g.oh, TH), Px = one ? 1 : class_stride(g.mw, g.ow, TW);
+  const int tiles_y = (g.oh + TH - 1) / TH, tiles_x = (g.ow + TW - 1) / TW;
+  for (int py = 0; py < Py; ++py)
+    for (int px = 0; px < Px; ++px) {
+      const int cy = (tiles_y - py + Py - 1) / Py, cx = (tiles_x - px + Px - 1) / Px;
+      if (cy > 0 && cx > 0) launch(TileClass{py, Py, px, Px}, cy * cx * g.n);
+    }
+}
+
 template <typename T, int TH, int TW, int NC>
 static void bwd_run(const SegLossArgs& a, const LossGeo& g, const float* grad_out, hipStream_t st) {
   const int bh = static_cast<int>((TH - 1) * g.mh.scale) + 3;
@@ -1002,10 +1051,11 @@ static void bwd_run(const SegLossArgs& a, const LossGeo& g, const float* grad_ou
                                       static_cast<size_t>(g.c) * TH * (bw | 1));
   auto k = seg_ce_bwd_run<T, TH, TW, NC>;
   allow_lds(k, lds);
-  k<<<tiles_of<TH, TW>(g), 256, lds, st>>>(
-      static_cast<const T*>(a.logits.data), g, a.ignore_index, a.class_weight,
-      a.pix_loss, a.pix_lse, a.stats, a.mode, grad_out, a.acc, a.acc_sn, a.acc_sc, a.acc_sh,
-      a.acc_sw);
+  for_tile_classes<TH, TW>(g, [&](TileClass cls, int grid) {
+    k<<<grid, 256, lds, st>>>(static_cast<const T*>(a.logits.data), g, a.ignore_index, a.class_weight,
+                              a.pix_loss, a.pix_lse, a.stats, a.mode, grad_out, a.acc, a.acc_sn, a.acc_sc,
+                              a.acc_sh, a.acc_sw, cls);
+  });
 }
 
 template <typename T, int TH, int TW, int NC>
@@ -1016,10 +1066,11 @@ static void bwd_run2(const SegLossArgs& a, const LossGeo& g, const float* grad_o
                                       static_cast<size_t>(g.c) * TH * (bw | 1));
   auto k = seg_ce_bwd_run2<T, TH, TW, NC>;
   allow_lds(k, lds);
-  k<<<tiles_of<TH, TW>(g), 256, lds, st>>>(
-      static_cast<const T*>(a.logits.data), g, a.ignore_index, a.class_weight,
-      a.pix_loss, a.pix_lse, a.stats, a.mode, grad_out, a.acc, a.acc_sn, a.acc_sc, a.acc_sh,
-      a.acc_sw);
+  for_tile_classes<TH, TW>(g, [&](TileClass cls, int grid) {
+    k<<<grid, 256, lds, st>>>(static_cast<const T*>(a.logits.data), g, a.ignore_index, a.class_weight,
+                              a.pix_loss, a.pix_lse, a.stats, a.mode, grad_out, a.acc, a.acc_sn, a.acc_sc,
+                              a.acc_sh, a.acc_sw, cls);
+  });
 }
 
 template <typename T, int TH, int TW, int NC>
@@ -1031,10 +1082,11 @@ static void bwd_tile(const SegLossArgs& a, const LossGeo& g, const float* grad_o
                                       static_cast<size_t>(g.c) * TH * (bw | 1));
   auto k = seg_ce_bwd_tile<T, TH, TW, NC>;
   allow_lds(k, lds);
-  k<<<tiles_of<TH, TW>(g), 256, lds, st>>>(
-      static_cast<const T*>(a.logits.data), g, a.ignore_index, a.class_weight,
-      a.pix_loss, a.pix_lse, a.stats, a.mode, grad_out, a.acc, a.acc_sn, a.acc_sc, a.acc_sh,
-      a.acc_sw);
+  for_tile_classes<TH, TW>(g, [&](TileClass cls, int grid) {
+    k<<<grid, 256, lds, st>>>(static_cast<const T*>(a.logits.data), g, a.ignore_index, a.class_weight,
+                              a.pix_loss, a.pix_lse, a.stats, a.mode, grad_out, a.acc, a.acc_sn, a.acc_sc,
+                              a.acc_sh, a.acc_sw, cls);
+  });
 }
 
 template <typename T, typename G>

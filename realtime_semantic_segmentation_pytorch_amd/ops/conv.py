@@ -494,6 +494,12 @@ def _choose(key, candidates):
     if saved is not None:  # an earlier run's winner for this shape (persistent tuning database)
         _DECISIONS[key] = (names.index(saved), saved, [])
         return names.index(saved)
+    if os.environ.get("RTSEG_DETERMINISTIC") == "1":
+        # config.deterministic (utils/runtime.py): a shape the database lacks takes the first
+        # native candidate instead of a timing, so every process runs the same kernels
+        fixed = next((i for i, n in enumerate(names) if n != "miopen"), 0)
+        _DECISIONS[key] = (fixed, names[fixed], [])
+        return fixed
     if torch.cuda.is_current_stream_capturing():
         return len(candidates) - 1  # MIOpen is last
     with torch.no_grad():

@@ -14,6 +14,13 @@ run and the benchmark use the same MIOpen configuration.
   whose shapes have run the search without a fault in every round; elsewhere MIOpen runs in
   immediate mode (the find database in ``miopen_db/`` where it has the shape, else heuristics).
 
+* ``config.deterministic``: bit-reproducible training steps, run to run and process to process
+  (``RTSEG_DETERMINISTIC=1``): conv kernels from the tuning database or a fixed rule, never a
+  timing (ops/conv.py ``_choose``), and MIOpen's deterministic solvers only.  The HIP kernels
+  are deterministic without it: BN / wgrad / loss partial sums are per-block slabs reduced in a
+  fixed order, and the loss backward's border atomics are split into launches in which no cell
+  has two writers (seg_loss.hip).
+
 Environment variables already set by the user win.  Must run before the first convolution.
 """
 from __future__ import annotations
@@ -33,7 +40,8 @@ _NAIVE = ("MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_FWD", "MIOPEN_DEBUG_CONV_DIRECT_N
 FIND_VERIFIED = ("ddrnet", "bisenetv2", "stdc", "pp_liteseg", "ppliteseg")
 
 
-def configure_backend(benchmark: bool = True, model=None, exclude_naive: bool = False) -> None:
+def configure_backend(benchmark: bool = True, model=None, exclude_naive: bool = False,
+                      deterministic: bool = False) -> None:
     """MIOpen setup.  ``benchmark``: find mode, honoured only for ``FIND_VERIFIED`` models (and
     always reset otherwise, so a process that trains several models never carries find mode
     over to an unverified one).  ``exclude_naive``: keep MIOpen's naive solvers out of the
@@ -48,4 +56,7 @@ def configure_backend(benchmark: bool = True, model=None, exclude_naive: bool = 
     import torch
 
     verified = model is None or str(model).lower() in FIND_VERIFIED
-    torch.backends.cudnn.benchmark = bool(benchmark) and verified
+    torch.backends.cudnn.benchmark = bool(benchmark) and verified and not deterministic
+    if deterministic:
+        os.environ["RTSEG_DETERMINISTIC"] = "1"
+        torch.backends.cudnn.deterministic = True

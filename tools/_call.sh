@@ -1,5 +1,10 @@
 set -o pipefail
-mkdir -p gpurun_out/r6_stag
-timeout -k 10 300 python -u -m pytest tests/test_conv_wres_gpu.py -k hreg -x -q --timeout 120 --timeout-method thread > gpurun_out/r6_stag/tests.log 2>&1 || { tail -30 gpurun_out/r6_stag/tests.log; exit 1; }
-tail -1 gpurun_out/r6_stag/tests.log
-for i in 1 2; do timeout -k 10 200 python -u tools/bench_hreg.py > gpurun_out/r6_stag/bench_$i.txt 2>&1 || exit 1; done
+D=gpurun_out/r6_det; mkdir -p $D
+for i in 1 2; do
+for v in 0 1; do
+RTSEG_LOSS_ONE_CLASS=$v timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > $D/ab_${v}_$i.json 2> $D/ab.err || { tail -20 $D/ab.err; exit 1; }
+echo "one_class=$v $(cut -c1-120 $D/ab_${v}_$i.json)"
+done; done
+cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/prof -o run -- python -u bench.py --steps 4 --warmup 3 > $D/prof.log 2>&1 || { tail $D/prof.log; exit 1; }
+find $D/prof -name "*kernel_stats.csv" | head -1 | xargs -I{} grep -E "seg_ce|cast_out" {}
