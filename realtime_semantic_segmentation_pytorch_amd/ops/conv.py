@@ -1174,11 +1174,20 @@ def _stem_infer(x: torch.Tensor, conv: nn.Module, bias) -> torch.Tensor:
     if x.data_ptr() % 16:
         x = x.clone(memory_format=torch.channels_last)
     stride, padding, dilation = _geom(conv)
-    y, _ = ops().conv_stem(x, wk, stride, padding, dilation, False)
+    if bias is not None:  # added to the fp32 accumulators by the BN epilogue (scale 1): one rounding
+        key = (bias.data_ptr(), bias._version, write_generation())
+        hit = getattr(conv, "_rtseg_stem_ss", None)
+        if hit is None or hit[0] != key:
+            ss = torch.zeros(2 * cp, device=x.device, dtype=torch.float32)
+            ss[:cp] = 1.0
+            ss[cp:cp + cout] = bias.detach().float()
+            hit = (key, ss)
+            setattr(conv, "_rtseg_stem_ss", hit)
+        y = ops().conv_stem_bn_act(x, wk, stride, padding, dilation, hit[1], 0)
+    else:
+        y, _ = ops().conv_stem(x, wk, stride, padding, dilation, False)
     if cp != cout:
         y = y[:, :cout].contiguous(memory_format=torch.channels_last)
-    if bias is not None:
-        y = y + bias.to(y.dtype).view(1, -1, 1, 1)
     return y
 
 

@@ -7,6 +7,7 @@ import torch
 import torch.nn.functional as F
 
 from realtime_semantic_segmentation_pytorch_amd import ops
+from _tol import bf16_close, f32_close  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -71,7 +72,7 @@ def test_halo_forward_and_stats(geom):
     y, part = torch.ops.rtseg.conv_halo(x, wk, [1, 1], [ph, pw], [1, 1], True, None, None, 0)
     ref = F.conv2d(x.float(), wt.float(), None, 1, (ph, pw))
     assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
-    _close(y, ref, 2e-2)
+    bf16_close(y, ref)
     rf = ref.double()  # the slab holds the statistics of the fp32 outputs (the accumulators)
     torch.testing.assert_close(part[:, :cout].double().sum(0), rf.sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
     torch.testing.assert_close(part[:, cout:].double().sum(0), rf.square().sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
@@ -104,7 +105,7 @@ def test_halo_bn_epilogue(act, with_res):
     if with_res:
         ref = ref + res.float()
     ref = ref.relu() if act == 1 else ref.clamp(0, 6) if act == 2 else ref
-    _close(y, ref, 2e-2)
+    bf16_close(y, ref)
 
 
 @pytest.mark.parametrize("geom", GEOMS)
@@ -123,7 +124,7 @@ def test_halo_dgrad(geom, with_addend):
     dx = torch.ops.rtseg.conv_halo_dgrad(dy, wt.permute(1, 2, 3, 0).contiguous(), list(x.shape), [1, 1], [ph, pw],
                                          [1, 1], add if with_addend else None, bits if with_addend == "masked" else None)
     ref = torch.nn.grad.conv2d_input(x.shape, wt.float(), dy.float(), 1, (ph, pw), 1)
-    _close(dx, ref + _addend_ref(add, bits, with_addend), 2e-2)
+    bf16_close(dx, ref + _addend_ref(add, bits, with_addend))
 
 
 def test_halo_routed_training_step(monkeypatch):

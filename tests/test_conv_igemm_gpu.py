@@ -6,6 +6,7 @@ import torch
 import torch.nn.functional as F
 
 from realtime_semantic_segmentation_pytorch_amd import ops
+from _tol import bf16_close, f32_close  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -76,7 +77,7 @@ def test_igemm_forward_and_stats(geom):
                                          None, None, 0)
     ref = F.conv2d(x.float(), wt.float(), None, s, p, d)
     assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
-    _close(y, ref, 2e-2)
+    bf16_close(y, ref)
     # the slab holds the statistics of the fp32 conv outputs (the kernel's accumulators)
     rf = ref.double()
     assert part.shape[0] <= 256 and part.shape[1] == 2 * cout
@@ -106,7 +107,7 @@ def test_igemm_bn_epilogue(act, with_res):
         ref = ref.relu()
     elif act == 2:
         ref = ref.clamp(0, 6)
-    _close(y, ref, 3e-2)
+    bf16_close(y, ref)
 
 
 DGRAD = [
@@ -132,7 +133,7 @@ def test_igemm_dgrad(geom):
                                           [d, d])
     ref = torch.nn.grad.conv2d_input(x.shape, wt.float(), dy.float(), s, p, d)
     assert dx.shape == x.shape and dx.is_contiguous(memory_format=torch.channels_last)
-    _close(dx, ref, 2e-2)
+    bf16_close(dx, ref)
 
 
 WGRAD = [
@@ -157,7 +158,7 @@ def test_igemm_wgrad(geom):
     dw = torch.ops.rtseg.conv_igemm_wgrad(x, dy, k, k, [s, s], [p, p], [d, d])
     ref = torch.nn.grad.conv2d_weight(x.float(), wt.shape, dy.float(), s, p, d)
     assert dw.shape == wt.shape and dw.dtype == torch.float32 and dw.is_contiguous()
-    _close(dw, ref, 1e-2)
+    f32_close(dw, ref)
 
 
 def _handoff_nodes(out):
@@ -182,7 +183,7 @@ def test_igemm_dgrad_addend(with_addend):
                                           [1, 1], None, add if with_addend else None,
                                           bits if with_addend == "masked" else None)
     ref = torch.nn.grad.conv2d_input(x.shape, wt.float(), dy.float(), 2, 1, 1)
-    _close(dx, ref + _addend_ref(add, bits, with_addend), 2e-2)
+    bf16_close(dx, ref + _addend_ref(add, bits, with_addend))
 
 
 def test_residual_grad_handoff_matches_plain_add(monkeypatch):
@@ -239,7 +240,7 @@ def test_igemm_dgrad_phase_addend(shape, with_addend):
     if with_addend:
         ref = ref + add.float()
     ref[:, :, ::2, ::2] += ph.float()
-    _close(dx, ref, 2e-2)
+    bf16_close(dx, ref)
     with pytest.raises(RuntimeError, match="phase_addend"):
         torch.ops.rtseg.conv_igemm_dgrad(dy, wt.permute(1, 2, 3, 0).contiguous(), list(x.shape), [2, 2], [1, 1],
                                          [1, 1], None, None, None, ph[:, :, 1:])
@@ -308,7 +309,7 @@ def test_igemm_dgrad_fused_phases(case, extras):
         ref = ref + add.float()
     if ph is not None:
         ref[:, :, ::s, ::s] += ph.float()
-    _close(fused, ref, 2e-2)
+    bf16_close(fused, ref)
     assert torch.equal(fused, split)
 
 

@@ -7,6 +7,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from realtime_semantic_segmentation_pytorch_amd import ops
+from _tol import bf16_close, f32_close  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -36,7 +37,7 @@ def test_stem7_matches_fp32(case, act):
         ref = ref if act == 0 else torch.relu(ref) if act == 1 else F.relu6(ref)
     y = torch.ops.rtseg.conv_stem7(x, wk, [s, s], ss, act if act is not None else 0)
     assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
-    _close(y, ref, 1e-2)
+    bf16_close(y, ref)
 
 
 def test_resnet_stem_eval_path_matches_torch(monkeypatch):

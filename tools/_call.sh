@@ -1,10 +1,6 @@
 set -o pipefail
-D=gpurun_out/r6_det; mkdir -p $D
-for i in 1 2; do
-for v in 0 1; do
-RTSEG_LOSS_ONE_CLASS=$v timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > $D/ab_${v}_$i.json 2> $D/ab.err || { tail -20 $D/ab.err; exit 1; }
-echo "one_class=$v $(cut -c1-120 $D/ab_${v}_$i.json)"
-done; done
-cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/prof -o run -- python -u bench.py --steps 4 --warmup 3 > $D/prof.log 2>&1 || { tail $D/prof.log; exit 1; }
-find $D/prof -name "*kernel_stats.csv" | head -1 | xargs -I{} grep -E "seg_ce|cast_out" {}
+D=gpurun_out/r6_tol; mkdir -p $D
+timeout -k 10 900 python -u -m pytest tests/test_conv_stem_gpu.py tests/test_zoo.py tests/test_routed_conv_gpu.py -v --timeout 200 --timeout-method thread > $D/tests2.log 2>&1; rc=$?
+grep -E "passed|failed" $D/tests2.log | tail -3
+grep -E "^FAILED|Greatest" $D/tests2.log | head -40
+exit $rc
