@@ -1,6 +1,9 @@
 set -o pipefail
-D=gpurun_out/r6_tol; mkdir -p $D
-timeout -k 10 900 python -u -m pytest tests/test_conv_stem_gpu.py tests/test_zoo.py tests/test_routed_conv_gpu.py -v --timeout 200 --timeout-method thread > $D/tests2.log 2>&1; rc=$?
-grep -E "passed|failed" $D/tests2.log | tail -3
-grep -E "^FAILED|Greatest" $D/tests2.log | head -40
-exit $rc
+D=gpurun_out/r6_iact; mkdir -p $D
+timeout -k 10 600 python -u -m pytest tests/test_ops_gpu.py tests/test_conv_igemm_gpu.py -k "interp or skip_grad" -v --timeout 120 --timeout-method thread > $D/tests.log 2>&1 || { grep -E "FAILED|Error|error" $D/tests.log | head -30; tail -5 $D/tests.log; exit 1; }
+tail -2 $D/tests.log
+for i in 1 2; do
+for v in 1 0; do
+RTSEG_INTERP_FUSED_ACT=$v timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 --no-infer > $D/ab_${v}_$i.json 2> $D/ab.err || { tail -20 $D/ab.err; exit 1; }
+echo "fused=$v $(cut -c1-110 $D/ab_${v}_$i.json)"
+done; done
