@@ -31,7 +31,7 @@ class BiSeNetv2(nn.Module):
     def forward(self, x, is_training=False):
         out_hw = x.shape[2:]
         x_d = self.detail_branch(x)
-        sem = self.semantic_branch(x)
+        sem = self.semantic_branch(x, want_aux=is_training)  # aux heads only when returned
         x_s, aux = (sem[0], sem[1:]) if self.use_aux else (sem, ())
         x = self.seg_head(self.bga_layer(x_d, x_s))
         x = ops.final_upsample(x, out_hw, True)
@@ -71,12 +71,12 @@ class SemanticBranch(nn.Sequential):
             for i, c in zip((2, 3, 4, 5), (16, 32, 64, 128)):
                 setattr(self, f"seg_head{i}", SegHead(c, num_class, act_type))
 
-    def forward(self, x):
+    def forward(self, x, want_aux=True):
         aux = []
         for i, stage in zip((2, 3, 4, 5), (self.stage1to2, self.stage3, self.stage4, self.stage5_1to4)):
             x = stage(x)
             if self.use_aux:
-                aux.append(getattr(self, f"seg_head{i}")(x))
+                aux.append(getattr(self, f"seg_head{i}")(x) if want_aux else None)
         x = self.stage5_5(x)
         return (x, *aux) if self.use_aux else x
 

@@ -60,7 +60,9 @@ class DDRNet(nn.Module):
         out_hw = x.shape[2:]
         x = self.conv3(self.conv2(self.conv1(x)))
         x_low, x_high = self.conv4(x)
-        aux = self.aux_head(x_high) if self.use_aux else None
+        # the aux head only when it is returned (the reference evaluates it in inference too and
+        # drops it: same outputs, ~4 kernels less per inference forward)
+        aux = self.aux_head(x_high) if self.use_aux and is_training else None
         x = self.seg_head(self.conv5(x_low, x_high))
         x = ops.final_upsample(x, out_hw, True)
         if torch.onnx.is_in_onnx_export():
@@ -110,9 +112,13 @@ class Stage4(nn.Module):
             self.bilateral_fusion2 = BilateralFusion(lo, hi, 2)
 
     def forward(self, x):
-        x_low, x_high = self.bilateral_fusion1(self.low_conv1(x), self.high_conv1(x))
+        # the two branches run concurrently in inference (ops/streams.py): batch-1 grids are small
+        x_low, x_high = ops.concurrent_branches(lambda: self.low_conv1(x), lambda: self.high_conv1(x), x.device)
+        x_low, x_high = self.bilateral_fusion1(x_low, x_high)
         if self.extra_conv:
-            x_low, x_high = self.bilateral_fusion2(self.low_conv2(x_low), self.high_conv2(x_high))
+            x_low, x_high = ops.concurrent_branches(lambda: self.low_conv2(x_low), lambda: self.high_conv2(x_high),
+                                                    x.device)
+            x_low, x_high = self.bilateral_fusion2(x_low, x_high)
         return x_low, x_high
 
 
@@ -128,10 +134,13 @@ class Stage5(nn.Module):
 
     def forward(self, x_low, x_high):
         hw = x_high.shape[2:]
-        x_low, x_high = self.bilateral_fusion(self.low_conv1(x_low), self.high_conv1(x_high))
-        x_low = self.dappm(self.low_conv2(x_low))
+        dev = x_high.device
+        x_low, x_high = ops.concurrent_branches(lambda: self.low_conv1(x_low), lambda: self.high_conv1(x_high), dev)
+        x_low, x_high = self.bilateral_fusion(x_low, x_high)
+        x_low, y_high = ops.concurrent_branches(lambda: self.dappm(self.low_conv2(x_low)),
+                                                lambda: self.high_conv2(x_high), dev)
         # high_conv2(x_high) + upsample(x_low) in one kernel
-        return ops.interpolate(x_low, hw, True, skip=self.high_conv2(x_high))
+        return ops.interpolate(x_low, hw, True, skip=y_high)
 
 
 class RB(nn.Module):

@@ -37,8 +37,8 @@ class ICNet(nn.Module):
         low = self.ppm(self.backbone(x_d4)[0])      # 1/32
         mid = self.backbone(x_d2)[1]                # 1/16
         high = self.bottom_branch(x)                # 1/8
-        mid, aux2 = self.cff42(low, mid)
-        high, aux3 = self.cff21(mid, high)
+        mid, aux2 = self.cff42(low, mid, is_training)  # aux classifiers only when returned
+        high, aux3 = self.cff21(mid, high, is_training)
         y = self.seg_head(ops.interpolate(high, (high.shape[2] * 2, high.shape[3] * 2), True))
         y = ops.final_upsample(y, (h, w), True)
         if self.use_aux and is_training:
@@ -56,9 +56,9 @@ class CascadeFeatureFusionUnit(nn.Module):
         if use_aux:
             self.classifier = SegHead(channel1, num_class, act_type)
 
-    def forward(self, x1, x2):
+    def forward(self, x1, x2, want_aux=True):
         x1 = ops.interpolate(x1, (x1.shape[2] * 2, x1.shape[3] * 2), True)
-        aux = self.classifier(x1) if self.use_aux else None
+        aux = self.classifier(x1) if self.use_aux and want_aux else None
         return self.conv2(x2, residual=self.conv1(x1), act=self.act), aux
 
 

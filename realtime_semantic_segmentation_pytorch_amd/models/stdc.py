@@ -66,7 +66,7 @@ class STDC(nn.Module):
         x3 = self.stage3(x)
         x4 = self.stage4(x3)
         x5 = self.stage5(x4)
-        aux = (self.aux_head3(x3), self.aux_head4(x4), self.aux_head5(x5)) if self.use_aux else ()
+        aux = (self.aux_head3(x3), self.aux_head4(x4), self.aux_head5(x5)) if self.use_aux and is_training else ()
         x5 = self.conv5(self.pool(x5) + self.arm5(x5))
         x4 = _up2(_up2(x5, skip=self.conv4(self.arm4(x4))))
         x = self.seg_head(self.ffm(x4, x3))

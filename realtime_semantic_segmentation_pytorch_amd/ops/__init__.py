@@ -30,6 +30,7 @@ from .gate import gate, gate_reference
 from .act import activation, convert_activations
 from .shuffle import channel_shuffle, convert_pixel_shuffle, pixel_shuffle, pixel_unshuffle
 from .augment import AugmentSpec, augment_batch, augment_reference, draw_params
+from .streams import concurrent_branches
 
 __all__ = [
     "load", "use_hip", "hip_disabled", "library_path",
@@ -43,5 +44,5 @@ __all__ = [
     "PrunedConv2d", "convert_pruned_convs", "pruned_conv2d", "has_dead_taps",
     "FusedSGD", "FusedAdam", "FusedAdamW", "conv_ok", "conv_bn_stats", "stem_store_skippable", "twin_conv_bn_stats", "conv_bn_act_eval", "conv_bn_act", "conv_forward", "RoutedConv2d", "GroupedConv2d", "convert_routed_convs", "invalidate_weight_shadows",
     "TransposedConv2d", "conv_transpose2d", "convert_transposed_convs", "deconv_ok", "gate", "gate_reference", "activation", "convert_activations", "channel_shuffle", "convert_pixel_shuffle", "pixel_shuffle", "pixel_unshuffle", "AugmentSpec", "augment_batch", "augment_reference", "draw_params",
-    "ConcatSink", "cat_bn_act", "bn_act", "bn_stats_begin", "bias_add", "bn_act_code", "bn_fused_ok", "convert_batchnorm", "FusedBatchNorm2d", "FusedSyncBatchNorm",
+    "concurrent_branches", "ConcatSink", "cat_bn_act", "bn_act", "bn_stats_begin", "bias_add", "bn_act_code", "bn_fused_ok", "convert_batchnorm", "FusedBatchNorm2d", "FusedSyncBatchNorm",
 ]
