@@ -101,7 +101,13 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::
   else if (hreg) {
     at::Tensor wpack = at::empty({conv_hreg_pack_elems(g, 0)}, wk.options());
     launch_conv_hreg(g, 0, wpack.data_ptr(), cur_stream(), kind == 4 ? 2 : kind == 8 ? 4 : kind == 9 ? 5 : 1);
-  } else launch_conv_igemm_fwd(g, cur_stream());
+  } else {
+    if (kind == 11) {
+      TORCH_CHECK(g.scale_shift != nullptr && !stats, "rtseg.conv_igemm_small: the inference BN epilogue only");
+      g.cfg = 5;
+    }
+    launch_conv_igemm_fwd(g, cur_stream());
+  }
   if (stats && part.size(0) > 256) {  // fold the per-tile rows so the BN finalize stays cheap
     const int rows = static_cast<int>(part.size(0));
     const int chunk = (rows + 255) / 256;
@@ -117,6 +123,14 @@ std::tuple<at::Tensor, at::Tensor> conv_igemm(const at::Tensor& x, const at::Ten
                                               const std::optional<at::Tensor>& scale_shift,
                                               const std::optional<at::Tensor>& residual, int64_t act) {
   return conv_fwd_impl(x, wk, stride, padding, dilation, stats, scale_shift, residual, act, 0);
+}
+
+// the gather kernel on 128 x 64 block tiles, 2 blocks per CU (inference BN epilogue only): small
+// batch-1 layers, timed against the shape-picked tiles and MIOpen (ops/conv.py conv_bn_act_eval)
+at::Tensor conv_igemm_small(const at::Tensor& x, const at::Tensor& wk, at::IntArrayRef stride, at::IntArrayRef padding,
+                            at::IntArrayRef dilation, const at::Tensor& scale_shift,
+                            const std::optional<at::Tensor>& residual, int64_t act) {
+  return std::get<0>(conv_fwd_impl(x, wk, stride, padding, dilation, false, scale_shift, residual, act, 11));
 }
 
 // the halo-tiled kernel (conv_halo.hip): stride-1 convs whose taps fit a 3 x 3 footprint
@@ -434,6 +448,8 @@ at::Tensor conv_stem_wgrad_bn(const at::Tensor& x, const at::Tensor& dy, const a
 TORCH_LIBRARY_FRAGMENT(rtseg, m) {
   m.def("conv_igemm(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats, "
         "Tensor? scale_shift, Tensor? residual, int act) -> (Tensor, Tensor)");
+  m.def("conv_igemm_small(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, Tensor scale_shift, "
+        "Tensor? residual, int act) -> Tensor");
   m.def("conv_igemm_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
         "Tensor? bias=None, Tensor? addend=None, Tensor? addend_mask=None, Tensor? phase_addend=None, "
         "bool fused_phases=False) -> Tensor");
@@ -468,6 +484,7 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
 
 TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
   m.impl("conv_igemm", &rtseg::conv_igemm);
+  m.impl("conv_igemm_small", &rtseg::conv_igemm_small);
   m.impl("conv_igemm_dgrad", &rtseg::conv_igemm_dgrad);
   m.impl("conv_halo", &rtseg::conv_halo);
   m.impl("conv_halo_dgrad", &rtseg::conv_halo_dgrad);

@@ -183,6 +183,8 @@ struct ConvGeom {
   // rows / columns of a stride-2 dx, [N][ceil(H/2)][ceil(W/2)][Cin]): the data gradient of a
   // stride-2 1 x 1 shortcut on the same input, computed as a plain GEMM (ops/conv.py _TwinConvFn)
   const void* res_phase0 = nullptr;
+  // igemm forward: a forced block-tile configuration (conv_igemm.hip kCfgs), -1 = by shape
+  int cfg = -1;
 };
 // BN activation-derivative sources (= ops/bn.py MASK_*)
 enum BnMaskMode : int { kBnMaskNone = 0, kBnMaskFromY = 1, kBnMaskFromX = 2, kBnMaskBits = 3 };

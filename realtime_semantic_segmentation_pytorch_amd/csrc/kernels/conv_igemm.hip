@@ -750,6 +750,9 @@ __global__ void igemm_wgrad_reduce(const float* __restrict__ ws, float* __restri
 //   2: 512 x  64, 8 x 1 waves (64 x 64),            2 stages, 144 KiB  -- Cout <= 64
 //   3: 256 x 256, 2 x 4 waves (64 x 128),           2 stages, 128 KiB  -- Cout >= 256
 //   4: 512 x 128, 4 x 2 waves (64 x 128),           2 stages, 160 KiB  -- Cout 65..128 (..255)
+//   5: 128 x  64, 2 x 2 waves (64 x 32),            3 stages,  72 KiB, 2 blocks per CU -- the
+//      inference BN epilogue only, on request (conv_igemm_small): batch-1 layers whose 256-pixel
+//      tiles leave most of the 256 CUs idle (DDRNet-23's 1/16 and 1/32 branches: 32-64 blocks)
 // The big wave tiles halve the LDS fragment reads per MFMA (profiles/r2_conv_igemm: 64 x 128
 // tiles beat MIOpen's forward and its backward-data by 1.1-1.5x at batch 32); problems with
 // fewer than one tile per CU fall back to the smaller tiles.
@@ -757,7 +760,9 @@ __global__ void igemm_wgrad_reduce(const float* __restrict__ ws, float* __restri
 struct Cfg {
   int id, bm, bn, wm;
 };
-constexpr Cfg kCfgs[] = {{0, 256, 64, 4}, {1, 256, 128, 4}, {2, 512, 64, 8}, {3, 256, 256, 2}, {4, 512, 128, 4}};
+constexpr Cfg kCfgs[] = {{0, 256, 64, 4}, {1, 256, 128, 4}, {2, 512, 64, 8}, {3, 256, 256, 2}, {4, 512, 128, 4},
+                         {5, 128, 64, 2}};
+constexpr int kShapeCfgs = 5;  // 0..4 are picked by shape / RTSEG_IGEMM_CFG; 5 only on request
 
 int64_t cfg_tiles(const Cfg& c, int64_t M, int cout) { return ((M + c.bm - 1) / c.bm) * ((cout + c.bn - 1) / c.bn); }
 
@@ -765,16 +770,16 @@ Cfg pick_cfg(int cout, int64_t M) {
   const char* e = std::getenv("RTSEG_IGEMM_CFG");
   if (e != nullptr && *e != '\0') {
     const int i = std::atoi(e);
-    if (i >= 0 && i < static_cast<int>(sizeof(kCfgs) / sizeof(kCfgs[0]))) return kCfgs[i];
+    if (i >= 0 && i < kShapeCfgs) return kCfgs[i];
   }
   const Cfg big = cout <= 64 ? kCfgs[2] : cout <= 128 ? kCfgs[4] : kCfgs[3];
   const Cfg small = cout <= 64 ? kCfgs[0] : kCfgs[1];
   return cfg_tiles(big, M, cout) >= 256 ? big : small;
 }
 
-int persistent_grid(int mtiles, int ntiles) {
+int persistent_grid(int mtiles, int ntiles, int per_cu = 1) {
   const int64_t tiles = static_cast<int64_t>(mtiles) * ntiles;
-  const int cap = std::max(ntiles, (256 / ntiles) * ntiles);  // one block per CU (LDS-bound)
+  const int cap = std::max(ntiles, (256 * per_cu / ntiles) * ntiles);  // per_cu blocks per CU (LDS-bound)
   return static_cast<int>(tiles < cap ? tiles : cap);
 }
 
@@ -800,6 +805,9 @@ void launch_cfg(const IgArgs& k, const Cfg& c, int grid, hipStream_t st) {
       break;
     case 4:
       if constexpr (EPI == 0) igemm_gather_kernel<512, 128, 4, 2, 2, 0, STATS, GB, PH><<<grid, 512, 0, st>>>(k);
+      break;
+    case 5:
+      if constexpr (EPI == 1 && STATS == 0 && PH == 0) igemm_gather_kernel<128, 64, 2, 2, 3, 1, 0, GB, 0><<<grid, 256, 0, st>>>(k);
       break;
     default: igemm_gather_kernel<256, 128, 4, 2, 3, EPI, STATS, GB, PH><<<grid, 512, 0, st>>>(k); break;
   }
@@ -830,7 +838,7 @@ __global__ void slab_compact_kernel(const float* __restrict__ in, int rows, int 
 }
 
 void launch_gather(const IgArgs& k, const Cfg& c, hipStream_t st) {
-  const int grid = persistent_grid(k.mtiles, k.ntiles);
+  const int grid = persistent_grid(k.mtiles, k.ntiles, c.id == 5 ? 2 : 1);
   if (grid <= 0) return;
   if (k.nph > 1) {  // fused dgrad phases: data-gradient epilogue only
     if (use_buffer_gather(k)) launch_cfg<0, 0, 1, 1>(k, c, grid, st);
@@ -901,6 +909,7 @@ void launch_conv_igemm_fwd(const ConvGeom& g, hipStream_t st) {
   Cfg c = pick_cfg(g.cout, static_cast<int64_t>(g.n) * g.ho * g.wo);
   // the inference BN epilogue (scale/shift/residual loads) spills on the 64 x 128 wave tiles
   if (g.scale_shift != nullptr && (c.id == 3 || c.id == 4)) c = kCfgs[1];
+  if (g.cfg == 5 && g.scale_shift != nullptr && g.part == nullptr) c = kCfgs[5];
   fill_common(k, c, g.n);
   launch_gather(k, c, st);
 }

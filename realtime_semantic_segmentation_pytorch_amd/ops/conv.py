@@ -1065,6 +1065,10 @@ def conv_bn_stats(x: torch.Tensor, conv: nn.Conv2d, store: bool = True):
     return _apply(x, conv, True, store)
 
 
+# inference: the 128 x 64-tile gather kernel as an autotune candidate (RTSEG_IGEMM_SMALL=0: off)
+_SMALL_TILES = os.environ.get("RTSEG_IGEMM_SMALL", "1") != "0"
+
+
 def conv_bn_act_eval(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, act_code: int, residual=None):
     """Inference: act(BN_running(conv(x)) + residual) in one kernel, or None -> caller's path.
     The kernel output has no autograd graph, so a frozen (eval-mode) BN inside a TRAINING step
@@ -1099,13 +1103,22 @@ def conv_bn_act_eval(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, act_code: 
     def ours():
         return op(x, wk, stride, padding, dilation, False, ss, res, act_code)[0]
 
+    def small():  # 128 x 64 tiles, 2 blocks per CU: batch-1 layers that 256-pixel tiles under-fill
+        return ops().conv_igemm_small(x, wk, stride, padding, dilation, ss, res, act_code)
+
     def theirs():
         y = F.conv2d(x, wk.permute(0, 3, 1, 2), None, stride, padding, dilation)
         ops().bn_apply(y, ss, res, act_code)
 
-    if _choose(key, [("igemm" if cin % 64 == 0 else "mfma", ours), ("miopen", theirs)]) != 0:
+    cands = [("igemm" if cin % 64 == 0 else "mfma", ours)]
+    npix = x.shape[0] * (-(-x.shape[2] // stride[0])) * (-(-x.shape[3] // stride[1]))
+    if cin % 64 == 0 and -(-npix // 256) * -(-cout // 128) < 256 and _SMALL_TILES:
+        cands.append(("igemm_s", small))
+    cands.append(("miopen", theirs))
+    pick = _choose(key, cands)
+    if cands[pick][0] == "miopen":
         return None
-    return ours()
+    return cands[pick][1]()
 
 
 def stem7_ok(conv: nn.Module, x: torch.Tensor) -> bool:
