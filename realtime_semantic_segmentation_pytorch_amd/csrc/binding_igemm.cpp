@@ -102,11 +102,17 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::
     at::Tensor wpack = at::empty({conv_hreg_pack_elems(g, 0)}, wk.options());
     launch_conv_hreg(g, 0, wpack.data_ptr(), cur_stream(), kind == 4 ? 2 : kind == 8 ? 4 : kind == 9 ? 5 : 1);
   } else {
-    if (kind == 11) {
+    if (kind == 11 || kind == 12) {
       TORCH_CHECK(g.scale_shift != nullptr && !stats, "rtseg.conv_igemm_small: the inference BN epilogue only");
       g.cfg = 5;
     }
-    launch_conv_igemm_fwd(g, cur_stream());
+    const int ks = kind == 12 ? conv_igemm_splitk(g) : 1;
+    if (ks > 1) {
+      at::Tensor ws = at::empty({static_cast<int64_t>(ks) * g.n * g.ho * g.wo * g.cout}, x.options().dtype(at::kFloat));
+      launch_conv_igemm_fwd_splitk(g, ws.data_ptr<float>(), ks, cur_stream());
+    } else {
+      launch_conv_igemm_fwd(g, cur_stream());
+    }
   }
   if (stats && part.size(0) > 256) {  // fold the per-tile rows so the BN finalize stays cheap
     const int rows = static_cast<int>(part.size(0));
@@ -129,8 +135,9 @@ std::tuple<at::Tensor, at::Tensor> conv_igemm(const at::Tensor& x, const at::Ten
 // batch-1 layers, timed against the shape-picked tiles and MIOpen (ops/conv.py conv_bn_act_eval)
 at::Tensor conv_igemm_small(const at::Tensor& x, const at::Tensor& wk, at::IntArrayRef stride, at::IntArrayRef padding,
                             at::IntArrayRef dilation, const at::Tensor& scale_shift,
-                            const std::optional<at::Tensor>& residual, int64_t act) {
-  return std::get<0>(conv_fwd_impl(x, wk, stride, padding, dilation, false, scale_shift, residual, act, 11));
+                            const std::optional<at::Tensor>& residual, int64_t act, bool split_k) {
+  return std::get<0>(conv_fwd_impl(x, wk, stride, padding, dilation, false, scale_shift, residual, act,
+                                   split_k ? 12 : 11));
 }
 
 // the halo-tiled kernel (conv_halo.hip): stride-1 convs whose taps fit a 3 x 3 footprint
@@ -449,7 +456,7 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
   m.def("conv_igemm(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats, "
         "Tensor? scale_shift, Tensor? residual, int act) -> (Tensor, Tensor)");
   m.def("conv_igemm_small(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, Tensor scale_shift, "
-        "Tensor? residual, int act) -> Tensor");
+        "Tensor? residual, int act, bool split_k=False) -> Tensor");
   m.def("conv_igemm_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
         "Tensor? bias=None, Tensor? addend=None, Tensor? addend_mask=None, Tensor? phase_addend=None, "
         "bool fused_phases=False) -> Tensor");

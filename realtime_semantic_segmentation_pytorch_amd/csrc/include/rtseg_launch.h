@@ -196,6 +196,10 @@ void launch_conv_mfma(const ConvGeom& g, hipStream_t st);
 // mode 0 = forward, 1 = data gradient, 2 = weight gradient.
 constexpr int kIgemmMaxTaps = 49;
 bool conv_igemm_supported(const ConvGeom& g, int mode);
+// batch-1 inference forward split over K: parts (1 = no split) and the launch (fp32 workspace of
+// parts * N * Ho * Wo * Cout floats; g.scale_shift required, g.res / g.act applied after the sum)
+int conv_igemm_splitk(const ConvGeom& g);
+void launch_conv_igemm_fwd_splitk(const ConvGeom& g, float* ws, int ksplit, hipStream_t st);
 // rows of the BN statistics slab [rows, 2*Cout] written by the forward when g.part != nullptr
 // (one per M tile and pixel wave); launch_slab_compact sums groups of `chunk` rows
 int conv_igemm_slabs(const ConvGeom& g);

@@ -80,6 +80,8 @@ struct IgArgs {
   int sh, sw;             // input pixel = (hv*sh + dh[t], wv*sw + dw[t])
   int wrow;               // weight row stride (elements) = KT * C
   int ntap, cch, nk;      // taps, 64-channel chunks per tap, K-steps per tile
+  int ksplit, nkp;        // EPI 2 (split K): K parts per output tile, K-steps per part (nk = ksplit * nkp)
+  float* ws;              // EPI 2: fp32 partial sums [ksplit][M][cout]
   int nph;                // output phases per launch (fused dgrad of a strided conv), else 1
   int wide;               // 16-byte epilogue stores (channel-group pairs swapped across half-waves)
   int phase_off[kMaxPhases];  // phase q: oph | opw << 8 (nph > 1; taps of phase q at q * ntap)
@@ -112,6 +114,10 @@ __device__ __forceinline__ void bdma16x2(__amdgpu_buffer_rsrc_t r, uint32_t v0, 
 }
 
 
+// EPI: 0 = plain / statistics / data-gradient epilogues, 1 = inference BN (+ residual + act),
+// 2 = split K: tile t of the walk is output tile t / ksplit over K part t % ksplit, whose fp32
+// partial sums go to a.ws; splitk_bn_kernel sums the parts in order and applies the BN epilogue
+// (batch-1 inference layers with too few output tiles to fill the CUs)
 // STATS: 0 = none, 1 = forward BN statistics of the output
 // GB: gather the activation rows through a buffer resource (range-checked voffsets, the
 // border handled by the range check) instead of 64-bit flat addresses with a zero source, and
@@ -144,7 +150,7 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
   const int mstep = G / a.ntiles;
   const int mfirst = lb / a.ntiles;
   const int my_tiles = mfirst < a.mtiles ? (a.mtiles - mfirst + mstep - 1) / mstep : 0;
-  const int nk = a.nk;
+  const int nk = EPI == 2 ? a.nkp : a.nk;
 
   // ---- DMA geometry: instruction I fills 8 rows (I*8 + lane/8) x 8 chunks of one operand
   const int lr8 = lane >> 3, lch = lane & 7;
@@ -179,6 +185,7 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
   auto set_rows = [&](int tile) {
     int mt = tile;
     if (PH) { mt = tile / P; st_phase = tile - mt * P; }
+    if constexpr (EPI == 2) mt = tile / a.ksplit;
 #pragma unroll
     for (int e = 0; e < PI; ++e) {
       const int m = mt * BM + (wid * PI + e) * 8 + lr8;
@@ -197,7 +204,12 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
   };
 
   // staging cursor (wave-uniform): tile ordinal, tap, channel chunk
-  int st_ord = 0, st_t = 0, st_c = 0, st_buf = 0;
+  int st_ord = 0, st_t = 0, st_c = 0, st_buf = 0, st_k = 0;
+  auto split_cursor = [&](int tile) {  // EPI 2: the first K-step (tap, chunk) of the tile's part
+    const int k0 = (tile % a.ksplit) * a.nkp;
+    st_t = k0 / a.cch;
+    st_c = k0 - st_t * a.cch;
+  };
   auto stage = [&]() {
     // uniform indices -> scalar (SMEM) tap-table loads: a VGPR-indexed kernarg load is a VMEM
     // load whose s_waitcnt vmcnt(0) would drain the whole DMA ring every K-step
@@ -241,11 +253,24 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
       }
     }
     if (++st_buf == NST) st_buf = 0;
-    if (++st_c == a.cch) {
-      st_c = 0;
-      if (++st_t == a.ntap) {
-        st_t = 0;
-        if (++st_ord < my_tiles) set_rows(mfirst + st_ord * mstep);
+    if constexpr (EPI == 2) {
+      if (++st_k == a.nkp) {  // this K part is staged: the next tile's part
+        st_k = 0;
+        if (++st_ord < my_tiles) {
+          set_rows(mfirst + st_ord * mstep);
+          split_cursor(mfirst + st_ord * mstep);
+        }
+      } else if (++st_c == a.cch) {
+        st_c = 0;
+        ++st_t;
+      }
+    } else {
+      if (++st_c == a.cch) {
+        st_c = 0;
+        if (++st_t == a.ntap) {
+          st_t = 0;
+          if (++st_ord < my_tiles) set_rows(mfirst + st_ord * mstep);
+        }
       }
     }
   };
@@ -283,6 +308,26 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
   for (int k = 0; k < NPS; ++k) pst[k] = 0.f;
 
   auto pack_tile = [&](int tile) __attribute__((always_inline)) {
+    if constexpr (EPI == 2) {  // fp32 partial sums of K part tile % ksplit, 16-byte stores
+      const int mt = tile / a.ksplit, kp = tile - mt * a.ksplit;
+#pragma unroll
+      for (int tj = 0; tj < TJ; ++tj) {
+        const int m = mt * BM + wm * (BM / WM) + tj * 32 + frow;
+#pragma unroll
+        for (int ti = 0; ti < TI; ++ti) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int co = co_lane + ti * 32 + 8 * g;
+            if (m < a.M && co < a.cout)
+              *reinterpret_cast<float4*>(a.ws + (static_cast<int64_t>(kp) * a.M + m) * a.cout + co) =
+                  make_float4(acc[ti][tj][4 * g], acc[ti][tj][4 * g + 1], acc[ti][tj][4 * g + 2], acc[ti][tj][4 * g + 3]);
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[ti][tj][r] = 0.f;
+        }
+      }
+      return;
+    }
     int mt = tile, oph = a.oph, opw = a.opw;
     bool phase0 = true;
     if (PH) {
@@ -438,7 +483,10 @@ __global__ void __launch_bounds__(WM* WN * 64) igemm_gather_kernel(const IgArgs 
   if (nk == 0) {  // empty tap set (a dgrad phase no tap reaches): the outputs are zero
     for (int i = 0; i < my_tiles; ++i) pack_tile(mfirst + i * mstep);
   } else {
-    if (my_tiles > 0) set_rows(mfirst);
+    if (my_tiles > 0) {
+      set_rows(mfirst);
+      if constexpr (EPI == 2) split_cursor(mfirst);
+    }
 #pragma unroll
     for (int p = 0; p < NST - 1; ++p)
       if (p < total) stage();
@@ -807,7 +855,8 @@ void launch_cfg(const IgArgs& k, const Cfg& c, int grid, hipStream_t st) {
       if constexpr (EPI == 0) igemm_gather_kernel<512, 128, 4, 2, 2, 0, STATS, GB, PH><<<grid, 512, 0, st>>>(k);
       break;
     case 5:
-      if constexpr (EPI == 1 && STATS == 0 && PH == 0) igemm_gather_kernel<128, 64, 2, 2, 3, 1, 0, GB, 0><<<grid, 256, 0, st>>>(k);
+      if constexpr ((EPI == 1 || EPI == 2) && STATS == 0 && PH == 0)
+        igemm_gather_kernel<128, 64, 2, 2, 3, EPI, 0, GB, 0><<<grid, 256, 0, st>>>(k);
       break;
     default: igemm_gather_kernel<256, 128, 4, 2, 3, EPI, STATS, GB, PH><<<grid, 512, 0, st>>>(k); break;
   }
@@ -845,7 +894,8 @@ void launch_gather(const IgArgs& k, const Cfg& c, hipStream_t st) {
     else launch_cfg<0, 0, 0, 1>(k, c, grid, st);
     return;
   }
-  if (k.ss != nullptr) launch_cfg<1, 0>(k, c, grid, st);
+  if (k.ws != nullptr) launch_cfg<2, 0>(k, c, grid, st);
+  else if (k.ss != nullptr) launch_cfg<1, 0>(k, c, grid, st);
   else if (k.part != nullptr) launch_cfg<0, 1>(k, c, grid, st);
   else launch_cfg<0, 0>(k, c, grid, st);
 }
@@ -912,6 +962,86 @@ void launch_conv_igemm_fwd(const ConvGeom& g, hipStream_t st) {
   if (g.cfg == 5 && g.scale_shift != nullptr && g.part == nullptr) c = kCfgs[5];
   fill_common(k, c, g.n);
   launch_gather(k, c, st);
+}
+
+// split-K epilogue: y[m][c] = act(sum_kp ws[kp][m][c] * scale[c] + shift[c] (+ res[m][c])), the
+// parts summed in order (deterministic); 8 channels per thread, 16-byte stores
+__global__ void __launch_bounds__(256) splitk_bn_kernel(const float* __restrict__ ws, int ksplit, int64_t M, int cout,
+                                                        const float* __restrict__ ss, const uint16_t* __restrict__ res,
+                                                        int act, uint16_t* __restrict__ y) {
+  const int cv = cout / 8;
+  const int64_t total = M * cv;
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t m = i / cv;
+    const int c0 = static_cast<int>(i - m * cv) * 8;
+    float v[8];
+    const float4* p = reinterpret_cast<const float4*>(ws + m * cout + c0);
+    float4 lo = p[0], hi = p[1];
+    v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+    for (int kp = 1; kp < ksplit; ++kp) {
+      const float4* q = reinterpret_cast<const float4*>(ws + (static_cast<int64_t>(kp) * M + m) * cout + c0);
+      lo = q[0]; hi = q[1];
+      v[0] += lo.x; v[1] += lo.y; v[2] += lo.z; v[3] += lo.w; v[4] += hi.x; v[5] += hi.y; v[6] += hi.z; v[7] += hi.w;
+    }
+    float r[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (res != nullptr) {
+      const uint4 rv = *reinterpret_cast<const uint4*>(res + m * cout + c0);
+      bf16x4_unpack(make_uint2(rv.x, rv.y), r);
+      bf16x4_unpack(make_uint2(rv.z, rv.w), r + 4);
+    }
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const float a0 = epi_act(fmaf(v[j], ss[c0 + j], ss[cout + c0 + j]) + r[j], act);
+      const float a1 = epi_act(fmaf(v[j + 1], ss[c0 + j + 1], ss[cout + c0 + j + 1]) + r[j + 1], act);
+      o[j / 2] = pack2(a0, a1);
+    }
+    *reinterpret_cast<uint4*>(y + m * cout + c0) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+// K parts for the batch-1 split-K forward (128 x 64 tiles): enough blocks for two per CU, each
+// part >= 4 K-steps, nk divisible by the part count; 1 = no split
+int conv_igemm_splitk(const ConvGeom& g) {
+  if (g.cout % 8 != 0 || g.cin % 64 != 0) return 1;
+  const int64_t M = static_cast<int64_t>(g.n) * g.ho * g.wo;
+  const int64_t tiles = cfg_tiles(kCfgs[5], M, g.cout);
+  const int nk = g.kh * g.kw * (g.cin / 64);
+  if (tiles >= 256) return 1;
+  int best = 1;
+  for (int s = 2; s <= 16; ++s)
+    if (nk % s == 0 && nk / s >= 4 && tiles * best < 512) best = s;
+  return best;
+}
+
+void launch_conv_igemm_fwd_splitk(const ConvGeom& g, float* ws, int ksplit, hipStream_t st) {
+  IgArgs k{};
+  k.x = static_cast<const uint16_t*>(g.x);
+  k.w = static_cast<const uint16_t*>(g.w);
+  k.y = static_cast<uint16_t*>(g.y);
+  k.H = g.h; k.W = g.w_in; k.C = g.cin;
+  k.Hv = g.ho; k.Wv = g.wo; k.Ho = g.ho; k.Wo = g.wo; k.cout = g.cout;
+  k.osh = 1; k.osw = 1; k.oph = 0; k.opw = 0; k.sh = g.sh; k.sw = g.sw;
+  k.wrow = g.kh * g.kw * g.cin;
+  k.cch = g.cin / 64;
+  k.ntap = 0;
+  const int64_t xb = static_cast<int64_t>(g.n) * g.h * g.w_in * g.cin * 2;
+  k.xbytes = xb <= (int64_t{1} << 31) ? static_cast<uint32_t>(xb) : 0u;
+  const int64_t yb = static_cast<int64_t>(g.n) * g.ho * g.wo * g.cout * 2;
+  k.ybytes = yb <= (int64_t{1} << 31) ? static_cast<uint32_t>(yb) : 0u;
+  for (int i = 0; i < g.kh; ++i)
+    for (int j = 0; j < g.kw; ++j) k.taps[k.ntap++] = pack_tap(i * g.dh - g.ph, j * g.dw - g.pw, i * g.kw + j, i, j);
+  const Cfg c = kCfgs[5];
+  fill_common(k, c, g.n);
+  k.ksplit = ksplit;
+  k.nkp = k.nk / ksplit;
+  k.mtiles *= ksplit;  // the walk's tiles: (output tile, K part) pairs
+  k.ws = ws;
+  launch_gather(k, c, st);
+  const int64_t M = static_cast<int64_t>(g.n) * g.ho * g.wo;
+  splitk_bn_kernel<<<stream_grid(M * (g.cout / 8), 256), 256, 0, st>>>(
+      ws, ksplit, M, g.cout, g.scale_shift, static_cast<const uint16_t*>(g.res), g.act, static_cast<uint16_t*>(g.y));
 }
 
 // g: forward geometry; g.x = dy [N,Ho,Wo,Cout], g.w = wt [Cin][KH][KW][Cout], g.y = dx [N,H,W,Cin]

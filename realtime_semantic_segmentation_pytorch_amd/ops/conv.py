@@ -1103,17 +1103,20 @@ def conv_bn_act_eval(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, act_code: 
     def ours():
         return op(x, wk, stride, padding, dilation, False, ss, res, act_code)[0]
 
-    def small():  # 128 x 64 tiles, 2 blocks per CU: batch-1 layers that 256-pixel tiles under-fill
-        return ops().conv_igemm_small(x, wk, stride, padding, dilation, ss, res, act_code)
+    def small(split_k=False):  # 128 x 64 tiles, 2 blocks per CU: batch-1 layers 256-pixel tiles under-fill
+        return ops().conv_igemm_small(x, wk, stride, padding, dilation, ss, res, act_code, split_k)
 
     def theirs():
         y = F.conv2d(x, wk.permute(0, 3, 1, 2), None, stride, padding, dilation)
         ops().bn_apply(y, ss, res, act_code)
 
     cands = [("igemm" if cin % 64 == 0 else "mfma", ours)]
-    npix = x.shape[0] * (-(-x.shape[2] // stride[0])) * (-(-x.shape[3] // stride[1]))
-    if cin % 64 == 0 and -(-npix // 256) * -(-cout // 128) < 256 and _SMALL_TILES:
+    if cin % 64 == 0 and _SMALL_TILES:
         cands.append(("igemm_s", small))
+        # ... split over K when even the small tiles leave CUs idle (fp32 parts + one BN pass)
+        npix = x.shape[0] * (-(-x.shape[2] // stride[0])) * (-(-x.shape[3] // stride[1]))
+        if -(-npix // 128) * -(-cout // 64) < 256:
+            cands.append(("igemm_k", lambda: small(True)))
     cands.append(("miopen", theirs))
     pick = _choose(key, cands)
     if cands[pick][0] == "miopen":

@@ -113,9 +113,12 @@ def test_igemm_bn_epilogue(act, with_res):
 @pytest.mark.parametrize("geom", [(1, 256, 16, 32, 256, 3, 1, 1), (1, 512, 8, 16, 512, 3, 1, 1),
                                   (1, 128, 33, 20, 256, 3, 2, 1), (2, 64, 9, 13, 72, 1, 1, 1)])
 @pytest.mark.parametrize("with_res", [False, True])
-def test_igemm_small_tiles_inference(geom, with_res):
+@pytest.mark.parametrize("split_k", [False, True])
+def test_igemm_small_tiles_inference(geom, with_res, split_k):
     """The 128 x 64-tile, 2-blocks-per-CU configuration (conv_igemm_small: batch-1 inference)
-    against fp32, and bitwise against the shape-picked tiles (same K order per output)."""
+    against fp32, and bitwise against the shape-picked tiles (same K order per output); with
+    split_k the layers with < 256 tiles sum K parts in fp32 and apply the BN epilogue after
+    (every geometry here but the last splits)."""
     n, cin, h, w, cout, k, s, d = geom
     x, wt = _case(*geom, seed=13)
     p = (k - 1) // 2 * d
@@ -126,13 +129,15 @@ def test_igemm_small_tiles_inference(geom, with_res):
     if with_res:
         res = torch.randn(n, cout, ho, wo, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=torch.channels_last)
     wk = wt.permute(0, 2, 3, 1).contiguous()
-    y = torch.ops.rtseg.conv_igemm_small(x, wk, [s, s], [p, p], [d, d], ss, res, 1)
+    y = torch.ops.rtseg.conv_igemm_small(x, wk, [s, s], [p, p], [d, d], ss, res, 1, split_k)
     ref = F.conv2d(x.float(), wt.float(), None, s, p, d) * ss[:cout].view(1, -1, 1, 1) + ss[cout:].view(1, -1, 1, 1)
     if with_res:
         ref = ref + res.float()
     bf16_close(y, ref.relu())
-    y0, _ = torch.ops.rtseg.conv_igemm(x, wk, [s, s], [p, p], [d, d], False, ss, res, 1)
-    assert torch.equal(y, y0)
+    assert torch.equal(y, torch.ops.rtseg.conv_igemm_small(x, wk, [s, s], [p, p], [d, d], ss, res, 1, split_k))
+    if not split_k:
+        y0, _ = torch.ops.rtseg.conv_igemm(x, wk, [s, s], [p, p], [d, d], False, ss, res, 1)
+        assert torch.equal(y, y0)
 
 
 DGRAD = [

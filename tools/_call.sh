@@ -1,9 +1,9 @@
 set -o pipefail
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
-D=gpurun_out/r6_small; mkdir -p $D
+D=gpurun_out/r6_splitk; mkdir -p $D
 timeout -k 10 400 python -u -m pytest tests/test_conv_igemm_gpu.py -k small -v --timeout 120 --timeout-method thread > $D/tests.log 2>&1 || { grep -E "FAILED|^E  " $D/tests.log | head -30; tail -3 $D/tests.log; exit 1; }
 tail -2 $D/tests.log
 for i in 1 2; do for v in 1 0; do
-RTSEG_IGEMM_SMALL=$v RTSEG_DECISIONS_OUT=$D/dec_$v.txt timeout -k 10 180 python3 tools/profile_infer.py --iters 300 > $D/infer_${v}_$i.txt 2>&1 || { tail -5 $D/infer_${v}_$i.txt; exit 1; }
+RTSEG_IGEMM_SMALL=$v timeout -k 10 180 python3 tools/profile_infer.py --iters 300 > $D/infer_${v}_$i.txt 2>&1 || { tail -5 $D/infer_${v}_$i.txt; exit 1; }
 echo "small=$v $(tail -1 $D/infer_${v}_$i.txt)"
 done; done
