@@ -60,7 +60,6 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::
                 "rtseg.conv_halo: needs stride 1, taps within 3 x 3, Cin % 64 == 0, Cout % 64 == 0");
   } else if (wres) {
     TORCH_CHECK(conv_wres_supported(g, 0), "rtseg.conv_wres: needs 3 x 3 / stride 1 / pad 1, Cin == 64, Cout % 64 == 0");
-    TORCH_CHECK(!(scale_shift.has_value() && scale_shift->defined()), "rtseg.conv_wres: no inference BN epilogue");
   } else if (hreg) {
     TORCH_CHECK(conv_hreg_supported(g, 0),
                 "rtseg.conv_hreg: needs 3 x 3 / stride 1 / pad 1, Cin % 64 == 0, Cout % 128 == 0");
@@ -129,6 +128,14 @@ std::tuple<at::Tensor, at::Tensor> conv_igemm(const at::Tensor& x, const at::Ten
                                               const std::optional<at::Tensor>& scale_shift,
                                               const std::optional<at::Tensor>& residual, int64_t act) {
   return conv_fwd_impl(x, wk, stride, padding, dilation, stats, scale_shift, residual, act, 0);
+}
+
+// conv_wres with the inference BN epilogue act(conv * scale + shift (+ residual)): 64-channel
+// 3 x 3 layers at batch-1 inference (DDRNet-23's 1/4-resolution stage)
+at::Tensor conv_wres_eval(const at::Tensor& x, const at::Tensor& wk, at::IntArrayRef stride, at::IntArrayRef padding,
+                          at::IntArrayRef dilation, const at::Tensor& scale_shift,
+                          const std::optional<at::Tensor>& residual, int64_t act) {
+  return std::get<0>(conv_fwd_impl(x, wk, stride, padding, dilation, false, scale_shift, residual, act, 2));
 }
 
 // the gather kernel on 128 x 64 block tiles, 2 blocks per CU (inference BN epilogue only): small
@@ -469,6 +476,8 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
   m.def("conv_hreg_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
         "Tensor? addend=None, int rows_per_wave=1, Tensor? addend_mask=None) -> Tensor");
   m.def("conv_wres(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats) -> (Tensor, Tensor)");
+  m.def("conv_wres_eval(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, Tensor scale_shift, "
+        "Tensor? residual, int act) -> Tensor");
   m.def("conv_wres_dgrad(Tensor dy, Tensor wt, int[] x_size, int[] stride, int[] padding, int[] dilation, "
         "Tensor? addend=None, Tensor? addend_mask=None) -> Tensor");
   m.def("conv_stem(Tensor x, Tensor wk, int[] stride, int[] padding, int[] dilation, bool stats, bool store=True) "
@@ -492,6 +501,7 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
 TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
   m.impl("conv_igemm", &rtseg::conv_igemm);
   m.impl("conv_igemm_small", &rtseg::conv_igemm_small);
+  m.impl("conv_wres_eval", &rtseg::conv_wres_eval);
   m.impl("conv_igemm_dgrad", &rtseg::conv_igemm_dgrad);
   m.impl("conv_halo", &rtseg::conv_halo);
   m.impl("conv_halo_dgrad", &rtseg::conv_halo_dgrad);

@@ -53,6 +53,8 @@ struct WresArgs {
   float* part;             // BN statistics slab [grid / ntiles][2 * cout], or null
   const uint16_t* addend;  // bf16 tensor of y's layout added to the result, or null
   const uint8_t* amask;    // bit mask of the addend (mask_addend4), or null
+  const float* ss;         // STATS 2 (inference): BN scale [cout] | shift [cout]; the addend is the residual
+  int act;                 // STATS 2: activation after the residual
   int H, W;                // gathered operand
   int Ho, Wo, cout;        // output
   int dh0, dw0;            // halo origin: input row of output row oy (tap-relative offset 0)
@@ -76,6 +78,8 @@ __device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t r, uint32_t voff, 
       : "memory");
 }
 
+// STATS: 0 = plain, 1 = BN statistics slab (training forward), 2 = inference BN epilogue
+// act(y * scale + shift + residual) (forward only)
 // NW waves; wave w owns TJ = kTH / NW consecutive output rows of the tile (32 pixels each) x all
 // 64 channels (TI = 2 channel tiles); PD = fragment prefetch distance in (tap, K sub-step) steps
 template <int STATS, int FLIP, int NW, int PD>
@@ -148,16 +152,16 @@ __global__ void __launch_bounds__(NW * 64) wres_conv_kernel(const WresArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  float pst[STATS ? 32 : 1];
+  float pst[STATS == 1 ? 32 : 1];
 #pragma unroll
-  for (int k = 0; k < (STATS ? 32 : 1); ++k) pst[k] = 0.f;
+  for (int k = 0; k < (STATS == 1 ? 32 : 1); ++k) pst[k] = 0.f;
 
   const int co_lane = co0 + 4 * fhi;  // + ti * 32 + 8 g
   auto epilogue = [&](int mt) __attribute__((always_inline)) {
     int n, oy0, ox0;
     tile_xyz(mt, n, oy0, ox0);
-    float ts[STATS ? 2 : 1][16], tq[STATS ? 2 : 1][16];
-    if constexpr (STATS) {
+    float ts[STATS == 1 ? 2 : 1][16], tq[STATS == 1 ? 2 : 1][16];
+    if constexpr (STATS == 1) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -177,7 +181,7 @@ __global__ void __launch_bounds__(NW * 64) wres_conv_kernel(const WresArgs a) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int co = co_lane + ti * 32 + 8 * g;
-          if ((g & 1) == 0 && FLIP == 1 && a.addend != nullptr && a.amask == nullptr) {  // uniform: 16-byte addend load
+          if ((g & 1) == 0 && (FLIP == 1 || STATS == 2) && a.addend != nullptr && a.amask == nullptr) {  // uniform: 16-byte addend load
             uint4 raw = make_uint4(0u, 0u, 0u, 0u);
             if (ok) raw = *reinterpret_cast<const uint4*>(a.addend + off + co + 4 * fhi);
             pair_unswap16(raw, adp[0], adp[1]);
@@ -185,7 +189,13 @@ __global__ void __launch_bounds__(NW * 64) wres_conv_kernel(const WresArgs a) {
           float v[4];
 #pragma unroll
           for (int q = 0; q < 4; ++q) v[q] = acc[ti][tj][4 * g + q];
-          if (FLIP == 1 && a.addend != nullptr && ok) {
+          if constexpr (STATS == 2) {  // inference BN: scale / shift per channel, residual (addend) below
+            const float4 sc = *reinterpret_cast<const float4*>(a.ss + co);
+            const float4 sf = *reinterpret_cast<const float4*>(a.ss + a.cout + co);
+            v[0] = fmaf(v[0], sc.x, sf.x); v[1] = fmaf(v[1], sc.y, sf.y);
+            v[2] = fmaf(v[2], sc.z, sf.z); v[3] = fmaf(v[3], sc.w, sf.w);
+          }
+          if ((FLIP == 1 || STATS == 2) && a.addend != nullptr && ok) {
             float r[4];
             if (a.amask == nullptr) {
               bf16x4_unpack(adp[g & 1], r);
@@ -196,6 +206,10 @@ __global__ void __launch_bounds__(NW * 64) wres_conv_kernel(const WresArgs a) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[q] += r[q];
           }
+          if constexpr (STATS == 2) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = epi_act(v[q], a.act);
+          }
           uint2 pk;
           pk.x = pack2(v[0], v[1]);
           pk.y = pack2(v[2], v[3]);
@@ -204,7 +218,7 @@ __global__ void __launch_bounds__(NW * 64) wres_conv_kernel(const WresArgs a) {
             const uint4 w = pair_swap16(pkp[0], pkp[1]);
             if (ok) *reinterpret_cast<uint4*>(a.y + off + co - 8 + 4 * fhi) = w;
           }
-          if constexpr (STATS) {  // statistics of the fp32 outputs; pixels past the image do not count
+          if constexpr (STATS == 1) {  // statistics of the fp32 outputs; pixels past the image do not count
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const float u = ok ? v[q] : 0.f;
@@ -217,7 +231,7 @@ __global__ void __launch_bounds__(NW * 64) wres_conv_kernel(const WresArgs a) {
         for (int r = 0; r < 16; ++r) acc[ti][tj][r] = 0.f;
       }
     }
-    if constexpr (STATS) {
+    if constexpr (STATS == 1) {
       float y1[32];
       stats_stage1<2>(ts, tq, y1);
 #pragma unroll
@@ -271,7 +285,7 @@ __global__ void __launch_bounds__(NW * 64) wres_conv_kernel(const WresArgs a) {
   }
   if (my_tiles > 0) epilogue(mfirst + (my_tiles - 1) * mstep);
 
-  if constexpr (STATS) {
+  if constexpr (STATS == 1) {
     // one slab row per block: the pixel waves' per-channel sums through LDS in a fixed order
     __syncthreads();  // all fragment reads done, no DMA in flight
     float* red = reinterpret_cast<float*>(lds);  // [NW][2][64]
@@ -359,9 +373,13 @@ void launch_conv_wres_fwd(const ConvGeom& g, hipStream_t st) {
   k.part = g.part;
   k.addend = nullptr;
   k.amask = nullptr;
+  k.ss = g.scale_shift;
+  k.act = g.act;
+  if (k.ss != nullptr) k.addend = static_cast<const uint16_t*>(g.res);  // the residual
   const int grid = wres_grid(k.mtiles, k.ntiles);
   if (grid <= 0) return;
-  if (k.part != nullptr) wres_launch<1, 0>(k, grid, st);
+  if (k.ss != nullptr) wres_launch<2, 0>(k, grid, st);
+  else if (k.part != nullptr) wres_launch<1, 0>(k, grid, st);
   else wres_launch<0, 0>(k, grid, st);
 }
 

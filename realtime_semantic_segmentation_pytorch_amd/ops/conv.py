@@ -1085,6 +1085,13 @@ def conv_bn_act_eval(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, act_code: 
     cin, cout = conv.in_channels, conv.out_channels
     if residual is None and stem7_ok(conv, x):
         return _stem7_eval(x, conv, bn, act_code)
+    if (residual is None and conv.bias is None and stem_infer_ok(conv, x) and cout % 16 == 0
+            and x.is_cuda and _autocast_bf16(x)):
+        # the 3 x 3 stem with the BN + act in its epilogue (one pass; the separate BN apply was
+        # 2 % of DDRNet-23's batch-1 inference, profiles/r6_infer)
+        from .bn import eval_coeffs
+
+        return _stem_infer(x, conv, None, eval_coeffs(bn)[1], act_code)
     if cout % 8 or cin % 32:
         return None
     x = x.to(torch.bfloat16)
@@ -1111,6 +1118,8 @@ def conv_bn_act_eval(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, act_code: 
         ops().bn_apply(y, ss, res, act_code)
 
     cands = [("igemm" if cin % 64 == 0 else "mfma", ours)]
+    if wres_ok(conv, cin, cout, _npix(x)):  # 64-channel 3 x 3: weights resident in LDS
+        cands.append(("wres", lambda: ops().conv_wres_eval(x, wk, stride, padding, dilation, ss, res, act_code)))
     if cin % 64 == 0 and _SMALL_TILES:
         cands.append(("igemm_s", small))
         # ... split over K when even the small tiles leave CUs idle (fp32 parts + one BN pass)
@@ -1173,9 +1182,10 @@ def stem_infer_ok(conv: nn.Module, x: torch.Tensor) -> bool:
             and os.environ.get("RTSEG_CONV_STEM", _STEM_DEFAULT) != "0")
 
 
-def _stem_infer(x: torch.Tensor, conv: nn.Module, bias) -> torch.Tensor:
+def _stem_infer(x: torch.Tensor, conv: nn.Module, bias, bn_ss=None, act_code: int = 0) -> torch.Tensor:
     """``conv(x)`` on ``conv_stem.hip``: the weight zero-padded to the kernel's 16-channel
-    granularity (cached, krsc bf16), the real channels sliced back out."""
+    granularity (cached, krsc bf16), the real channels sliced back out.  ``bn_ss`` (fp32 [2 Cout],
+    Cout % 16 == 0): an eval BN's scale | shift applied with ``act_code`` in the epilogue."""
     cout = conv.out_channels
     cp = -(-cout // 16) * 16
 
@@ -1190,6 +1200,8 @@ def _stem_infer(x: torch.Tensor, conv: nn.Module, bias) -> torch.Tensor:
     if x.data_ptr() % 16:
         x = x.clone(memory_format=torch.channels_last)
     stride, padding, dilation = _geom(conv)
+    if bn_ss is not None:
+        return ops().conv_stem_bn_act(x, wk, stride, padding, dilation, bn_ss, act_code)
     if bias is not None:  # added to the fp32 accumulators by the BN epilogue (scale 1): one rounding
         key = (bias.data_ptr(), bias._version, write_generation())
         hit = getattr(conv, "_rtseg_stem_ss", None)

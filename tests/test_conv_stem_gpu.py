@@ -337,3 +337,31 @@ def test_stem_bn_backward_sums_recompute(geom, act):
     scale = gd.abs().sum((0, 2, 3)).max().item()
     torch.testing.assert_close(got[:cout], ref_s, atol=1e-4 * scale, rtol=1e-4)
     torch.testing.assert_close(got[cout:], ref_q, atol=1e-4 * scale * xd.abs().max().item(), rtol=1e-4)
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+@pytest.mark.parametrize("act", ["relu", "none"])
+def test_stem_eval_bn_in_epilogue(stride, act):
+    """ops.conv_bn_act in bf16 inference on a 3-channel 3 x 3 stem: the eval BN (+ ReLU) runs in
+    conv_stem.hip's epilogue (one pass) and matches fp32 BN(conv) of the bf16 operands."""
+    import torch.nn as nn
+
+    assert ops.load()
+    torch.manual_seed(3)
+    conv = nn.Conv2d(3, 32, 3, stride, 1, bias=False).to(DEV)
+    bn = nn.BatchNorm2d(32).to(DEV)
+    with torch.no_grad():
+        bn.running_mean.uniform_(-0.2, 0.2)
+        bn.running_var.uniform_(0.5, 2.0)
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.3, 0.3)
+    conv.eval(), bn.eval()
+    x = torch.randn(2, 3, 66, 130, device=DEV).contiguous(memory_format=torch.channels_last)
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        got = ops.conv_bn_act(x, conv, bn, act)
+    xb, wb = x.to(torch.bfloat16).float(), conv.weight.to(torch.bfloat16).float()
+    with torch.no_grad():
+        ref = bn(F.conv2d(xb, wb, None, stride, 1))
+    ref = ref.relu() if act == "relu" else ref
+    assert got.dtype == torch.bfloat16 and got.is_contiguous(memory_format=torch.channels_last)
+    bf16_close(got, ref)

@@ -74,6 +74,30 @@ def test_wres_forward_and_stats(geom):
     assert torch.equal(y2, y) and (p2 is None or p2.numel() == 0)
 
 
+@pytest.mark.parametrize("geom", FWD)
+@pytest.mark.parametrize("act", [0, 1, 2])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_wres_inference_bn_epilogue(geom, act, with_res):
+    """conv_wres_eval: act(conv * scale + shift (+ residual)) from the fp32 accumulators (batch-1
+    inference of the 64-channel 3 x 3 layers) against fp32; the conv part is the training
+    kernel's (same accumulation): equal to applying the epilogue to its fp32 outputs."""
+    n, h, w, cout = geom
+    g = torch.Generator().manual_seed(5)
+    x = _t((n, 64, h, w), g).contiguous(memory_format=torch.channels_last)
+    wt = _t((cout, 64, 3, 3), g, 1 / 24)
+    wk = wt.permute(0, 2, 3, 1).contiguous()
+    ss = torch.cat([torch.rand(cout, generator=g) + 0.5, torch.randn(cout, generator=g)]).to(DEV).contiguous()
+    res = _t((n, cout, h, w), g).contiguous(memory_format=torch.channels_last) if with_res else None
+    y = torch.ops.rtseg.conv_wres_eval(x, wk, [1, 1], [1, 1], [1, 1], ss, res, act)
+    ref = F.conv2d(x.float(), wt.float(), None, 1, 1) * ss[:cout].view(1, -1, 1, 1) + ss[cout:].view(1, -1, 1, 1)
+    if with_res:
+        ref = ref + res.float()
+    ref = ref.relu() if act == 1 else ref.clamp(0, 6) if act == 2 else ref
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    bf16_close(y, ref)
+    assert torch.equal(y, torch.ops.rtseg.conv_wres_eval(x, wk, [1, 1], [1, 1], [1, 1], ss, res, act))
+
+
 @pytest.mark.parametrize("geom", DGRAD)
 @pytest.mark.parametrize("with_addend", [False, True, "masked"])
 def test_wres_dgrad(geom, with_addend):

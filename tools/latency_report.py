@@ -15,9 +15,16 @@ import csv
 
 
 def period(names, max_p=20000):
+    """Kernels per replay: the smallest p whose last three windows hold the same kernels.  Compared
+    as multisets: with concurrent streams (ops/streams.py) the start-time order of kernels on two
+    queues differs from replay to replay."""
     n = len(names)
     for p in range(1, min(max_p, n // 3) + 1):
         if names[n - p:] == names[n - 2 * p:n - p] == names[n - 3 * p:n - 2 * p]:
+            return p
+    for p in range(1, min(max_p, n // 3) + 1):
+        a = collections.Counter(names[n - p:])
+        if a == collections.Counter(names[n - 2 * p:n - p]) == collections.Counter(names[n - 3 * p:n - 2 * p]):
             return p
     return None
 
