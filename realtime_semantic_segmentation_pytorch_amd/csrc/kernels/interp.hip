@@ -14,6 +14,8 @@
 #include "rtseg_common.h"
 #include "rtseg_launch.h"
 
+#include <cstdlib>
+
 namespace rtseg {
 
 struct Shape4 { int n, c, h, w; int64_t sn, sc, sh, sw; };
@@ -153,6 +155,57 @@ __global__ void __launch_bounds__(256) interp_fwd_cl_pix_lds(
     for (int64_t e = nvec * 16 / static_cast<int64_t>(sizeof(T)) + threadIdx.x; e < nelem; e += 256)
       y[static_cast<int64_t>(p0) * C + e] = st[e];
     __syncthreads();
+  }
+}
+
+// Large up-scaling of a few-channel map into a dense channels-last output (the models' final
+// x8 logits upsample in inference: 19 channels, 38-byte pixels): one block per output ROW.  The
+// row's two source rows are staged in LDS as fp32 and blended vertically once; the column map
+// (x0, lambda) of every output column is tabulated once; then every thread writes 16-byte runs of
+// the flat output row (8 consecutive elements, crossing pixel boundaries), each element two LDS
+// reads and one lerp.  The per-pixel kernel above spends ~76 scalar loads per 19-channel pixel.
+template <typename T, int ACT>
+__global__ void __launch_bounds__(256) interp_fwd_cl_rows(const T* __restrict__ x, Shape4 xs, T* __restrict__ y,
+                                                          Shape4 ys, LinMap mh, LinMap mw) {
+  extern __shared__ __attribute__((aligned(16))) float rl[];
+  const int C = ys.c, Wi = xs.w, Wo = ys.w;
+  float* row = rl;                                          // [Wi][C] blended source row
+  float* lam = rl + Wi * C;                                 // [Wo] horizontal weights
+  int* col = reinterpret_cast<int*>(lam + Wo);              // [Wo] left source column
+  const int oy = blockIdx.x % ys.h, n = blockIdx.x / ys.h;
+  int y0, y1; float ly;
+  mh.map(oy, y0, y1, ly);
+  const T* r0 = x + n * xs.sn + y0 * xs.sh;
+  const T* r1 = x + n * xs.sn + y1 * xs.sh;
+  for (int e = threadIdx.x; e < Wi * C; e += 256) {
+    const int ix = e / C, c = e - ix * C;
+    const float a = Io<T>::ld(r0 + ix * xs.sw + c), b = Io<T>::ld(r1 + ix * xs.sw + c);
+    row[e] = a + ly * (b - a);
+  }
+  for (int ox = threadIdx.x; ox < Wo; ox += 256) {
+    int x0, x1; float lx;
+    mw.map(ox, x0, x1, lx);
+    col[ox] = x0;
+    lam[ox] = x1 == x0 ? 0.f : lx;  // clamped last column: no right tap
+  }
+  __syncthreads();
+  constexpr int E = 16 / static_cast<int>(sizeof(T));
+  const int nvec = Wo * C / E;
+  T* out = y + n * ys.sn + oy * ys.sh;
+  for (int v = threadIdx.x; v < nvec; v += 256) {
+    int e = v * E;
+    int ox = e / C, c = e - ox * C;
+    alignas(16) T o[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      const float* p = row + col[ox] * C + c;
+      const float l = lam[ox];
+      const float a = p[0];
+      const float val = l == 0.f ? a : a + l * (p[C] - a);
+      Io<T>::st(o + j, act_fwd<ACT>(val));
+      if (++c == C) { c = 0; ++ox; }
+    }
+    *reinterpret_cast<uint4*>(out + static_cast<int64_t>(v) * E) = *reinterpret_cast<const uint4*>(o);
   }
 }
 
@@ -363,6 +416,17 @@ static void fwd_dispatch(const Tensor4& x, const Tensor4* skip, const Tensor4& y
                         y.sn == static_cast<int64_t>(y.h) * y.w * y.c &&
                         reinterpret_cast<uintptr_t>(y.data) % 16 == 0;
   const size_t lds = static_cast<size_t>(256) * y.c * sizeof(T);
+  // the row kernel: no skip, >= x4 horizontally, a 16-byte multiple per output row, LDS for two
+  // fp32 source rows and the column table (RTSEG_INTERP_ROWS=0: off)
+  static const bool rows_on = [] { const char* e = std::getenv("RTSEG_INTERP_ROWS"); return !(e && e[0] == '0'); }();
+  const size_t rlds = (static_cast<size_t>(x.w) * y.c + 2 * static_cast<size_t>(y.w)) * 4;
+  if (rows_on && !SKIP && dense_cl && x.sc == 1 && y.c > 1 && y.c < 64 && y.w >= 4 * x.w && rlds <= 65536 &&
+      (static_cast<int64_t>(y.w) * y.c * static_cast<int64_t>(sizeof(T))) % 16 == 0 &&
+      static_cast<int64_t>(y.n) * y.h < (int64_t{1} << 31)) {
+    interp_fwd_cl_rows<T, ACT><<<static_cast<int>(y.n * y.h), 256, rlds, st>>>(
+        static_cast<const T*>(x.data), xs, static_cast<T*>(y.data), ys, mh, mw);
+    return;
+  }
   if (dense_cl && x.sc == 1 && y.c > 1 && lds <= 32768 && npix < (int64_t{1} << 31)) {
     interp_fwd_cl_pix_lds<T, ACT, SKIP><<<stream_grid(npix, 256), 256, lds, st>>>(
         static_cast<const T*>(x.data), xs, kp, ks, static_cast<T*>(y.data), ys, mh, mw, FastDiv::make(y.w),

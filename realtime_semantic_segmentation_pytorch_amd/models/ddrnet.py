@@ -228,13 +228,15 @@ class DAPPM(nn.Module):
 
     def forward(self, x):
         hw = x.shape[2:]
-        y0 = self.conv0(x)
         # the five branches land in one concat buffer (ops/concat.py)
         sink = ops.ConcatSink([self.hid] * 5)
-        prev = self.conv1(x, sink=(sink, 0))
+        # the pooled 1 x 1 projections do not depend on the chain: in inference they run on a side
+        # stream while conv0 / conv1 run (ops/streams.py); in training they interleave as before
+        (y0, prev), pooled = ops.concurrent_branches(
+            lambda: (self.conv0(x), self.conv1(x, sink=(sink, 0))),
+            lambda: [getattr(self, f"pool{i}")(x) for i in range(2, 6)], x.device)
         branches = [prev]
         for i in range(2, 6):
-            pooled = getattr(self, f"pool{i}")(x)
-            prev = getattr(self, f"conv{i}")(ops.interpolate(pooled, hw, True, skip=prev), sink=(sink, i - 1))
+            prev = getattr(self, f"conv{i}")(ops.interpolate(pooled[i - 2], hw, True, skip=prev), sink=(sink, i - 1))
             branches.append(prev)
         return self.conv_last(sink.cat(branches)) + y0

@@ -10,16 +10,21 @@ replayed graph keeps the concurrency at no host cost.
 
 Only without autograd (inference / validation): in training the branches stay on one stream,
 where the batch already fills the GPU and autograd's stream semantics would need every saved
-tensor re-recorded.  ``RTSEG_BRANCH_STREAMS=0``: off (A/B).
+tensor re-recorded.
+
+Measured (profiles/r6_infer, DDRNet-23 bf16 batch 1, 1024 x 2048): +8.7 % (722 -> 786 FPS) while
+the low-resolution layers ran on 256-pixel tiles; after the small-tile / split-K inference
+kernels (ops/conv.py conv_bn_act_eval) fill the CUs on their own it is neutral (905 / 908 on,
+906 / 909 off).  So it is opt-in: ``RTSEG_BRANCH_STREAMS=1``.
 """
 from __future__ import annotations
 
 import os
-from typing import Callable, Dict, Tuple
+from typing import Any, Callable, Dict, Tuple
 
 import torch
 
-_ON = os.environ.get("RTSEG_BRANCH_STREAMS", "1") != "0"
+_ON = os.environ.get("RTSEG_BRANCH_STREAMS", "0") == "1"
 _SIDE: Dict[int, torch.cuda.Stream] = {}
 FORKS = [0]  # concurrent launches issued (tests)
 
@@ -32,11 +37,11 @@ def _side(device: torch.device) -> torch.cuda.Stream:
     return s
 
 
-def concurrent_branches(fa: Callable[[], torch.Tensor], fb: Callable[[], torch.Tensor],
-                        device: torch.device) -> Tuple[torch.Tensor, torch.Tensor]:
+def concurrent_branches(fa: Callable[[], Any], fb: Callable[[], Any], device: torch.device) -> Tuple[Any, Any]:
     """``(fa(), fb())`` with ``fb`` on a side stream when no autograd graph is recorded.  The
     caller keeps ``fb``'s inputs alive until this returns (they are read on the side stream);
-    ``fb``'s output is recorded on the current stream, which waits for the side stream."""
+    ``fb``'s output (a tensor or a list / tuple of tensors) is recorded on the current stream,
+    which waits for the side stream."""
     if not _ON or torch.is_grad_enabled() or device.type != "cuda":
         return fa(), fb()
     main = torch.cuda.current_stream(device)
@@ -46,6 +51,7 @@ def concurrent_branches(fa: Callable[[], torch.Tensor], fb: Callable[[], torch.T
         b = fb()
     a = fa()
     main.wait_stream(side)
-    b.record_stream(main)
+    for t in (b if isinstance(b, (list, tuple)) else (b,)):
+        t.record_stream(main)
     FORKS[0] += 1
     return a, b

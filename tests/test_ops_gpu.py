@@ -43,6 +43,28 @@ def test_interp_fwd_bwd(dtype, cl, align, shape, size):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape,size", [((1, 19, 128, 256), (1024, 2048)), ((2, 19, 9, 13), (72, 104)),
+                                        ((1, 3, 20, 24), (80, 96))])
+@pytest.mark.parametrize("align", [True, False])
+def test_interp_final_upsample_rows(monkeypatch, dtype, shape, size, align):
+    """The row-staged kernel (interp_fwd_cl_rows: a dense channels-last few-channel output,
+    >= x4 wide -- the models' final logits upsample in inference) against fp32 PyTorch and
+    against the per-pixel kernel it replaces (RTSEG_INTERP_ROWS=0 in a subprocess is not needed:
+    the two differ only by the fp32 blend order, <= 1 bf16 ulp)."""
+    _lib_loaded()
+    torch.manual_seed(4)
+    x = torch.randn(shape, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        y = ops.interpolate(x, size, align)
+    ref = F.interpolate(x.float(), size, mode="bilinear", align_corners=align)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    if dtype == torch.float32:
+        torch.testing.assert_close(y, ref, atol=1e-5, rtol=1e-5)
+    else:
+        torch.testing.assert_close(y.float(), ref, rtol=2.0 ** -8, atol=1e-3 * ref.abs().max().item())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("act", [None, "relu"])
 def test_interp_skip_act(dtype, act):
     _lib_loaded()
