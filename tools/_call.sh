@@ -1,10 +1,9 @@
 set -o pipefail
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
-D=gpurun_out/r6_tune2; mkdir -p $D
+D=gpurun_out/r6_haloeval; mkdir -p $D
 cp miopen_db/rtseg_conv_decisions.json $D/db.json
-RTSEG_TUNE_DB_OUT=$D/db.json timeout -k 10 600 python -u bench.py --model bisenetv2 --batch 16 --steps 10 --warmup 3 --no-infer > $D/bisenetv2.json 2> $D/bisenetv2.err || { tail -20 $D/bisenetv2.err; exit 1; }
-cut -c1-160 $D/bisenetv2.json
-RTSEG_TUNE_DB_OUT=$D/db.json timeout -k 10 600 python -u bench.py --model stdc --arch stdc2 --detail-head --batch 16 --steps 10 --warmup 3 --no-infer > $D/stdc2.json 2> $D/stdc2.err || { tail -20 $D/stdc2.err; exit 1; }
-cut -c1-160 $D/stdc2.json
-RTSEG_TUNE_DB_OUT=$D/db.json timeout -k 10 600 python -u bench.py --kd --batch 16 --steps 10 --warmup 3 --no-infer > $D/kd.json 2> $D/kd.err || { tail -20 $D/kd.err; exit 1; }
-cut -c1-160 $D/kd.json
+for i in 1 2; do for v in auto 0; do
+if [ $v = auto ]; then OUTV="RTSEG_TUNE_DB_OUT=$D/db.json"; else OUTV=""; fi
+env $OUTV RTSEG_CONV_HALO=$v timeout -k 10 180 python3 tools/profile_infer.py --iters 300 > $D/infer_${v}_$i.txt 2>&1 || { tail -5 $D/infer_${v}_$i.txt; exit 1; }
+echo "halo=$v $(tail -1 $D/infer_${v}_$i.txt)"
+done; done
