@@ -1,9 +1,4 @@
 set -o pipefail
-export TMPDIR=/tmp PYTHONUNBUFFERED=1
-D=gpurun_out/r6_haloeval; mkdir -p $D
-cp miopen_db/rtseg_conv_decisions.json $D/db.json
-for i in 1 2; do for v in auto 0; do
-if [ $v = auto ]; then OUTV="RTSEG_TUNE_DB_OUT=$D/db.json"; else OUTV=""; fi
-env $OUTV RTSEG_CONV_HALO=$v timeout -k 10 180 python3 tools/profile_infer.py --iters 300 > $D/infer_${v}_$i.txt 2>&1 || { tail -5 $D/infer_${v}_$i.txt; exit 1; }
-echo "halo=$v $(tail -1 $D/infer_${v}_$i.txt)"
-done; done
+bash tools/gpu_pmc.sh gpurun_out/r6_pmc hreg4+st:128,128,256,128 hreg4_dg:128,128,256,128 whalo2:128,128,256,128 igemm+st:256,64,128,256 wres+st:64,256,512,64 || exit 1
+python3 tools/pmc_table.py gpurun_out/r6_pmc/summary.txt > gpurun_out/r6_pmc/pmc_table.txt 2>&1 || true
+cat gpurun_out/r6_pmc/pmc_table.txt | head -30
