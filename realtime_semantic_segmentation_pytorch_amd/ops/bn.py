@@ -39,6 +39,11 @@ _HANDOFF = os.environ.get("RTSEG_RES_HANDOFF", "1") != "0"
 _MASKED_HANDOFF = os.environ.get("RTSEG_MASKED_HANDOFF", "0") == "1"
 # the stem BN's forward apply as a recompute of the stem conv (RTSEG_STEM_BN_RECOMPUTE=0: off, A/B)
 _STEM_BN_RECOMPUTE = os.environ.get("RTSEG_STEM_BN_RECOMPUTE", "1") != "0"
+# single-GPU BN backward started early on a side stream by the consumer conv (bn_bwd_early).
+# Opt-in (RTSEG_BN_OVERLAP=1): bitwise equal, but DDRNet-23 b32 measured 573.3 / 575.0 images/s with
+# it against 578.6 / 579.5 without on one box (profiles/r6_negative). The memory-bound BN passes slow
+# the weight-gradient kernels they share the CUs with more than they hide.
+_OVERLAP = os.environ.get("RTSEG_BN_OVERLAP", "0") == "1"
 
 
 def act_code(act) -> Optional[int]:
@@ -130,8 +135,14 @@ class _BNActFn(torch.autograd.Function):
         ctx.act, ctx.mask, ctx.pg = act, mask, pg
         # SyncBN: the consumer conv's backward may issue this node's gradient all-reduce early,
         # between its data and weight gradients (syncbn_bwd_early), and park it here
-        ctx.early = [] if pg is not None and not getattr(bn, "_rtseg_no_early", False) else None
-        ctx.bn_module = bn if pg is not None else None
+        # Single GPU: the consumer conv may run this node's whole backward early, on a side stream
+        # under its weight gradient (bn_bwd_early). This covers BNs without a residual, concat slice
+        # or stem hand-off, i.e. an RB's conv1 -> BN -> ReLU -> conv2.
+        overlap = (_OVERLAP and pg is None and residual is None and out2 is None and x.is_cuda
+                   and use_batch_stats and x.dtype == torch.bfloat16)
+        ctx.early = ([] if (pg is not None or overlap) and not getattr(bn, "_rtseg_no_early", False)
+                     else None)
+        ctx.bn_module = bn if (pg is not None or overlap) else None
         # a stem conv produced x (ops/conv.py bn_fuse_slot): this node's dx pass moves into that
         # conv's weight gradient (conv_stem_wgrad_bn)
         prod = x.grad_fn if use_batch_stats and residual is None and out2 is None else None
@@ -174,6 +185,14 @@ class _BNActFn(torch.autograd.Function):
             # a stats-only stem launch (RTSEG_STEM_NO_STORE=1) never wrote x, and this backward
             # reads it (the hand-off above was not taken: a second backward, another consumer)
             _stem_materialize(x.grad_fn, x)
+        if ctx.pg is None and ctx.early:  # the whole backward ran early on the side stream
+            key, res, ev = ctx.early.pop()
+            torch.cuda.current_stream(dy_in.device if dy_in is not None else None).wait_event(ev)
+            if dy2 is None and _same_grad(dy_in, key):
+                e_dx, e_dw, e_db = res
+                EARLY_USED[0] += 1
+                return (e_dx, e_dw, e_db, None, None, None, None, None, None, None, None)
+            ctx.bn_module._rtseg_no_early = True  # another consumer's gradient was added: not again
         if ctx.pg is not None:
             early = ctx.early.pop() if ctx.early else None
             if early is not None:
@@ -284,6 +303,60 @@ def _stem_handoff(ctx, stem, dy, x, y, mi, ss, sums, weight, want_dw):
 
 
 EARLY_ISSUED = [0]  # SyncBN backward all-reduces issued early by a consumer conv (tests)
+EARLY_OVERLAPPED = [0]  # single-GPU BN backwards started on the side stream (tests)
+EARLY_USED = [0]  # ... whose results the BN node returned (tests)
+_SIDE = {}
+
+
+def _side_stream(device) -> torch.cuda.Stream:
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _SIDE.get(idx)
+    if s is None:
+        s = _SIDE[idx] = torch.cuda.Stream(device=idx)
+    return s
+
+
+def bn_bwd_early(node, dy: torch.Tensor) -> bool:
+    """Called by the consumer conv's backward right after its data gradient ``dy`` (ops/conv.py):
+    multi-rank SyncBN -> :func:`syncbn_bwd_early`; single GPU -> this BN node's whole backward
+    (reduction, finalize, dx / dw / db) is launched now on a side stream, so its memory-bound passes
+    run beside the conv's compute-bound weight gradient on the main stream. The node's backward
+    waits on the event, and it uses the results only if the gradient it receives is exactly ``dy``
+    (``_same_grad``: the conv was the output's only consumer)."""
+    if getattr(node, "pg", None) is not None:
+        return syncbn_bwd_early(node, dy)
+    early = getattr(node, "early", None)
+    if early is None or early or getattr(node, "dy2_slot", None) is not None or node.has_res:
+        return False
+    if node.stem_node is not None:
+        return False
+    x, y, mi, ss, sums, weight = node.saved_tensors
+    if (dy.dtype != x.dtype or dy.shape != x.shape or dy.data_ptr() % 16
+            or not dy.is_contiguous(memory_format=torch.channels_last)):
+        return False
+    if not getattr(x.grad_fn, "y_stored", True):
+        return False
+    want_dw = node.has_w and (node.needs_input_grad[1] or node.needs_input_grad[2])
+    main = torch.cuda.current_stream(dy.device)
+    side = _side_stream(dy.device)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        bsums = ops().bn_bwd_sums(dy, x, y, mi, ss, node.act, node.mask, None)
+        dx, _, dw, db = ops().bn_backward(dy, x, y, bsums, sums, mi, ss, weight, node.act, node.mask, False,
+                                          node.batch_stats, want_dw, None, None)
+        ev = torch.cuda.Event()
+        ev.record(side)
+    # cross-stream lifetimes: dy / x / y were made on the main stream and are read on the side one;
+    # the results are made on the side stream and used on the main one after the event
+    for t in (dy, x, y, mi, ss, bsums) + ((sums,) if sums is not None else ()) + ((weight,) if weight is not None else ()):
+        if t is not None and t.is_cuda:
+            t.record_stream(side)
+    for t in (dx, dw, db):
+        if t is not None:
+            t.record_stream(main)
+    early.append(((dy, dy._version), (dx, dw if want_dw else None, db if want_dw else None), ev))
+    EARLY_OVERLAPPED[0] += 1
+    return True
 
 
 def syncbn_bwd_early(node, dy: torch.Tensor) -> bool:

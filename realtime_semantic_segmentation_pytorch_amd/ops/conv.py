@@ -621,8 +621,9 @@ class _ConvFn(torch.autograd.Function):
         ctx.ran = not ctx.needs_input_grad[0]  # consumer_for: only a node that will produce dx
         _register_consumer(x, ctx)
         ctx.wdtype = weight.dtype
-        # a multi-rank SyncBN node that produced x: its backward all-reduce is issued from this
-        # node's backward, between dgrad and wgrad (ops.bn.syncbn_bwd_early)
+        # a BN node that produced x: from this node's backward, between dgrad and wgrad, a multi-rank
+        # SyncBN issues its all-reduce and a single-GPU BN runs its backward on a side stream
+        # (ops.bn.bn_bwd_early)
         prod = x.grad_fn
         ctx.bn_node = prod if getattr(prod, "early", None) is not None else None
         # a 3-channel stem conv on an input that needs no gradient: a following batch-statistics
@@ -654,10 +655,10 @@ class _ConvFn(torch.autograd.Function):
         node, ctx.bn_node = ctx.bn_node, None
         on_dx = None
         if node is not None:
-            from .bn import syncbn_bwd_early
+            from .bn import bn_bwd_early
 
             def on_dx(dx):
-                syncbn_bwd_early(node, dx)
+                bn_bwd_early(node, dx)
         dx, dw = _conv_bwd(x, wk, ctx.conv, ctx.key, dy, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
                            ctx.wdtype, addend, on_dx)
         return dx, dw, None, None, None
