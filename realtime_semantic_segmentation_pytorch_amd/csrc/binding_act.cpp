@@ -63,6 +63,24 @@ static at::Tensor act_fwd(const at::Tensor& x, int64_t kind, const std::optional
   return y;
 }
 
+// inference: prelu(x * scale + shift) with an eval BN's fp32 [2C] scale | shift and a per-channel
+// PReLU weight [C]: BN + PReLU in one pass (ops/bn.py bn_act)
+static at::Tensor bn_prelu_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& ss) {
+  TORCH_CHECK(x.dim() == 4 && w.numel() == x.size(1) && w.scalar_type() == at::kFloat && ss.scalar_type() == at::kFloat &&
+                  ss.numel() == 2 * x.size(1) && ss.is_contiguous() && w.is_contiguous(),
+              "rtseg.bn_prelu_fwd: per-channel PReLU weight [C] and fp32 scale_shift [2C]");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const auto fmt = fmt_of(x);
+  at::Tensor xx = dense_aligned(x, fmt);
+  ActArgs r = act_args(xx, 0, w, 0.0, 0.0);
+  at::Tensor y = at::empty_like(xx, xx.options().memory_format(fmt));
+  r.x = xx.data_ptr();
+  r.out = y.data_ptr();
+  r.ss = ss.data_ptr<float>();
+  launch_act(r, cur_stream());
+  return y;
+}
+
 // -> (dx, dw); dw is empty unless a PReLU weight is given
 static std::tuple<at::Tensor, at::Tensor> act_bwd(const at::Tensor& dy, const at::Tensor& x, int64_t kind,
                                                   const std::optional<at::Tensor>& w, double a, double b) {
@@ -94,10 +112,12 @@ static std::tuple<at::Tensor, at::Tensor> act_bwd(const at::Tensor& dy, const at
 
 TORCH_LIBRARY_FRAGMENT(rtseg, m) {
   m.def("act_fwd(Tensor x, int kind, Tensor? w, float a, float b) -> Tensor");
+  m.def("bn_prelu_fwd(Tensor x, Tensor w, Tensor scale_shift) -> Tensor");
   m.def("act_bwd(Tensor dy, Tensor x, int kind, Tensor? w, float a, float b) -> (Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
   m.impl("act_fwd", &rtseg::act_fwd);
+  m.impl("bn_prelu_fwd", &rtseg::bn_prelu_fwd);
   m.impl("act_bwd", &rtseg::act_bwd);
 }

@@ -412,6 +412,9 @@ struct ActArgs {
   int C;
   int64_t inner;
   float a, b;
+  // forward of a per-channel PReLU only: an eval BN's scale [C] | shift [C] applied first, so
+  // BN + PReLU of inference is one pass (ops/bn.py bn_act), or null
+  const float* ss = nullptr;
 };
 struct ActPreluPlan {
   bool planes;

@@ -130,11 +130,13 @@ __global__ void __launch_bounds__(kActBlock) act_ew_kernel(const T* __restrict__
 // per-channel PReLU forward: channel of element i = (i / inner) % C (n < 2^32, host-checked)
 template <typename T>
 __global__ void __launch_bounds__(kActBlock) prelu_fwd_kernel(const T* __restrict__ x, const float* __restrict__ w,
-                                                              T* __restrict__ y, uint32_t n, FastDiv fin, FastDiv fc) {
+                                                              T* __restrict__ y, uint32_t n, FastDiv fin, FastDiv fc,
+                                                              const float* __restrict__ ss, int C) {
   for (uint32_t i = blockIdx.x * kActBlock + threadIdx.x; i < n; i += gridDim.x * kActBlock) {
     uint32_t c;
     fc.divmod(fin.div(i), c);
-    const float v = Io<T>::ld(x + i);
+    float v = Io<T>::ld(x + i);
+    if (ss != nullptr) v = fmaf(v, ss[c], ss[C + c]);  // eval BN first (per-channel weight: c = channel)
     Io<T>::st(y + i, v > 0.f ? v : w[c] * v);
   }
 }
@@ -174,7 +176,8 @@ __global__ void __launch_bounds__(kActBlock) prelu_bwd_rows_kernel(const T* __re
 // 16-byte-vector forms for channels-last with C % V == 0: a lane owns V consecutive channels
 template <typename T>
 __global__ void __launch_bounds__(kActBlock) prelu_fwd_vec_kernel(const T* __restrict__ x, const float* __restrict__ w,
-                                                                  T* __restrict__ y, uint32_t nv, FastDiv fcv) {
+                                                                  T* __restrict__ y, uint32_t nv, FastDiv fcv,
+                                                                  const float* __restrict__ ss, int C) {
   constexpr int V = Vec<T>::N;
   typedef typename Vec<T>::type VT;
   for (uint32_t i = blockIdx.x * kActBlock + threadIdx.x; i < nv; i += gridDim.x * kActBlock) {
@@ -182,6 +185,10 @@ __global__ void __launch_bounds__(kActBlock) prelu_fwd_vec_kernel(const T* __res
     fcv.divmod(i, cg);  // channel group of vector i
     float v[V];
     unpack<T, V>(reinterpret_cast<const VT*>(x)[i], v);
+    if (ss != nullptr) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) v[e] = fmaf(v[e], ss[cg * V + e], ss[C + cg * V + e]);
+    }
 #pragma unroll
     for (int e = 0; e < V; ++e) v[e] = v[e] > 0.f ? v[e] : w[cg * V + e] * v[e];
     reinterpret_cast<VT*>(y)[i] = pack<T, V>(v);
@@ -322,11 +329,12 @@ void launch_typed(const ActArgs& a, hipStream_t st) {
     if (channel_w && p.vec > 1) {
       const uint32_t nv = static_cast<uint32_t>(a.n / p.vec);
       prelu_fwd_vec_kernel<T><<<stream_grid(nv, kActBlock), kActBlock, 0, st>>>(
-          static_cast<const T*>(a.x), a.w, static_cast<T*>(a.out), nv, FastDiv::make(static_cast<uint32_t>(a.C / p.vec)));
+          static_cast<const T*>(a.x), a.w, static_cast<T*>(a.out), nv, FastDiv::make(static_cast<uint32_t>(a.C / p.vec)),
+          a.ss, a.C);
     } else if (channel_w) {
       prelu_fwd_kernel<T><<<stream_grid(a.n, kActBlock), kActBlock, 0, st>>>(
           static_cast<const T*>(a.x), a.w, static_cast<T*>(a.out), static_cast<uint32_t>(a.n),
-          FastDiv::make(static_cast<uint32_t>(a.inner)), FastDiv::make(static_cast<uint32_t>(a.C)));
+          FastDiv::make(static_cast<uint32_t>(a.inner)), FastDiv::make(static_cast<uint32_t>(a.C)), a.ss, a.C);
     } else {
       ew_dispatch<T, false>(a, grid, st);
     }

@@ -472,6 +472,39 @@ def bn_stats_begin(x: torch.Tensor, bn, part: Optional[torch.Tensor] = None):
     return sums, dist.all_reduce(sums, group=pg, async_op=True)
 
 
+BN_PRELU_FUSED = [0]  # inference BN + PReLU passes run as one kernel (tests)
+
+
+def _bn_prelu_eval(x: torch.Tensor, bn, act_module) -> Optional[torch.Tensor]:
+    """Inference ``prelu(bn_running(x))`` in one pass (act.hip with the BN scale / shift applied
+    first), for a per-channel PReLU -- ESPNet-style models run BN then PReLU after every conv, two
+    full passes and two launches each at batch 1 (profiles/r6_zoo_latency).  None -> stock path."""
+    m = getattr(act_module, "activation", act_module)  # models.modules.Activation wraps it
+    if not isinstance(m, nn.PReLU) or torch.is_grad_enabled() or not x.is_cuda or x.dim() != 4:
+        return None
+    if bn.training or not bn.track_running_stats or bn.running_mean is None or not isinstance(
+            bn, (nn.BatchNorm2d, nn.SyncBatchNorm)):
+        return None
+    w = m.weight
+    c = x.shape[1]
+    if w.numel() not in (1, c) or w.dtype != torch.float32 or x.dtype not in (torch.float32, torch.bfloat16,
+                                                                                 torch.float16):
+        return None
+    if w.numel() != c:  # a scalar PReLU (the ConvBNAct default): its slope per channel, cached
+        key = (w.data_ptr(), w._version, c, write_generation())
+        hit = getattr(m, "_rtseg_wc", None)
+        if hit is None or hit[0] != key:
+            hit = (key, w.detach().reshape(1).expand(c).contiguous())
+            m._rtseg_wc = hit
+        w = hit[1]
+    if not (x.is_contiguous() or x.is_contiguous(memory_format=torch.channels_last)) or x.numel() >= 2 ** 32:
+        return None
+    if not use_hip(x, "act"):
+        return None
+    BN_PRELU_FUSED[0] += 1
+    return ops().bn_prelu_fwd(x, w.contiguous(), eval_coeffs(bn)[1])
+
+
 def bn_act(x: torch.Tensor, bn, act=None, residual: Optional[torch.Tensor] = None,
            act_module: Optional[nn.Module] = None, part: Optional[torch.Tensor] = None,
            sink=None, pending=None) -> torch.Tensor:
@@ -499,6 +532,10 @@ def bn_act(x: torch.Tensor, bn, act=None, residual: Optional[torch.Tensor] = Non
         return y
     if pending is not None:
         pending[1].wait()  # (stock path: the statistics are recomputed by the module)
+    if act_module is not None and residual is None and sink is None:
+        y = _bn_prelu_eval(x, bn, act_module)
+        if y is not None:
+            return y
     y = bn(x)
     if residual is not None:
         y = y + residual

@@ -76,3 +76,52 @@ def test_zoo_model_trains_through_hip_activations():
     y.float().square().mean().backward()
     prelus = [m for m in model.modules() if isinstance(m, nn.PReLU)]
     assert prelus and all(p.weight.grad is not None and torch.isfinite(p.weight.grad).all() for p in prelus)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cl", [False, True])
+@pytest.mark.parametrize("c", [16, 19, 64])
+def test_bn_prelu_eval_fused(dtype, cl, c):
+    """Inference BN + per-channel PReLU as one pass (ops/bn.py _bn_prelu_eval -> bn_prelu_fwd)
+    against BatchNorm2d.eval() then PReLU in fp32; and through a ConvBNAct module tail."""
+    import torch.nn as nn
+
+    from realtime_semantic_segmentation_pytorch_amd import ops
+    from realtime_semantic_segmentation_pytorch_amd.models.modules import ConvBNAct
+    from realtime_semantic_segmentation_pytorch_amd.ops import bn as bn_mod
+
+    assert ops.load()
+    torch.manual_seed(c)
+    bn = nn.BatchNorm2d(c).cuda().eval()
+    pr = nn.PReLU(c).cuda()
+    with torch.no_grad():
+        bn.running_mean.uniform_(-0.5, 0.5)
+        bn.running_var.uniform_(0.5, 2.0)
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.3, 0.3)
+        pr.weight.uniform_(0.05, 0.4)
+    x = torch.randn(2, c, 17, 30, device="cuda").to(dtype)
+    if cl:
+        x = x.contiguous(memory_format=torch.channels_last)
+    _, ss = bn_mod.eval_coeffs(bn)
+    with torch.no_grad():
+        y = torch.ops.rtseg.bn_prelu_fwd(x, pr.weight.contiguous(), ss)
+        ref = pr(bn(x.float()))
+    tol = dict(rtol=1e-5, atol=1e-5) if dtype == torch.float32 else dict(rtol=2 ** -8, atol=1e-2)
+    torch.testing.assert_close(y.float(), ref, **tol)
+    assert y.is_contiguous(memory_format=torch.channels_last) == cl or not cl
+
+    m = ops.convert_batchnorm(ConvBNAct(c, c, 3, act_type="prelu")).cuda().eval()
+    with torch.no_grad():
+        m[1].running_mean.uniform_(-0.5, 0.5)
+        m[1].running_var.uniform_(0.5, 2.0)
+    before = bn_mod.BN_PRELU_FUSED[0]
+    with torch.no_grad():
+        got = m(x.float())
+    assert bn_mod.BN_PRELU_FUSED[0] > before
+    with torch.no_grad():
+        conv_out = torch.nn.functional.conv2d(x.float(), m[0].weight, m[0].bias, 1, 1)
+        want = torch.nn.functional.prelu(torch.nn.functional.batch_norm(
+            conv_out, m[1].running_mean, m[1].running_var, m[1].weight, m[1].bias, False, 0.0, m[1].eps),
+            m[2].activation.weight)  # scalar PReLU (the ConvBNAct default): expanded per channel
+    torch.testing.assert_close(got.float(), want, rtol=1e-4, atol=1e-4)
