@@ -301,10 +301,12 @@ static void check_wt(const at::Tensor& wt, int64_t taps, int64_t cout) {
 
 static at::Tensor dw_conv_fwd(const at::Tensor& x, const at::Tensor& wt, const std::optional<at::Tensor>& bias,
                               int64_t cout, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
-                              int64_t dh, int64_t dw) {
+                              int64_t dh, int64_t dw, int64_t act) {
   check_cl(x, "input");
+  TORCH_CHECK(act >= 0 && act <= 2, "rtseg.dw_conv_fwd: act must be 0 (none), 1 (ReLU) or 2 (ReLU6)");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   DwGeom g = dw_geom(x.size(0), x.size(1), x.size(2), x.size(3), cout, kh, kw, sh, sw, ph, pw, dh, dw);
+  g.act = static_cast<int>(act);
   check_wt(wt, kh * kw, cout);
   const float* b = nullptr;
   if (bias.has_value()) {
@@ -374,7 +376,7 @@ static at::Tensor dw_conv_wgrad(const at::Tensor& dy, const at::Tensor& x, int64
 
 TORCH_LIBRARY_FRAGMENT(rtseg, m) {
   m.def("dw_conv_fwd(Tensor x, Tensor wt, Tensor? bias, int cout, int kh, int kw, int sh, int sw, int ph, int pw, "
-        "int dh, int dw) -> Tensor");
+        "int dh, int dw, int act=0) -> Tensor");
   m.def("dw_conv_fwd_stats(Tensor x, Tensor wt, int cout, int kh, int kw, int sh, int sw, int ph, int pw, "
         "int dh, int dw) -> (Tensor, Tensor)");
   m.def("dw_conv_dgrad(Tensor dy, Tensor wt, int cin, int h, int w, int kh, int kw, int sh, int sw, int ph, "

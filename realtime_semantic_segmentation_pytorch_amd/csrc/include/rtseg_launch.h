@@ -147,6 +147,7 @@ void launch_shadow_crsk(const int64_t* tiles, int ntiles, hipStream_t st);
 struct DwGeom {
   int n, h, w, cin, cout, mult;  // mult = cout / cin
   int ho, wo, kh, kw, sh, sw, ph, pw, dh, dw;
+  int act = 0;  // forward: activation after the bias (0 none, 1 ReLU, 2 ReLU6; an eval BN folded in)
 };
 struct DwWgradPlan {
   int vec, lanes, chunks, nt, tap_groups, slices;  // nt = taps per wgrad thread

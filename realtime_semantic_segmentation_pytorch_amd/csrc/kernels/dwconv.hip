@@ -152,6 +152,12 @@ __global__ void __launch_bounds__(kDwBlock) dw_fwd_kernel(DwGeom g, DwDivs fd, c
         for (int j = 0; j < g.kw; ++j) tap(i, j);
     }
     T* yp = y + ((static_cast<int64_t>(n) * g.ho + ho) * g.wo + wo) * g.cout + co;
+    if constexpr (!STATS) {
+      if (g.act != 0) {  // an eval BN folded into weights / bias, then its ReLU / ReLU6 (uniform)
+#pragma unroll
+        for (int e = 0; e < OV; ++e) acc[e] = g.act == 1 ? fmaxf(acc[e], 0.f) : fminf(fmaxf(acc[e], 0.f), 6.f);
+      }
+    }
 #pragma unroll
     for (int q = 0; q < OV / VEC; ++q) Vec<T, VEC>::store(yp + q * VEC, acc + q * VEC);
     if constexpr (STATS) {

@@ -94,6 +94,13 @@ class _FusedTail:
             if out is not None:
                 y, part = out
                 return ops.bn_act(y, bn, own, act_module=own, part=part, sink=sink)
+        elif residual is None and sink is None and isinstance(conv, ops.DepthwiseConv2d) and isinstance(
+                bn, (nn.BatchNorm2d, nn.SyncBatchNorm)):
+            # inference: the eval BN (+ ReLU / ReLU6) folded into the depth-wise kernel (one pass)
+            code = ops.bn_act_code(own)
+            y = ops.dw_conv_bn_eval(x, conv, bn, code) if code is not None else None
+            if y is not None:
+                return y
         y = ops.conv_forward(x, conv)
         if residual is None:
             return ops.bn_act(y, bn, own, act_module=own, sink=sink)

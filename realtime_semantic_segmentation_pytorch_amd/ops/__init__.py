@@ -15,7 +15,7 @@ from .detail import detail_loss, detail_loss_reference, detail_target_reference
 from .postprocess import colorize, colorize_reference
 from .confmat import confusion_matrix, confusion_matrix_reference
 from .concat import ConcatSink, cat_bn_act
-from .dwconv import DepthwiseConv2d, convert_depthwise, depthwise_ok, dw_conv2d, dw_conv_bn_stats
+from .dwconv import DepthwiseConv2d, convert_depthwise, depthwise_ok, dw_conv2d, dw_conv_bn_eval, dw_conv_bn_stats
 from .pool import (avg_pool2d, max_pool2d, adaptive_avg_pool2d, convert_pooling, AvgPool2d, MaxPool2d,
                    AdaptiveAvgPool2d, MaxUnpool2d, max_pool2d_with_indices, max_unpool2d, AdaptiveMaxPool2d,
                    adaptive_max_pool2d)
@@ -37,7 +37,7 @@ __all__ = [
     "interpolate", "final_upsample", "defer_final_upsample", "DeferredLogits", "materialize",
     "seg_cross_entropy", "seg_cross_entropy_reference", "MODE_OHEM", "MODE_MEAN", "MODE_SUM",
     "colorize", "colorize_reference", "kd_kl_div", "kd_kl_div_reference", "detail_loss", "detail_loss_reference", "detail_target_reference", "confusion_matrix", "confusion_matrix_reference",
-    "DepthwiseConv2d", "convert_depthwise", "depthwise_ok", "dw_conv2d", "dw_conv_bn_stats",
+    "DepthwiseConv2d", "convert_depthwise", "depthwise_ok", "dw_conv2d", "dw_conv_bn_eval", "dw_conv_bn_stats",
     "avg_pool2d", "max_pool2d", "adaptive_avg_pool2d", "convert_pooling", "AvgPool2d", "MaxPool2d",
     "AdaptiveAvgPool2d", "AdaptiveMaxPool2d", "adaptive_max_pool2d", "MaxUnpool2d", "max_pool2d_with_indices", "max_unpool2d", "TapConv2d", "convert_tap_convs", "tap_conv2d", "tapconv_ok",
     "DilatedGroupConv2d", "convert_dilated_group_convs", "dilated_group_conv2d", "dilated_group_ok",

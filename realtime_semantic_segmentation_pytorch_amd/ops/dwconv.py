@@ -147,6 +147,43 @@ def dw_conv_bn_stats(x: torch.Tensor, conv: nn.Conv2d):
     return _DWConvFn.apply(x.to(dt), conv.weight, None, geom, True)
 
 
+DW_BN_FOLDED = [0]  # inference depth-wise conv + eval BN (+ ReLU / ReLU6) passes run as one (tests)
+
+
+def dw_conv_bn_eval(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, act_code: int):
+    """Inference ``act(bn_running(dwconv(x)))`` as ONE depth-wise kernel: a depth-wise conv has one
+    weight column per output channel, so the eval BN folds exactly into fp32 weights (x scale) and a
+    bias (shift + bias x scale), and the ReLU / ReLU6 runs in the store.  BiSeNetV2's gather-expansion
+    layers are DW -> BN pairs throughout (reference models/bisenetv2.py).  The folded tensors are
+    cached on the conv, keyed on every source's storage / version.  None -> the caller's path."""
+    if act_code not in (0, 1, 2) or torch.is_grad_enabled() or not depthwise_ok(conv):
+        return None
+    if bn.training or not bn.track_running_stats or bn.running_mean is None:
+        return None
+    if not (x.dim() == 4 and use_hip(x, "dw") and _channels_inner(x) and os.environ.get("RTSEG_DWCONV", "1") != "0"):
+        return None
+    dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
+    if dt not in _DTYPES or conv.weight.dtype not in _DTYPES:
+        return None
+    from .bn import eval_coeffs
+
+    kh, kw = conv.kernel_size
+    cout = conv.out_channels
+    srcs = (conv.weight, conv.bias, bn.weight, bn.bias, bn.running_mean, bn.running_var)
+    key = tuple((t.data_ptr(), t._version) if t is not None else None for t in srcs) + (write_generation(),)
+    hit = getattr(conv, "_rtseg_dw_bn", None)
+    if hit is None or hit[0] != key:
+        _, ss = eval_coeffs(bn)
+        scale, shift = ss[:cout], ss[cout:]
+        wt = _dw_weight(conv.weight, cout, kh * kw) * scale.view(1, -1)
+        b = shift + (conv.bias.detach().float() * scale if conv.bias is not None else 0.0)
+        hit = (key, wt.contiguous(), b.contiguous())
+        conv._rtseg_dw_bn = hit
+    DW_BN_FOLDED[0] += 1
+    return ops().dw_conv_fwd(_cl_aligned(x.to(dt)), hit[1], hit[2], cout, kh, kw, conv.stride[0], conv.stride[1],
+                             conv.padding[0], conv.padding[1], conv.dilation[0], conv.dilation[1], act_code)
+
+
 def dw_conv2d_reference(x, weight, bias, stride, padding, dilation):
     return F.conv2d(x, weight, bias, stride, padding, dilation, x.shape[1])
 

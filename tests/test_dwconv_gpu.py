@@ -139,3 +139,43 @@ def test_dwconvbnact_training_uses_epilogue_stats(mult, monkeypatch):
     torch.testing.assert_close(x.grad, xr.grad, rtol=1e-3, atol=1e-4)
     torch.testing.assert_close(m[1].running_mean, ref[1].running_mean, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(m[1].running_var, ref[1].running_var, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("mult,stride,act,bias", [(1, 1, "relu", False), (1, 2, "none", False), (6, 1, "none", False),
+                                                 (6, 2, "relu6", False), (1, 1, "relu", True)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_dw_bn_eval_folded(mult, stride, act, bias, dtype):
+    """Inference DWConvBNAct: the eval BN folded into the depth-wise weights / bias and the ReLU /
+    ReLU6 applied in the kernel's store (ops.dw_conv_bn_eval), against conv -> BN -> act in fp32."""
+    import torch.nn.functional as F
+
+    from realtime_semantic_segmentation_pytorch_amd.models.modules import DWConvBNAct
+    from realtime_semantic_segmentation_pytorch_amd.ops import dwconv as dw_mod
+
+    assert ops.load()
+    torch.manual_seed(mult + stride)
+    cin = 32
+    m = DWConvBNAct(cin, cin * mult, 3, stride, act_type=act)
+    if bias:
+        m[0] = torch.nn.Conv2d(cin, cin * mult, 3, stride, 1, groups=cin, bias=True)
+    m = ops.convert_batchnorm(ops.convert_depthwise(m)).cuda().eval()
+    with torch.no_grad():
+        m[1].running_mean.uniform_(-0.3, 0.3)
+        m[1].running_var.uniform_(0.5, 2.0)
+        m[1].weight.uniform_(0.5, 1.5)
+        m[1].bias.uniform_(-0.3, 0.3)
+    x = torch.randn(2, cin, 33, 40, device="cuda").contiguous(memory_format=torch.channels_last)
+    before = dw_mod.DW_BN_FOLDED[0]
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16):
+        got = m(x)
+    assert dw_mod.DW_BN_FOLDED[0] == before + 1
+    xr = x.to(dtype).float()
+    wr = m[0].weight.float() if dtype == torch.float32 else m[0].weight.to(dtype).float()
+    with torch.no_grad():
+        ref = F.conv2d(xr, wr, m[0].bias, stride, 1, 1, cin)
+        ref = F.batch_norm(ref, m[1].running_mean, m[1].running_var, m[1].weight, m[1].bias, False, 0.0, m[1].eps)
+    ref = ref.relu() if act == "relu" else ref.clamp(0, 6) if act == "relu6" else ref
+    if dtype == torch.float32:
+        torch.testing.assert_close(got.float(), ref, rtol=1e-4, atol=1e-4)
+    else:
+        torch.testing.assert_close(got.float(), ref, rtol=2 ** -7, atol=2e-3 * ref.abs().max().item())
