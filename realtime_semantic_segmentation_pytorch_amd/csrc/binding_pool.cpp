@@ -49,6 +49,27 @@ static std::tuple<at::Tensor, at::Tensor> pool2d_fwd(const at::Tensor& x, at::In
   return {y, idx};
 }
 
+// pool2d_fwd into a caller-owned output y (e.g. a channel slice of a concat buffer: the kernel
+// indexes y by its strides, 16-byte vectors when the slice's offset and row stride allow) -> idx
+static at::Tensor pool2d_fwd_out(const at::Tensor& x, const at::Tensor& y, at::IntArrayRef kernel,
+                                 at::IntArrayRef stride, at::IntArrayRef padding, int64_t mode,
+                                 bool count_include_pad) {
+  check_x(x);
+  check_x(y);
+  const PoolParams p = pool_params(kernel, stride, padding, mode, count_include_pad, false);
+  const int64_t oh = (x.size(2) + 2 * p.ph - p.kh) / p.sh + 1;
+  const int64_t ow = (x.size(3) + 2 * p.pw - p.kw) / p.sw + 1;
+  TORCH_CHECK(y.size(0) == x.size(0) && y.size(1) == x.size(1) && y.size(2) == oh && y.size(3) == ow,
+              "rtseg.pool_fwd_out: output shape does not match the pooling geometry");
+  TORCH_CHECK(y.scalar_type() == x.scalar_type() && y.device() == x.device(), "rtseg.pool_fwd_out: dtype/device");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  at::Tensor idx;
+  if (mode == kPoolMax) idx = at::empty({x.size(0), oh, ow, x.size(1)}, x.options().dtype(at::kByte));
+  else idx = at::empty({0}, x.options().dtype(at::kByte));
+  launch_pool_fwd(view4(x), view4(y), p, mode == kPoolMax ? idx.data_ptr<uint8_t>() : nullptr, cur_stream());
+  return idx;
+}
+
 static at::Tensor pool2d_bwd(const at::Tensor& gy, const at::Tensor& idx, int64_t in_h, int64_t in_w,
                              at::IntArrayRef kernel, at::IntArrayRef stride, at::IntArrayRef padding, int64_t mode,
                              bool count_include_pad) {
@@ -158,6 +179,8 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
   m.def("max_unpool_bwd(Tensor gy, Tensor idx) -> Tensor");
   m.def("pool2d_fwd(Tensor x, int[] kernel, int[] stride, int[] padding, int mode, bool count_include_pad) "
         "-> (Tensor, Tensor)");
+  m.def("pool2d_fwd_out(Tensor x, Tensor(a!) y, int[] kernel, int[] stride, int[] padding, int mode, "
+        "bool count_include_pad) -> Tensor");
   m.def("pool2d_bwd(Tensor gy, Tensor idx, int in_h, int in_w, int[] kernel, int[] stride, int[] padding, int mode, "
         "bool count_include_pad) -> Tensor");
   m.def("adaptive_avg_pool_fwd(Tensor x, int out_h, int out_w) -> Tensor");
@@ -166,6 +189,7 @@ TORCH_LIBRARY_FRAGMENT(rtseg, m) {
 
 TORCH_LIBRARY_IMPL(rtseg, CUDA, m) {
   m.impl("pool2d_fwd", &rtseg::pool2d_fwd);
+  m.impl("pool2d_fwd_out", &rtseg::pool2d_fwd_out);
   m.impl("pool2d_bwd", &rtseg::pool2d_bwd);
   m.impl("adaptive_avg_pool_fwd", &rtseg::adaptive_avg_pool_fwd);
   m.impl("adaptive_avg_pool_bwd", &rtseg::adaptive_avg_pool_bwd);

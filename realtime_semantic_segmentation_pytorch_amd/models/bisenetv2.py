@@ -93,7 +93,14 @@ class StemBlock(nn.Module):
 
     def forward(self, x):
         x = self.conv_init(x)
-        return self.conv_last(torch.cat([self.left_branch(x), self.right_branch(x)], dim=1))
+        # K11: both branches land in one concat buffer -- the left branch's BN kernel stores into
+        # its slice, the max pool runs inside the cat node into the other (ops.ConcatSink): no
+        # pooled tensor and no cat kernel in forward, no slice copies in backward
+        c = x.shape[1]  # both branches keep conv_init's width
+        sink = ops.ConcatSink([c, c])
+        left = self.left_branch[1](self.left_branch[0](x), sink=(sink, 0))
+        rp = self.right_branch
+        return self.conv_last(sink.cat([left, sink.max_pool(1, x, rp.kernel_size, rp.stride, rp.padding)]))
 
 
 class GatherExpansionLayer(nn.Module):

@@ -39,51 +39,93 @@ class ConcatSink:
         self.total = sum(self.widths)
         self.buf: Optional[torch.Tensor] = None
         self.written: dict = {}  # branch index -> (output tensor, its BN autograd node)
+        self.pooled: dict = {}  # branch index -> (kernel, stride, padding) of a PooledPart
 
     def slot(self, i: int, like: torch.Tensor) -> Optional[torch.Tensor]:
         """Channel slice ``i`` of the buffer for a branch output shaped like ``like`` (allocated
         on first use), or None when the fused kernels cannot store there."""
-        if like.dim() != 4 or like.shape[1] != self.widths[i] or not like.is_cuda or not _ENABLED:
+        if like.dim() != 4 or not like.is_cuda:
+            return None
+        return self._slot(i, tuple(like.shape), like.dtype, like.device)
+
+    def _slot(self, i, shape, dtype, device) -> Optional[torch.Tensor]:
+        n, c, h, w = shape
+        if c != self.widths[i] or not _ENABLED:
             return None
         if torch.onnx.is_in_onnx_export() or torch.jit.is_tracing():
             return None  # exported graphs keep the plain cat
-        vec = 16 // like.element_size()
+        vec = 128 // torch.finfo(dtype).bits
         if self.offsets[i] % vec or self.total % vec or self.widths[i] % vec or self.widths[i] // vec > 256:
             return None
-        n, _, h, w = like.shape
         if self.buf is None:
-            self.buf = torch.empty((n, self.total, h, w), dtype=like.dtype, device=like.device,
+            self.buf = torch.empty((n, self.total, h, w), dtype=dtype, device=device,
                                    memory_format=torch.channels_last)
-        elif self.buf.dtype != like.dtype or self.buf.shape[0] != n or tuple(self.buf.shape[2:]) != (h, w):
+        elif self.buf.dtype != dtype or self.buf.shape[0] != n or tuple(self.buf.shape[2:]) != (h, w):
             return None
         return self.buf[:, self.offsets[i]:self.offsets[i] + self.widths[i]]
+
+    def max_pool(self, i: int, x: torch.Tensor, kernel_size: int, stride: int, padding: int = 0):
+        """Branch ``i`` = ``max_pool2d(x, kernel_size, stride, padding)``, pooled by the cat node
+        itself straight into its channel slice (:class:`PooledPart`; the pool kernel indexes its
+        output by strides, ``pool2d_fwd_out``) -- or the pooled tensor when that path is off."""
+        from .pool import _hip_ok, max_pool2d
+
+        k, s, p = int(kernel_size), int(stride), int(padding)
+        if x.dim() == 4 and x.is_cuda and _hip_ok(x) and x.dtype != torch.float16:
+            n, c, h, w = x.shape
+            shape = (n, c, (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1)
+            if self._slot(i, shape, x.dtype, x.device) is not None:
+                self.pooled[i] = (k, s, p)
+                return PooledPart(x, k, s, p)
+        return max_pool2d(x, k, s, p)
 
     def record(self, i: int, out: torch.Tensor, node) -> None:
         self.written[i] = (out, node)
 
     def cat(self, xs: List[torch.Tensor]) -> torch.Tensor:
-        if self.buf is None or not self.written:
-            return torch.cat(xs, dim=1)
-        return _CatSinkFn.apply(self, *xs)
+        if self.buf is None or not (self.written or self.pooled):
+            return torch.cat([x.materialize() if isinstance(x, PooledPart) else x for x in xs], dim=1)
+        return _CatSinkFn.apply(self, *[x.x if isinstance(x, PooledPart) else x for x in xs])
+
+
+class PooledPart:
+    """A max-pool concat branch that the cat node computes into its buffer slice (no pooled
+    tensor, no cat read of it; backward: the pool backward reads the slice of the cat's gradient
+    at its row stride)."""
+    __slots__ = ("x", "k", "s", "p")
+
+    def __init__(self, x, k, s, p):
+        self.x, self.k, self.s, self.p = x, k, s, p
+
+    def materialize(self) -> torch.Tensor:
+        from .pool import max_pool2d
+
+        return max_pool2d(self.x, self.k, self.s, self.p)
 
 
 class _CatSinkFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, sink: ConcatSink, *xs):
-        nodes = []
+        nodes, pools = [], {}
         for i, x in enumerate(xs):
             hit = sink.written.get(i)
-            if hit is not None and hit[0] is x:
+            sl = sink.buf[:, sink.offsets[i]:sink.offsets[i] + sink.widths[i]]
+            if i in sink.pooled:  # x is the pool's input: pooled straight into the slice
+                k, s, p = sink.pooled[i]
+                idx = _ops().pool2d_fwd_out(x, sl, [k, k], [s, s], [p, p], 1, True)
+                pools[i] = (idx, x.shape[2], x.shape[3], k, s, p)
+                nodes.append(None)
+            elif hit is not None and hit[0] is x:
                 nodes.append(hit[1])
             else:  # a branch no fused kernel stored (STDC's pooled x1): copy it in
-                sink.buf[:, sink.offsets[i]:sink.offsets[i] + sink.widths[i]].copy_(x)
+                sl.copy_(x)
                 nodes.append(None)
         # the node keeps only the slice geometry and the BN nodes: the buffer (about to carry this
         # node as its grad_fn) and the branch outputs are released from the sink -- no
         # tensor -> grad_fn -> sink -> tensor reference cycle holding GPU memory until a GC pass
-        ctx.geom, ctx.nodes = list(zip(sink.offsets, sink.widths)), nodes
+        ctx.geom, ctx.nodes, ctx.pools = list(zip(sink.offsets, sink.widths)), nodes, pools
         ctx.set_materialize_grads(False)
-        out, sink.buf, sink.written = sink.buf, None, {}
+        out, sink.buf, sink.written, sink.pooled = sink.buf, None, {}, {}
         return out
 
     @staticmethod
@@ -92,9 +134,12 @@ class _CatSinkFn(torch.autograd.Function):
             return (None,) * (1 + len(ctx.nodes))
         cl = g.is_contiguous(memory_format=torch.channels_last) and g.data_ptr() % 16 == 0
         grads = []
-        for (off, width), node in zip(ctx.geom, ctx.nodes):
+        for i, ((off, width), node) in enumerate(zip(ctx.geom, ctx.nodes)):
             sl = g[:, off:off + width]
-            if cl and node is not None and getattr(node, "dy2_slot", None) is not None:
+            if i in ctx.pools:  # the max-pool backward reads the slice at its row stride
+                idx, h, w, k, s, p = ctx.pools[i]
+                grads.append(_ops().pool2d_bwd(sl, idx, h, w, [k, k], [s, s], [p, p], 1, True))
+            elif cl and node is not None and getattr(node, "dy2_slot", None) is not None:
                 node.dy2_slot.append(sl)  # the BN backward reads it in place
                 grads.append(None)
             else:

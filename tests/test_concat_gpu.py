@@ -156,3 +156,57 @@ def test_cgnet_block_uses_cat_bn():
         y = blk(x)
     y.float().sum().backward()
     assert concat_mod.CAT_BN_CALLS[0] == before + 1
+
+
+def _stem_step(mod, x, sink_on, monkeypatch, amp):
+    monkeypatch.setattr(concat_mod, "_ENABLED", sink_on)
+    m = copy.deepcopy(mod)
+    xx = x.clone().requires_grad_(True)
+    with torch.autocast(x.device.type, dtype=torch.bfloat16, enabled=amp):
+        y = m(xx)
+    gen = torch.Generator().manual_seed(0)
+    (y.float() * torch.randn(y.shape, generator=gen).to(y.device)).sum().backward()
+    return y, xx.grad.float(), {k: p.grad.float() for k, p in m.named_parameters()}
+
+
+@pytest.mark.parametrize("amp", [False, True])
+def test_bisenetv2_stem_concat_conv_without_cat(amp, monkeypatch):
+    """K11 at a concat -> conv site (BiSeNetV2's stem, reference models/bisenetv2.py:84-96:
+    ``conv_last(cat([left_branch(x), maxpool(x)]))``): the left BN stores into its slice of the
+    concat buffer, the max pool runs inside the cat node into the other (pool2d_fwd_out) and
+    its backward reads the gradient slice at its row stride.  No torch.cat runs; the result
+    matches the same module on torch.cat and, in fp32, a CPU fp32 run of the stock module."""
+    from realtime_semantic_segmentation_pytorch_amd.models.bisenetv2 import StemBlock
+
+    torch.manual_seed(3)
+    mod = StemBlock(3, 16).train()
+    ref = copy.deepcopy(mod)
+    mod = ops.convert_batchnorm(mod).cuda().to(**CL)
+    x = torch.randn(2, 3, 64, 96)
+    cats = []
+    real_cat = torch.cat
+    def spy(*a, **k):
+        out = real_cat(*a, **k)
+        if out.dim() == 4:  # the stem's concat (small 1-D cats of BN sums do not count)
+            cats.append(tuple(out.shape))
+        return out
+
+    monkeypatch.setattr(torch, "cat", spy)
+    y1, dx1, g1 = _stem_step(mod, x.cuda().contiguous(**CL), True, monkeypatch, amp)
+    assert not cats, f"the sink path ran torch.cat: {cats}"
+    monkeypatch.setattr(torch, "cat", real_cat)
+    y0, dx0, g0 = _stem_step(mod, x.cuda().contiguous(**CL), False, monkeypatch, amp)
+    rel = lambda a, b: float((a - b).norm() / (b.norm() + 1e-12))  # noqa: E731
+    if amp:  # the BN slice gradient is summed in fp32 inside the kernel instead of a bf16 add
+        assert rel(y1.float(), y0.float()) < 1e-2
+        assert rel(dx1, dx0) < 2e-2, rel(dx1, dx0)
+        for k in g0:
+            assert rel(g1[k], g0[k]) < 3e-2, (k, rel(g1[k], g0[k]))
+        return
+    torch.testing.assert_close(y1, y0, rtol=1e-6, atol=1e-6)
+    assert rel(dx1, dx0) < 1e-5, rel(dx1, dx0)
+    yr, dxr, gr = _stem_step(ref.double(), x.double(), False, monkeypatch, False)
+    assert rel(y1.double().cpu(), yr) < 1e-4
+    assert rel(dx1.double().cpu(), dxr.double()) < 1e-4, rel(dx1.double().cpu(), dxr.double())
+    for k in gr:
+        assert rel(g1[k].double().cpu(), gr[k].double()) < 1e-3, (k, rel(g1[k].double().cpu(), gr[k].double()))
