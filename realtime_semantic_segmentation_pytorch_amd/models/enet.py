@@ -48,15 +48,21 @@ class InitialBlock(nn.Module):
             raise AssertionError("out_channels should be larger than in_channels.\n")
         self.conv = ConvBNAct(in_channels, out_channels - in_channels, kernel_size, 2, act_type=act_type, **kwargs)
         self.pool = nn.MaxPool2d(3, 2, 1)
+        self.widths = (out_channels - in_channels, in_channels)
 
     def forward(self, x):
-        y, p = self.conv(x), self.pool(x)
-        # under autocast the conv branch is bf16 while max-pooling the fp32 input image stays fp32:
-        # torch.cat would promote the block -- and every activation of the 10 networks built on
+        # K11: the conv branch's BN kernel stores into its slice of one concat buffer and the max
+        # pool runs inside the cat node into the other (ops.ConcatSink, as BiSeNetV2's stem); with
+        # unaligned widths (ENet's 13 || 3) or an unfused activation the parts are copied in.
+        # Under autocast the conv branch is bf16 while max-pooling the fp32 input image stays fp32:
+        # a plain cat would promote the block -- and every activation of the 10 networks built on
         # it (ENet, ERFNet, LEDNet, AGLNet, ESNet, FDDWNet, ...) -- to fp32, with a bf16 cast before
         # each conv (profiles/r4_zoo_models).  Max pooling commutes with the rounding, so the cast
         # of the pooled branch is exact w.r.t. pooling the rounded input
-        return torch.cat([y, p.to(y.dtype)], dim=1)
+        sink = ops.ConcatSink(self.widths)
+        y = self.conv(x, sink=(sink, 0))
+        pl = self.pool
+        return sink.cat([y, sink.max_pool(1, x, pl.kernel_size, pl.stride, pl.padding, dtype=y.dtype)])
 
 
 class BottleNeck1(nn.Module):

@@ -64,13 +64,18 @@ class ConcatSink:
             return None
         return self.buf[:, self.offsets[i]:self.offsets[i] + self.widths[i]]
 
-    def max_pool(self, i: int, x: torch.Tensor, kernel_size: int, stride: int, padding: int = 0):
+    def max_pool(self, i: int, x: torch.Tensor, kernel_size: int, stride: int, padding: int = 0,
+                 dtype: Optional[torch.dtype] = None):
         """Branch ``i`` = ``max_pool2d(x, kernel_size, stride, padding)``, pooled by the cat node
         itself straight into its channel slice (:class:`PooledPart`; the pool kernel indexes its
-        output by strides, ``pool2d_fwd_out``) -- or the pooled tensor when that path is off."""
+        output by strides, ``pool2d_fwd_out``) -- or the pooled tensor when that path is off.
+        ``dtype``: the concat's dtype (autocast: a bf16 conv branch next to a pooled fp32 image);
+        a pool input of another dtype takes the tensor path, cast to it."""
         from .pool import _hip_ok, max_pool2d
 
         k, s, p = int(kernel_size), int(stride), int(padding)
+        if dtype is not None and x.dtype != dtype:
+            return max_pool2d(x, k, s, p).to(dtype)
         if x.dim() == 4 and x.is_cuda and _hip_ok(x) and x.dtype != torch.float16:
             n, c, h, w = x.shape
             shape = (n, c, (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1)

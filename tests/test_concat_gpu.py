@@ -210,3 +210,36 @@ def test_bisenetv2_stem_concat_conv_without_cat(amp, monkeypatch):
     assert rel(dx1.double().cpu(), dxr.double()) < 1e-4, rel(dx1.double().cpu(), dxr.double())
     for k in gr:
         assert rel(g1[k].double().cpu(), gr[k].double()) < 1e-3, (k, rel(g1[k].double().cpu(), gr[k].double()))
+
+
+@pytest.mark.parametrize("act", ["relu", "prelu"])
+@pytest.mark.parametrize("amp", [False, True])
+def test_initial_block_pooled_sink(act, amp, monkeypatch):
+    """The ENet-family InitialBlock (reference models/enet.py:38-48; 10 zoo networks):
+    conv-BN-act || max-pool into one concat buffer.  ReLU: both parts are written in place;
+    PReLU (unfused activation): the pool still runs into its slice, the conv part is copied.
+    Against the same block on torch.cat (and, fp32, a CPU fp64 run)."""
+    from realtime_semantic_segmentation_pytorch_amd.models.enet import InitialBlock
+
+    torch.manual_seed(5)
+    mod = InitialBlock(16, 64, act).train()
+    ref = copy.deepcopy(mod)
+    mod = ops.convert_batchnorm(mod).cuda().to(**CL)
+    x = torch.randn(2, 16, 48, 80)
+    y1, dx1, g1 = _stem_step(mod, x.cuda().contiguous(**CL), True, monkeypatch, amp)
+    assert y1.dtype == (torch.bfloat16 if amp else torch.float32)
+    y0, dx0, g0 = _stem_step(mod, x.cuda().contiguous(**CL), False, monkeypatch, amp)
+    rel = lambda a, b: float((a - b).norm() / (b.norm() + 1e-12))  # noqa: E731
+    if amp:
+        assert rel(y1.float(), y0.float()) < 1e-2
+        assert rel(dx1, dx0) < 2e-2, rel(dx1, dx0)
+        for k in g0:
+            assert rel(g1[k], g0[k]) < 3e-2, (k, rel(g1[k], g0[k]))
+        return
+    torch.testing.assert_close(y1, y0, rtol=1e-6, atol=1e-6)
+    assert rel(dx1, dx0) < 1e-5, rel(dx1, dx0)
+    yr, dxr, gr = _stem_step(ref.double(), x.double(), False, monkeypatch, False)
+    assert rel(y1.double().cpu(), yr) < 1e-4
+    assert rel(dx1.double().cpu(), dxr.double()) < 1e-4
+    for k in gr:
+        assert rel(g1[k].double().cpu(), gr[k].double()) < 1e-3, k
