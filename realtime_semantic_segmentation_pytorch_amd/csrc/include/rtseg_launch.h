@@ -151,6 +151,7 @@ struct DwGeom {
 };
 struct DwWgradPlan {
   int vec, lanes, chunks, nt, tap_groups, slices;  // nt = taps per wgrad thread
+  int pairs = 0;  // 1: the channel-multiplier kernel (bf16, mult 2/3/4/6): threads own input-channel pairs
 };
 int dw_vec(int dtype, int c);
 DwWgradPlan dw_wgrad_plan(const DwGeom& g, int dtype);

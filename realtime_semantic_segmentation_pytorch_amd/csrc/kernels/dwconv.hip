@@ -82,18 +82,20 @@ __global__ void __launch_bounds__(kDwBlock) dw_fwd_kernel(DwGeom g, DwDivs fd, c
                                                           const float* __restrict__ wt,
                                                           const float* __restrict__ bias, T* __restrict__ y,
                                                           float* __restrict__ part = nullptr) {
-  static_assert(!CSW || (MT == 1 && KS > 0), "channel-stationary weights: MT 1, compile-time taps");
+  static_assert(!CSW || (MT >= 1 && KS > 0), "channel-stationary weights: compile-time taps");
   constexpr int OV = MT > 1 ? VEC * MT : VEC;  // output channels per thread
+  // SV: the widest vector (<= 8) dividing OV -- output stores (co and Cout are multiples of OV)
+  constexpr int SV = OV % 8 == 0 ? 8 : OV % 4 == 0 ? 4 : OV % 2 == 0 ? 2 : 1;
   const int cv_n = MT > 1 ? g.cin / VEC : g.cout / VEC;
   const uint32_t total = static_cast<uint32_t>(g.n) * g.ho * g.wo * cv_n;  // < 2^31 (host splits)
-  float wreg[CSW ? KS * KS : 1][CSW ? VEC : 1];
-  float breg[CSW ? VEC : 1];
+  float wreg[CSW ? KS * KS : 1][CSW ? OV : 1];
+  float breg[CSW ? OV : 1];
   if constexpr (CSW) {
-    const int co = static_cast<int>((blockIdx.x * kDwBlock + threadIdx.x) % static_cast<uint32_t>(cv_n)) * VEC;
+    const int co = static_cast<int>((blockIdx.x * kDwBlock + threadIdx.x) % static_cast<uint32_t>(cv_n)) * OV;
 #pragma unroll
-    for (int t = 0; t < KS * KS; ++t) load_wvec<VEC>(wt + t * g.cout + co, wreg[t]);
+    for (int t = 0; t < KS * KS; ++t) load_wvec<OV>(wt + t * g.cout + co, wreg[t]);
 #pragma unroll
-    for (int v = 0; v < VEC; ++v) breg[v] = bias ? bias[co + v] : 0.f;
+    for (int v = 0; v < OV; ++v) breg[v] = bias ? bias[co + v] : 0.f;
   }
   float ssum[STATS ? OV : 1], ssq[STATS ? OV : 1];
   if constexpr (STATS) {
@@ -125,7 +127,7 @@ __global__ void __launch_bounds__(kDwBlock) dw_fwd_kernel(DwGeom g, DwDivs fd, c
       float xv[VEC], wv[OV];
       if constexpr (CSW) {
 #pragma unroll
-        for (int v = 0; v < VEC; ++v) wv[v] = wreg[KS > 0 ? i * KS + j : 0][v];
+        for (int v = 0; v < OV; ++v) wv[v] = wreg[KS > 0 ? i * KS + j : 0][v];
       } else {
         load_wvec<OV>(wp, wv);
       }
@@ -159,7 +161,7 @@ __global__ void __launch_bounds__(kDwBlock) dw_fwd_kernel(DwGeom g, DwDivs fd, c
       }
     }
 #pragma unroll
-    for (int q = 0; q < OV / VEC; ++q) Vec<T, VEC>::store(yp + q * VEC, acc + q * VEC);
+    for (int q = 0; q < OV / SV; ++q) Vec<T, SV>::store(yp + q * SV, acc + q * SV);
     if constexpr (STATS) {
 #pragma unroll
       for (int e = 0; e < OV; ++e) {
@@ -204,11 +206,23 @@ __global__ void __launch_bounds__(kDwBlock) dw_fwd_kernel(DwGeom g, DwDivs fd, c
 }
 
 // ---------------------------------------------------------------- data grad
-template <typename T, int VEC, int MT, int KS>
+// CSW (MT > 1, KS > 0): channel-stationary grid (as the forward's), the thread's KS x KS x VEC*MT
+// weights in registers and its VEC*MT contiguous dy values per tap in SV-wide loads -- instead of
+// MT x (VEC dy + VEC fp32 weight) loads per tap
+template <typename T, int VEC, int MT, int KS, bool CSW = false>
 __global__ void __launch_bounds__(kDwBlock) dw_dgrad_kernel(DwGeom g, DwDivs fd, const T* __restrict__ dy,
                                                             const float* __restrict__ wt, T* __restrict__ dx) {
+  static_assert(!CSW || (MT > 1 && KS > 0), "channel-stationary dgrad: multiplier path, compile-time taps");
+  constexpr int OV = MT > 1 ? VEC * MT : VEC;
+  constexpr int SV = OV % 8 == 0 ? 8 : OV % 4 == 0 ? 4 : OV % 2 == 0 ? 2 : 1;
   const int cv_n = g.cin / VEC;
   const uint32_t total = static_cast<uint32_t>(g.n) * g.h * g.w * cv_n;  // < 2^31 (host splits)
+  float wreg[CSW ? KS * KS : 1][CSW ? OV : 1];
+  if constexpr (CSW) {
+    const int c0 = static_cast<int>((blockIdx.x * kDwBlock + threadIdx.x) % static_cast<uint32_t>(cv_n)) * OV;
+#pragma unroll
+    for (int t = 0; t < KS * KS; ++t) load_wvec<OV>(wt + t * g.cout + c0, wreg[t]);
+  }
   for (uint32_t it = blockIdx.x * kDwBlock + threadIdx.x; it < total; it += gridDim.x * kDwBlock) {
     uint32_t cvu, wiu, hiu;
     const uint32_t pix = fd.c.divmod(it, cvu);
@@ -231,6 +245,13 @@ __global__ void __launch_bounds__(kDwBlock) dw_dgrad_kernel(DwGeom g, DwDivs fd,
         load_wvec<VEC>(wp + ci, wv);
 #pragma unroll
         for (int v = 0; v < VEC; ++v) acc[v] = fmaf(ok ? dv[v] : 0.f, wv[v], acc[v]);
+      } else if constexpr (CSW) {
+        const int c0 = ci * MT;
+        float dv[OV];
+#pragma unroll
+        for (int q = 0; q < OV / SV; ++q) Vec<T, SV>::load(dp + c0 + q * SV, dv + q * SV);
+#pragma unroll
+        for (int e = 0; e < OV; ++e) acc[e / MT] = fmaf(ok ? dv[e] : 0.f, wreg[i * KS + j][e], acc[e / MT]);
       } else if constexpr (MT > 1) {
         // the VEC*MT output channels fed by this input vector are contiguous
         const int c0 = ci * MT;
@@ -265,6 +286,72 @@ __global__ void __launch_bounds__(kDwBlock) dw_dgrad_kernel(DwGeom g, DwDivs fd,
         for (int j = 0; j < g.kw; ++j) tap(i, j);
     }
     Vec<T, VEC>::store(dx + ((static_cast<int64_t>(n) * g.h + hi) * g.w + wi) * g.cin + ci, acc);
+  }
+}
+
+// Stride-2 3 x 3 (pad 1, dilation 1) data gradient of a channel-multiplier conv, channel-stationary:
+// a thread owns a 2 x 2 block of dx pixels (2a + p, 2b + q) of one input-channel vector.  Only
+// taps on the stride grid contribute, so the block needs exactly the 2 x 2 dy pixels (a | a+1,
+// b | b+1) -- 4 loads of the VEC*MT contiguous dy values instead of 4 x 9 clamped tap loads:
+//   dx(2a,   2b  ) = dy(a,b) w11
+//   dx(2a,   2b+1) = dy(a,b+1) w10 + dy(a,b) w12
+//   dx(2a+1, 2b  ) = dy(a+1,b) w01 + dy(a,b) w21
+//   dx(2a+1, 2b+1) = dy(a+1,b+1) w00 + dy(a+1,b) w02 + dy(a,b+1) w20 + dy(a,b) w22
+// (hi = 2 ho - 1 + i: ho = (hi + 1 - i) / 2 on the grid).  fd: divisors (cv_n, ceil(W/2), ceil(H/2)).
+template <typename T, int VEC, int MT>
+__global__ void __launch_bounds__(kDwBlock) dw_dgrad_s2_kernel(DwGeom g, DwDivs fd, const T* __restrict__ dy,
+                                                               const float* __restrict__ wt, T* __restrict__ dx) {
+  constexpr int OV = VEC * MT;
+  constexpr int SV = OV % 8 == 0 ? 8 : OV % 4 == 0 ? 4 : OV % 2 == 0 ? 2 : 1;
+  const int cv_n = g.cin / VEC;
+  const int A = (g.h + 1) / 2, B = (g.w + 1) / 2;
+  const uint32_t total = static_cast<uint32_t>(g.n) * A * B * cv_n;  // < 2^31 (host splits)
+  float wreg[9][OV];
+  {
+    const int c0 = static_cast<int>((blockIdx.x * kDwBlock + threadIdx.x) % static_cast<uint32_t>(cv_n)) * OV;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) load_wvec<OV>(wt + t * g.cout + c0, wreg[t]);
+  }
+  for (uint32_t it = blockIdx.x * kDwBlock + threadIdx.x; it < total; it += gridDim.x * kDwBlock) {
+    uint32_t cvu, bu, au;
+    const uint32_t pix = fd.c.divmod(it, cvu);
+    const uint32_t r = fd.w.divmod(pix, bu);
+    const int n = static_cast<int>(fd.h.divmod(r, au));
+    const int a = static_cast<int>(au), b = static_cast<int>(bu), ci = static_cast<int>(cvu) * VEC;
+    const bool r1 = a + 1 < g.ho, c1 = b + 1 < g.wo;  // the second dy row / column exists
+    const T* d00 = dy + ((static_cast<int64_t>(n) * g.ho + a) * g.wo + b) * g.cout + ci * MT;
+    const int64_t rs = r1 ? static_cast<int64_t>(g.wo) * g.cout : 0, cs = c1 ? g.cout : 0;  // clamped steps
+    float v00[OV], v01[OV], v10[OV], v11[OV];
+#pragma unroll
+    for (int q = 0; q < OV / SV; ++q) {
+      Vec<T, SV>::load(d00 + q * SV, v00 + q * SV);
+      Vec<T, SV>::load(d00 + cs + q * SV, v01 + q * SV);
+      Vec<T, SV>::load(d00 + rs + q * SV, v10 + q * SV);
+      Vec<T, SV>::load(d00 + rs + cs + q * SV, v11 + q * SV);
+    }
+#pragma unroll
+    for (int e = 0; e < OV; ++e) {
+      v01[e] = c1 ? v01[e] : 0.f;
+      v10[e] = r1 ? v10[e] : 0.f;
+      v11[e] = r1 && c1 ? v11[e] : 0.f;
+    }
+    float o00[VEC], o01[VEC], o10[VEC], o11[VEC];
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) o00[v] = o01[v] = o10[v] = o11[v] = 0.f;
+#pragma unroll
+    for (int e = 0; e < OV; ++e) {
+      const int v = e / MT;
+      o00[v] = fmaf(v00[e], wreg[4][e], o00[v]);
+      o01[v] = fmaf(v01[e], wreg[3][e], fmaf(v00[e], wreg[5][e], o01[v]));
+      o10[v] = fmaf(v10[e], wreg[1][e], fmaf(v00[e], wreg[7][e], o10[v]));
+      o11[v] = fmaf(v11[e], wreg[0][e], fmaf(v10[e], wreg[2][e], fmaf(v01[e], wreg[6][e], fmaf(v00[e], wreg[8][e], o11[v]))));
+    }
+    T* x00 = dx + ((static_cast<int64_t>(n) * g.h + 2 * a) * g.w + 2 * b) * g.cin + ci;
+    const bool hr = 2 * a + 1 < g.h, hc = 2 * b + 1 < g.w;
+    Vec<T, VEC>::store(x00, o00);
+    if (hc) Vec<T, VEC>::store(x00 + g.cin, o01);
+    if (hr) Vec<T, VEC>::store(x00 + static_cast<int64_t>(g.w) * g.cin, o10);
+    if (hr && hc) Vec<T, VEC>::store(x00 + static_cast<int64_t>(g.w) * g.cin + g.cin, o11);
   }
 }
 
@@ -357,6 +444,94 @@ __global__ void __launch_bounds__(kDwBlock) dw_wgrad_kernel(DwGeom g, DwDivs fd,
   }
 }
 
+// Channel-multiplier weight gradient (bf16, MT = 2/3/4/6: BiSeNetV2's x6 gather-expansion):
+// a thread owns one PAIR of input channels (ci, ci + 1) and the 2*MT contiguous output channels
+// they feed.  Per pixel: the 2*MT dy values in 8-byte (even MT) or 4-byte loads, then per tap ONE
+// 4-byte load of the input pair -- where dw_wgrad_kernel<VEC = 8> issues two 2-byte scalar loads
+// + selects per tap for every 8 outputs and idles a quarter of its lanes (8-wide output vectors
+// over a 6x channel count).  Lanes = input-channel pairs (a power of two for the zoo's 16..128
+// channel inputs: no idle lanes); all KH*KW (<= 9) taps per thread, partials reduced through LDS
+// into the same [G][taps][Cout] slab dw_wgrad_reduce_kernel sums (deterministic, no atomics).
+template <int MT>
+__global__ void __launch_bounds__(kDwBlock) dw_wgrad_pair_kernel(DwGeom g, DwDivs fd, const uint16_t* __restrict__ dy,
+                                                                 const uint16_t* __restrict__ x,
+                                                                 float* __restrict__ part, int lanes) {
+  constexpr int OV = 2 * MT;  // outputs per thread
+  const int rows = kDwBlock / lanes;
+  const int lane = threadIdx.x % lanes;
+  const int row = threadIdx.x / lanes;
+  const int pv = blockIdx.y * lanes + lane;  // input-channel pair
+  const bool active = pv < g.cin / 2;
+  const int ci = pv * 2, co = ci * MT;
+  const int taps = g.kh * g.kw;
+  float acc[kMaxTaps][OV];
+#pragma unroll
+  for (int t = 0; t < kMaxTaps; ++t)
+#pragma unroll
+    for (int v = 0; v < OV; ++v) acc[t][v] = 0.f;
+  const uint32_t npix = static_cast<uint32_t>(g.n) * g.ho * g.wo;
+  if (active) {
+    for (uint32_t p = blockIdx.x * rows + row; p < npix; p += gridDim.x * rows) {
+      uint32_t wou, hou;
+      const uint32_t r = fd.w.divmod(p, wou);
+      const int n = static_cast<int>(fd.h.divmod(r, hou));
+      const int wo = static_cast<int>(wou), ho = static_cast<int>(hou);
+      uint32_t dw32[MT];  // OV bf16 = MT dwords
+      const uint16_t* dp = dy + static_cast<int64_t>(p) * g.cout + co;
+      if constexpr (MT % 2 == 0) {
+#pragma unroll
+        for (int q = 0; q < MT / 2; ++q) {
+          const uint2 u = reinterpret_cast<const uint2*>(dp)[q];
+          dw32[2 * q] = u.x;
+          dw32[2 * q + 1] = u.y;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < MT; ++q) dw32[q] = reinterpret_cast<const uint32_t*>(dp)[q];
+      }
+      float dv[OV];
+#pragma unroll
+      for (int q = 0; q < MT; ++q) {
+        dv[2 * q] = __uint_as_float(dw32[q] << 16);
+        dv[2 * q + 1] = __uint_as_float(dw32[q] & 0xffff0000u);
+      }
+      const int hb = ho * g.sh - g.ph, wb = wo * g.sw - g.pw;
+      const uint16_t* xn = x + static_cast<int64_t>(n) * g.h * g.w * g.cin + ci;
+#pragma unroll
+      for (int t = 0; t < kMaxTaps; ++t) {
+        const int tap = min(t, taps - 1);
+        const int i = tap / g.kw, j = tap - (tap / g.kw) * g.kw;
+        const int hi = hb + i * g.dh, wi = wb + j * g.dw;
+        const bool ok = t < taps && hi >= 0 && hi < g.h && wi >= 0 && wi < g.w;
+        const int hc = min(max(hi, 0), g.h - 1), wc = min(max(wi, 0), g.w - 1);
+        const uint32_t xu = *reinterpret_cast<const uint32_t*>(xn + (static_cast<int64_t>(hc) * g.w + wc) * g.cin);
+        const float x0 = ok ? __uint_as_float(xu << 16) : 0.f;
+        const float x1 = ok ? __uint_as_float(xu & 0xffff0000u) : 0.f;
+#pragma unroll
+        for (int v = 0; v < OV; ++v) acc[t][v] = fmaf(v < MT ? x0 : x1, dv[v], acc[t][v]);
+      }
+    }
+  }
+  __shared__ float red[kDwBlock * OV];
+  const int64_t slab = static_cast<int64_t>(blockIdx.x) * taps * g.cout;
+  const int c0 = blockIdx.y * lanes * OV;  // first output channel of this block
+#pragma unroll
+  for (int t = 0; t < kMaxTaps; ++t) {
+    if (t < taps) {  // block-uniform
+      __syncthreads();
+#pragma unroll
+      for (int v = 0; v < OV; ++v) red[(row * lanes + lane) * OV + v] = acc[t][v];
+      __syncthreads();
+      for (int k = threadIdx.x; k < lanes * OV; k += kDwBlock) {
+        float s = 0.f;
+        for (int rr = 0; rr < rows; ++rr) s += red[rr * lanes * OV + k];
+        const int c = c0 + k;
+        if (c < g.cout) part[slab + static_cast<int64_t>(t) * g.cout + c] = s;
+      }
+    }
+  }
+}
+
 // dw[co][tap] = sum_G part[G][tap][co]   (output in the [Cout, 1, KH, KW] layout).
 // One block per 64 columns; 16 waves split the G rows (latency-bound reduction).
 constexpr int kRedWaves = 16;
@@ -444,11 +619,21 @@ static bool dw_cs_enabled() {
   return on;
 }
 
+// Multiplier convs (MT > 1) with a 3 x 3 kernel run channel-stationary on input-channel PAIRS:
+// VEC = 2, so a thread's 9 x 2*MT weights fit in registers (108 for BiSeNetV2's x6) and it loads
+// per tap one 4-byte input pair (forward) or 2*MT contiguous dy values (dgrad), where VEC = 8
+// re-loaded 9 x 8*MT fp32 weights per output pixel.  RTSEG_DW_MT_CS=0: off (A/B)
+static bool dw_mt_cs(const DwGeom& g) {
+  static const bool on = [] { const char* e = std::getenv("RTSEG_DW_MT_CS"); return !(e && e[0] == '0'); }();
+  return on && mt_of(g.mult) > 1 && g.kh == 3 && g.kw == 3 && g.cin % 2 == 0;
+}
+
 void launch_dw_fwd(const DwGeom& g0, int dtype, const void* x, const float* wt, const float* bias, void* y,
                    hipStream_t st) {
   const int mt = mt_of(g0.mult);
+  const bool mcs = dw_mt_cs(g0);
   // MT > 1: vectors over the INPUT channels (each feeds VEC*MT contiguous outputs)
-  const int vec = mt > 1 ? dw_vec(dtype, g0.cin) : dw_vec(dtype, g0.cout);
+  const int vec = mcs ? 2 : mt > 1 ? dw_vec(dtype, g0.cin) : dw_vec(dtype, g0.cout);
   const int cv_n = (mt > 1 ? g0.cin : g0.cout) / vec;
   const int64_t per_img = static_cast<int64_t>(g0.ho) * g0.wo * cv_n;
   const int nb = batch_chunk(per_img, g0.n);
@@ -459,14 +644,14 @@ void launch_dw_fwd(const DwGeom& g0, int dtype, const void* x, const float* wt, 
     const char* xb = static_cast<const char*>(x) + static_cast<int64_t>(n0) * g.h * g.w * g.cin * eb;
     char* yb = static_cast<char*>(y) + static_cast<int64_t>(n0) * g.ho * g.wo * g.cout * eb;
     const DwDivs fd{FastDiv::make(cv_n), FastDiv::make(g.wo), FastDiv::make(g.ho)};
-    const bool cs3 = mt == 1 && g.kh == 3 && g.kw == 3 && dw_cs_enabled();
+    const bool cs3 = (mt == 1 && g.kh == 3 && g.kw == 3 && dw_cs_enabled()) || mcs;
     const int grid = cs3 ? dw_stats_grid(per_img * g.n, cv_n) : stream_grid(per_img * g.n, kDwBlock);
     dw_dispatch(dtype, vec, g.mult, [&](auto t, auto v, auto m) {
       using T = decltype(t);
       constexpr int V = decltype(v)::value, M = decltype(m)::value;
-      if constexpr (M == 1) {
+      if constexpr (M == 1 || (M > 1 && V == 2)) {
         if (cs3) {  // 3 x 3, channel-stationary: weights in registers, 9 loads in flight
-          dw_fwd_kernel<T, V, 1, 3, false, true><<<grid, kDwBlock, 0, st>>>(
+          dw_fwd_kernel<T, V, M, 3, false, true><<<grid, kDwBlock, 0, st>>>(
               g, fd, reinterpret_cast<const T*>(xb), wt, bias, reinterpret_cast<T*>(yb));
           return;
         }
@@ -492,7 +677,7 @@ static int dw_stats_grid(int64_t items, int cv_n) {
 
 static int dw_fwd_stats_vec(const DwGeom& g, int dtype) {
   const int mt = mt_of(g.mult);
-  return mt > 1 ? dw_vec(dtype, g.cin) : dw_vec(dtype, g.cout);
+  return dw_mt_cs(g) ? 2 : mt > 1 ? dw_vec(dtype, g.cin) : dw_vec(dtype, g.cout);
 }
 
 int dw_fwd_stats_rows(const DwGeom& g0, int dtype) {
@@ -531,6 +716,12 @@ void launch_dw_fwd_stats(const DwGeom& g0, int dtype, const void* x, const float
               g, fd, reinterpret_cast<const T*>(xb), wt, nullptr, reinterpret_cast<T*>(yb), part);
           return;
         }
+      } else if constexpr (M > 1 && V == 2) {
+        if (dw_mt_cs(g)) {
+          dw_fwd_kernel<T, V, M, 3, true, true><<<grid, kDwBlock, 0, st>>>(
+              g, fd, reinterpret_cast<const T*>(xb), wt, nullptr, reinterpret_cast<T*>(yb), part);
+          return;
+        }
       }
       if constexpr (M != 0) {
         dw_fwd_kernel<T, V, M, 0, true><<<grid, kDwBlock, 0, st>>>(g, fd, reinterpret_cast<const T*>(xb), wt, nullptr,
@@ -542,8 +733,33 @@ void launch_dw_fwd_stats(const DwGeom& g0, int dtype, const void* x, const float
 }
 
 void launch_dw_dgrad(const DwGeom& g0, int dtype, const void* dy, const float* wt, void* dx, hipStream_t st) {
-  const int vec = dw_vec(dtype, g0.cin);
+  const bool mcs = dw_mt_cs(g0);
+  // stride-2 3 x 3 pad-1 multiplier convs: the 2 x 2 dx-block kernel (dw_dgrad_s2_kernel)
+  const bool s2 = mcs && g0.sh == 2 && g0.sw == 2 && g0.ph == 1 && g0.pw == 1 && g0.dh == 1 && g0.dw == 1;
+  const int vec = mcs ? 2 : dw_vec(dtype, g0.cin);
   const int cv_n = g0.cin / vec;
+  if (s2) {
+    const int A = (g0.h + 1) / 2, B = (g0.w + 1) / 2;
+    const int64_t per_img = static_cast<int64_t>(A) * B * cv_n;
+    const int nb = batch_chunk(per_img, g0.n);
+    const int64_t eb = elem_bytes(dtype);
+    for (int n0 = 0; n0 < g0.n; n0 += nb) {
+      DwGeom g = g0;
+      g.n = n0 + nb <= g0.n ? nb : g0.n - n0;
+      const char* dyb = static_cast<const char*>(dy) + static_cast<int64_t>(n0) * g.ho * g.wo * g.cout * eb;
+      char* dxb = static_cast<char*>(dx) + static_cast<int64_t>(n0) * g.h * g.w * g.cin * eb;
+      const DwDivs fd{FastDiv::make(cv_n), FastDiv::make(B), FastDiv::make(A)};
+      const int grid = dw_stats_grid(per_img * g.n, cv_n);
+      dw_dispatch(dtype, vec, g.mult, [&](auto t, auto v, auto m) {
+        using T = decltype(t);
+        constexpr int V = decltype(v)::value, M = decltype(m)::value;
+        if constexpr (M > 1 && V == 2)
+          dw_dgrad_s2_kernel<T, V, M><<<grid, kDwBlock, 0, st>>>(g, fd, reinterpret_cast<const T*>(dyb), wt,
+                                                                 reinterpret_cast<T*>(dxb));
+      });
+    }
+    return;
+  }
   const int64_t per_img = static_cast<int64_t>(g0.h) * g0.w * cv_n;
   const int nb = batch_chunk(per_img, g0.n);
   const int64_t eb = elem_bytes(dtype);
@@ -553,18 +769,52 @@ void launch_dw_dgrad(const DwGeom& g0, int dtype, const void* dy, const float* w
     const char* dyb = static_cast<const char*>(dy) + static_cast<int64_t>(n0) * g.ho * g.wo * g.cout * eb;
     char* dxb = static_cast<char*>(dx) + static_cast<int64_t>(n0) * g.h * g.w * g.cin * eb;
     const DwDivs fd{FastDiv::make(cv_n), FastDiv::make(g.w), FastDiv::make(g.h)};
-    const int grid = stream_grid(per_img * g.n, kDwBlock);
+    const int grid = mcs ? dw_stats_grid(per_img * g.n, cv_n) : stream_grid(per_img * g.n, kDwBlock);
     dw_dispatch(dtype, vec, g.mult, [&](auto t, auto v, auto m) {
       using T = decltype(t);
       constexpr int V = decltype(v)::value, M = decltype(m)::value;
+      if constexpr (M > 1 && V == 2) {
+        if (mcs) {  // channel-stationary 3 x 3 (dw_mt_cs)
+          dw_dgrad_kernel<T, V, M, 3, true><<<grid, kDwBlock, 0, st>>>(g, fd, reinterpret_cast<const T*>(dyb), wt,
+                                                                        reinterpret_cast<T*>(dxb));
+          return;
+        }
+      }
       dw_dgrad_kernel<T, V, M, 0><<<grid, kDwBlock, 0, st>>>(g, fd, reinterpret_cast<const T*>(dyb), wt,
                                                                reinterpret_cast<T*>(dxb));
     });
   }
 }
 
+// RTSEG_DW_WG_PAIR=0: the channel-multiplier wgrad on dw_wgrad_kernel (A/B)
+static bool dw_wg_pair_enabled() {
+  static const bool on = [] { const char* e = std::getenv("RTSEG_DW_WG_PAIR"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
 DwWgradPlan dw_wgrad_plan(const DwGeom& g, int dtype) {
   DwWgradPlan p;
+  const int mt = mt_of(g.mult);
+  if (dtype == kBF16 && mt > 1 && g.cin % 2 == 0 && g.kh * g.kw <= kMaxTaps && dw_wg_pair_enabled()) {
+    p.pairs = 1;
+    p.vec = 2 * mt;
+    const int pv_n = g.cin / 2;
+    p.lanes = 64;
+    while (p.lanes > 1 && p.lanes / 2 >= pv_n) p.lanes /= 2;
+    p.chunks = (pv_n + p.lanes - 1) / p.lanes;
+    p.nt = kMaxTaps;
+    p.tap_groups = 1;
+    const int64_t npix = static_cast<int64_t>(g.n) * g.ho * g.wo;
+    const int rows = kDwBlock / p.lanes;
+    int64_t G = 1024 / p.chunks;
+    if (const char* e = std::getenv("RTSEG_DW_WG_SLICES")) G = std::max(1, std::atoi(e)) / p.chunks;
+    if (G > 1024) G = 1024;
+    const int64_t gmax = (npix + static_cast<int64_t>(rows) * 16 - 1) / (static_cast<int64_t>(rows) * 16);
+    if (G > gmax) G = gmax;
+    if (G < 1) G = 1;
+    p.slices = static_cast<int>(G);
+    return p;
+  }
   p.vec = dw_vec(dtype, g.cout);
   const int cv_n = g.cout / p.vec;
   p.lanes = 64;
@@ -592,6 +842,20 @@ void launch_dw_wgrad(const DwGeom& g, int dtype, const void* dy, const void* x, 
   const DwWgradPlan p = dw_wgrad_plan(g, dtype);
   dim3 grid(p.slices, p.chunks, p.tap_groups);
   const DwDivs fd{FastDiv::make(1), FastDiv::make(g.wo), FastDiv::make(g.ho)};
+  const int taps = g.kh * g.kw;
+  const int rb = (taps * g.cout + 63) / 64;
+  if (p.pairs) {
+    const uint16_t* dyp = static_cast<const uint16_t*>(dy);
+    const uint16_t* xp = static_cast<const uint16_t*>(x);
+    switch (g.mult) {
+      case 2: dw_wgrad_pair_kernel<2><<<grid, kDwBlock, 0, st>>>(g, fd, dyp, xp, part, p.lanes); break;
+      case 3: dw_wgrad_pair_kernel<3><<<grid, kDwBlock, 0, st>>>(g, fd, dyp, xp, part, p.lanes); break;
+      case 4: dw_wgrad_pair_kernel<4><<<grid, kDwBlock, 0, st>>>(g, fd, dyp, xp, part, p.lanes); break;
+      default: dw_wgrad_pair_kernel<6><<<grid, kDwBlock, 0, st>>>(g, fd, dyp, xp, part, p.lanes); break;
+    }
+    dw_wgrad_reduce_kernel<<<rb, kRedWaves * 64, 0, st>>>(part, p.slices, taps, g.cout, dw);
+    return;
+  }
   dw_dispatch(dtype, p.vec, g.mult, [&](auto t, auto v, auto m) {
     using T = decltype(t);
     constexpr int V = decltype(v)::value, M = decltype(m)::value;
@@ -604,8 +868,6 @@ void launch_dw_wgrad(const DwGeom& g, int dtype, const void* dy, const void* x, 
     else
       dw_wgrad_kernel<T, V, M, kMaxTaps><<<grid, kDwBlock, 0, st>>>(g, fd, dyp, xp, part, p.lanes);
   });
-  const int taps = g.kh * g.kw;
-  const int rb = (taps * g.cout + 63) / 64;
   dw_wgrad_reduce_kernel<<<rb, kRedWaves * 64, 0, st>>>(part, p.slices, taps, g.cout, dw);
 }
 

@@ -24,6 +24,13 @@ GEOMS = [
     (8, 5, (3, 3), 1, 1, (10, 12)),     # multiplier without a compiled fast path
     (8, 3, (3, 3), 2, 1, (13, 17)),
     (128, 6, (3, 3), 1, 1, (16, 32)),   # BiSeNetV2 stage-5 shape class
+    # round 6: channel-stationary input-pair kernels (fwd / dgrad), the pair wgrad and the
+    # stride-2 2x2-block dgrad -- odd sizes hit its edge rows / columns
+    (16, 6, (3, 3), 2, 1, (21, 31)),
+    (10, 2, (3, 3), 2, 1, (9, 14)),     # 5 input pairs, multiplier 2
+    (12, 4, (3, 3), 1, 2, (11, 13)),    # multiplier 4, dilated
+    (6, 3, (3, 3), 1, 1, (7, 9)),       # multiplier 3 (odd output vectors)
+    (7, 2, (3, 3), 2, 1, (9, 9)),       # odd input channels: no pair path
 ]
 
 
