@@ -212,7 +212,7 @@ __global__ void __launch_bounds__(kDwBlock) dw_fwd_kernel(DwGeom g, DwDivs fd, c
 template <typename T, int VEC, int MT, int KS, bool CSW = false>
 __global__ void __launch_bounds__(kDwBlock) dw_dgrad_kernel(DwGeom g, DwDivs fd, const T* __restrict__ dy,
                                                             const float* __restrict__ wt, T* __restrict__ dx) {
-  static_assert(!CSW || (MT > 1 && KS > 0), "channel-stationary dgrad: multiplier path, compile-time taps");
+  static_assert(!CSW || (MT >= 1 && KS > 0), "channel-stationary dgrad: compile-time taps");
   constexpr int OV = MT > 1 ? VEC * MT : VEC;
   constexpr int SV = OV % 8 == 0 ? 8 : OV % 4 == 0 ? 4 : OV % 2 == 0 ? 2 : 1;
   const int cv_n = g.cin / VEC;
@@ -242,7 +242,12 @@ __global__ void __launch_bounds__(kDwBlock) dw_dgrad_kernel(DwGeom g, DwDivs fd,
       if constexpr (MT == 1) {
         float dv[VEC], wv[VEC];
         Vec<T, VEC>::load(dp + ci, dv);
-        load_wvec<VEC>(wp + ci, wv);
+        if constexpr (CSW) {
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) wv[v] = wreg[i * KS + j][v];
+        } else {
+          load_wvec<VEC>(wp + ci, wv);
+        }
 #pragma unroll
         for (int v = 0; v < VEC; ++v) acc[v] = fmaf(ok ? dv[v] : 0.f, wv[v], acc[v]);
       } else if constexpr (CSW) {
@@ -733,10 +738,12 @@ void launch_dw_fwd_stats(const DwGeom& g0, int dtype, const void* x, const float
 }
 
 void launch_dw_dgrad(const DwGeom& g0, int dtype, const void* dy, const float* wt, void* dx, hipStream_t st) {
-  const bool mcs = dw_mt_cs(g0);
+  // channel-stationary 3 x 3: multiplier convs on input pairs (dw_mt_cs), plain ones (MT 1) on
+  // their usual channel vectors with the 9 x VEC weights in registers (the forward's RTSEG_DW_CS)
+  const bool mcs = dw_mt_cs(g0) || (mt_of(g0.mult) == 1 && g0.kh == 3 && g0.kw == 3 && dw_cs_enabled());
   // stride-2 3 x 3 pad-1 multiplier convs: the 2 x 2 dx-block kernel (dw_dgrad_s2_kernel)
   const bool s2 = mcs && g0.sh == 2 && g0.sw == 2 && g0.ph == 1 && g0.pw == 1 && g0.dh == 1 && g0.dw == 1;
-  const int vec = mcs ? 2 : dw_vec(dtype, g0.cin);
+  const int vec = dw_mt_cs(g0) ? 2 : dw_vec(dtype, g0.cin);
   const int cv_n = g0.cin / vec;
   if (s2) {
     const int A = (g0.h + 1) / 2, B = (g0.w + 1) / 2;
@@ -753,7 +760,7 @@ void launch_dw_dgrad(const DwGeom& g0, int dtype, const void* dy, const float* w
       dw_dispatch(dtype, vec, g.mult, [&](auto t, auto v, auto m) {
         using T = decltype(t);
         constexpr int V = decltype(v)::value, M = decltype(m)::value;
-        if constexpr (M > 1 && V == 2)
+        if constexpr ((M > 1 && V == 2) || M == 1)
           dw_dgrad_s2_kernel<T, V, M><<<grid, kDwBlock, 0, st>>>(g, fd, reinterpret_cast<const T*>(dyb), wt,
                                                                  reinterpret_cast<T*>(dxb));
       });
@@ -773,8 +780,8 @@ void launch_dw_dgrad(const DwGeom& g0, int dtype, const void* dy, const float* w
     dw_dispatch(dtype, vec, g.mult, [&](auto t, auto v, auto m) {
       using T = decltype(t);
       constexpr int V = decltype(v)::value, M = decltype(m)::value;
-      if constexpr (M > 1 && V == 2) {
-        if (mcs) {  // channel-stationary 3 x 3 (dw_mt_cs)
+      if constexpr ((M > 1 && V == 2) || M == 1) {
+        if (mcs) {  // channel-stationary 3 x 3
           dw_dgrad_kernel<T, V, M, 3, true><<<grid, kDwBlock, 0, st>>>(g, fd, reinterpret_cast<const T*>(dyb), wt,
                                                                         reinterpret_cast<T*>(dxb));
           return;
@@ -828,7 +835,12 @@ DwWgradPlan dw_wgrad_plan(const DwGeom& g, int dtype) {
   // ~1024 blocks over 256 CUs, <= 512 slabs (the column reduce reads G rows), and
   // every block keeps >= 16 pixels per row
   int64_t G = 1024 / (static_cast<int64_t>(p.chunks) * p.tap_groups);
-  if (G > 512) G = 512;
+  int64_t gcap = 512;
+  if (const char* e = std::getenv("RTSEG_DW_WG_SLICES1")) {  // (tuning experiments)
+    gcap = std::max(1, std::atoi(e));
+    G = gcap / (static_cast<int64_t>(p.chunks) * p.tap_groups);
+  }
+  if (G > gcap) G = gcap;
   const int64_t gmax = (npix + static_cast<int64_t>(rows) * 16 - 1) / (static_cast<int64_t>(rows) * 16);
   if (G > gmax) G = gmax;
   if (G < 1) G = 1;

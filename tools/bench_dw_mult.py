@@ -20,6 +20,12 @@ SHAPES = [
     (16, 64, 64, 128, 6, 1),
     (16, 64, 64, 128, 6, 2),
     (16, 128, 32, 64, 6, 1),
+    # plain depth-wise (multiplier 1): the GE layers' second DW and the stride-2 shortcut DW
+    (16, 96, 128, 256, 1, 1),
+    (16, 192, 64, 128, 1, 1),
+    (16, 384, 32, 64, 1, 1),
+    (16, 16, 256, 512, 1, 2),
+    (16, 32, 128, 256, 1, 2),
 ]
 
 
