@@ -152,6 +152,7 @@ struct DwGeom {
 struct DwWgradPlan {
   int vec, lanes, chunks, nt, tap_groups, slices;  // nt = taps per wgrad thread
   int pairs = 0;  // 1: the channel-multiplier kernel (bf16, mult 2/3/4/6): threads own input-channel pairs
+  int quad = 0;   // 1: plain 3 x 3 stride-1 kernel over 4-pixel row segments (dw_wgrad_quad_kernel)
 };
 int dw_vec(int dtype, int c);
 DwWgradPlan dw_wgrad_plan(const DwGeom& g, int dtype);

@@ -360,6 +360,61 @@ __global__ void __launch_bounds__(kDwBlock) dw_dgrad_s2_kernel(DwGeom g, DwDivs 
   }
 }
 
+// Plain (multiplier 1) 3 x 3 stride-1 data gradient (column dilation 1) over 4-pixel dx row
+// segments, channel-stationary (9 x VEC weights in registers): per kernel row the segment needs 6
+// dy columns -- 18 loads per 4 dx pixels instead of 36.  fd: divisors (cv_n, ceil(W/4), H).
+template <typename T, int VEC>
+__global__ void __launch_bounds__(kDwBlock) dw_dgrad_quad_kernel(DwGeom g, DwDivs fd, const T* __restrict__ dy,
+                                                                 const float* __restrict__ wt, T* __restrict__ dx) {
+  const int cv_n = g.cin / VEC;
+  const int wq_n = (g.w + 3) / 4;
+  const uint32_t total = static_cast<uint32_t>(g.n) * g.h * wq_n * cv_n;  // < 2^31 (host splits)
+  float wreg[9][VEC];
+  {
+    const int c0 = static_cast<int>((blockIdx.x * kDwBlock + threadIdx.x) % static_cast<uint32_t>(cv_n)) * VEC;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) load_wvec<VEC>(wt + t * g.cout + c0, wreg[t]);
+  }
+  for (uint32_t it = blockIdx.x * kDwBlock + threadIdx.x; it < total; it += gridDim.x * kDwBlock) {
+    uint32_t cvu, wqu, hiu;
+    const uint32_t pix = fd.c.divmod(it, cvu);
+    const uint32_t r = fd.w.divmod(pix, wqu);
+    const int n = static_cast<int>(fd.h.divmod(r, hiu));
+    const int hi = static_cast<int>(hiu), wi0 = static_cast<int>(wqu) * 4, ci = static_cast<int>(cvu) * VEC;
+    float acc[4][VEC];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) acc[q][v] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int ho = hi + g.ph - i * g.dh;  // stride 1: always on the grid
+      const bool rok = ho >= 0 && ho < g.ho;
+      const T* dr = dy + (static_cast<int64_t>(n) * g.ho + min(max(ho, 0), g.ho - 1)) * g.wo * g.cout + ci;
+      // dx column wi0 + q takes dy column wi0 + q + pw - j (j = 0..2): columns wi0 + pw - 2 + c, c = 0..5
+      float dv[6][VEC];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        const int wo = wi0 + g.pw - 2 + c;
+        const bool ok = rok && wo >= 0 && wo < g.wo;
+        Vec<T, VEC>::load(dr + static_cast<int64_t>(min(max(wo, 0), g.wo - 1)) * g.cout, dv[c]);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) dv[c][v] = ok ? dv[c][v] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) acc[q][v] = fmaf(dv[q + 2 - j][v], wreg[i * 3 + j][v], acc[q][v]);
+    }
+    T* xo = dx + ((static_cast<int64_t>(n) * g.h + hi) * g.w + wi0) * g.cin + ci;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (wi0 + q < g.w) Vec<T, VEC>::store(xo + static_cast<int64_t>(q) * g.cin, acc[q]);
+  }
+}
+
 // ---------------------------------------------------------------- weight grad
 // grid: x = pixel slices (G), y = channel chunks, z = tap groups.  Block = LANES
 // channel-vector lanes x ROWS pixel rows; each thread accumulates <= kMaxTaps
@@ -533,6 +588,83 @@ __global__ void __launch_bounds__(kDwBlock) dw_wgrad_pair_kernel(DwGeom g, DwDiv
         const int c = c0 + k;
         if (c < g.cout) part[slab + static_cast<int64_t>(t) * g.cout + c] = s;
       }
+    }
+  }
+}
+
+// Plain (multiplier 1) 3 x 3 stride-1 weight gradient (column dilation 1, any row dilation) over
+// 4-pixel row segments: per kernel row the segment needs 6 input columns, so a thread loads 4 dy +
+// 3 x 6 input vectors per 4 output pixels where dw_wgrad_kernel loads 4 x (1 + 9) -- the
+// L1 / address traffic, not HBM, bounds that kernel (more slices do not help).  Same lanes /
+// slab / column-reduce layout as dw_wgrad_kernel with NT = 9.
+template <typename T, int VEC>
+__global__ void __launch_bounds__(kDwBlock) dw_wgrad_quad_kernel(DwGeom g, DwDivs fd, const T* __restrict__ dy,
+                                                                 const T* __restrict__ x, float* __restrict__ part,
+                                                                 int lanes) {
+  const int rows = kDwBlock / lanes;
+  const int lane = threadIdx.x % lanes;
+  const int row = threadIdx.x / lanes;
+  const int cv = blockIdx.y * lanes + lane;
+  const bool active = cv < g.cout / VEC;
+  const int co = cv * VEC;
+  float acc[9][VEC];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) acc[t][v] = 0.f;
+  const int wq_n = (g.wo + 3) / 4;
+  const uint32_t nq = static_cast<uint32_t>(g.n) * g.ho * wq_n;
+  if (active) {
+    for (uint32_t p = blockIdx.x * rows + row; p < nq; p += gridDim.x * rows) {
+      uint32_t wqu, hou;
+      const uint32_t r = fd.w.divmod(p, wqu);
+      const int n = static_cast<int>(fd.h.divmod(r, hou));
+      const int ho = static_cast<int>(hou), wo0 = static_cast<int>(wqu) * 4;
+      float dv[4][VEC];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool ok = wo0 + q < g.wo;
+        Vec<T, VEC>::load(dy + ((static_cast<int64_t>(n) * g.ho + ho) * g.wo + min(wo0 + q, g.wo - 1)) * g.cout + co,
+                          dv[q]);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) dv[q][v] = ok ? dv[q][v] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int hi = ho - g.ph + i * g.dh;
+        const bool rok = hi >= 0 && hi < g.h;
+        const T* xr = x + (static_cast<int64_t>(n) * g.h + min(max(hi, 0), g.h - 1)) * g.w * g.cin + co;
+        float xv[6][VEC];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+          const int wi = wo0 - g.pw + c;
+          const bool ok = rok && wi >= 0 && wi < g.w;
+          Vec<T, VEC>::load(xr + static_cast<int64_t>(min(max(wi, 0), g.w - 1)) * g.cin, xv[c]);
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) xv[c][v] = ok ? xv[c][v] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) acc[i * 3 + j][v] = fmaf(xv[q + j][v], dv[q][v], acc[i * 3 + j][v]);
+      }
+    }
+  }
+  __shared__ float red[kDwBlock * 8];
+  const int64_t slab = static_cast<int64_t>(blockIdx.x) * 9 * g.cout;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    __syncthreads();
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) red[(row * lanes + lane) * VEC + v] = acc[t][v];
+    __syncthreads();
+    for (int k = threadIdx.x; k < lanes * VEC; k += kDwBlock) {
+      float s = 0.f;
+      for (int rr = 0; rr < rows; ++rr) s += red[rr * lanes * VEC + k];
+      const int c = blockIdx.y * lanes * VEC + k;
+      if (c < g.cout) part[slab + static_cast<int64_t>(t) * g.cout + c] = s;
     }
   }
 }
@@ -745,6 +877,29 @@ void launch_dw_dgrad(const DwGeom& g0, int dtype, const void* dy, const float* w
   const bool s2 = mcs && g0.sh == 2 && g0.sw == 2 && g0.ph == 1 && g0.pw == 1 && g0.dh == 1 && g0.dw == 1;
   const int vec = dw_mt_cs(g0) ? 2 : dw_vec(dtype, g0.cin);
   const int cv_n = g0.cin / vec;
+  // plain 3 x 3 stride-1 (column dilation 1): the 4-pixel row-segment kernel
+  const bool q1 = mcs && mt_of(g0.mult) == 1 && g0.sh == 1 && g0.sw == 1 && g0.dw == 1;
+  if (q1) {
+    const int wq = (g0.w + 3) / 4;
+    const int64_t per_img = static_cast<int64_t>(g0.h) * wq * cv_n;
+    const int nb = batch_chunk(per_img, g0.n);
+    const int64_t eb = elem_bytes(dtype);
+    for (int n0 = 0; n0 < g0.n; n0 += nb) {
+      DwGeom g = g0;
+      g.n = n0 + nb <= g0.n ? nb : g0.n - n0;
+      const char* dyb = static_cast<const char*>(dy) + static_cast<int64_t>(n0) * g.ho * g.wo * g.cout * eb;
+      char* dxb = static_cast<char*>(dx) + static_cast<int64_t>(n0) * g.h * g.w * g.cin * eb;
+      const DwDivs fd{FastDiv::make(cv_n), FastDiv::make(wq), FastDiv::make(g.h)};
+      const int grid = dw_stats_grid(per_img * g.n, cv_n);
+      dw_dispatch(dtype, vec, 1, [&](auto t, auto v, auto) {
+        using T = decltype(t);
+        constexpr int V = decltype(v)::value;
+        dw_dgrad_quad_kernel<T, V><<<grid, kDwBlock, 0, st>>>(g, fd, reinterpret_cast<const T*>(dyb), wt,
+                                                              reinterpret_cast<T*>(dxb));
+      });
+    }
+    return;
+  }
   if (s2) {
     const int A = (g0.h + 1) / 2, B = (g0.w + 1) / 2;
     const int64_t per_img = static_cast<int64_t>(A) * B * cv_n;
@@ -823,6 +978,7 @@ DwWgradPlan dw_wgrad_plan(const DwGeom& g, int dtype) {
     return p;
   }
   p.vec = dw_vec(dtype, g.cout);
+  p.quad = mt == 1 && g.kh == 3 && g.kw == 3 && g.sh == 1 && g.sw == 1 && g.dw == 1 && dw_cs_enabled() ? 1 : 0;
   const int cv_n = g.cout / p.vec;
   p.lanes = 64;
   while (p.lanes > 1 && p.lanes / 2 >= cv_n) p.lanes /= 2;
@@ -830,7 +986,7 @@ DwWgradPlan dw_wgrad_plan(const DwGeom& g, int dtype) {
   const int taps = g.kh * g.kw;
   p.nt = taps <= 3 ? 3 : taps <= 5 ? 5 : kMaxTaps;
   p.tap_groups = (taps + p.nt - 1) / p.nt;
-  const int64_t npix = static_cast<int64_t>(g.n) * g.ho * g.wo;
+  const int64_t npix = static_cast<int64_t>(g.n) * g.ho * (p.quad ? (g.wo + 3) / 4 : g.wo);  // work items
   const int rows = kDwBlock / p.lanes;
   // ~1024 blocks over 256 CUs, <= 512 slabs (the column reduce reads G rows), and
   // every block keeps >= 16 pixels per row
@@ -865,6 +1021,17 @@ void launch_dw_wgrad(const DwGeom& g, int dtype, const void* dy, const void* x, 
       case 4: dw_wgrad_pair_kernel<4><<<grid, kDwBlock, 0, st>>>(g, fd, dyp, xp, part, p.lanes); break;
       default: dw_wgrad_pair_kernel<6><<<grid, kDwBlock, 0, st>>>(g, fd, dyp, xp, part, p.lanes); break;
     }
+    dw_wgrad_reduce_kernel<<<rb, kRedWaves * 64, 0, st>>>(part, p.slices, taps, g.cout, dw);
+    return;
+  }
+  if (p.quad) {
+    const DwDivs fq{FastDiv::make(1), FastDiv::make((g.wo + 3) / 4), FastDiv::make(g.ho)};
+    dw_dispatch(dtype, p.vec, 1, [&](auto t, auto v, auto) {
+      using T = decltype(t);
+      constexpr int V = decltype(v)::value;
+      dw_wgrad_quad_kernel<T, V><<<grid, kDwBlock, 0, st>>>(g, fq, static_cast<const T*>(dy), static_cast<const T*>(x),
+                                                           part, p.lanes);
+    });
     dw_wgrad_reduce_kernel<<<rb, kRedWaves * 64, 0, st>>>(part, p.slices, taps, g.cout, dw);
     return;
   }
