@@ -77,7 +77,10 @@ __device__ __forceinline__ void load_wvec(const float* p, float* w) {
 // per output pixel -- the unrolled taps then issue only their input loads (KS^2 in flight).  Per
 // output that removes 9 x 32 B of weight loads against 9 x 16 B of activations (the reason an
 // unrolled 3 x 3 without it measured 4-5x slower: see launch_dw_fwd).
-template <typename T, int VEC, int MT, int KS, bool STATS = false, bool CSW = false>
+// QD (MT 1, 3 x 3, CSW, stride 1, column dilation 1): a thread computes 4 consecutive output pixels
+// of its channel vector from 6 input columns per kernel row (18 loads instead of 36); fd.w then
+// divides the 4-pixel segments of a row.
+template <typename T, int VEC, int MT, int KS, bool STATS = false, bool CSW = false, bool QD = false>
 __global__ void __launch_bounds__(kDwBlock) dw_fwd_kernel(DwGeom g, DwDivs fd, const T* __restrict__ x,
                                                           const float* __restrict__ wt,
                                                           const float* __restrict__ bias, T* __restrict__ y,
@@ -87,7 +90,8 @@ __global__ void __launch_bounds__(kDwBlock) dw_fwd_kernel(DwGeom g, DwDivs fd, c
   // SV: the widest vector (<= 8) dividing OV -- output stores (co and Cout are multiples of OV)
   constexpr int SV = OV % 8 == 0 ? 8 : OV % 4 == 0 ? 4 : OV % 2 == 0 ? 2 : 1;
   const int cv_n = MT > 1 ? g.cin / VEC : g.cout / VEC;
-  const uint32_t total = static_cast<uint32_t>(g.n) * g.ho * g.wo * cv_n;  // < 2^31 (host splits)
+  static_assert(!QD || (MT == 1 && KS == 3 && CSW), "row segments: plain 3 x 3 channel-stationary");
+  const uint32_t total = static_cast<uint32_t>(g.n) * g.ho * (QD ? (g.wo + 3) / 4 : g.wo) * cv_n;  // < 2^31
   float wreg[CSW ? KS * KS : 1][CSW ? OV : 1];
   float breg[CSW ? OV : 1];
   if constexpr (CSW) {
@@ -110,6 +114,55 @@ __global__ void __launch_bounds__(kDwBlock) dw_fwd_kernel(DwGeom g, DwDivs fd, c
     const int cv = static_cast<int>(cvu), wo = static_cast<int>(wou), ho = static_cast<int>(hou);
     const int co = MT > 1 ? cv * VEC * MT : cv * VEC;  // first output channel
     const int ci = cv * VEC;                             // first input channel (MT > 1)
+    if constexpr (QD) {
+      const int wo0 = wo * 4;
+      float a4[4][VEC];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) a4[q][v] = breg[v];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int hi = ho - g.ph + i * g.dh;
+        const bool rok = hi >= 0 && hi < g.h;
+        const T* xr = x + (static_cast<int64_t>(n) * g.h + min(max(hi, 0), g.h - 1)) * g.w * g.cin + co;
+        float xv[6][VEC];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {  // output wo0 + q, tap j reads column wo0 + q + j - pw
+          const int wi = wo0 - g.pw + c;
+          const bool ok = rok && wi >= 0 && wi < g.w;
+          Vec<T, VEC>::load(xr + static_cast<int64_t>(min(max(wi, 0), g.w - 1)) * g.cin, xv[c]);
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) xv[c][v] = ok ? xv[c][v] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) a4[q][v] = fmaf(xv[q + j][v], wreg[i * 3 + j][v], a4[q][v]);
+      }
+      T* yq = y + ((static_cast<int64_t>(n) * g.ho + ho) * g.wo + wo0) * g.cout + co;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (wo0 + q >= g.wo) break;
+        if constexpr (!STATS) {
+          if (g.act != 0) {
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) a4[q][v] = g.act == 1 ? fmaxf(a4[q][v], 0.f) : fminf(fmaxf(a4[q][v], 0.f), 6.f);
+          }
+        }
+        Vec<T, VEC>::store(yq + static_cast<int64_t>(q) * g.cout, a4[q]);
+        if constexpr (STATS) {
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) {
+            ssum[v] += a4[q][v];
+            ssq[v] = fmaf(a4[q][v], a4[q][v], ssq[v]);
+          }
+        }
+      }
+      continue;
+    }
     float acc[OV];
 #pragma unroll
     for (int v = 0; v < OV; ++v) {
@@ -765,6 +818,14 @@ static bool dw_mt_cs(const DwGeom& g) {
   return on && mt_of(g.mult) > 1 && g.kh == 3 && g.kw == 3 && g.cin % 2 == 0;
 }
 
+// Plain 3 x 3 stride-1 forwards (column dilation 1) on 4-pixel row segments (dw_fwd_kernel QD);
+// RTSEG_DW_QD=0: one pixel per thread (A/B)
+static bool dw_fwd_qd(const DwGeom& g) {
+  static const bool on = [] { const char* e = std::getenv("RTSEG_DW_QD"); return !(e && e[0] == '0'); }();
+  return on && mt_of(g.mult) == 1 && g.kh == 3 && g.kw == 3 && g.sh == 1 && g.sw == 1 && g.dw == 1 &&
+         dw_cs_enabled();
+}
+
 void launch_dw_fwd(const DwGeom& g0, int dtype, const void* x, const float* wt, const float* bias, void* y,
                    hipStream_t st) {
   const int mt = mt_of(g0.mult);
@@ -772,7 +833,9 @@ void launch_dw_fwd(const DwGeom& g0, int dtype, const void* x, const float* wt, 
   // MT > 1: vectors over the INPUT channels (each feeds VEC*MT contiguous outputs)
   const int vec = mcs ? 2 : mt > 1 ? dw_vec(dtype, g0.cin) : dw_vec(dtype, g0.cout);
   const int cv_n = (mt > 1 ? g0.cin : g0.cout) / vec;
-  const int64_t per_img = static_cast<int64_t>(g0.ho) * g0.wo * cv_n;
+  const bool qd = dw_fwd_qd(g0);
+  const int wq = qd ? (g0.wo + 3) / 4 : g0.wo;  // work items per output row
+  const int64_t per_img = static_cast<int64_t>(g0.ho) * wq * cv_n;
   const int nb = batch_chunk(per_img, g0.n);
   const int64_t eb = elem_bytes(dtype);
   for (int n0 = 0; n0 < g0.n; n0 += nb) {
@@ -780,12 +843,19 @@ void launch_dw_fwd(const DwGeom& g0, int dtype, const void* x, const float* wt, 
     g.n = n0 + nb <= g0.n ? nb : g0.n - n0;
     const char* xb = static_cast<const char*>(x) + static_cast<int64_t>(n0) * g.h * g.w * g.cin * eb;
     char* yb = static_cast<char*>(y) + static_cast<int64_t>(n0) * g.ho * g.wo * g.cout * eb;
-    const DwDivs fd{FastDiv::make(cv_n), FastDiv::make(g.wo), FastDiv::make(g.ho)};
+    const DwDivs fd{FastDiv::make(cv_n), FastDiv::make(wq), FastDiv::make(g.ho)};
     const bool cs3 = (mt == 1 && g.kh == 3 && g.kw == 3 && dw_cs_enabled()) || mcs;
     const int grid = cs3 ? dw_stats_grid(per_img * g.n, cv_n) : stream_grid(per_img * g.n, kDwBlock);
     dw_dispatch(dtype, vec, g.mult, [&](auto t, auto v, auto m) {
       using T = decltype(t);
       constexpr int V = decltype(v)::value, M = decltype(m)::value;
+      if constexpr (M == 1) {
+        if (qd) {
+          dw_fwd_kernel<T, V, 1, 3, false, true, true><<<grid, kDwBlock, 0, st>>>(
+              g, fd, reinterpret_cast<const T*>(xb), wt, bias, reinterpret_cast<T*>(yb));
+          return;
+        }
+      }
       if constexpr (M == 1 || (M > 1 && V == 2)) {
         if (cs3) {  // 3 x 3, channel-stationary: weights in registers, 9 loads in flight
           dw_fwd_kernel<T, V, M, 3, false, true><<<grid, kDwBlock, 0, st>>>(
@@ -822,7 +892,7 @@ int dw_fwd_stats_rows(const DwGeom& g0, int dtype) {
   if (mt == 0) return 0;
   const int vec = dw_fwd_stats_vec(g0, dtype);
   const int cv_n = (mt > 1 ? g0.cin : g0.cout) / vec;
-  const int64_t per_img = static_cast<int64_t>(g0.ho) * g0.wo * cv_n;
+  const int64_t per_img = static_cast<int64_t>(g0.ho) * (dw_fwd_qd(g0) ? (g0.wo + 3) / 4 : g0.wo) * cv_n;
   const int nb = batch_chunk(per_img, g0.n);
   int rows = 0;
   for (int n0 = 0; n0 < g0.n; n0 += nb) rows += dw_stats_grid(per_img * std::min(nb, g0.n - n0), cv_n);
@@ -834,7 +904,9 @@ void launch_dw_fwd_stats(const DwGeom& g0, int dtype, const void* x, const float
   const int mt = mt_of(g0.mult);
   const int vec = dw_fwd_stats_vec(g0, dtype);
   const int cv_n = (mt > 1 ? g0.cin : g0.cout) / vec;
-  const int64_t per_img = static_cast<int64_t>(g0.ho) * g0.wo * cv_n;
+  const bool qd = dw_fwd_qd(g0);
+  const int wq = qd ? (g0.wo + 3) / 4 : g0.wo;  // work items per output row (as dw_fwd_stats_rows)
+  const int64_t per_img = static_cast<int64_t>(g0.ho) * wq * cv_n;
   const int nb = batch_chunk(per_img, g0.n);
   const int64_t eb = elem_bytes(dtype);
   for (int n0 = 0; n0 < g0.n; n0 += nb) {
@@ -842,12 +914,17 @@ void launch_dw_fwd_stats(const DwGeom& g0, int dtype, const void* x, const float
     g.n = n0 + nb <= g0.n ? nb : g0.n - n0;
     const char* xb = static_cast<const char*>(x) + static_cast<int64_t>(n0) * g.h * g.w * g.cin * eb;
     char* yb = static_cast<char*>(y) + static_cast<int64_t>(n0) * g.ho * g.wo * g.cout * eb;
-    const DwDivs fd{FastDiv::make(cv_n), FastDiv::make(g.wo), FastDiv::make(g.ho)};
+    const DwDivs fd{FastDiv::make(cv_n), FastDiv::make(wq), FastDiv::make(g.ho)};
     const int grid = dw_stats_grid(per_img * g.n, cv_n);
     dw_dispatch(dtype, vec, g.mult, [&](auto t, auto v, auto m) {
       using T = decltype(t);
       constexpr int V = decltype(v)::value, M = decltype(m)::value;
       if constexpr (M == 1) {
+        if (qd) {
+          dw_fwd_kernel<T, V, 1, 3, true, true, true><<<grid, kDwBlock, 0, st>>>(
+              g, fd, reinterpret_cast<const T*>(xb), wt, nullptr, reinterpret_cast<T*>(yb), part);
+          return;
+        }
         if (g.kh == 3 && g.kw == 3 && dw_cs_enabled()) {  // the grid is channel-stationary already
           dw_fwd_kernel<T, V, 1, 3, true, true><<<grid, kDwBlock, 0, st>>>(
               g, fd, reinterpret_cast<const T*>(xb), wt, nullptr, reinterpret_cast<T*>(yb), part);
