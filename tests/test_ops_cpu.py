@@ -341,3 +341,36 @@ def test_cat_bn_act_cpu_matches_cat_then_bn():
         torch.testing.assert_close(y, ref)
         torch.testing.assert_close(bn.running_mean, b2.running_mean)
         torch.testing.assert_close(bn.running_var, b2.running_var)
+
+
+def test_concat_sink_pooled_part_cpu_fallback():
+    """ConcatSink.max_pool off the GPU: a plain pooled tensor (cast to the concat dtype when asked),
+    and cat() is torch.cat -- the reference's StemBlock / InitialBlock semantics."""
+    x = torch.randn(2, 16, 9, 14)
+    sink = ops.ConcatSink([16, 16])
+    p = sink.max_pool(1, x, 3, 2, 1)
+    assert isinstance(p, torch.Tensor)
+    torch.testing.assert_close(p, F.max_pool2d(x, 3, 2, 1))
+    y = torch.randn(2, 16, 5, 7)
+    torch.testing.assert_close(sink.cat([y, p]), torch.cat([y, p], 1))
+    pb = ops.ConcatSink([16, 16]).max_pool(1, x, 3, 2, 1, dtype=torch.bfloat16)
+    assert pb.dtype == torch.bfloat16
+    torch.testing.assert_close(pb, F.max_pool2d(x, 3, 2, 1).to(torch.bfloat16))
+
+
+def test_stem_blocks_cpu_match_plain_cat():
+    """BiSeNetV2's StemBlock and the ENet-family InitialBlock (concat sinks on the GPU) equal the
+    reference formulation -- conv_last(cat(left, maxpool)) / cat(conv, maxpool) -- on the CPU."""
+    from realtime_semantic_segmentation_pytorch_amd.models.bisenetv2 import StemBlock
+    from realtime_semantic_segmentation_pytorch_amd.models.enet import InitialBlock
+
+    torch.manual_seed(0)
+    stem = StemBlock(3, 16).eval()
+    x = torch.randn(2, 3, 32, 48)
+    with torch.no_grad():
+        s = stem.conv_init(x)
+        want = stem.conv_last(torch.cat([stem.left_branch(s), stem.right_branch(s)], 1))
+        torch.testing.assert_close(stem(x), want)
+        ib = InitialBlock(16, 64, "relu").eval()
+        z = torch.randn(2, 16, 20, 30)
+        torch.testing.assert_close(ib(z), torch.cat([ib.conv(z), ib.pool(z)], 1))
